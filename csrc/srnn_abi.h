@@ -1,0 +1,87 @@
+// srnn_abi.h — C ABI of libsrnn.so (mirrored by ctypes structures in
+// self_replicating_neural_networks_amd/ops/_lib.py; keep the field order in sync).
+#pragma once
+#include <stdint.h>
+
+extern "C" {
+
+struct SrnnCfg {
+  int32_t kind;        // 0 weightwise, 1 aggregating, 2 recurrent, 3 fft
+  int32_t width;
+  int32_t depth;
+  int32_t aggregates;
+  int32_t aggregator;  // 0 mean, 1 max, 2 max with the reference's and/or quirk
+  int32_t shuffler;    // 0 none, 1 random
+  int32_t pp;          // padded row stride (floats)
+  int32_t p;           // weights per particle
+};
+
+struct SrnnArgs {
+  int64_t n;            // work items (rows) of this call
+  int64_t n_total;      // soup: global population size
+  int64_t lo;           // soup: first global slot owned by this rank
+  int32_t steps;        // fixpoint run: step limit
+  int32_t epochs;       // train: epochs; soup: train count
+  int32_t severity;     // soup: learn_from_severity
+  int32_t early_exit;   // fixpoint run: stop at fixpoint / divergence
+  int32_t flags;        // bit0 shuffle samples, bit1 remove_divergent, bit2 remove_zero, bit3 count fix_sec
+  int32_t gen;          // soup generation (time)
+  float eps;
+  float lr;
+  float attacking_rate;
+  float learn_from_rate;
+  uint64_t seed;
+  uint32_t ctr;         // op counter for per-particle random streams
+  uint32_t pad0;
+  float* W;             // rows [n][pp] (in/out)
+  float* W2;            // second table (source rows / output rows)
+  float* traj;          // fixpoint run trajectory [(steps+1)][n][pp] or null
+  const int64_t* idx_f; // apply: applying-net row per item (null = identity)
+  const int64_t* idx_t; // apply: target row per item (null = identity)
+  const int64_t* idx_o; // apply: output row per item (null = identity)
+  const int64_t* uid;   // per-row uid (keys random streams); null -> row index
+  int8_t* cls;          // per-row class
+  int32_t* nsteps;      // per-row steps taken
+  float* loss;          // per-row loss
+  uint64_t* counts;     // [5] class histogram (atomic adds)
+  int32_t* i32a;        // soup: attack target per global slot
+  int32_t* i32b;        // soup: teacher per global slot
+  int32_t* i32c;        // soup: per-local-victim attack count; later respawn flags as int32
+  int32_t* i32d;        // soup: exclusive offsets [n+1]
+  int32_t* i32e;        // soup: fill cursor per local victim
+  int32_t* i32f;        // soup: attacker list (CSR payload)
+  int64_t* uid_out;     // respawn: uid column to update
+  const int64_t* uid_base;  // respawn: device scalar, first uid for this rank
+  const int32_t* gen_ptr;   // soup: device scalar generation (graph replay); null -> gen
+  int8_t* action;       // soup: action code per local row
+  int64_t* counterpart; // soup: counterpart slot per local row
+  int8_t* respawn;      // soup: 0 none, 1 divergent_dead, 2 zweo_dead
+  void* temp;           // scratch for device scans
+  int64_t temp_bytes;
+  int32_t dev;          // 0 host (CPU tensors), 1 device (HIP)
+  int32_t pad1;
+  void* stream;         // hipStream_t for dev == 1
+};
+
+enum SrnnOp {
+  OP_INIT = 0,          // W[i] = fresh particle keyed by uid[i]
+  OP_APPLY = 1,         // W2[idx_o[i]] = f_{W[idx_f[i]]}(W[idx_t[i]])
+  OP_RUN_FIXPOINT = 2,  // run_net semantics per row (in place), cls + nsteps (+traj)
+  OP_TRAIN = 3,         // `epochs` self-train epochs (in place), loss
+  OP_LEARN = 4,         // `epochs` epochs on samples of W2[idx_t[i]], loss
+  OP_CLASSIFY = 5,      // cls + counts
+  OP_PERTURB = 6,       // W[i] +-= U(0,1) * eps, p=1/2 each (known-fixpoint variation)
+  OP_SOUP_DECIDE = 7,   // per global slot: attack target / teacher; per local victim count
+  OP_SOUP_FILL = 8,     // CSR attacker lists per local victim
+  OP_SOUP_EVOLVE = 9,   // fused attack -> learn -> train -> respawn flags for local rows
+  OP_SCAN = 10,         // i32d[0..n] = exclusive scan of i32c[0..n)
+  OP_RESPAWN = 11,      // rows with respawn != 0: uid_out = *uid_base + i32d[i], fresh weights
+  OP_VARY_RUN = 12,     // known-fixpoint variation run: nsteps = time to vergence, loss = time as fixpoint
+};
+
+int srnn_abi_version();
+int srnn_has_config(const SrnnCfg* cfg);
+int srnn_run(int op, const SrnnCfg* cfg, const SrnnArgs* args);
+const char* srnn_last_error();
+int64_t srnn_scan_temp_bytes(int64_t n);
+}

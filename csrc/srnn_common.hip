@@ -1,0 +1,86 @@
+// srnn_common.hip — ABI entry points, error handling and device scans of libsrnn.so.
+#include "srnn_kernels.h"
+#include <hipcub/hipcub.hpp>
+#include <cstring>
+#include <string>
+
+namespace srnn {
+static thread_local std::string g_err;
+void set_error(const char* msg) { g_err = msg ? msg : ""; }
+}  // namespace srnn
+
+extern "C" int srnn_dispatch_ww(int op, const SrnnCfg* c, const SrnnArgs* a);
+extern "C" int srnn_dispatch_agg(int op, const SrnnCfg* c, const SrnnArgs* a);
+extern "C" int srnn_dispatch_rnn(int op, const SrnnCfg* c, const SrnnArgs* a);
+extern "C" int srnn_dispatch_fft(int op, const SrnnCfg* c, const SrnnArgs* a);
+
+__global__ void k_scan_tail(int32_t* out, const int32_t* in, int64_t n) {
+  // out[0] = 0 (inclusive scan was written to out+1)
+  out[0] = 0;
+  (void)in;
+  (void)n;
+}
+
+static int dispatch(int op, const SrnnCfg* c, const SrnnArgs* a) {
+  switch (c->kind) {
+    case 0: return srnn_dispatch_ww(op, c, a);
+    case 1: return srnn_dispatch_agg(op, c, a);
+    case 2: return srnn_dispatch_rnn(op, c, a);
+    case 3: return srnn_dispatch_fft(op, c, a);
+    default: srnn::set_error("unknown network kind"); return -1;
+  }
+}
+
+extern "C" {
+
+int srnn_abi_version() { return 4; }
+
+const char* srnn_last_error() { return srnn::g_err.c_str(); }
+
+int srnn_has_config(const SrnnCfg* cfg) {
+  int r = dispatch(-1, cfg, nullptr);
+  return r == 0 ? 1 : 0;
+}
+
+int64_t srnn_scan_temp_bytes(int64_t n) {
+  size_t bytes = 0;
+  hipcub::DeviceScan::InclusiveSum(nullptr, bytes, (const int32_t*)nullptr, (int32_t*)nullptr, (int)n);
+  return (int64_t)bytes;
+}
+
+int srnn_run(int op, const SrnnCfg* cfg, const SrnnArgs* a) {
+  srnn::set_error("");
+  if (op == OP_SCAN) {
+    // i32d[0] = 0, i32d[k+1] = sum_{q<=k} i32c[q]
+    if (!a->dev) {
+      int64_t acc = 0;
+      a->i32d[0] = 0;
+      for (int64_t k = 0; k < a->n; ++k) {
+        acc += a->i32c[k];
+        a->i32d[k + 1] = (int32_t)acc;
+      }
+      return 0;
+    }
+    hipStream_t st = (hipStream_t)a->stream;
+    if (a->n > 0) {
+      size_t bytes = (size_t)a->temp_bytes;
+      hipError_t e = hipcub::DeviceScan::InclusiveSum(a->temp, bytes, a->i32c, a->i32d + 1, (int)a->n, st);
+      if (e != hipSuccess) {
+        srnn::set_error(hipGetErrorString(e));
+        return -3;
+      }
+    }
+    hipLaunchKernelGGL(k_scan_tail, dim3(1), dim3(1), 0, st, a->i32d, a->i32c, a->n);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) {
+      srnn::set_error(hipGetErrorString(e));
+      return -3;
+    }
+    return 0;
+  }
+  int r = dispatch(op, cfg, a);
+  if (r == 1) srnn::set_error("network shape not instantiated in libsrnn (add it to csrc/srnn_<kind>.hip)");
+  return r;
+}
+
+}  // extern "C"

@@ -1,0 +1,700 @@
+// srnn_core.h — per-particle math of the self-replicating-network engine.
+//
+// Every function here is `SRNN_HD` (host + device): the same code runs inside the
+// lane-per-particle HIP kernels (srnn_kernels.hip) and inside the host thread-pool
+// loops used on CPU tensors.  One particle = one flat fp32 weight vector laid out in
+// Keras `get_weights()` order (layer by layer, each kernel row-major (in, out); a
+// SimpleRNN layer contributes [kernel, recurrent_kernel]) — reference
+// code/network.py:100-104.  Networks are linear and bias-free.
+//
+// Architectures are compile-time templates so that every loop over weights is fully
+// unrolled and the weights of a particle live in VGPRs.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <math.h>
+
+#define SRNN_HD __host__ __device__ __forceinline__
+
+namespace srnn {
+
+// ----------------------------------------------------------------------------------
+// Philox4x32-10 counter-based RNG.  ctr = (c0,c1,c2,c3), key = (k0,k1).
+// Streams: key = seed, ctr = (id_lo, id_hi, step, purpose).
+// ----------------------------------------------------------------------------------
+struct U4 { uint32_t x, y, z, w; };
+
+SRNN_HD void mulhilo(uint32_t a, uint32_t b, uint32_t& hi, uint32_t& lo) {
+  uint64_t p = (uint64_t)a * (uint64_t)b;
+  hi = (uint32_t)(p >> 32);
+  lo = (uint32_t)p;
+}
+
+SRNN_HD U4 philox(U4 c, uint32_t k0, uint32_t k1) {
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    uint32_t hi0, lo0, hi1, lo1;
+    mulhilo(0xD2511F53u, c.x, hi0, lo0);
+    mulhilo(0xCD9E8D57u, c.z, hi1, lo1);
+    U4 n;
+    n.x = hi1 ^ c.y ^ k0;
+    n.y = lo1;
+    n.z = hi0 ^ c.w ^ k1;
+    n.w = lo0;
+    c = n;
+    k0 += 0x9E3779B9u;
+    k1 += 0xBB67AE85u;
+  }
+  return c;
+}
+
+enum Purpose : uint32_t {
+  P_INIT = 1,        // glorot uniform init         ctr=(uid, blk)
+  P_NORMAL = 2,      // normals for orthogonal init ctr=(uid, blk)
+  P_SHUFFLE = 3,     // per-epoch sample permutation ctr=(uid, op_ctr)
+  P_AGGSHUF = 4,     // aggregating shuffle_random   ctr=(uid, op_ctr)
+  P_SOUP = 5,        // soup decisions               ctr=(slot, generation)
+  P_PERTURB = 6,     // known-fixpoint variation     ctr=(uid, op_ctr)
+};
+
+struct Rng {
+  uint32_t k0, k1;
+  SRNN_HD U4 draw(uint64_t id, uint32_t step, uint32_t purpose) const {
+    U4 c{(uint32_t)id, (uint32_t)(id >> 32), step, purpose};
+    return philox(c, k0, k1);
+  }
+};
+
+// uniform in [0,1) with 24 random bits
+SRNN_HD float u01(uint32_t x) { return (float)(x >> 8) * (1.0f / 16777216.0f); }
+// uniform in (0,1]
+SRNN_HD float u01_open0(uint32_t x) { return (float)((x >> 8) + 1u) * (1.0f / 16777216.0f); }
+
+SRNN_HD bool finitef(float v) { return (__builtin_isfinite(v)) != 0; }
+
+// ----------------------------------------------------------------------------------
+// Dense layer helpers (row-major (IN, OUT) kernel, y = x . K, fma chain over i).
+// ----------------------------------------------------------------------------------
+template <int IN, int OUT>
+SRNN_HD void dense_fwd(const float* __restrict__ k, const float* __restrict__ x, float* __restrict__ y) {
+#pragma unroll
+  for (int j = 0; j < OUT; ++j) {
+    float acc = x[0] * k[j];
+#pragma unroll
+    for (int i = 1; i < IN; ++i) acc = fmaf(x[i], k[i * OUT + j], acc);
+    y[j] = acc;
+  }
+}
+
+// gx = K . gy  (gradient wrt the input), then K -= lr * x^T gy  (in place).
+template <int IN, int OUT>
+SRNN_HD void dense_bwd_update(float* __restrict__ k, const float* __restrict__ x, const float* __restrict__ gy,
+                              float* __restrict__ gx, float lr, bool want_gx) {
+  if (want_gx) {
+#pragma unroll
+    for (int i = 0; i < IN; ++i) {
+      float acc = k[i * OUT] * gy[0];
+#pragma unroll
+      for (int j = 1; j < OUT; ++j) acc = fmaf(k[i * OUT + j], gy[j], acc);
+      gx[i] = acc;
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < IN; ++i)
+#pragma unroll
+    for (int j = 0; j < OUT; ++j) k[i * OUT + j] -= lr * (x[i] * gy[j]);
+}
+
+// ----------------------------------------------------------------------------------
+// A plain MLP  IN -> W (x D-1 hidden W->W) -> OUT, linear, no bias.
+// Kernels flat: [IN*W][ (D-1) * W*W ][ W*OUT ].
+// ----------------------------------------------------------------------------------
+template <int IN, int W, int D, int OUT>
+struct MLP {
+  static constexpr int P = IN * W + (D - 1) * W * W + W * OUT;
+  static constexpr int off(int l) { return l == 0 ? 0 : IN * W + (l - 1) * W * W; }
+  static constexpr int NACT = IN + D * W;  // activations kept for backprop (inputs of every layer)
+
+  // forward; acts receives the input of every layer: [x (IN)][h1 (W)]...[hD (W)]
+  SRNN_HD static void forward(const float* __restrict__ w, const float* __restrict__ x, float* __restrict__ acts,
+                              float* __restrict__ y) {
+#pragma unroll
+    for (int i = 0; i < IN; ++i) acts[i] = x[i];
+    dense_fwd<IN, W>(w, acts, acts + IN);
+#pragma unroll
+    for (int l = 1; l < D; ++l) dense_fwd<W, W>(w + off(l), acts + IN + (l - 1) * W, acts + IN + l * W);
+    dense_fwd<W, OUT>(w + off(D), acts + IN + (D - 1) * W, y);
+  }
+
+  SRNN_HD static void forward_only(const float* __restrict__ w, const float* __restrict__ x, float* __restrict__ y) {
+    float h[W], g[W];
+    dense_fwd<IN, W>(w, x, h);
+#pragma unroll
+    for (int l = 1; l < D; ++l) {
+      dense_fwd<W, W>(w + off(l), h, g);
+#pragma unroll
+      for (int j = 0; j < W; ++j) h[j] = g[j];
+    }
+    dense_fwd<W, OUT>(w + off(D), h, y);
+  }
+
+  // one SGD step given dL/dy (gy), activations from forward(); updates w in place.
+  SRNN_HD static void backward_update(float* __restrict__ w, const float* __restrict__ acts,
+                                      const float* __restrict__ gy, float lr) {
+    float g[W], gn[W];
+    dense_bwd_update<W, OUT>(w + off(D), acts + IN + (D - 1) * W, gy, g, lr, true);
+#pragma unroll
+    for (int l = D - 1; l >= 1; --l) {
+      dense_bwd_update<W, W>(w + off(l), acts + IN + (l - 1) * W, g, gn, lr, true);
+#pragma unroll
+      for (int j = 0; j < W; ++j) g[j] = gn[j];
+    }
+    dense_bwd_update<IN, W>(w, acts, g, gn, lr, false);
+  }
+};
+
+// ----------------------------------------------------------------------------------
+// Layer shape tables (used for coordinates and init) as constexpr data.
+// ----------------------------------------------------------------------------------
+struct Shape { int r, c, off; int ortho; };
+
+template <int NL>
+struct ShapeTable { Shape s[NL]; };
+
+// normalize_id (reference code/network.py:216-220): v/m if m > 1 else v
+constexpr float norm_id(int v, int m) { return m > 1 ? (float)v / (float)m : (float)v; }
+
+template <int P>
+struct CoordTable { float c[P][3]; };
+
+template <int P, int NL>
+constexpr CoordTable<P> make_coords(const ShapeTable<NL> t) {
+  CoordTable<P> ct{};
+  int k = 0;
+  for (int l = 0; l < NL; ++l)
+    for (int i = 0; i < t.s[l].r; ++i)
+      for (int j = 0; j < t.s[l].c; ++j) {
+        ct.c[k][0] = norm_id(l, NL - 1);
+        ct.c[k][1] = norm_id(i, t.s[l].r - 1);
+        ct.c[k][2] = norm_id(j, t.s[l].c - 1);
+        ++k;
+      }
+  return ct;
+}
+
+// ----------------------------------------------------------------------------------
+// Common per-particle predicates (reference code/network.py:44-62, 133-157)
+// ----------------------------------------------------------------------------------
+template <int P>
+SRNN_HD bool is_diverged(const float* w) {
+  bool bad = false;
+#pragma unroll
+  for (int k = 0; k < P; ++k) bad |= !finitef(w[k]);
+  return bad;
+}
+template <int P>
+SRNN_HD bool is_zero(const float* w, float eps) {  // inclusive bounds
+  bool ok = true;
+#pragma unroll
+  for (int k = 0; k < P; ++k) ok &= (-eps <= w[k]) && (w[k] <= eps);
+  return ok;
+}
+template <int P>
+SRNN_HD bool within_eps(const float* a, const float* b, float eps) {  // strict |a-b| < eps, NaN -> handled by caller
+  bool ok = true;
+#pragma unroll
+  for (int k = 0; k < P; ++k) ok &= !(fabsf(a[k] - b[k]) >= eps);
+  return ok;
+}
+
+enum Cls : int8_t { C_DIVERGENT = 0, C_FIX_ZERO = 1, C_FIX_OTHER = 2, C_FIX_SEC = 3, C_OTHER = 4 };
+
+// Fisher-Yates permutation of [0,n) driven by one philox stream; perm in byte scratch.
+SRNN_HD void fisher_yates(uint8_t* perm, int n, const Rng& rng, uint64_t id, uint32_t step, uint32_t purpose) {
+  for (int i = 0; i < n; ++i) perm[i] = (uint8_t)i;
+  U4 r{0, 0, 0, 0};
+  int used = 4;
+  uint32_t blk = 0;
+  for (int i = n - 1; i > 0; --i) {
+    if (used == 4) {
+      // fold the block counter into the high bits of step to give each block its own counter
+      r = rng.draw(id, step * 64u + blk, purpose);
+      ++blk;
+      used = 0;
+    }
+    uint32_t x = used == 0 ? r.x : used == 1 ? r.y : used == 2 ? r.z : r.w;
+    ++used;
+    int j = (int)(u01(x) * (float)(i + 1));
+    if (j > i) j = i;
+    uint8_t t = perm[i];
+    perm[i] = perm[j];
+    perm[j] = t;
+  }
+}
+
+// glorot uniform for a (r, c) kernel at flat offset `off` of particle `uid`
+SRNN_HD void glorot_fill(float* w, int off, int r, int c, const Rng& rng, uint64_t uid) {
+  const float lim = sqrtf(6.0f / (float)(r + c));
+  const int n = r * c;
+  for (int b = 0; b < (n + 3) / 4; ++b) {
+    U4 u = rng.draw(uid, (uint32_t)off * 1024u + (uint32_t)b, P_INIT);  // blocks unique per (layer offset, block)
+    uint32_t xs[4] = {u.x, u.y, u.z, u.w};
+    for (int q = 0; q < 4; ++q) {
+      int k = b * 4 + q;
+      if (k < n) w[off + k] = -lim + 2.0f * lim * u01(xs[q]);
+    }
+  }
+}
+
+// orthogonal (n, n) kernel by modified Gram-Schmidt of a gaussian matrix with
+// sign(diag R) correction == QR with positive diagonal (Haar distributed).
+template <int N>
+SRNN_HD void orthogonal_fill(float* w, int off, const Rng& rng, uint64_t uid) {
+  float a[N][N];  // a[row][col]
+  int cnt = 0;
+  U4 u{0, 0, 0, 0};
+  float nrm[4] = {0, 0, 0, 0};
+  uint32_t blk = 0;
+  for (int i = 0; i < N; ++i)
+    for (int j = 0; j < N; ++j) {
+      if ((cnt & 3) == 0) {
+        u = rng.draw(uid, (uint32_t)off * 1024u + blk, P_NORMAL);
+        ++blk;
+        float r1 = sqrtf(-2.0f * logf(u01_open0(u.x)));
+        float t1 = 6.283185307179586f * u01(u.y);
+        float r2 = sqrtf(-2.0f * logf(u01_open0(u.z)));
+        float t2 = 6.283185307179586f * u01(u.w);
+        nrm[0] = r1 * cosf(t1);
+        nrm[1] = r1 * sinf(t1);
+        nrm[2] = r2 * cosf(t2);
+        nrm[3] = r2 * sinf(t2);
+      }
+      a[i][j] = nrm[cnt & 3];
+      ++cnt;
+    }
+  // Gram-Schmidt on columns
+  for (int j = 0; j < N; ++j) {
+    for (int p = 0; p < j; ++p) {
+      float d = 0.f;
+      for (int i = 0; i < N; ++i) d += a[i][p] * a[i][j];
+      for (int i = 0; i < N; ++i) a[i][j] -= d * a[i][p];
+    }
+    float s = 0.f;
+    for (int i = 0; i < N; ++i) s += a[i][j] * a[i][j];
+    float inv = 1.0f / sqrtf(s);
+    for (int i = 0; i < N; ++i) a[i][j] *= inv;
+  }
+  for (int i = 0; i < N; ++i)
+    for (int j = 0; j < N; ++j) w[off + i * N + j] = a[i][j];
+}
+
+// ----------------------------------------------------------------------------------
+// Training context: scratch memory for frozen samples / permutation.
+// On device it points into LDS (lane-private slices), on host into a stack array.
+// ----------------------------------------------------------------------------------
+struct TrainCtx {
+  float lr;
+  Rng rng;
+  uint64_t uid;      // particle uid (keys shuffles)
+  uint32_t ctr;      // op counter (one per epoch consumed)
+  float4* samp;      // >= P float4 slots
+  uint8_t* perm;     // >= P bytes
+  bool shuffle;
+};
+
+struct ApplyCtx {
+  Rng rng;
+  uint64_t uid;      // uid of the particle whose weights are written (keys shuffle_random)
+  uint32_t ctr;
+  int aggregator;    // 0 mean, 1 max, 2 max (reference and/or quirk)
+  int shuffler;      // 0 none, 1 random
+  uint8_t* perm;     // >= P bytes when shuffler == 1
+};
+
+// ==================================================================================
+// Weightwise(W, D): MLP 4 -> W ... -> 1 evaluated at every (weight, layer, cell, pos)
+// point of the target (reference code/network.py:213-289).
+// ==================================================================================
+template <int W_, int D_>
+struct Weightwise {
+  static constexpr int KIND = 0;
+  static constexpr int W = W_, D = D_, A = 0;
+  using Net = MLP<4, W, D, 1>;
+  static constexpr int P = Net::P;
+  static constexpr int PP = (P + 3) & ~3;
+  static constexpr int NL = D + 1;
+  static constexpr ShapeTable<NL> shapes() {
+    ShapeTable<NL> t{};
+    for (int l = 0; l < NL; ++l) {
+      t.s[l].r = l == 0 ? 4 : W;
+      t.s[l].c = l == D ? 1 : W;
+      t.s[l].off = Net::off(l);
+      t.s[l].ortho = 0;
+    }
+    return t;
+  }
+  static constexpr CoordTable<P> coords = make_coords<P, NL>(shapes());
+
+  // out = f_a(t): every target weight replaced by the net's output at its point.
+  SRNN_HD static void apply(const float* __restrict__ a, const float* __restrict__ t, float* __restrict__ out,
+                            const ApplyCtx&) {
+#pragma unroll
+    for (int k = 0; k < P; ++k) {
+      float x[4] = {t[k], coords.c[k][0], coords.c[k][1], coords.c[k][2]};
+      float y[1];
+      Net::forward_only(a, x, y);
+      out[k] = y[0];
+    }
+  }
+
+  // One Keras epoch of fit(x, y, batch_size=1, shuffle=True) on the samples of `s`
+  // (x_k = point k of s, y_k = s[k]); samples frozen at epoch start. Returns mean loss.
+  SRNN_HD static float train_epoch(float* __restrict__ w, const float* __restrict__ s, TrainCtx& c) {
+#pragma unroll
+    for (int k = 0; k < P; ++k) c.samp[k] = make_float4(s[k], coords.c[k][0], coords.c[k][1], coords.c[k][2]);
+    if (c.shuffle) fisher_yates(c.perm, P, c.rng, c.uid, c.ctr, P_SHUFFLE);
+    float loss = 0.f;
+    for (int q = 0; q < P; ++q) {
+      int idx = c.shuffle ? (int)c.perm[q] : q;
+      float4 smp = c.samp[idx];
+      float x[4] = {smp.x, smp.y, smp.z, smp.w};
+      float acts[Net::NACT], y[1];
+      Net::forward(w, x, acts, y);
+      float e = y[0] - smp.x;
+      loss += e * e;
+      float gy[1] = {2.0f * e};
+      Net::backward_update(w, acts, gy, c.lr);
+    }
+    c.ctr += 1;
+    return loss / (float)P;
+  }
+
+  SRNN_HD static void init(float* w, const Rng& rng, uint64_t uid) {
+    constexpr ShapeTable<NL> t = shapes();
+#pragma unroll
+    for (int l = 0; l < NL; ++l) glorot_fill(w, t.s[l].off, t.s[l].r, t.s[l].c, rng, uid);
+  }
+};
+
+// chunk layout of aggregating / fft nets (reference code/network.py:389-403)
+template <int P, int A>
+struct Chunks {
+  static constexpr int CS = P / A;
+  static constexpr int LEFT = P - CS * A;
+  static_assert(CS >= 1, "aggregates > weights");
+  static_assert(P / CS == A, "collect_weights would not produce `aggregates` chunks (SURVEY S4)");
+  static constexpr int start(int k) { return k * CS; }
+  static constexpr int len(int k) { return k == A - 1 ? CS + LEFT : CS; }
+};
+
+template <int P, int A>
+SRNN_HD void aggregate(const float* __restrict__ t, float* __restrict__ g, int aggregator) {
+  using C = Chunks<P, A>;
+#pragma unroll
+  for (int k = 0; k < A; ++k) {
+    if (aggregator == 0) {
+      double acc = 0.0;  // reference sums python floats (double)
+#pragma unroll
+      for (int i = 0; i < C::len(k); ++i) acc += (double)t[C::start(k) + i];
+      g[k] = (float)(acc / (double)C::len(k));
+    } else {
+      float m = t[C::start(k)];
+#pragma unroll
+      for (int i = 0; i < C::len(k); ++i) {
+        float v = t[C::start(k) + i];
+        if (aggregator == 1) m = (v > m) ? v : m;
+        else m = (v > m && v != 0.0f) ? v : m;  // `weight > max and weight or max` quirk
+      }
+      g[k] = m;
+    }
+  }
+}
+
+template <int P>
+SRNN_HD void shuffle_out(float* __restrict__ out, const ApplyCtx& c) {
+  if (c.shuffler != 1) return;
+  fisher_yates(c.perm, P, c.rng, c.uid, c.ctr, P_AGGSHUF);
+  float tmp[P];
+#pragma unroll
+  for (int k = 0; k < P; ++k) tmp[k] = out[k];
+  // out[k] = tmp[perm[k]]  (dynamic index into the copy; P is small)
+  for (int k = 0; k < P; ++k) {
+    int src = c.perm[k];
+    float v = tmp[0];
+#pragma unroll
+    for (int q = 1; q < P; ++q) v = (src == q) ? tmp[q] : v;
+    out[k] = v;
+  }
+}
+
+// ==================================================================================
+// Aggregating(A, W, D): chunk-mean -> MLP A->...->A -> broadcast back
+// (reference code/network.py:292-439).
+// ==================================================================================
+template <int A_, int W_, int D_>
+struct Aggregating {
+  static constexpr int KIND = 1;
+  static constexpr int W = W_, D = D_, A = A_;
+  using Net = MLP<A, W, D, A>;
+  static constexpr int P = Net::P;
+  static constexpr int PP = (P + 3) & ~3;
+  static constexpr int NL = D + 1;
+  using C = Chunks<P, A>;
+
+  SRNN_HD static void apply(const float* __restrict__ a, const float* __restrict__ t, float* __restrict__ out,
+                            const ApplyCtx& c) {
+    float g[A], h[A];
+    aggregate<P, A>(t, g, c.aggregator);
+    Net::forward_only(a, g, h);
+#pragma unroll
+    for (int k = 0; k < A; ++k)
+#pragma unroll
+      for (int i = 0; i < C::len(k); ++i) out[C::start(k) + i] = h[k];
+    shuffle_out<P>(out, c);
+  }
+
+  // one sample x = y = aggregated weights (reference :414-417); loss mean over A outputs
+  SRNN_HD static float train_epoch(float* __restrict__ w, const float* __restrict__ s, TrainCtx& c) {
+    float g[A], acts[Net::NACT], h[A], gy[A];
+    aggregate<P, A>(s, g, 0);
+    Net::forward(w, g, acts, h);
+    float loss = 0.f;
+#pragma unroll
+    for (int k = 0; k < A; ++k) {
+      float e = h[k] - g[k];
+      loss += e * e;
+      gy[k] = 2.0f * e / (float)A;
+    }
+    Net::backward_update(w, acts, gy, c.lr);
+    c.ctr += 1;
+    return loss / (float)A;
+  }
+
+  SRNN_HD static void init(float* w, const Rng& rng, uint64_t uid) {
+    glorot_fill(w, 0, A, W, rng, uid);
+    for (int l = 1; l < D; ++l) glorot_fill(w, Net::off(l), W, W, rng, uid);
+    glorot_fill(w, Net::off(D), W, A, rng, uid);
+  }
+};
+
+// ==================================================================================
+// FFT(A, W, D): defined real-valued semantics of the reference's broken FFT net
+// (code/network.py:442-521):
+//   g_k   = Re(FFT_A(t[0:A]))_k              (np.fft.fftn(flat, (A,)) truncates to A)
+//   h     = MLP(g)
+//   out_m = Re(IFFT_P(pad(h, P)))_m          (np.fft.ifftn(h, (P,)) zero-pads to P)
+// The target's weights are used (the reference FFT'd the applying net's own weights).
+// ==================================================================================
+template <int A_, int W_, int D_>
+struct FFTNet {
+  static constexpr int KIND = 3;
+  static constexpr int W = W_, D = D_, A = A_;
+  using Net = MLP<A, W, D, A>;
+  static constexpr int P = Net::P;
+  static constexpr int PP = (P + 3) & ~3;
+  static_assert(A <= P, "fft aggregates must be <= weights");
+
+  SRNN_HD static void reduce(const float* __restrict__ t, float* __restrict__ g) {
+#pragma unroll
+    for (int k = 0; k < A; ++k) {
+      float acc = 0.f;
+#pragma unroll
+      for (int n = 0; n < A; ++n) acc = fmaf(t[n], cosf(6.283185307179586f * (float)((k * n) % A) / (float)A), acc);
+      g[k] = acc;
+    }
+  }
+  SRNN_HD static void apply(const float* __restrict__ a, const float* __restrict__ t, float* __restrict__ out,
+                            const ApplyCtx& c) {
+    float g[A], h[A];
+    reduce(t, g);
+    Net::forward_only(a, g, h);
+#pragma unroll
+    for (int m = 0; m < P; ++m) {
+      float acc = 0.f;
+#pragma unroll
+      for (int k = 0; k < A; ++k) acc = fmaf(h[k], cosf(6.283185307179586f * (float)((k * m) % P) / (float)P), acc);
+      out[m] = acc / (float)P;
+    }
+    shuffle_out<P>(out, c);
+  }
+  SRNN_HD static float train_epoch(float* __restrict__ w, const float* __restrict__ s, TrainCtx& c) {
+    float g[A], acts[Net::NACT], h[A], gy[A];
+    reduce(s, g);
+    Net::forward(w, g, acts, h);
+    float loss = 0.f;
+#pragma unroll
+    for (int k = 0; k < A; ++k) {
+      float e = h[k] - g[k];
+      loss += e * e;
+      gy[k] = 2.0f * e / (float)A;
+    }
+    Net::backward_update(w, acts, gy, c.lr);
+    c.ctr += 1;
+    return loss / (float)A;
+  }
+  SRNN_HD static void init(float* w, const Rng& rng, uint64_t uid) {
+    glorot_fill(w, 0, A, W, rng, uid);
+    for (int l = 1; l < D; ++l) glorot_fill(w, Net::off(l), W, W, rng, uid);
+    glorot_fill(w, Net::off(D), W, A, rng, uid);
+  }
+};
+
+// ==================================================================================
+// Recurrent(W, D): stacked linear SimpleRNN (1 -> W, W -> W x (D-1), W -> 1) run over
+// the flat weight sequence; per-step output replaces the weight
+// (reference code/network.py:524-574).  Weights: [K0 R0 K1 R1 ... KD RD].
+// ==================================================================================
+template <int W_, int D_>
+struct Recurrent {
+  static constexpr int KIND = 2;
+  static constexpr int W = W_, D = D_, A = 0;
+  static constexpr int NL = D + 1;  // rnn layers
+  static constexpr int in_(int l) { return l == 0 ? 1 : W; }
+  static constexpr int un_(int l) { return l == D ? 1 : W; }
+  static constexpr int koff(int l) {
+    int o = 0;
+    for (int q = 0; q < l; ++q) o += in_(q) * un_(q) + un_(q) * un_(q);
+    return o;
+  }
+  static constexpr int roff(int l) { return koff(l) + in_(l) * un_(l); }
+  static constexpr int P = koff(NL);
+  static constexpr int PP = (P + 3) & ~3;
+  static constexpr int HS = D * W + 1;  // hidden units summed over layers
+
+  // one time step of layer l: hn = x.K + hp.R
+  template <int L>
+  SRNN_HD static void cell(const float* __restrict__ w, const float* __restrict__ x, const float* __restrict__ hp,
+                           float* __restrict__ hn) {
+    constexpr int I = in_(L), U = un_(L);
+    float xk[U], hr[U];
+    dense_fwd<I, U>(w + koff(L), x, xk);
+    dense_fwd<U, U>(w + roff(L), hp, hr);
+#pragma unroll
+    for (int j = 0; j < U; ++j) hn[j] = xk[j] + hr[j];
+  }
+
+  template <int L>
+  SRNN_HD static void step_layers(const float* __restrict__ w, const float* __restrict__ x, float* __restrict__ h) {
+    // h holds the hidden state of all layers: layer l at offset l*W
+    constexpr int U = un_(L);
+    float hn[U];
+    cell<L>(w, x, h + L * W, hn);
+#pragma unroll
+    for (int j = 0; j < U; ++j) h[L * W + j] = hn[j];
+    if constexpr (L < D) step_layers<L + 1>(w, h + L * W, h);
+  }
+
+  SRNN_HD static void apply(const float* __restrict__ a, const float* __restrict__ t, float* __restrict__ out,
+                            const ApplyCtx&) {
+    float h[HS];
+#pragma unroll
+    for (int q = 0; q < HS; ++q) h[q] = 0.f;
+#pragma unroll
+    for (int s = 0; s < P; ++s) {
+      float x[1] = {t[s]};
+      step_layers<0>(a, x, h);
+      out[s] = h[D * W];
+    }
+  }
+
+  // backward through one layer at one time step. dh: gradient wrt this layer's output
+  // at time s (already includes the carry from s+1). Writes dx (grad wrt layer input)
+  // and the new carry (dh . R^T); accumulates kernel grads into gw.
+  template <int L>
+  SRNN_HD static void cell_bwd(const float* __restrict__ w, float* __restrict__ gw, const float* __restrict__ x,
+                               const float* __restrict__ hp, const float* __restrict__ dh, float* __restrict__ dx,
+                               float* __restrict__ carry) {
+    constexpr int I = in_(L), U = un_(L);
+#pragma unroll
+    for (int i = 0; i < I; ++i)
+#pragma unroll
+      for (int j = 0; j < U; ++j) gw[koff(L) + i * U + j] = fmaf(x[i], dh[j], gw[koff(L) + i * U + j]);
+#pragma unroll
+    for (int i = 0; i < U; ++i)
+#pragma unroll
+      for (int j = 0; j < U; ++j) gw[roff(L) + i * U + j] = fmaf(hp[i], dh[j], gw[roff(L) + i * U + j]);
+    if (L > 0) {
+#pragma unroll
+      for (int i = 0; i < I; ++i) {
+        float acc = 0.f;
+#pragma unroll
+        for (int j = 0; j < U; ++j) acc = fmaf(w[koff(L) + i * U + j], dh[j], acc);
+        dx[i] = acc;
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < U; ++i) {
+      float acc = 0.f;
+#pragma unroll
+      for (int j = 0; j < U; ++j) acc = fmaf(w[roff(L) + i * U + j], dh[j], acc);
+      carry[i] = acc;
+    }
+  }
+
+  template <int L>
+  SRNN_HD static void bwd_layers(const float* __restrict__ w, float* __restrict__ gw, const float* __restrict__ hs_t,
+                                 const float* __restrict__ hs_p, float x0, float* __restrict__ dtop,
+                                 float* __restrict__ carry) {
+    // dtop: gradient wrt layer L's output coming from layer L+1 (or the loss)
+    constexpr int U = un_(L), I = in_(L);
+    float dh[U], dx[I > 0 ? I : 1], cr[U];
+#pragma unroll
+    for (int j = 0; j < U; ++j) dh[j] = dtop[j] + carry[L * W + j];
+    float xin[I];
+    if constexpr (L == 0) xin[0] = x0;
+    else {
+#pragma unroll
+      for (int i = 0; i < I; ++i) xin[i] = hs_t[(L - 1) * W + i];
+    }
+    cell_bwd<L>(w, gw, xin, hs_p + L * W, dh, dx, cr);
+#pragma unroll
+    for (int j = 0; j < U; ++j) carry[L * W + j] = cr[j];
+    if constexpr (L > 0) bwd_layers<L - 1>(w, gw, hs_t, hs_p, x0, dx, carry);
+  }
+
+  // one sample x = y = s (1, P, 1), loss mean over P; one SGD step (BPTT)
+  SRNN_HD static float train_epoch(float* __restrict__ w, const float* __restrict__ s, TrainCtx& c) {
+    float hs[P][HS];  // hidden states of every layer at every step
+    float h[HS];
+#pragma unroll
+    for (int q = 0; q < HS; ++q) h[q] = 0.f;
+#pragma unroll
+    for (int t = 0; t < P; ++t) {
+      float x[1] = {s[t]};
+      step_layers<0>(w, x, h);
+#pragma unroll
+      for (int q = 0; q < HS; ++q) hs[t][q] = h[q];
+    }
+    float gw[P];
+#pragma unroll
+    for (int k = 0; k < P; ++k) gw[k] = 0.f;
+    float carry[HS];
+#pragma unroll
+    for (int q = 0; q < HS; ++q) carry[q] = 0.f;
+    float loss = 0.f;
+    float zeros[HS];
+#pragma unroll
+    for (int q = 0; q < HS; ++q) zeros[q] = 0.f;
+#pragma unroll
+    for (int t = P - 1; t >= 0; --t) {
+      float e = hs[t][D * W] - s[t];
+      loss += e * e;
+      float dtop[1] = {2.0f * e / (float)P};
+      bwd_layers<D>(w, gw, hs[t], t > 0 ? hs[t - 1] : zeros, s[t], dtop, carry);
+    }
+#pragma unroll
+    for (int k = 0; k < P; ++k) w[k] -= c.lr * gw[k];
+    c.ctr += 1;
+    return loss / (float)P;
+  }
+
+  template <int L>
+  SRNN_HD static void init_layers(float* w, const Rng& rng, uint64_t uid) {
+    glorot_fill(w, koff(L), in_(L), un_(L), rng, uid);
+    orthogonal_fill<un_(L)>(w, roff(L), rng, uid);
+    if constexpr (L < D) init_layers<L + 1>(w, rng, uid);
+  }
+  SRNN_HD static void init(float* w, const Rng& rng, uint64_t uid) { init_layers<0>(w, rng, uid); }
+};
+
+}  // namespace srnn

@@ -1,0 +1,471 @@
+// srnn_kernels.h — population-batched operators, instantiated per architecture.
+//
+// Each operator is written once as a per-item function `Item<Net>::op(args, i, scratch)`
+// (host + device).  `k_op<Net, OP>` runs it lane-per-particle on the GPU (one wave per
+// 64 particles, the particle's weights in VGPRs, lane-private sample / permutation
+// scratch in LDS); `host_op<Net, OP>` runs the identical code over a host thread pool for
+// CPU tensors.  Reference hot loops replaced here: the per-weight `model.predict` of
+// code/network.py:265-279, the Keras `fit` epochs of :613-626, the run_net loop of
+// code/experiment.py:70-91 and the per-particle soup loop of code/soup.py:51-103.
+#pragma once
+#include "srnn_core.h"
+#include "srnn_abi.h"
+#include <thread>
+#include <vector>
+#include <algorithm>
+#include <climits>
+
+namespace srnn {
+
+void set_error(const char* msg);
+
+constexpr int TB = 64;  // threads per block: one wave; lane-private LDS scratch per thread
+
+enum Action : int8_t { A_NONE = 0, A_ATTACKING = 1, A_LEARN_FROM = 2, A_TRAIN_SELF = 3 };
+
+template <class F>
+void host_parallel(int64_t n, F&& f) {
+  unsigned hw = std::thread::hardware_concurrency();
+  int64_t nt = std::min<int64_t>(hw ? hw : 1, 16);
+  if (n < 256 || nt <= 1) {
+    for (int64_t i = 0; i < n; ++i) f(i);
+    return;
+  }
+  nt = std::min<int64_t>(nt, (n + 127) / 128);
+  std::vector<std::thread> th;
+  int64_t chunk = (n + nt - 1) / nt;
+  for (int64_t t = 0; t < nt; ++t) {
+    int64_t b = t * chunk, e = std::min(n, b + chunk);
+    if (b >= e) break;
+    th.emplace_back([b, e, &f]() {
+      for (int64_t i = b; i < e; ++i) f(i);
+    });
+  }
+  for (auto& x : th) x.join();
+}
+
+SRNN_HD int32_t atomic_add_i32(int32_t* p, int32_t v) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return atomicAdd(p, v);
+#else
+  return __atomic_fetch_add(p, v, __ATOMIC_RELAXED);
+#endif
+}
+
+template <class Net>
+struct Item {
+  static constexpr int P = Net::P;
+  static constexpr int PP = Net::PP;
+
+  SRNN_HD static void load(const float* __restrict__ row, float* __restrict__ w) {
+    const float4* r4 = reinterpret_cast<const float4*>(row);
+#pragma unroll
+    for (int q = 0; q < PP / 4; ++q) {
+      float4 v = r4[q];
+      if (4 * q + 0 < P) w[4 * q + 0] = v.x;
+      if (4 * q + 1 < P) w[4 * q + 1] = v.y;
+      if (4 * q + 2 < P) w[4 * q + 2] = v.z;
+      if (4 * q + 3 < P) w[4 * q + 3] = v.w;
+    }
+  }
+  SRNN_HD static void store(float* __restrict__ row, const float* __restrict__ w) {
+    float4* r4 = reinterpret_cast<float4*>(row);
+#pragma unroll
+    for (int q = 0; q < PP / 4; ++q) {
+      float4 v;
+      v.x = 4 * q + 0 < P ? w[4 * q + 0] : 0.f;
+      v.y = 4 * q + 1 < P ? w[4 * q + 1] : 0.f;
+      v.z = 4 * q + 2 < P ? w[4 * q + 2] : 0.f;
+      v.w = 4 * q + 3 < P ? w[4 * q + 3] : 0.f;
+      r4[q] = v;
+    }
+  }
+  SRNN_HD static void copy(float* __restrict__ d, const float* __restrict__ s) {
+#pragma unroll
+    for (int k = 0; k < P; ++k) d[k] = s[k];
+  }
+  SRNN_HD static Rng rng(const SrnnArgs& a) { return Rng{(uint32_t)a.seed, (uint32_t)(a.seed >> 32)}; }
+  SRNN_HD static uint64_t uid_of(const SrnnArgs& a, int64_t i) { return a.uid ? (uint64_t)a.uid[i] : (uint64_t)i; }
+  SRNN_HD static ApplyCtx actx(const SrnnArgs& a, const SrnnCfg& c, uint64_t uid, uint32_t ctr, uint8_t* perm) {
+    ApplyCtx x;
+    x.rng = rng(a);
+    x.uid = uid;
+    x.ctr = ctr;
+    x.aggregator = c.aggregator;
+    x.shuffler = c.shuffler;
+    x.perm = perm;
+    return x;
+  }
+
+  // ---------------------------------------------------------------- init
+  SRNN_HD static void init(const SrnnCfg&, const SrnnArgs& a, int64_t i, float4*, uint8_t*) {
+    float w[P];
+    Net::init(w, rng(a), uid_of(a, i));
+    store(a.W + i * PP, w);
+  }
+
+  // ---------------------------------------------------------------- apply (attack)
+  SRNN_HD static void apply(const SrnnCfg& c, const SrnnArgs& a, int64_t i, float4*, uint8_t* perm) {
+    int64_t fi = a.idx_f ? a.idx_f[i] : i;
+    int64_t ti = a.idx_t ? a.idx_t[i] : i;
+    int64_t oi = a.idx_o ? a.idx_o[i] : i;
+    float f[P], t[P], o[P];
+    load(a.W + fi * PP, f);
+    load(a.W + ti * PP, t);
+    uint64_t ouid = a.uid ? (uint64_t)a.uid[ti] : (uint64_t)ti;
+    Net::apply(f, t, o, actx(a, c, ouid, a.ctr, perm));
+    store(a.W2 + oi * PP, o);
+  }
+
+  // classification of the current weights (reference code/experiment.py:79-91)
+  SRNN_HD static int8_t classify_w(const float* w, float eps, bool with_sec, const ApplyCtx& x) {
+    if (is_diverged<P>(w)) return C_DIVERGENT;
+    float f1[P];
+    Net::apply(w, w, f1, x);
+    if (!is_diverged<P>(f1) && within_eps<P>(f1, w, eps)) return is_zero<P>(w, eps) ? C_FIX_ZERO : C_FIX_OTHER;
+    if (with_sec) {
+      float f2[P];
+      Net::apply(w, f1, f2, x);
+      if (!is_diverged<P>(f2) && within_eps<P>(f2, w, eps)) return C_FIX_SEC;
+    }
+    return C_OTHER;
+  }
+
+  // ---------------------------------------------------------------- run_net
+  // reference code/experiment.py:70-77: while i < limit and not diverged and not fixpoint: self_attack
+  SRNN_HD static void run_fixpoint(const SrnnCfg& c, const SrnnArgs& a, int64_t i, float4*, uint8_t* perm) {
+    float w[P], nw[P];
+    load(a.W + i * PP, w);
+    uint64_t uid = uid_of(a, i);
+    ApplyCtx x = actx(a, c, uid, a.ctr, perm);
+    if (a.traj) store(a.traj + i * PP, w);
+    int s = 0;
+    for (; s < a.steps; ++s) {
+      if (a.early_exit) {
+        if (is_diverged<P>(w)) break;
+        Net::apply(w, w, nw, x);
+        if (!is_diverged<P>(nw) && within_eps<P>(nw, w, a.eps)) break;  // is_fixpoint()
+      } else {
+        Net::apply(w, w, nw, x);
+      }
+      copy(w, nw);
+      x.ctr += 1;
+      if (a.traj) store(a.traj + ((int64_t)(s + 1) * a.n + i) * PP, w);
+    }
+    store(a.W + i * PP, w);
+    if (a.nsteps) a.nsteps[i] = s;
+    if (a.cls) a.cls[i] = classify_w(w, a.eps, (a.flags & 8) != 0, x);
+  }
+
+  // ---------------------------------------------------------------- known-fixpoint variation
+  // reference code/setups/known-fixpoint-variation.py:66-83
+  SRNN_HD static void vary_run(const SrnnCfg& c, const SrnnArgs& a, int64_t i, float4*, uint8_t* perm) {
+    float w[P], nw[P];
+    load(a.W + i * PP, w);
+    ApplyCtx x = actx(a, c, uid_of(a, i), a.ctr, perm);
+    int tts = 0, taf = 0;
+    bool still = true;
+    for (int s = 0; s < a.steps; ++s) {
+      Net::apply(w, w, nw, x);
+      copy(w, nw);
+      if (is_zero<P>(w, a.eps) || is_diverged<P>(w)) break;
+      Net::apply(w, w, nw, x);
+      bool fix = !is_diverged<P>(nw) && within_eps<P>(nw, w, a.eps);
+      if (fix) {
+        if (still) ++taf;
+        else still = true;
+      } else {
+        still = false;
+      }
+      ++tts;
+    }
+    store(a.W + i * PP, w);
+    a.nsteps[i] = tts;
+    a.loss[i] = (float)taf;
+  }
+
+  // ---------------------------------------------------------------- perturb (vary)
+  SRNN_HD static void perturb(const SrnnCfg&, const SrnnArgs& a, int64_t i, float4*, uint8_t*) {
+    float w[P];
+    load(a.W + i * PP, w);
+    Rng r = rng(a);
+    uint64_t uid = uid_of(a, i);
+#pragma unroll
+    for (int k = 0; k < P; ++k) {
+      U4 u = r.draw(uid, a.ctr * 1024u + (uint32_t)k, P_PERTURB);
+      double mag = (double)u01(u.y) * (double)a.eps;
+      w[k] = u01(u.x) < 0.5f ? (float)((double)w[k] + mag) : (float)((double)w[k] - mag);
+    }
+    store(a.W + i * PP, w);
+  }
+
+  // ---------------------------------------------------------------- train / learn_from
+  SRNN_HD static void train(const SrnnCfg&, const SrnnArgs& a, int64_t i, float4* samp, uint8_t* perm, bool learn) {
+    float w[P], s[P];
+    load(a.W + i * PP, w);
+    if (learn) load(a.W2 + (a.idx_t ? a.idx_t[i] : i) * PP, s);
+    TrainCtx tc;
+    tc.lr = a.lr;
+    tc.rng = rng(a);
+    tc.uid = uid_of(a, i);
+    tc.ctr = a.ctr;
+    tc.samp = samp;
+    tc.perm = perm;
+    tc.shuffle = (a.flags & 1) != 0;
+    float loss = 0.f;
+    for (int e = 0; e < a.epochs; ++e) {
+      if (!learn) copy(s, w);
+      loss = Net::train_epoch(w, s, tc);
+    }
+    store(a.W + i * PP, w);
+    if (a.loss) a.loss[i] = loss;
+  }
+
+  // ---------------------------------------------------------------- classify
+  SRNN_HD static int8_t classify(const SrnnCfg& c, const SrnnArgs& a, int64_t i, uint8_t* perm) {
+    float w[P];
+    load(a.W + i * PP, w);
+    int8_t k = classify_w(w, a.eps, (a.flags & 8) != 0, actx(a, c, uid_of(a, i), a.ctr, perm));
+    if (a.cls) a.cls[i] = k;
+    return k;
+  }
+
+  // ---------------------------------------------------------------- soup
+  // decisions of global slot i (reference code/soup.py:56-63, one draw per decision)
+  SRNN_HD static void soup_decide(const SrnnArgs& a, int64_t i) {
+    const int32_t gen = a.gen_ptr ? a.gen_ptr[0] : a.gen;
+    U4 d = rng(a).draw((uint64_t)i, (uint32_t)gen, P_SOUP);
+    int32_t at = -1, te = -1;
+    if (u01(d.x) < a.attacking_rate) at = (int32_t)(((uint64_t)d.y * (uint64_t)a.n_total) >> 32);
+    if (u01(d.z) < a.learn_from_rate) te = (int32_t)(((uint64_t)d.w * (uint64_t)a.n_total) >> 32);
+    a.i32a[i] = at;
+    a.i32b[i] = te;
+    if (at >= a.lo && at < a.lo + a.n) atomic_add_i32(a.i32c + (at - a.lo), 1);
+  }
+  SRNN_HD static void soup_fill(const SrnnArgs& a, int64_t i) {
+    int32_t at = a.i32a[i];
+    if (at >= a.lo && at < a.lo + a.n) {
+      int64_t v = at - a.lo;
+      int32_t pos = a.i32d[v] + atomic_add_i32(a.i32e + v, 1);
+      a.i32f[pos] = (int32_t)i;
+    }
+  }
+
+  // Synchronous (Jacobi) generation for local row j: every read is from the
+  // generation-start table W2 (global rows), the result goes to W (local rows).
+  SRNN_HD static void soup_evolve(const SrnnCfg& c, const SrnnArgs& a, int64_t j, float4* samp, uint8_t* perm) {
+    const int64_t g = a.lo + j;
+    float w[P], f[P], o[P];
+    load(a.W2 + g * PP, w);
+    const uint64_t uid = uid_of(a, j);
+    const int32_t gen = a.gen_ptr ? a.gen_ptr[0] : a.gen;
+    ApplyCtx x = actx(a, c, uid, (uint32_t)gen * 1024u, perm);
+    // 1. attacks received, in ascending attacker slot order
+    const int32_t beg = a.i32d[j], end = a.i32d[j + 1];
+    int32_t last = -1;
+    for (int32_t q = beg; q < end; ++q) {
+      int32_t best = INT_MAX;
+      for (int32_t r = beg; r < end; ++r) {
+        int32_t v = a.i32f[r];
+        best = (v > last && v < best) ? v : best;
+      }
+      last = best;
+      load(a.W2 + (int64_t)best * PP, f);
+      Net::apply(f, w, o, x);
+      x.ctr += 1;
+      copy(w, o);
+    }
+    int8_t act = A_NONE;
+    int64_t cp = -1;
+    if (a.i32a[g] >= 0) {
+      act = A_ATTACKING;
+      cp = a.i32a[g];
+    }
+    TrainCtx tc;
+    tc.lr = a.lr;
+    tc.rng = rng(a);
+    tc.uid = uid;
+    tc.ctr = (uint32_t)gen * 1024u + 512u;
+    tc.samp = samp;
+    tc.perm = perm;
+    tc.shuffle = (a.flags & 1) != 0;
+    float loss = 0.f;
+    // 2. learn_from a teacher (its generation-start weights)
+    const int32_t te = a.i32b[g];
+    if (te >= 0) {
+      load(a.W2 + (int64_t)te * PP, f);
+      for (int e = 0; e < a.severity; ++e) loss = Net::train_epoch(w, f, tc);
+      act = A_LEARN_FROM;
+      cp = te;
+    }
+    // 3. self-train
+    for (int e = 0; e < a.epochs; ++e) {
+      copy(f, w);
+      loss = Net::train_epoch(w, f, tc);
+      act = A_TRAIN_SELF;
+      cp = -1;
+    }
+    // 4. respawn flags (reference code/soup.py:77-86; zero test on the old particle)
+    int8_t rs = 0;
+    if ((a.flags & 2) && is_diverged<P>(w)) rs = 1;
+    else if ((a.flags & 4) && is_zero<P>(w, a.eps)) rs = 2;
+    store(a.W + j * PP, w);
+    a.action[j] = act;
+    a.counterpart[j] = cp;
+    a.loss[j] = loss;
+    a.respawn[j] = rs;
+    a.i32c[j] = rs != 0 ? 1 : 0;
+  }
+
+  SRNN_HD static void respawn(const SrnnArgs& a, int64_t j) {
+    if (a.respawn[j] == 0) return;
+    uint64_t uid = (uint64_t)(a.uid_base[0] + (int64_t)a.i32d[j]);
+    a.uid_out[j] = (int64_t)uid;
+    float w[P];
+    Net::init(w, rng(a), uid);
+    store(a.W + j * PP, w);
+  }
+};
+
+// ==================================================================================
+// Device kernels
+// ==================================================================================
+template <class Net, int OP>
+__global__ __launch_bounds__(TB) void k_op(SrnnCfg c, SrnnArgs a) {
+  using I = Item<Net>;
+  constexpr int P = Net::P;
+  constexpr bool NEED_SAMP = (OP == OP_TRAIN || OP == OP_LEARN || OP == OP_SOUP_EVOLVE) && Net::KIND == 0;
+  constexpr int SAMP = NEED_SAMP ? P + 1 : 1;  // +1 float4: odd stride across lanes
+  constexpr int PERM = (P + 4) & ~3;
+  __shared__ float4 s_samp[TB * SAMP];
+  __shared__ uint8_t s_perm[TB * PERM];
+  const int64_t i = (int64_t)blockIdx.x * TB + threadIdx.x;
+  float4* samp = s_samp + threadIdx.x * SAMP;
+  uint8_t* perm = s_perm + threadIdx.x * PERM;
+
+  if constexpr (OP == OP_SOUP_DECIDE) {
+    if (i < a.n_total) I::soup_decide(a, i);
+    return;
+  } else if constexpr (OP == OP_SOUP_FILL) {
+    if (i < a.n_total) I::soup_fill(a, i);
+    return;
+  } else if constexpr (OP == OP_CLASSIFY) {
+    int8_t k = -1;
+    if (i < a.n) k = I::classify(c, a, i, perm);
+    if (a.counts) {
+#pragma unroll
+      for (int q = 0; q < 5; ++q) {
+        unsigned long long m = __ballot(k == q);
+        if ((threadIdx.x & 63) == 0 && m) atomicAdd(a.counts + q, (uint64_t)__popcll(m));
+      }
+    }
+    return;
+  } else {
+    if (i >= a.n) return;
+    if constexpr (OP == OP_INIT) I::init(c, a, i, samp, perm);
+    else if constexpr (OP == OP_APPLY) I::apply(c, a, i, samp, perm);
+    else if constexpr (OP == OP_RUN_FIXPOINT) I::run_fixpoint(c, a, i, samp, perm);
+    else if constexpr (OP == OP_TRAIN) I::train(c, a, i, samp, perm, false);
+    else if constexpr (OP == OP_LEARN) I::train(c, a, i, samp, perm, true);
+    else if constexpr (OP == OP_PERTURB) I::perturb(c, a, i, samp, perm);
+    else if constexpr (OP == OP_SOUP_EVOLVE) I::soup_evolve(c, a, i, samp, perm);
+    else if constexpr (OP == OP_RESPAWN) I::respawn(a, i);
+    else if constexpr (OP == OP_VARY_RUN) I::vary_run(c, a, i, samp, perm);
+  }
+}
+
+template <class Net, int OP>
+int launch(const SrnnCfg& c, const SrnnArgs& a) {
+  int64_t items = (OP == OP_SOUP_DECIDE || OP == OP_SOUP_FILL) ? a.n_total : a.n;
+  if (items <= 0) return 0;
+  int64_t blocks = (items + TB - 1) / TB;
+  if (blocks > 0x7fffffffLL) {
+    set_error("grid too large");
+    return -2;
+  }
+  hipStream_t st = (hipStream_t)a.stream;
+  hipLaunchKernelGGL((k_op<Net, OP>), dim3((unsigned)blocks), dim3(TB), 0, st, c, a);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) {
+    set_error(hipGetErrorString(e));
+    return -3;
+  }
+  return 0;
+}
+
+// ==================================================================================
+// Host execution of the same per-item code (CPU tensors)
+// ==================================================================================
+template <class Net, int OP>
+int host_run(const SrnnCfg& c, const SrnnArgs& a) {
+  using I = Item<Net>;
+  constexpr int P = Net::P;
+  int64_t items = (OP == OP_SOUP_DECIDE || OP == OP_SOUP_FILL) ? a.n_total : a.n;
+  if (OP == OP_CLASSIFY && a.counts) {
+    uint64_t local[5] = {0, 0, 0, 0, 0};
+    std::vector<int8_t> ks((size_t)items);
+    host_parallel(items, [&](int64_t i) {
+      uint8_t perm[P + 4];
+      ks[(size_t)i] = I::classify(c, a, i, perm);
+    });
+    for (int64_t i = 0; i < items; ++i) local[ks[(size_t)i]]++;
+    for (int q = 0; q < 5; ++q) a.counts[q] += local[q];
+    return 0;
+  }
+  host_parallel(items, [&](int64_t i) {
+    float4 samp[P + 1];
+    uint8_t perm[P + 4];
+    if constexpr (OP == OP_SOUP_DECIDE) I::soup_decide(a, i);
+    else if constexpr (OP == OP_SOUP_FILL) I::soup_fill(a, i);
+    else if constexpr (OP == OP_CLASSIFY) I::classify(c, a, i, perm);
+    else if constexpr (OP == OP_INIT) I::init(c, a, i, samp, perm);
+    else if constexpr (OP == OP_APPLY) I::apply(c, a, i, samp, perm);
+    else if constexpr (OP == OP_RUN_FIXPOINT) I::run_fixpoint(c, a, i, samp, perm);
+    else if constexpr (OP == OP_TRAIN) I::train(c, a, i, samp, perm, false);
+    else if constexpr (OP == OP_LEARN) I::train(c, a, i, samp, perm, true);
+    else if constexpr (OP == OP_PERTURB) I::perturb(c, a, i, samp, perm);
+    else if constexpr (OP == OP_SOUP_EVOLVE) I::soup_evolve(c, a, i, samp, perm);
+    else if constexpr (OP == OP_RESPAWN) I::respawn(a, i);
+    else if constexpr (OP == OP_VARY_RUN) I::vary_run(c, a, i, samp, perm);
+  });
+  return 0;
+}
+
+template <class Net, int OP>
+int run_one(const SrnnCfg& c, const SrnnArgs& a) {
+  return a.dev ? launch<Net, OP>(c, a) : host_run<Net, OP>(c, a);
+}
+
+template <class Net>
+int run_net_op(int op, const SrnnCfg& c, const SrnnArgs& a) {
+  switch (op) {
+    case OP_INIT: return run_one<Net, OP_INIT>(c, a);
+    case OP_APPLY: return run_one<Net, OP_APPLY>(c, a);
+    case OP_RUN_FIXPOINT: return run_one<Net, OP_RUN_FIXPOINT>(c, a);
+    case OP_TRAIN: return run_one<Net, OP_TRAIN>(c, a);
+    case OP_LEARN: return run_one<Net, OP_LEARN>(c, a);
+    case OP_CLASSIFY: return run_one<Net, OP_CLASSIFY>(c, a);
+    case OP_PERTURB: return run_one<Net, OP_PERTURB>(c, a);
+    case OP_SOUP_DECIDE: return run_one<Net, OP_SOUP_DECIDE>(c, a);
+    case OP_SOUP_FILL: return run_one<Net, OP_SOUP_FILL>(c, a);
+    case OP_SOUP_EVOLVE: return run_one<Net, OP_SOUP_EVOLVE>(c, a);
+    case OP_RESPAWN: return run_one<Net, OP_RESPAWN>(c, a);
+    case OP_VARY_RUN: return run_one<Net, OP_VARY_RUN>(c, a);
+    default: set_error("unknown op"); return -1;
+  }
+}
+
+}  // namespace srnn
+
+// Registration: each srnn_<kind>.hip lists its instantiated shapes with this macro and
+// exports `int srnn_dispatch_<kind>(int op, const SrnnCfg*, const SrnnArgs*)`
+// returning 1 on "shape not instantiated".
+#define SRNN_TRY(NETTYPE, W_, D_, A_)                                                  \
+  if (c->width == (W_) && c->depth == (D_) && c->aggregates == (A_)) {                 \
+    if (c->p != NETTYPE::P || c->pp != NETTYPE::PP) {                                  \
+      srnn::set_error("layout mismatch (p/pp) for instantiated shape");                \
+      return -4;                                                                       \
+    }                                                                                  \
+    if (op < 0) return 0;                                                              \
+    return srnn::run_net_op<NETTYPE>(op, *c, *a);                                      \
+  }

@@ -1,0 +1,135 @@
+"""ctypes binding of ``libsrnn.so`` (csrc/): the native population kernels.
+
+The library is built in-tree by ``csrc/Makefile`` (``hipcc --offload-arch=gfx950``) and
+loaded with ``ctypes`` — no torch C++ extension machinery, so the .so has no libtorch
+dependency and device pointers / the HIP stream are passed as plain integers
+(``tensor.data_ptr()``, ``torch.cuda.current_stream().cuda_stream``).  Kernels launched
+this way are captured by ``torch.cuda.CUDAGraph`` (a hipGraph on ROCm) like any other
+launch on the capturing stream.
+
+Field order of ``SrnnCfg``/``SrnnArgs`` mirrors ``csrc/srnn_abi.h``.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+import threading
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libsrnn.so")
+CSRC = os.path.normpath(os.path.join(_HERE, "..", "..", "csrc"))
+ABI_VERSION = 4
+
+OP_INIT = 0
+OP_APPLY = 1
+OP_RUN_FIXPOINT = 2
+OP_TRAIN = 3
+OP_LEARN = 4
+OP_CLASSIFY = 5
+OP_PERTURB = 6
+OP_SOUP_DECIDE = 7
+OP_SOUP_FILL = 8
+OP_SOUP_EVOLVE = 9
+OP_SCAN = 10
+OP_RESPAWN = 11
+OP_VARY_RUN = 12
+
+FLAG_SHUFFLE = 1
+FLAG_REMOVE_DIVERGENT = 2
+FLAG_REMOVE_ZERO = 4
+FLAG_FIX_SEC = 8
+
+
+class SrnnCfg(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_int32) for n in
+                ("kind", "width", "depth", "aggregates", "aggregator", "shuffler", "pp", "p")]
+
+
+_P = ctypes.c_void_p
+
+
+class SrnnArgs(ctypes.Structure):
+    _fields_ = [
+        ("n", ctypes.c_int64), ("n_total", ctypes.c_int64), ("lo", ctypes.c_int64),
+        ("steps", ctypes.c_int32), ("epochs", ctypes.c_int32), ("severity", ctypes.c_int32),
+        ("early_exit", ctypes.c_int32), ("flags", ctypes.c_int32), ("gen", ctypes.c_int32),
+        ("eps", ctypes.c_float), ("lr", ctypes.c_float),
+        ("attacking_rate", ctypes.c_float), ("learn_from_rate", ctypes.c_float),
+        ("seed", ctypes.c_uint64), ("ctr", ctypes.c_uint32), ("pad0", ctypes.c_uint32),
+        ("W", _P), ("W2", _P), ("traj", _P),
+        ("idx_f", _P), ("idx_t", _P), ("idx_o", _P), ("uid", _P),
+        ("cls", _P), ("nsteps", _P), ("loss", _P), ("counts", _P),
+        ("i32a", _P), ("i32b", _P), ("i32c", _P), ("i32d", _P), ("i32e", _P), ("i32f", _P),
+        ("uid_out", _P), ("uid_base", _P), ("gen_ptr", _P),
+        ("action", _P), ("counterpart", _P), ("respawn", _P),
+        ("temp", _P), ("temp_bytes", ctypes.c_int64),
+        ("dev", ctypes.c_int32), ("pad1", ctypes.c_int32), ("stream", _P),
+    ]
+
+
+class NativeLibraryError(RuntimeError):
+    pass
+
+
+_lib = None
+_lock = threading.Lock()
+
+
+def build(force: bool = False, jobs: int = 8) -> str:
+    """Compile libsrnn.so for gfx950 in-tree (make -C csrc)."""
+    cmd = ["make", "-C", CSRC, f"-j{jobs}"]
+    if force:
+        subprocess.run(["make", "-C", CSRC, "clean"], check=True)
+    subprocess.run(cmd, check=True)
+    return LIB_PATH
+
+
+def lib():
+    """Load libsrnn.so; raise loudly if it is missing (no silent eager fallback)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        if not os.path.exists(LIB_PATH):
+            if os.environ.get("SRNN_AUTOBUILD", "1") == "1" and os.path.isdir(CSRC):
+                build()
+            else:
+                raise NativeLibraryError(f"{LIB_PATH} is missing: run `make -C csrc` (hipcc, gfx950)")
+        L = ctypes.CDLL(LIB_PATH)
+        L.srnn_abi_version.restype = ctypes.c_int
+        L.srnn_has_config.argtypes = [ctypes.POINTER(SrnnCfg)]
+        L.srnn_has_config.restype = ctypes.c_int
+        L.srnn_run.argtypes = [ctypes.c_int, ctypes.POINTER(SrnnCfg), ctypes.POINTER(SrnnArgs)]
+        L.srnn_run.restype = ctypes.c_int
+        L.srnn_last_error.restype = ctypes.c_char_p
+        L.srnn_scan_temp_bytes.argtypes = [ctypes.c_int64]
+        L.srnn_scan_temp_bytes.restype = ctypes.c_int64
+        v = L.srnn_abi_version()
+        if v != ABI_VERSION:
+            raise NativeLibraryError(f"libsrnn ABI {v} != expected {ABI_VERSION}: rebuild with `make -C csrc`")
+        _lib = L
+        return _lib
+
+
+def make_cfg(spec) -> SrnnCfg:
+    return SrnnCfg(*spec.native_cfg_tuple())
+
+
+def has_config(spec) -> bool:
+    return bool(lib().srnn_has_config(ctypes.byref(make_cfg(spec))))
+
+
+def run(op: int, spec, args: SrnnArgs, cfg: SrnnCfg = None) -> None:
+    L = lib()
+    cfg = cfg if cfg is not None else make_cfg(spec)
+    r = L.srnn_run(op, ctypes.byref(cfg), ctypes.byref(args))
+    if r != 0:
+        msg = L.srnn_last_error().decode(errors="replace")
+        raise NativeLibraryError(f"srnn op {op} failed ({r}): {msg} [spec={spec}]")
+
+
+def scan_temp_bytes(n: int) -> int:
+    return int(lib().srnn_scan_temp_bytes(int(n)))

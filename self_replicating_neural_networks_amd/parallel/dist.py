@@ -1,0 +1,96 @@
+"""Process-group plumbing for population sharding (one process per GPU).
+
+The reference is single-process; here a population of ``n_total`` particles
+is sharded contiguously over the ranks of a ``torch.distributed`` group.  On ROCm the
+``"nccl"`` backend is RCCL, whose collectives run over the xGMI links of an MI355X node;
+CPU tests use ``"gloo"``.  Only three collective shapes are needed:
+
+* all-gather of weight rows (cross-shard attacks / learn_from partners),
+* all-reduce of int64 class histograms (fixpoint-fraction statistics),
+* all-gather of per-rank respawn counts (globally sequential uids).
+"""
+from __future__ import annotations
+
+import dataclasses
+import os
+from typing import Optional
+
+import torch
+import torch.distributed as dist
+
+
+@dataclasses.dataclass
+class Dist:
+    rank: int = 0
+    world: int = 1
+    local_rank: int = 0
+    group: Optional[object] = None
+
+    @property
+    def enabled(self) -> bool:
+        return self.world > 1
+
+    def shard(self, n_total: int):
+        """Contiguous [lo, hi) rows of this rank (sizes differ by at most one)."""
+        lo = (self.rank * n_total) // self.world
+        hi = ((self.rank + 1) * n_total) // self.world
+        return lo, hi
+
+    def shard_sizes(self, n_total: int):
+        return [((r + 1) * n_total) // self.world - (r * n_total) // self.world for r in range(self.world)]
+
+    # ---------------------------------------------------------------- collectives
+    def all_gather_rows(self, out: torch.Tensor, local: torch.Tensor, n_total: int):
+        """out[n_total, PP] <- concatenation of every rank's local rows."""
+        if not self.enabled:
+            if out.data_ptr() != local.data_ptr():
+                out.copy_(local)
+            return out
+        sizes = self.shard_sizes(n_total)
+        if len(set(sizes)) == 1:
+            dist.all_gather_into_tensor(out, local, group=self.group)
+        else:
+            parts = list(torch.split(out, sizes))
+            dist.all_gather(parts, local, group=self.group)
+        return out
+
+    def all_reduce_sum(self, t: torch.Tensor):
+        if self.enabled:
+            dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group)
+        return t
+
+    def all_gather_scalar(self, out: torch.Tensor, local: torch.Tensor):
+        """out[world] <- every rank's 1-element ``local``."""
+        if self.enabled:
+            dist.all_gather_into_tensor(out, local.reshape(1), group=self.group)
+        else:
+            out.copy_(local.reshape(1))
+        return out
+
+    def barrier(self):
+        if self.enabled:
+            dist.barrier(group=self.group)
+
+
+def from_env(backend: Optional[str] = None, device_type: str = "cuda") -> Dist:
+    """Initialise the default process group from torchrun's env (RANK/WORLD_SIZE/...)."""
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world <= 1:
+        return Dist(0, 1, 0, None)
+    if not dist.is_initialized():
+        if backend is None:
+            backend = "nccl" if device_type == "cuda" else "gloo"
+        kw = {}
+        if backend == "nccl":
+            torch.cuda.set_device(local_rank)
+            kw["device_id"] = torch.device("cuda", local_rank)
+        dist.init_process_group(backend=backend, **kw)
+    return Dist(dist.get_rank(), dist.get_world_size(), local_rank, None)
+
+
+def current() -> Dist:
+    if dist.is_available() and dist.is_initialized():
+        return Dist(dist.get_rank(), dist.get_world_size(), int(os.environ.get("LOCAL_RANK", "0")), None)
+    return Dist()

@@ -1,0 +1,125 @@
+"""Device-resident particle populations.
+
+``Population`` is the unit of computation of the framework: a weight table
+``W[N, spec.PP]`` (fp32, one particle per row, Keras flat order) plus a uid per row.
+Reference-style objects (``WeightwiseNeuralNetwork``, ``ParticleDecorator``, ``Soup``) are
+views of rows of a population; the batched methods here replace the reference's
+per-object Python loops (``code/experiment.py:70-91``, ``code/setups/*.py`` trial loops).
+"""
+from __future__ import annotations
+
+from typing import Dict, Optional
+
+import numpy as np
+import torch
+
+from .arch import ArchSpec
+from .ops import kernels as K
+from .oracle.core import CLASS_NAMES
+
+
+def counts_dict(counts) -> Dict[str, int]:
+    c = counts.tolist() if hasattr(counts, "tolist") else list(counts)
+    return {name: int(c[i]) for i, name in enumerate(CLASS_NAMES)}
+
+
+class Population:
+    """N particles of one architecture on one device."""
+
+    def __init__(self, spec: ArchSpec, n: int, device="cpu", seed: int = 0, uid_start: int = 0,
+                 weights: Optional[torch.Tensor] = None, lr: float = 0.01):
+        self.spec = spec
+        self.device = torch.device(device)
+        self.seed = int(seed)
+        self.lr = float(lr)
+        self.ctr = 0  # op counter: keys the per-particle random streams of shuffles etc.
+        self.uid = torch.arange(uid_start, uid_start + n, dtype=torch.int64, device=self.device)
+        self.W = torch.zeros((n, spec.PP), dtype=torch.float32, device=self.device)
+        if weights is None:
+            K.init_rows(spec, self.W, self.uid, self.seed)
+        else:
+            self.set_weights(weights)
+
+    # -------------------------------------------------------------- helpers
+    def __len__(self):
+        return self.W.shape[0]
+
+    @property
+    def n(self):
+        return self.W.shape[0]
+
+    def _next_ctr(self, k=1):
+        c = self.ctr
+        self.ctr += k
+        return c
+
+    def weights(self) -> torch.Tensor:
+        """[N, P] view without the row padding."""
+        return self.W[:, : self.spec.P]
+
+    def set_weights(self, w):
+        w = torch.as_tensor(np.asarray(w, dtype=np.float32) if not torch.is_tensor(w) else w, dtype=torch.float32)
+        if w.dim() == 1:
+            w = w[None]
+        if w.shape[0] != self.n or w.shape[1] not in (self.spec.P, self.spec.PP):
+            raise ValueError(f"weights must be [{self.n}, {self.spec.P}], got {tuple(w.shape)}")
+        self.W.zero_()
+        self.W[:, : w.shape[1]] = w.to(self.device)
+        if w.shape[1] == self.spec.PP:
+            self.W[:, self.spec.P:] = 0
+
+    # -------------------------------------------------------------- dynamics
+    def self_apply(self, steps: int = 1) -> "Population":
+        """``self_attack`` for every particle, ``steps`` times (no early exit)."""
+        K.run_fixpoint(self.spec, self.W, steps, 1e-14, early_exit=False, with_sec=False, uid=self.uid,
+                       seed=self.seed, ctr=self._next_ctr(steps))
+        return self
+
+    def attack(self, attackers: torch.Tensor, victims: torch.Tensor) -> "Population":
+        """victims[i] <- f_{attackers[i]}(victims[i]), all attackers using pre-call weights;
+        repeated victims are applied in order (sequential per victim)."""
+        attackers = attackers.to(self.device, torch.int64).contiguous()
+        victims = victims.to(self.device, torch.int64).contiguous()
+        src = self.W.clone()
+        if victims.numel() and torch.unique(victims).numel() != victims.numel():
+            # several attacks on one victim: apply them in order
+            for a, v in zip(attackers.tolist(), victims.tolist()):
+                out = self.W.clone()
+                K.apply(self.spec, torch.cat([src[a:a + 1], self.W[v:v + 1]]), out[:2],
+                        idx_f=torch.tensor([0], device=self.device), idx_t=torch.tensor([1], device=self.device),
+                        idx_o=torch.tensor([0], device=self.device), n=1, uid=self.uid[[v, v]].contiguous(),
+                        seed=self.seed, ctr=self._next_ctr())
+                self.W[v] = out[0]
+            return self
+        tmp = torch.cat([src, self.W])  # rows [0,N): attacker snapshot, [N,2N): current
+        out = self.W
+        K.apply(self.spec, tmp, out, idx_f=attackers, idx_t=(victims + self.n).contiguous(), idx_o=victims,
+                n=victims.numel(), uid=torch.cat([self.uid, self.uid]).contiguous(), seed=self.seed, ctr=self._next_ctr())
+        return self
+
+    def train(self, epochs: int = 1, shuffle: bool = True) -> torch.Tensor:
+        return K.train(self.spec, self.W, epochs, self.lr, shuffle, uid=self.uid, seed=self.seed,
+                       ctr=self._next_ctr(epochs))
+
+    def learn_from(self, teachers: torch.Tensor, idx_t=None, epochs: int = 1, shuffle: bool = True) -> torch.Tensor:
+        return K.learn_from(self.spec, self.W, teachers, idx_t, epochs, self.lr, shuffle, uid=self.uid,
+                            seed=self.seed, ctr=self._next_ctr(epochs))
+
+    def run_fixpoint(self, steps: int = 100, eps: float = 1e-4, early_exit: bool = True, record: bool = False,
+                     with_sec: bool = True):
+        return K.run_fixpoint(self.spec, self.W, steps, eps, early_exit, with_sec, record, uid=self.uid,
+                              seed=self.seed, ctr=self._next_ctr(steps + 2))
+
+    def classify(self, eps: float = 1e-4, with_sec: bool = True):
+        return K.classify(self.spec, self.W, eps, with_sec, uid=self.uid, seed=self.seed, ctr=self._next_ctr())
+
+    def count(self, eps: float = 1e-4, with_sec: bool = True) -> Dict[str, int]:
+        _, counts = self.classify(eps, with_sec)
+        return counts_dict(counts.cpu())
+
+    def perturb(self, e: float) -> "Population":
+        K.perturb(self.spec, self.W, e, uid=self.uid, seed=self.seed, ctr=self._next_ctr())
+        return self
+
+    def vary_run(self, steps: int, eps: float):
+        return K.vary_run(self.spec, self.W, steps, eps, uid=self.uid, seed=self.seed, ctr=self._next_ctr(2 * steps))

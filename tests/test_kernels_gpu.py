@@ -1,0 +1,111 @@
+"""HIP kernels (gfx950) vs the float32 numpy oracle, and vs the host path of the
+same C++ code.  Every test here needs a ROCm device and the native library: the HIP
+path must be the one that runs (no eager fallback exists)."""
+import numpy as np
+import pytest
+import torch
+
+from self_replicating_neural_networks_amd.arch import ArchSpec
+from self_replicating_neural_networks_amd.ops import kernels as K
+from self_replicating_neural_networks_amd.oracle import core as O
+from self_replicating_neural_networks_amd.soup_engine import SoupEngine
+
+pytestmark = pytest.mark.gpu
+
+SPECS = [ArchSpec.weightwise(2, 2), ArchSpec.weightwise(4, 3), ArchSpec.aggregating(4, 2, 2),
+         ArchSpec.aggregating(4, 2, 2, shuffler="random"), ArchSpec.recurrent(2, 2), ArchSpec.fft(4, 2, 2)]
+
+
+def _rel(a, b):
+    a, b = np.asarray(a, np.float64), np.asarray(b, np.float64)
+    m = np.isfinite(a) & np.isfinite(b)
+    return float(np.max(np.abs(a[m] - b[m]) / (np.abs(b[m]) + 1e-3))) if m.any() else 0.0
+
+
+@pytest.mark.parametrize("spec", SPECS, ids=lambda s: f"{s.kind}-{s.width}-{s.depth}-{s.shuffler}")
+def test_init_apply_train_classify_vs_oracle(cuda, spec):
+    n, seed = 2048, 11
+    uid = torch.arange(n, dtype=torch.int64, device=cuda) + 5
+    W = torch.zeros(n, spec.PP, device=cuda)
+    K.init_rows(spec, W, uid, seed)
+    ow = O.init(spec, uid.cpu().numpy(), seed)
+    assert _rel(W[:, :spec.P].cpu().numpy(), ow) < 1e-4
+    # padding stays zero
+    assert torch.all(W[:, spec.P:] == 0)
+    # attack: row i attacked by row i-1
+    out = torch.zeros_like(W)
+    idx_f = torch.roll(torch.arange(n, device=cuda), 1).contiguous()
+    K.apply(spec, W, out, idx_f=idx_f, uid=uid, seed=seed, ctr=3)
+    oo = O.apply(spec, np.roll(ow, 1, axis=0), ow, seed=seed, uids=uid.cpu().numpy(), ctr=3)
+    assert _rel(out[:, :spec.P].cpu().numpy(), oo) < 2e-3
+    # self-train epoch
+    W2 = W.clone()
+    loss = K.train(spec, W2, epochs=1, lr=0.01, uid=uid, seed=seed, ctr=9)
+    tw, tl = O.train_epoch(spec, ow, ow, 0.01, True, seed, uid.cpu().numpy(), 9)
+    assert _rel(W2[:, :spec.P].cpu().numpy(), tw) < 2e-3
+    assert _rel(loss.cpu().numpy(), tl) < 2e-3
+    # classification
+    cls, counts = K.classify(spec, W, 1e-4, uid=uid, seed=seed)
+    ocls = O.classify(spec, ow, 1e-4)
+    assert (cls.cpu().numpy() == ocls).mean() > 0.99
+    assert int(counts.sum()) == n
+
+
+@pytest.mark.parametrize("spec", SPECS[:3] + SPECS[4:5], ids=lambda s: f"{s.kind}-{s.width}-{s.depth}")
+def test_device_matches_host_path(cuda, spec):
+    """Same C++ per-particle code on CPU threads and on the GPU."""
+    n, seed = 1000, 5
+    uid = torch.arange(n, dtype=torch.int64)
+    Wc = torch.zeros(n, spec.PP)
+    K.init_rows(spec, Wc, uid, seed)
+    Wg = Wc.to(cuda)
+    K.train(spec, Wc, epochs=3, uid=uid, seed=seed)
+    K.train(spec, Wg, epochs=3, uid=uid.to(cuda), seed=seed)
+    assert _rel(Wg.cpu().numpy(), Wc.numpy()) < 1e-4
+    cc, _ = K.run_fixpoint(spec, Wc, 5, 1e-4)[:2]
+    cg, _ = K.run_fixpoint(spec, Wg, 5, 1e-4)[:2]
+    assert (cc.numpy() == cg.cpu().numpy()).mean() > 0.99
+
+
+def test_run_fixpoint_statistics_weightwise(cuda):
+    """applying-fixpoints (code/setups/applying-fixpoints.py): 100 self-applications of
+    WW(2,2); published 23/50 divergent, 27/50 fix_zero (log.txt:1-2)."""
+    spec = ArchSpec.weightwise(2, 2)
+    n = 20000
+    uid = torch.arange(n, dtype=torch.int64, device=cuda)
+    W = torch.zeros(n, spec.PP, device=cuda)
+    K.init_rows(spec, W, uid, 2024)
+    cls, _, _ = K.run_fixpoint(spec, W, 100, 1e-4, early_exit=False)
+    c = np.bincount(cls.cpu().numpy(), minlength=5)
+    p_div = c[0] / n
+    assert abs(p_div - 0.46) < 0.05, c
+    assert c[0] + c[1] > 0.97 * n, c
+
+
+def test_soup_engine_gpu_vs_oracle(cuda):
+    spec = ArchSpec.weightwise(2, 2)
+    params = dict(attacking_rate=0.1, learn_from_rate=0.1, train=3, remove_divergent=True, remove_zero=True,
+                  epsilon=1e-4)
+    e = SoupEngine(spec, 3000, params, device=cuda, seed=7)
+    W0 = e.table[:, :spec.P].cpu().numpy().copy()
+    uids = e.uid.cpu().numpy().astype(np.uint64)
+    e.evolve(1)
+    W1, act, cp, loss, resp = O.soup_generation_sync(spec, W0, uids, 1, 7, params)
+    keep = resp == 0
+    assert _rel(e.table[:, :spec.P].cpu().numpy()[keep], W1[keep]) < 2e-3
+    assert (e.action.cpu().numpy() == act).all()
+    assert (e.counterpart.cpu().numpy() == cp).all()
+    assert (e.respawn.cpu().numpy() == resp).mean() > 0.999
+
+
+def test_soup_graph_replay_matches_eager(cuda):
+    spec = ArchSpec.weightwise(2, 2)
+    params = dict(train=2, remove_divergent=True, remove_zero=True, epsilon=1e-4)
+    a = SoupEngine(spec, 4096, params, device=cuda, seed=3)
+    b = SoupEngine(spec, 4096, params, device=cuda, seed=3)
+    assert b.capture(warmup=1)
+    a.evolve(1 + 5)  # capture() ran one eager warmup generation and captured (not ran) one
+    b.evolve(5)
+    torch.cuda.synchronize()
+    assert torch.equal(a.uid, b.uid)
+    assert torch.allclose(a.table, b.table, equal_nan=True)
