@@ -391,7 +391,7 @@ def perturb(w, e, seed, uids, ctr):
     w = np.array(w, dtype=np.float32, copy=True)
     for k in range(w.shape[1]):
         u = draw(seed, uids, (int(ctr) * 1024 + k) & M32, P_PERTURB)
-        mag = u01(u[1]).astype(np.float64) * float(e)
+        mag = u01(u[1]).astype(np.float64) * float(np.float32(e))  # kernel argument is fp32
         up = u01(u[0]) < np.float32(0.5)
         w[:, k] = np.where(up, (w[:, k].astype(np.float64) + mag), (w[:, k].astype(np.float64) - mag)).astype(np.float32)
     return w

@@ -25,6 +25,7 @@ class Dist:
     world: int = 1
     local_rank: int = 0
     group: Optional[object] = None
+    _pad_bufs: dict = dataclasses.field(default_factory=dict, repr=False)
 
     @property
     def enabled(self) -> bool:
@@ -50,8 +51,21 @@ class Dist:
         if len(set(sizes)) == 1:
             dist.all_gather_into_tensor(out, local, group=self.group)
         else:
-            parts = list(torch.split(out, sizes))
-            dist.all_gather(parts, local, group=self.group)
+            # uneven shards: gather max-size padded blocks, then compact
+            m = max(sizes)
+            key = (tuple(local.shape[1:]), local.dtype, local.device, m)
+            buf = self._pad_bufs.get(key)
+            if buf is None:
+                buf = (torch.zeros((m,) + tuple(local.shape[1:]), dtype=local.dtype, device=local.device),
+                       torch.zeros((self.world * m,) + tuple(local.shape[1:]), dtype=local.dtype, device=local.device))
+                self._pad_bufs[key] = buf
+            send, recv = buf
+            send[: local.shape[0]].copy_(local)
+            dist.all_gather_into_tensor(recv, send, group=self.group)
+            o = 0
+            for r, sz in enumerate(sizes):
+                out[o:o + sz].copy_(recv[r * m:r * m + sz])
+                o += sz
         return out
 
     def all_reduce_sum(self, t: torch.Tensor):

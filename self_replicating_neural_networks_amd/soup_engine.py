@@ -196,11 +196,23 @@ class SoupEngine:
     def evolve(self, iterations: int = 1, record: bool = False):
         for _ in range(iterations):
             self.time += 1
-            if self._graph is not None and not record:
+            if record and self.recorder is not None:
+                slot_uid = self.global_uids()  # uid of every slot at generation start
+                self._generation(record=True)
+                self.recorder.on_generation_end(self, self.time, slot_uid)
+            elif self._graph is not None:
                 self._replay_one()
             else:
-                self._generation(record=record)
+                self._generation()
         return self
+
+    def global_uids(self):
+        """uid of every global slot (host numpy); all-gathered when sharded."""
+        if not self.dist.enabled:
+            return self.uid.cpu().numpy().copy()
+        out = torch.zeros(self.n_total, dtype=torch.int64, device=self.device)
+        self.dist.all_gather_rows(out, self.uid, self.n_total)
+        return out.cpu().numpy()
 
     # ------------------------------------------------------------------ HIP graph
     def capture(self, warmup: int = 1) -> bool:

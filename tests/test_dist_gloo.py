@@ -1,0 +1,60 @@
+"""Population sharding over a process group (gloo on CPU): results are independent of the
+number of ranks (R-invariance)."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from self_replicating_neural_networks_amd.arch import ArchSpec
+from self_replicating_neural_networks_amd.parallel.dist import Dist
+from self_replicating_neural_networks_amd.soup_engine import SoupEngine
+
+PARAMS = dict(attacking_rate=0.2, learn_from_rate=0.2, train=2, learn_from_severity=1, remove_divergent=True,
+              remove_zero=True, epsilon=1e-4)
+N_TOTAL, GENS = 203, 6  # uneven shards on purpose
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, spec_json, out_dir):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        d = Dist(rank, world, 0, None)
+        spec = ArchSpec.from_json(spec_json)
+        e = SoupEngine(spec, N_TOTAL, PARAMS, device="cpu", seed=21, dist=d)
+        e.stats = True
+        e.evolve(GENS)
+        counts = e.count()
+        np.savez(os.path.join(out_dir, f"r{rank}.npz"), W=e.local_rows().numpy(), uid=e.uid.numpy(),
+                 next_uid=e.next_uid.numpy(), counts=np.array([counts[k] for k in sorted(counts)]))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_sharded_soup_equals_single_rank(tmp_path, world):
+    spec = ArchSpec.weightwise(2, 2)
+    ref = SoupEngine(spec, N_TOTAL, PARAMS, device="cpu", seed=21)
+    ref.evolve(GENS)
+    ref_counts = ref.count()
+    mp.start_processes(_worker, args=(world, _free_port(), spec.to_json(), str(tmp_path)), nprocs=world,
+                       start_method="spawn", join=True)
+    parts = [np.load(os.path.join(tmp_path, f"r{r}.npz")) for r in range(world)]
+    W = np.concatenate([p["W"] for p in parts])
+    uid = np.concatenate([p["uid"] for p in parts])
+    assert np.array_equal(uid, ref.uid.numpy())
+    assert np.array_equal(W, ref.table.numpy(), equal_nan=True)  # bitwise: per-row math is identical
+    for p in parts:
+        assert int(p["next_uid"][0]) == int(ref.next_uid[0])
+        assert list(p["counts"]) == [ref_counts[k] for k in sorted(ref_counts)]

@@ -1,0 +1,123 @@
+"""Soup: sequential (reference-exact) and device (synchronous, fused) modes."""
+import numpy as np
+import pytest
+import torch
+
+from self_replicating_neural_networks_amd.arch import ArchSpec
+from self_replicating_neural_networks_amd.compat import network as N
+from self_replicating_neural_networks_amd.oracle import core as O
+from self_replicating_neural_networks_amd.soup import Soup
+from self_replicating_neural_networks_amd.soup_engine import SoupEngine
+from self_replicating_neural_networks_amd.utils import rng
+
+PARAMS = dict(attacking_rate=0.1, learn_from_rate=0.1, train=3, learn_from_severity=2, remove_divergent=True,
+              remove_zero=True, epsilon=1e-4)
+
+
+def gen():
+    return N.TrainingNeuralNetworkDecorator(N.WeightwiseNeuralNetwork(2, 2)).with_params(epsilon=1e-4)
+
+
+@pytest.mark.parametrize("spec", [ArchSpec.weightwise(2, 2), ArchSpec.aggregating(4, 2, 2), ArchSpec.recurrent(2, 2),
+                                  ArchSpec.fft(4, 2, 2)], ids=lambda s: s.kind)
+def test_engine_generation_matches_oracle(spec):
+    e = SoupEngine(spec, 400, PARAMS, seed=11)
+    for g in range(3):
+        W0 = e.table[:, :spec.P].numpy().copy()
+        uids = e.uid.numpy().astype(np.uint64).copy()
+        e.evolve(1)
+        W1, act, cp, loss, resp = O.soup_generation_sync(spec, W0, uids, g + 1, 11, PARAMS)
+        keep = resp == 0
+        got = e.table[:, :spec.P].numpy()
+        ok = np.all(np.isfinite(W1), 1) & keep
+        scale = np.max(np.abs(W1[ok]), 1, keepdims=True) + 1e-6
+        # recurrent BPTT amplifies fp32 rounding-order differences (fma contraction)
+        assert np.max(np.abs(got[ok] - W1[ok]) / scale) < (1e-2 if spec.kind == "recurrent" else 1e-3)
+        assert (e.action.numpy() == act).all() and (e.counterpart.numpy() == cp).all()
+        assert (e.respawn.numpy() == resp).all()
+        # state drifts chaotically after respawns: resync oracle input each generation
+
+
+def test_engine_uids_sequential_and_respawn_init():
+    spec = ArchSpec.weightwise(2, 2)
+    e = SoupEngine(spec, 300, dict(PARAMS, train=0, learn_from_rate=-1, attacking_rate=0.5), seed=2)
+    seen = set(e.uid.tolist())
+    for _ in range(20):
+        before = e.next_uid.item()
+        e.evolve(1)
+        resp = int((e.respawn != 0).sum())
+        assert e.next_uid.item() == before + resp
+        new = sorted(set(e.uid.tolist()) - seen)
+        assert new == list(range(before, before + resp))
+        seen |= set(e.uid.tolist())
+    assert len(set(e.uid.tolist())) == 300
+
+
+def test_engine_count_and_stats():
+    spec = ArchSpec.weightwise(2, 2)
+    e = SoupEngine(spec, 256, PARAMS, seed=4)
+    e.stats = True
+    e.evolve(2)
+    c = e.count()
+    assert sum(c.values()) == 256
+    assert int(e.counts.sum()) == 256
+
+
+def test_sequential_soup_reference_algorithm():
+    rng.set_seed(3)
+    s = Soup(10, gen, mode="sequential").with_params(remove_divergent=True, remove_zero=True, train=2)
+    s.seed()
+    s.evolve(5)
+    c = s.count()
+    assert sum(c.values()) == 10
+    assert s.time == 5
+    for uid, p in s.historical_particles.items():
+        assert p.states[0]["action"] == "init"
+        for st in p.states[1:]:
+            assert st["weights"].dtype == np.float32 and st["weights"].shape == (14,)
+            assert st.get("action") in ("train_self", "divergent_dead", "zweo_dead", None)
+    rec = s.without_particles()
+    assert all(isinstance(v, list) for v in rec.historical_particles.values())
+    assert "particles" not in rec.__dict__
+
+
+def test_sequential_soup_is_deterministic_under_seed():
+    def run():
+        rng.set_seed(99)
+        s = Soup(8, gen, mode="sequential").with_params(train=1)
+        s.seed()
+        s.evolve(3)
+        return np.stack([p.get_weights_flat() for p in s.particles])
+    a, b = run(), run()
+    assert np.array_equal(a, b)
+
+
+def test_device_soup_records_reference_schema():
+    rng.set_seed(5)
+    s = Soup(64, gen, mode="device", device="cpu").with_params(remove_divergent=True, remove_zero=True, train=2)
+    s.seed()
+    s.evolve(4)
+    assert len(s.particles) == 64
+    assert sum(s.count().values()) == 64
+    p = s.particles[0]
+    assert [st["time"] for st in p.states][:5] == [0, 1, 2, 3, 4] or p.states[0]["action"] == "init"
+    st = p.states[-1]
+    assert {"class", "weights", "time"} <= set(st)
+    if st.get("action") == "train_self":
+        assert st["fitted"] == 2 and isinstance(st["loss"], float)
+    assert st["class"] == "WeightwiseNeuralNetwork"
+    # particle views behave like nets
+    assert isinstance(p.is_fixpoint(), bool)
+    assert p.get_weights()[0].shape == (4, 2)
+
+
+def test_device_vs_sequential_statistics_training_soup():
+    """Both modes converge the same way: with train=20 nearly every WW particle becomes a
+    non-trivial fixpoint or stays `other` (reference code/results/Soup/log.txt: 13 / 7)."""
+    spec = ArchSpec.weightwise(2, 2)
+    e = SoupEngine(spec, 2000, dict(PARAMS, train=20, learn_from_severity=1), seed=8)
+    e.evolve(30)
+    c = e.count()
+    frac_other_or_fix = (c["fix_other"] + c["other"]) / 2000
+    assert frac_other_or_fix > 0.9
+    assert c["fix_other"] / 2000 > 0.3
