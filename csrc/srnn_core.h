@@ -72,6 +72,31 @@ SRNN_HD float u01_open0(uint32_t x) { return (float)((x >> 8) + 1u) * (1.0f / 16
 
 SRNN_HD bool finitef(float v) { return (__builtin_isfinite(v)) != 0; }
 
+// Permutation of [0, n) (n <= 16) packed as nibbles of a 64-bit register: Fisher-Yates
+// with the swap index j = (r16 * (i+1)) >> 16 from two Philox draws (15 x 16-bit chunks;
+// bias (i+1)/65536).  No memory traffic: replaces the LDS byte shuffle for small nets.
+template <int N>
+SRNN_HD uint64_t shuffle16(const Rng& rng, uint64_t id, uint32_t step, uint32_t purpose) {
+  static_assert(N <= 16, "nibble permutation holds at most 16 entries");
+  uint64_t p = 0;
+#pragma unroll
+  for (int k = 0; k < N; ++k) p |= (uint64_t)k << (4 * k);
+  U4 r0 = rng.draw(id, step * 64u, purpose);
+  U4 r1 = rng.draw(id, step * 64u + 1u, purpose);
+  const uint32_t words[8] = {r0.x, r0.y, r0.z, r0.w, r1.x, r1.y, r1.z, r1.w};
+#pragma unroll
+  for (int i = N - 1; i > 0; --i) {
+    const int c = N - 1 - i;  // chunk index (static)
+    const uint32_t r16 = (words[c >> 1] >> (16 * (c & 1))) & 0xFFFFu;
+    const uint32_t j = (r16 * (uint32_t)(i + 1)) >> 16;
+    const uint64_t ni = (p >> (4 * i)) & 15u;
+    const uint64_t nj = (p >> (4 * j)) & 15u;
+    const uint64_t x = ni ^ nj;
+    p ^= (x << (4 * i)) | (x << (4 * j));
+  }
+  return p;
+}
+
 // ----------------------------------------------------------------------------------
 // Dense layer helpers (row-major (IN, OUT) kernel, y = x . K, fma chain over i).
 // ----------------------------------------------------------------------------------
@@ -86,7 +111,8 @@ SRNN_HD void dense_fwd(const float* __restrict__ k, const float* __restrict__ x,
   }
 }
 
-// gx = K . gy  (gradient wrt the input), then K -= lr * x^T gy  (in place).
+// gx = K . gy  (gradient wrt the input), then K += x^T (-lr gy)  (in place; one fma per
+// weight: the step -lr*gy is formed once per output unit).
 template <int IN, int OUT>
 SRNN_HD void dense_bwd_update(float* __restrict__ k, const float* __restrict__ x, const float* __restrict__ gy,
                               float* __restrict__ gx, float lr, bool want_gx) {
@@ -99,10 +125,13 @@ SRNN_HD void dense_bwd_update(float* __restrict__ k, const float* __restrict__ x
       gx[i] = acc;
     }
   }
+  float step[OUT];
+#pragma unroll
+  for (int j = 0; j < OUT; ++j) step[j] = -lr * gy[j];
 #pragma unroll
   for (int i = 0; i < IN; ++i)
 #pragma unroll
-    for (int j = 0; j < OUT; ++j) k[i * OUT + j] -= lr * (x[i] * gy[j]);
+    for (int j = 0; j < OUT; ++j) k[i * OUT + j] = fmaf(x[i], step[j], k[i * OUT + j]);
 }
 
 // ----------------------------------------------------------------------------------
@@ -297,9 +326,10 @@ struct TrainCtx {
   Rng rng;
   uint64_t uid;      // particle uid (keys shuffles)
   uint32_t ctr;      // op counter (one per epoch consumed)
-  float4* samp;      // >= P float4 slots
-  uint8_t* perm;     // >= P bytes
+  float4* samp;      // >= P float4 slots, slot k at samp[k * stride]
+  uint8_t* perm;     // >= P bytes (only for P > 16)
   bool shuffle;
+  int stride;        // device: threads per block (slot-major, lane fastest: conflict-free b128)
 };
 
 struct ApplyCtx {
@@ -351,12 +381,24 @@ struct Weightwise {
   // (x_k = point k of s, y_k = s[k]); samples frozen at epoch start. Returns mean loss.
   SRNN_HD static float train_epoch(float* __restrict__ w, const float* __restrict__ s, TrainCtx& c) {
 #pragma unroll
-    for (int k = 0; k < P; ++k) c.samp[k] = make_float4(s[k], coords.c[k][0], coords.c[k][1], coords.c[k][2]);
-    if (c.shuffle) fisher_yates(c.perm, P, c.rng, c.uid, c.ctr, P_SHUFFLE);
+    for (int k = 0; k < P; ++k)
+      c.samp[k * c.stride] = make_float4(s[k], coords.c[k][0], coords.c[k][1], coords.c[k][2]);
+    uint64_t pn = 0;
+    if constexpr (P <= 16) {
+      if (c.shuffle) pn = shuffle16<P>(c.rng, c.uid, c.ctr, P_SHUFFLE);
+      else
+#pragma unroll
+        for (int k = 0; k < P; ++k) pn |= (uint64_t)k << (4 * k);
+    } else {
+      if (c.shuffle) fisher_yates(c.perm, P, c.rng, c.uid, c.ctr, P_SHUFFLE);
+    }
     float loss = 0.f;
+#pragma unroll
     for (int q = 0; q < P; ++q) {
-      int idx = c.shuffle ? (int)c.perm[q] : q;
-      float4 smp = c.samp[idx];
+      int idx;
+      if constexpr (P <= 16) idx = (int)((pn >> (4 * q)) & 15u);
+      else idx = c.shuffle ? (int)c.perm[q] : q;
+      float4 smp = c.samp[idx * c.stride];
       float x[4] = {smp.x, smp.y, smp.z, smp.w};
       float acts[Net::NACT], y[1];
       Net::forward(w, x, acts, y);
@@ -683,7 +725,7 @@ struct Recurrent {
       bwd_layers<D>(w, gw, hs[t], t > 0 ? hs[t - 1] : zeros, s[t], dtop, carry);
     }
 #pragma unroll
-    for (int k = 0; k < P; ++k) w[k] -= c.lr * gw[k];
+    for (int k = 0; k < P; ++k) w[k] = fmaf(gw[k], -c.lr, w[k]);
     c.ctr += 1;
     return loss / (float)P;
   }

@@ -52,6 +52,14 @@ SRNN_HD int32_t atomic_add_i32(int32_t* p, int32_t v) {
 #endif
 }
 
+// stride (in float4) between the sample slots of one lane: TB in LDS on the device,
+// 1 in the host scratch array
+#if defined(__HIP_DEVICE_COMPILE__)
+#define SAMP_STRIDE TB
+#else
+#define SAMP_STRIDE 1
+#endif
+
 template <class Net>
 struct Item {
   static constexpr int P = Net::P;
@@ -212,6 +220,7 @@ struct Item {
     tc.samp = samp;
     tc.perm = perm;
     tc.shuffle = (a.flags & 1) != 0;
+    tc.stride = SAMP_STRIDE;
     float loss = 0.f;
     for (int e = 0; e < a.epochs; ++e) {
       if (!learn) copy(s, w);
@@ -289,6 +298,7 @@ struct Item {
     tc.samp = samp;
     tc.perm = perm;
     tc.shuffle = (a.flags & 1) != 0;
+    tc.stride = SAMP_STRIDE;
     float loss = 0.f;
     // 2. learn_from a teacher (its generation-start weights)
     const int32_t te = a.i32b[g];
@@ -335,12 +345,12 @@ __global__ __launch_bounds__(TB) void k_op(SrnnCfg c, SrnnArgs a) {
   using I = Item<Net>;
   constexpr int P = Net::P;
   constexpr bool NEED_SAMP = (OP == OP_TRAIN || OP == OP_LEARN || OP == OP_SOUP_EVOLVE) && Net::KIND == 0;
-  constexpr int SAMP = NEED_SAMP ? P + 1 : 1;  // +1 float4: odd stride across lanes
+  constexpr int SAMP = NEED_SAMP ? P : 1;  // slot-major [P][TB]: lane fastest
   constexpr int PERM = (P + 4) & ~3;
   __shared__ float4 s_samp[TB * SAMP];
   __shared__ uint8_t s_perm[TB * PERM];
   const int64_t i = (int64_t)blockIdx.x * TB + threadIdx.x;
-  float4* samp = s_samp + threadIdx.x * SAMP;
+  float4* samp = s_samp + threadIdx.x;  // slot k of this lane at samp[k * TB]
   uint8_t* perm = s_perm + threadIdx.x * PERM;
 
   if constexpr (OP == OP_SOUP_DECIDE) {

@@ -76,6 +76,25 @@ def fisher_yates(n_items, seed, ids, step, purpose):
     return perm
 
 
+def shuffle16(n_items, seed, ids, step, purpose):
+    """Nibble-register Fisher-Yates of csrc shuffle16 (n <= 16): j = (r16 * (i+1)) >> 16."""
+    ids = np.asarray(ids, dtype=np.uint64).reshape(-1)
+    n = ids.shape[0]
+    perm = np.tile(np.arange(n_items, dtype=np.int64), (n, 1))
+    rows = np.arange(n)
+    r0 = draw(seed, ids, np.uint64((int(step) * 64) & M32), purpose)
+    r1 = draw(seed, ids, np.uint64((int(step) * 64 + 1) & M32), purpose)
+    words = list(r0) + list(r1)
+    for i in range(n_items - 1, 0, -1):
+        c = n_items - 1 - i
+        r16 = (words[c >> 1].astype(np.uint64) >> np.uint64(16 * (c & 1))) & np.uint64(0xFFFF)
+        j = ((r16 * np.uint64(i + 1)) >> np.uint64(16)).astype(np.int64)
+        a = perm[rows, i].copy()
+        perm[rows, i] = perm[rows, j]
+        perm[rows, j] = a
+    return perm
+
+
 # ------------------------------------------------------------------------------ init
 def _glorot(w, off, r, c, seed, uids):
     lim = np.sqrt(np.float32(6.0) / np.float32(r + c)).astype(np.float32)
@@ -150,7 +169,8 @@ def _mlp_backward_update(mats, acts, gy, lr):
     for l in range(len(mats) - 1, -1, -1):
         m = mats[l]
         gx = np.einsum("nij,nj->ni", m, g).astype(np.float32) if l > 0 else None
-        m -= np.float32(lr) * (acts[l][:, :, None] * g[:, None, :])
+        step = (np.float32(-lr) * g).astype(np.float32)
+        m += acts[l][:, :, None] * step[:, None, :]
         g = gx
 
 
@@ -279,7 +299,12 @@ def train_epoch(spec: ArchSpec, w, s, lr=0.01, shuffle=True, seed=0, uids=None, 
     mats = _mats(spec, w)
     if spec.kind == "weightwise":
         x, y = samples(spec, s)
-        perm = fisher_yates(spec.P, seed, uids, ctr, P_SHUFFLE) if shuffle else np.tile(np.arange(spec.P), (n, 1))
+        if not shuffle:
+            perm = np.tile(np.arange(spec.P), (n, 1))
+        elif spec.P <= 16:
+            perm = shuffle16(spec.P, seed, uids, ctr, P_SHUFFLE)
+        else:
+            perm = fisher_yates(spec.P, seed, uids, ctr, P_SHUFFLE)
         loss = np.zeros(n, dtype=np.float32)
         rows = np.arange(n)
         for q in range(spec.P):
@@ -320,7 +345,7 @@ def train_epoch(spec: ArchSpec, w, s, lr=0.01, shuffle=True, seed=0, uids=None, 
             carry[l] = np.einsum("nij,nj->ni", R, dh).astype(np.float32)
             dtop = dx
     for m, g in zip(mats, grads):
-        m -= np.float32(lr) * g
+        m += g * np.float32(-lr)
     return _flat(spec, mats), loss / np.float32(T)
 
 
