@@ -24,7 +24,7 @@ struct SrnnArgs {
   int32_t epochs;       // train: epochs; soup: train count
   int32_t severity;     // soup: learn_from_severity
   int32_t early_exit;   // fixpoint run: stop at fixpoint / divergence
-  int32_t flags;        // bit0 shuffle samples, bit1 remove_divergent, bit2 remove_zero, bit3 count fix_sec
+  int32_t flags;        // bit0 shuffle, bit1 remove_divergent, bit2 remove_zero, bit3 fix_sec, bit4 per-row respawn flags
   int32_t gen;          // soup generation (time)
   float eps;
   float lr;
@@ -71,15 +71,15 @@ enum SrnnOp {
   OP_LEARN = 4,         // `epochs` epochs on samples of W2[idx_t[i]], loss
   OP_CLASSIFY = 5,      // cls + counts
   OP_PERTURB = 6,       // W[i] +-= U(0,1) * eps, p=1/2 each (known-fixpoint variation)
-  OP_SOUP_DECIDE = 7,   // per global slot: attack target / teacher; per local victim count
-  OP_SOUP_FILL = 8,     // CSR attacker lists per local victim
+  OP_SOUP_DECIDE = 7,   // per global slot: decisions; attacks on local victims linked (i32e head, i32f next)
+  OP_RESPAWN_SEQ = 8,   // single rank: scan respawn flags, new uids from *uid_base (updated), re-init, ++*gen_ptr
   OP_SOUP_EVOLVE = 9,   // fused attack -> learn -> train -> respawn flags for local rows
   OP_SCAN = 10,         // i32d[0..n] = exclusive scan of i32c[0..n)
   OP_RESPAWN = 11,      // rows with respawn != 0: uid_out = *uid_base + i32d[i], fresh weights
   OP_VARY_RUN = 12,     // known-fixpoint variation run: nsteps = time to vergence, loss = time as fixpoint
 };
 
-int srnn_abi_version();
+int srnn_abi_version();  // 5
 int srnn_has_config(const SrnnCfg* cfg);
 int srnn_run(int op, const SrnnCfg* cfg, const SrnnArgs* args);
 const char* srnn_last_error();

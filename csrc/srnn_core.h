@@ -168,17 +168,43 @@ struct MLP {
   }
 
   // one SGD step given dL/dy (gy), activations from forward(); updates w in place.
+  // Folded form: the step st = -lr * dL/d(out) is propagated instead of the gradient
+  // (st_in = K . st_out with the pre-update K), so every weight costs one fma and no
+  // layer needs a separate -lr scaling.
   SRNN_HD static void backward_update(float* __restrict__ w, const float* __restrict__ acts,
                                       const float* __restrict__ gy, float lr) {
-    float g[W], gn[W];
-    dense_bwd_update<W, OUT>(w + off(D), acts + IN + (D - 1) * W, gy, g, lr, true);
+    float so[OUT > W ? OUT : W], si[IN > W ? IN : W];
+#pragma unroll
+    for (int j = 0; j < OUT; ++j) so[j] = -lr * gy[j];
+    step_layer<W, OUT>(w + off(D), acts + IN + (D - 1) * W, so, si, true);
 #pragma unroll
     for (int l = D - 1; l >= 1; --l) {
-      dense_bwd_update<W, W>(w + off(l), acts + IN + (l - 1) * W, g, gn, lr, true);
 #pragma unroll
-      for (int j = 0; j < W; ++j) g[j] = gn[j];
+      for (int j = 0; j < W; ++j) so[j] = si[j];
+      step_layer<W, W>(w + off(l), acts + IN + (l - 1) * W, so, si, true);
     }
-    dense_bwd_update<IN, W>(w, acts, g, gn, lr, false);
+#pragma unroll
+    for (int j = 0; j < W; ++j) so[j] = si[j];
+    step_layer<IN, W>(w, acts, so, si, false);
+  }
+
+  // si = K . so (pre-update K) ; K += x (x) so
+  template <int I, int O>
+  SRNN_HD static void step_layer(float* __restrict__ k, const float* __restrict__ x, const float* __restrict__ so,
+                                 float* __restrict__ si, bool want_in) {
+    if (want_in) {
+#pragma unroll
+      for (int i = 0; i < I; ++i) {
+        float acc = k[i * O] * so[0];
+#pragma unroll
+        for (int j = 1; j < O; ++j) acc = fmaf(k[i * O + j], so[j], acc);
+        si[i] = acc;
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < I; ++i)
+#pragma unroll
+      for (int j = 0; j < O; ++j) k[i * O + j] = fmaf(x[i], so[j], k[i * O + j]);
   }
 };
 

@@ -240,23 +240,31 @@ struct Item {
   }
 
   // ---------------------------------------------------------------- soup
-  // decisions of global slot i (reference code/soup.py:56-63, one draw per decision)
-  SRNN_HD static void soup_decide(const SrnnArgs& a, int64_t i) {
-    const int32_t gen = a.gen_ptr ? a.gen_ptr[0] : a.gen;
-    U4 d = rng(a).draw((uint64_t)i, (uint32_t)gen, P_SOUP);
-    int32_t at = -1, te = -1;
+  // Decisions of global slot g in generation `gen` (reference code/soup.py:56-63): a pure
+  // function of (seed, slot, generation), so any rank can recompute any slot's decision.
+  SRNN_HD static void decision(const SrnnArgs& a, int64_t g, int32_t gen, int32_t& at, int32_t& te) {
+    U4 d = rng(a).draw((uint64_t)g, (uint32_t)gen, P_SOUP);
+    at = -1;
+    te = -1;
     if (u01(d.x) < a.attacking_rate) at = (int32_t)(((uint64_t)d.y * (uint64_t)a.n_total) >> 32);
     if (u01(d.z) < a.learn_from_rate) te = (int32_t)(((uint64_t)d.w * (uint64_t)a.n_total) >> 32);
-    a.i32a[i] = at;
-    a.i32b[i] = te;
-    if (at >= a.lo && at < a.lo + a.n) atomic_add_i32(a.i32c + (at - a.lo), 1);
   }
-  SRNN_HD static void soup_fill(const SrnnArgs& a, int64_t i) {
-    int32_t at = a.i32a[i];
+  SRNN_HD static int32_t gen_of(const SrnnArgs& a) { return a.gen_ptr ? a.gen_ptr[0] : a.gen; }
+
+  // Every global slot: link attacks on this rank's victims into per-victim lists
+  // (head[victim] in i32e, pre-set to -1; next[attacker] in i32f).  Optional i32a/i32b
+  // receive the decisions (diagnostics/tests).
+  SRNN_HD static void soup_decide(const SrnnArgs& a, int64_t i) {
+    int32_t at, te;
+    decision(a, i, gen_of(a), at, te);
+    if (a.i32a) a.i32a[i] = at;
+    if (a.i32b) a.i32b[i] = te;
     if (at >= a.lo && at < a.lo + a.n) {
-      int64_t v = at - a.lo;
-      int32_t pos = a.i32d[v] + atomic_add_i32(a.i32e + v, 1);
-      a.i32f[pos] = (int32_t)i;
+#if defined(__HIP_DEVICE_COMPILE__)
+      a.i32f[i] = atomicExch(a.i32e + (at - a.lo), (int32_t)i);
+#else
+      a.i32f[i] = __atomic_exchange_n(a.i32e + (at - a.lo), (int32_t)i, __ATOMIC_RELAXED);
+#endif
     }
   }
 
@@ -267,28 +275,29 @@ struct Item {
     float w[P], f[P], o[P];
     load(a.W2 + g * PP, w);
     const uint64_t uid = uid_of(a, j);
-    const int32_t gen = a.gen_ptr ? a.gen_ptr[0] : a.gen;
+    const int32_t gen = gen_of(a);
     ApplyCtx x = actx(a, c, uid, (uint32_t)gen * 1024u, perm);
-    // 1. attacks received, in ascending attacker slot order
-    const int32_t beg = a.i32d[j], end = a.i32d[j + 1];
+    // 1. attacks received, in ascending attacker slot order (the list is in arrival order)
+    const int32_t head = a.i32e[j];
+    a.i32e[j] = -1;  // list consumed: reset for the next generation's decide
     int32_t last = -1;
-    for (int32_t q = beg; q < end; ++q) {
+    while (head >= 0) {
       int32_t best = INT_MAX;
-      for (int32_t r = beg; r < end; ++r) {
-        int32_t v = a.i32f[r];
-        best = (v > last && v < best) ? v : best;
-      }
+      for (int32_t r = head; r >= 0; r = a.i32f[r]) best = (r > last && r < best) ? r : best;
+      if (best == INT_MAX) break;
       last = best;
       load(a.W2 + (int64_t)best * PP, f);
       Net::apply(f, w, o, x);
       x.ctr += 1;
       copy(w, o);
     }
+    int32_t my_at, te;
+    decision(a, g, gen, my_at, te);
     int8_t act = A_NONE;
     int64_t cp = -1;
-    if (a.i32a[g] >= 0) {
+    if (my_at >= 0) {
       act = A_ATTACKING;
-      cp = a.i32a[g];
+      cp = my_at;
     }
     TrainCtx tc;
     tc.lr = a.lr;
@@ -301,7 +310,6 @@ struct Item {
     tc.stride = SAMP_STRIDE;
     float loss = 0.f;
     // 2. learn_from a teacher (its generation-start weights)
-    const int32_t te = a.i32b[g];
     if (te >= 0) {
       load(a.W2 + (int64_t)te * PP, f);
       for (int e = 0; e < a.severity; ++e) loss = Net::train_epoch(w, f, tc);
@@ -320,11 +328,18 @@ struct Item {
     if ((a.flags & 2) && is_diverged<P>(w)) rs = 1;
     else if ((a.flags & 4) && is_zero<P>(w, a.eps)) rs = 2;
     store(a.W + j * PP, w);
-    a.action[j] = act;
-    a.counterpart[j] = cp;
-    a.loss[j] = loss;
+    if (a.action) a.action[j] = act;
+    if (a.counterpart) a.counterpart[j] = cp;
+    if (a.loss) a.loss[j] = loss;
     a.respawn[j] = rs;
-    a.i32c[j] = rs != 0 ? 1 : 0;
+    if (a.i32c) {
+#if defined(__HIP_DEVICE_COMPILE__)
+      // one wave per block (TB == 64): per-block respawn count for k_respawn_seq
+      (void)0;
+#else
+      a.i32c[j] = rs != 0 ? 1 : 0;
+#endif
+    }
   }
 
   SRNN_HD static void respawn(const SrnnArgs& a, int64_t j) {
@@ -356,9 +371,6 @@ __global__ __launch_bounds__(TB) void k_op(SrnnCfg c, SrnnArgs a) {
   if constexpr (OP == OP_SOUP_DECIDE) {
     if (i < a.n_total) I::soup_decide(a, i);
     return;
-  } else if constexpr (OP == OP_SOUP_FILL) {
-    if (i < a.n_total) I::soup_fill(a, i);
-    return;
   } else if constexpr (OP == OP_CLASSIFY) {
     if (i < a.n) I::classify(c, a, i, perm);  // histogram: k_classify_count
     return;
@@ -370,9 +382,35 @@ __global__ __launch_bounds__(TB) void k_op(SrnnCfg c, SrnnArgs a) {
     else if constexpr (OP == OP_TRAIN) I::train(c, a, i, samp, perm, false);
     else if constexpr (OP == OP_LEARN) I::train(c, a, i, samp, perm, true);
     else if constexpr (OP == OP_PERTURB) I::perturb(c, a, i, samp, perm);
-    else if constexpr (OP == OP_SOUP_EVOLVE) I::soup_evolve(c, a, i, samp, perm);
     else if constexpr (OP == OP_RESPAWN) I::respawn(a, i);
     else if constexpr (OP == OP_VARY_RUN) I::vary_run(c, a, i, samp, perm);
+  }
+}
+
+// Fused soup generation body: one wave per block; after the per-particle work the wave
+// publishes its 64-bit respawn ballot (i32c as u64[block]) for the single-rank respawn scan, or per-row
+// flags (i32c[row]) when OP_SCAN follows (sharded path, a.i32d != null flags that mode).
+template <class Net>
+__global__ __launch_bounds__(TB) void k_soup_evolve(SrnnCfg c, SrnnArgs a) {
+  using I = Item<Net>;
+  constexpr int P = Net::P;
+  constexpr int SAMP = Net::KIND == 0 ? P : 1;
+  constexpr int PERM = (P + 4) & ~3;
+  __shared__ float4 s_samp[TB * SAMP];
+  __shared__ uint8_t s_perm[TB * PERM];
+  const int64_t i = (int64_t)blockIdx.x * TB + threadIdx.x;
+  bool rs = false;
+  if (i < a.n) {
+    I::soup_evolve(c, a, i, s_samp + threadIdx.x, s_perm + threadIdx.x * PERM);
+    rs = a.respawn[i] != 0;
+  }
+  if (a.i32c) {
+    if (a.flags & 16) {
+      if (i < a.n) a.i32c[i] = rs ? 1 : 0;
+    } else {
+      unsigned long long m = __ballot(rs);
+      if (threadIdx.x == 0) reinterpret_cast<unsigned long long*>(a.i32c)[blockIdx.x] = m;
+    }
   }
 }
 
@@ -402,7 +440,7 @@ __global__ __launch_bounds__(TBC) void k_classify_count(SrnnCfg c, SrnnArgs a) {
 
 template <class Net, int OP>
 int launch(const SrnnCfg& c, const SrnnArgs& a) {
-  int64_t items = (OP == OP_SOUP_DECIDE || OP == OP_SOUP_FILL) ? a.n_total : a.n;
+  int64_t items = (OP == OP_SOUP_DECIDE) ? a.n_total : a.n;
   if (items <= 0) return 0;
   int64_t blocks = (items + TB - 1) / TB;
   if (blocks > 0x7fffffffLL) {
@@ -410,7 +448,9 @@ int launch(const SrnnCfg& c, const SrnnArgs& a) {
     return -2;
   }
   hipStream_t st = (hipStream_t)a.stream;
-  if (OP == OP_CLASSIFY && a.counts) {
+  if (OP == OP_SOUP_EVOLVE) {
+    hipLaunchKernelGGL((k_soup_evolve<Net>), dim3((unsigned)blocks), dim3(TB), 0, st, c, a);
+  } else if (OP == OP_CLASSIFY && a.counts) {
     hipLaunchKernelGGL((k_classify_count<Net>), dim3((unsigned)((items + TBC - 1) / TBC)), dim3(TBC), 0, st, c, a);
   } else {
     hipLaunchKernelGGL((k_op<Net, OP>), dim3((unsigned)blocks), dim3(TB), 0, st, c, a);
@@ -430,7 +470,7 @@ template <class Net, int OP>
 int host_run(const SrnnCfg& c, const SrnnArgs& a) {
   using I = Item<Net>;
   constexpr int P = Net::P;
-  int64_t items = (OP == OP_SOUP_DECIDE || OP == OP_SOUP_FILL) ? a.n_total : a.n;
+  int64_t items = (OP == OP_SOUP_DECIDE) ? a.n_total : a.n;
   if (OP == OP_CLASSIFY && a.counts) {
     uint64_t local[5] = {0, 0, 0, 0, 0};
     std::vector<int8_t> ks((size_t)items);
@@ -446,7 +486,6 @@ int host_run(const SrnnCfg& c, const SrnnArgs& a) {
     float4 samp[P + 1];
     uint8_t perm[P + 4];
     if constexpr (OP == OP_SOUP_DECIDE) I::soup_decide(a, i);
-    else if constexpr (OP == OP_SOUP_FILL) I::soup_fill(a, i);
     else if constexpr (OP == OP_CLASSIFY) I::classify(c, a, i, perm);
     else if constexpr (OP == OP_INIT) I::init(c, a, i, samp, perm);
     else if constexpr (OP == OP_APPLY) I::apply(c, a, i, samp, perm);
@@ -458,6 +497,84 @@ int host_run(const SrnnCfg& c, const SrnnArgs& a) {
     else if constexpr (OP == OP_RESPAWN) I::respawn(a, i);
     else if constexpr (OP == OP_VARY_RUN) I::vary_run(c, a, i, samp, perm);
   });
+  return 0;
+}
+
+// Single-rank respawn: one 1024-thread workgroup scans the respawn flags in slot
+// order, assigns the new uids (*uid_base is next_uid), re-initialises those rows, then
+// advances next_uid and the generation counter -- replacing scan + torch bookkeeping
+// kernels with one launch (the flags are sparse; each thread walks a contiguous chunk).
+constexpr int TBR = 1024;
+template <class Net>
+__global__ __launch_bounds__(TBR) void k_respawn_seq(SrnnCfg c, SrnnArgs a) {
+  using I = Item<Net>;
+  __shared__ int32_t s_cnt[TBR];
+  // i32c as u64[b] = respawn ballot of evolve block b (64 rows); thread t owns blocks
+  // [t*ch, (t+1)*ch): no per-row memory traffic, bits give the rows in slot order.
+  const unsigned long long* masks = reinterpret_cast<const unsigned long long*>(a.i32c);
+  const int64_t nb = (a.n + TB - 1) / TB;
+  const int64_t ch = (nb + TBR - 1) / TBR;
+  const int64_t b0 = (int64_t)threadIdx.x * ch;
+  const int64_t b1 = b0 + ch < nb ? b0 + ch : nb;
+  int32_t cnt = 0;
+  for (int64_t b = b0; b < b1; ++b) cnt += __popcll(masks[b]);
+  s_cnt[threadIdx.x] = cnt;
+  __syncthreads();
+  for (int off = 1; off < TBR; off <<= 1) {  // Hillis-Steele inclusive scan
+    int32_t v = threadIdx.x >= off ? s_cnt[threadIdx.x - off] : 0;
+    __syncthreads();
+    s_cnt[threadIdx.x] += v;
+    __syncthreads();
+  }
+  const int64_t base = *(volatile const int64_t*)a.uid_base;
+  int64_t k = base + s_cnt[threadIdx.x] - cnt;
+  if (cnt) {
+    for (int64_t b = b0; b < b1; ++b) {
+      unsigned long long m = masks[b];
+      while (m) {
+        const int bit = __ffsll((long long)m) - 1;
+        m &= m - 1;
+        const int64_t r = b * TB + bit;
+        a.uid_out[r] = k;
+        float w[Net::P];
+        Net::init(w, I::rng(a), (uint64_t)k);
+        I::store(a.W + r * Net::PP, w);
+        ++k;
+      }
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    ((int64_t*)a.uid_base)[0] = base + s_cnt[TBR - 1];
+    if (a.gen_ptr) ((int32_t*)a.gen_ptr)[0] += 1;
+  }
+  if (a.counts && threadIdx.x < 5) a.counts[threadIdx.x] = 0;  // fresh histogram for the census
+}
+
+template <class Net>
+int respawn_seq(const SrnnCfg& c, const SrnnArgs& a) {
+  if (a.dev) {
+    hipLaunchKernelGGL((k_respawn_seq<Net>), dim3(1), dim3(TBR), 0, (hipStream_t)a.stream, c, a);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) {
+      set_error(hipGetErrorString(e));
+      return -3;
+    }
+    return 0;
+  }
+  int64_t k = a.uid_base[0];
+  for (int64_t i = 0; i < a.n; ++i) {
+    if (a.respawn[i] == 0) continue;
+    a.uid_out[i] = k;
+    float w[Net::P];
+    Net::init(w, Item<Net>::rng(a), (uint64_t)k);
+    Item<Net>::store(a.W + i * Net::PP, w);
+    ++k;
+  }
+  ((int64_t*)a.uid_base)[0] = k;
+  if (a.gen_ptr) ((int32_t*)a.gen_ptr)[0] += 1;
+  if (a.counts)
+    for (int q = 0; q < 5; ++q) a.counts[q] = 0;
   return 0;
 }
 
@@ -477,7 +594,7 @@ int run_net_op(int op, const SrnnCfg& c, const SrnnArgs& a) {
     case OP_CLASSIFY: return run_one<Net, OP_CLASSIFY>(c, a);
     case OP_PERTURB: return run_one<Net, OP_PERTURB>(c, a);
     case OP_SOUP_DECIDE: return run_one<Net, OP_SOUP_DECIDE>(c, a);
-    case OP_SOUP_FILL: return run_one<Net, OP_SOUP_FILL>(c, a);
+    case OP_RESPAWN_SEQ: return respawn_seq<Net>(c, a);
     case OP_SOUP_EVOLVE: return run_one<Net, OP_SOUP_EVOLVE>(c, a);
     case OP_RESPAWN: return run_one<Net, OP_RESPAWN>(c, a);
     case OP_VARY_RUN: return run_one<Net, OP_VARY_RUN>(c, a);

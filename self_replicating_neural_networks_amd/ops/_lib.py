@@ -19,7 +19,7 @@ import threading
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libsrnn.so")
 CSRC = os.path.normpath(os.path.join(_HERE, "..", "..", "csrc"))
-ABI_VERSION = 4
+ABI_VERSION = 5
 
 OP_INIT = 0
 OP_APPLY = 1
@@ -29,7 +29,7 @@ OP_LEARN = 4
 OP_CLASSIFY = 5
 OP_PERTURB = 6
 OP_SOUP_DECIDE = 7
-OP_SOUP_FILL = 8
+OP_RESPAWN_SEQ = 8
 OP_SOUP_EVOLVE = 9
 OP_SCAN = 10
 OP_RESPAWN = 11

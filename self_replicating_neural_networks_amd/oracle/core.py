@@ -165,13 +165,14 @@ def _mlp_forward(mats, x):
 
 
 def _mlp_backward_update(mats, acts, gy, lr):
-    g = gy
+    """Folded SGD step (csrc MLP::backward_update): st = -lr*dL/dout propagated with the
+    pre-update kernels; every weight gets K += x (x) st."""
+    st = (np.float32(-lr) * gy).astype(np.float32)
     for l in range(len(mats) - 1, -1, -1):
         m = mats[l]
-        gx = np.einsum("nij,nj->ni", m, g).astype(np.float32) if l > 0 else None
-        step = (np.float32(-lr) * g).astype(np.float32)
-        m += acts[l][:, :, None] * step[:, None, :]
-        g = gx
+        nxt = np.einsum("nij,nj->ni", m, st).astype(np.float32) if l > 0 else None
+        m += acts[l][:, :, None] * st[:, None, :]
+        st = nxt
 
 
 # ------------------------------------------------------------------------------ aggregation

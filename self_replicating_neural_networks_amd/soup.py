@@ -237,7 +237,7 @@ class StateRecorder:
 
     def on_evolved(self, eng):
         uid_slots = eng.uid.clone()
-        self._snap = (eng.next_rows[:, : eng.spec.P].clone(), eng.action.clone(), eng.counterpart.clone(),
+        self._snap = (eng.rows_out[:, : eng.spec.P].clone(), eng.action.clone(), eng.counterpart.clone(),
                       eng.loss.clone(), eng.respawn.clone(), uid_slots)
 
     def on_generation_end(self, eng, time, uid_of_slot):

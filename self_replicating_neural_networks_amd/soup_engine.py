@@ -67,33 +67,36 @@ class SoupEngine:
             raise ValueError("soup slots are int32 on device")
         dev, PP = self.device, spec.PP
         i32 = dict(dtype=torch.int32, device=dev)
-        # generation-start table (global rows when sharded) and the local output rows
-        self.table = torch.zeros((self.n_total if self.dist.enabled else self.n, PP), dtype=torch.float32, device=dev)
-        self.next_rows = torch.zeros((self.n, PP), dtype=torch.float32, device=dev)
+        if self.dist.enabled:
+            # generation-start table of every global row + this rank's output rows
+            self.table = torch.zeros((self.n_total, PP), dtype=torch.float32, device=dev)
+            self.next_rows = torch.zeros((self.n, PP), dtype=torch.float32, device=dev)
+        else:
+            # ping-pong pair: generation t reads buf[p], writes buf[1-p]
+            self._bufs = [torch.zeros((self.n, PP), dtype=torch.float32, device=dev) for _ in range(2)]
+            self._p = 0
         self.uid = torch.arange(self.lo, self.hi, dtype=torch.int64, device=dev)
         self.next_uid = torch.full((1,), self.n_total, dtype=torch.int64, device=dev)
         self.uid_base = torch.zeros(1, dtype=torch.int64, device=dev)
-        self.gen_dev = torch.zeros(1, dtype=torch.int32, device=dev)
+        self.gen_dev = torch.ones(1, dtype=torch.int32, device=dev)  # generation about to run
         self.time = 0
-        self.att = torch.empty(self.n_total, **i32)
-        self.teacher = torch.empty(self.n_total, **i32)
-        self.cnt = torch.zeros(self.n, **i32)
+        self.head = torch.full((self.n,), -1, **i32)       # first attacker of each local victim
+        self.next_att = torch.full((self.n_total,), -1, **i32)  # attacker -> next attacker of its victim
+        self.flags32 = torch.zeros(self.n, **i32)
         self.off = torch.zeros(self.n + 1, **i32)
-        self.cursor = torch.zeros(self.n, **i32)
-        self.alist = torch.zeros(max(self.n_total, 1), **i32)
         self.action = torch.zeros(self.n, dtype=torch.int8, device=dev)
         self.counterpart = torch.full((self.n,), -1, dtype=torch.int64, device=dev)
         self.loss = torch.zeros(self.n, dtype=torch.float32, device=dev)
         self.respawn = torch.zeros(self.n, dtype=torch.int8, device=dev)
         self.counts = torch.zeros(5, dtype=torch.int64, device=dev)
         self.rank_totals = torch.zeros(self.dist.world, **i32)
-        tb = _lib.scan_temp_bytes(self.n) if dev.type == "cuda" else 0
+        tb = _lib.scan_temp_bytes(self.n) if dev.type == "cuda" and self.dist.enabled else 0
         self.scan_temp = torch.empty(max(tb, 16), dtype=torch.uint8, device=dev)
         self.cfg = _lib.make_cfg(spec)
         self.recorder = None
         self.stats = False          # classify + all-reduce every generation
         self.stats_with_sec = True
-        self._graph = None
+        self._graphs = None
         # initial particles: uids 0..n_total-1, keyed init (identical for any rank count)
         local = self.local_rows()
         if weights is not None:
@@ -107,9 +110,18 @@ class SoupEngine:
             self.dist.all_gather_rows(self.table, self.next_rows, self.n_total)
 
     # ------------------------------------------------------------------ views
+    @property
+    def table_in(self) -> torch.Tensor:
+        """Generation-start table read by the next generation."""
+        return self.table if self.dist.enabled else self._bufs[self._p]
+
+    @property
+    def rows_out(self) -> torch.Tensor:
+        return self.next_rows if self.dist.enabled else self._bufs[1 - self._p]
+
     def local_rows(self) -> torch.Tensor:
         """Current weights of this rank's particles ([n, PP])."""
-        return self.table[self.lo:self.hi] if self.dist.enabled else self.table
+        return self.table[self.lo:self.hi] if self.dist.enabled else self._bufs[self._p]
 
     @property
     def eps(self) -> float:
@@ -142,47 +154,46 @@ class SoupEngine:
     # ------------------------------------------------------------------ one generation
     def _generation(self, record: bool = False):
         spec, cfg = self.spec, self.cfg
-        self.gen_dev.add_(1)
         a = self._args()
-        a.W2 = _p(self.table)
-        a.W = _p(self.next_rows)
+        a.W2 = _p(self.table_in)
+        a.W = _p(self.rows_out)
         a.uid = _p(self.uid)
-        a.i32a, a.i32b = _p(self.att), _p(self.teacher)
-        a.i32c, a.i32d, a.i32e, a.i32f = _p(self.cnt), _p(self.off), _p(self.cursor), _p(self.alist)
+        a.i32e, a.i32f = _p(self.head), _p(self.next_att)
+        a.i32c, a.i32d = _p(self.flags32), _p(self.off)
         a.action, a.counterpart, a.loss, a.respawn = _p(self.action), _p(self.counterpart), _p(self.loss), _p(self.respawn)
         a.temp, a.temp_bytes = _p(self.scan_temp), self.scan_temp.numel()
-        a.uid_out, a.uid_base = _p(self.uid), _p(self.uid_base)
-        self.cnt.zero_()
-        self.cursor.zero_()
+        a.uid_out = _p(self.uid)
+        if self.dist.enabled:
+            a.flags |= 16  # per-row respawn flags for the scan (else per-block counts)
+        # head[] is -1 on entry: set at construction, reset by the evolve kernel after use
         _lib.run(_lib.OP_SOUP_DECIDE, spec, a, cfg)
-        _lib.run(_lib.OP_SCAN, spec, a, cfg)
-        _lib.run(_lib.OP_SOUP_FILL, spec, a, cfg)
         _lib.run(_lib.OP_SOUP_EVOLVE, spec, a, cfg)
         if record and self.recorder is not None:
             self.recorder.on_evolved(self)
-        # respawn: cnt now holds int32 respawn flags
-        _lib.run(_lib.OP_SCAN, spec, a, cfg)
         if self.dist.enabled:
+            # globally sequential uids: rank r starts after the respawns of ranks < r
+            _lib.run(_lib.OP_SCAN, spec, a, cfg)
             self.dist.all_gather_scalar(self.rank_totals, self.off[self.n:self.n + 1])
             prefix = self.rank_totals[: self.dist.rank].sum().to(torch.int64)
             self.uid_base.copy_(self.next_uid + prefix)
             self.next_uid.add_(self.rank_totals.sum().to(torch.int64))
-        else:
-            self.uid_base.copy_(self.next_uid)
-            self.next_uid.add_(self.off[self.n:self.n + 1].to(torch.int64))
-        _lib.run(_lib.OP_RESPAWN, spec, a, cfg)
-        # publish
-        if self.dist.enabled:
+            a.uid_base = _p(self.uid_base)
+            _lib.run(_lib.OP_RESPAWN, spec, a, cfg)
+            self.gen_dev.add_(1)
             self.dist.all_gather_rows(self.table, self.next_rows, self.n_total)
         else:
-            self.table.copy_(self.next_rows)
+            a.uid_base = _p(self.next_uid)  # updated in place, gen_dev advanced by the kernel
+            a.counts = _p(self.counts)       # zeroed by the kernel for the census below
+            _lib.run(_lib.OP_RESPAWN_SEQ, spec, a, cfg)
+            self._p = 1 - self._p
         if self.stats:
             # per-generation fixpoint-fraction statistics (reference Soup.count, code/soup.py:89-103)
-            self.classify_local(self.stats_with_sec)
+            self.classify_local(self.stats_with_sec, zero=self.dist.enabled)
             self.dist.all_reduce_sum(self.counts)
 
-    def classify_local(self, with_sec: bool = True):
-        self.counts.zero_()
+    def classify_local(self, with_sec: bool = True, zero: bool = True):
+        if zero:
+            self.counts.zero_()
         cls, _ = K.classify(self.spec, self.local_rows(), self.eps, with_sec, uid=self.uid, seed=self.seed,
                             ctr=0x7FFFFFF0, counts=self.counts)
         return cls
@@ -200,8 +211,9 @@ class SoupEngine:
                 slot_uid = self.global_uids()  # uid of every slot at generation start
                 self._generation(record=True)
                 self.recorder.on_generation_end(self, self.time, slot_uid)
-            elif self._graph is not None:
-                self._replay_one()
+            elif self._graphs is not None:
+                self._graphs[self._p].replay()
+                self._p = 1 - self._p
             else:
                 self._generation()
         return self
@@ -214,27 +226,29 @@ class SoupEngine:
         self.dist.all_gather_rows(out, self.uid, self.n_total)
         return out.cpu().numpy()
 
-    # ------------------------------------------------------------------ HIP graph
+    # ------------------------------------------------------------------ HIP graphs
     def capture(self, warmup: int = 1) -> bool:
-        """Capture one generation in a hipGraph (single rank, ROCm device only).
-
-        Everything that changes per generation lives in device memory (generation
-        counter, uid counter), so replaying the graph advances the soup exactly like the
-        eager path."""
+        """Capture the generation for both ping-pong parities in two hipGraphs (single
+        rank, ROCm device).  Everything that changes per generation lives in device
+        memory (generation counter, next uid), so replays advance the soup exactly like
+        the eager path."""
         if self.device.type != "cuda" or self.dist.enabled:
             return False
         s = torch.cuda.Stream(self.device)
         s.wait_stream(torch.cuda.current_stream(self.device))
         with torch.cuda.stream(s):
-            for _ in range(warmup):
+            for _ in range(max(warmup, 0)):
                 self.time += 1
                 self._generation()
         torch.cuda.current_stream(self.device).wait_stream(s)
-        g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g, stream=s):
-            self._generation()
-        self._graph = g
+        graphs = []
+        p0 = self._p
+        for _ in range(2):
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, stream=s):
+                self._generation()  # flips self._p during capture (nothing ran)
+            graphs.append(g)
+        self._p = p0
+        # graphs[k] was captured with parity p0 ^ k; index them by parity
+        self._graphs = graphs if p0 == 0 else graphs[::-1]
         return True
-
-    def _replay_one(self):
-        self._graph.replay()

@@ -54,7 +54,7 @@ def test_sharded_soup_equals_single_rank(tmp_path, world):
     W = np.concatenate([p["W"] for p in parts])
     uid = np.concatenate([p["uid"] for p in parts])
     assert np.array_equal(uid, ref.uid.numpy())
-    assert np.array_equal(W, ref.table.numpy(), equal_nan=True)  # bitwise: per-row math is identical
+    assert np.array_equal(W, ref.local_rows().numpy(), equal_nan=True)  # bitwise: per-row math is identical
     for p in parts:
         assert int(p["next_uid"][0]) == int(ref.next_uid[0])
         assert list(p["counts"]) == [ref_counts[k] for k in sorted(ref_counts)]

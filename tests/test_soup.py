@@ -23,12 +23,12 @@ def gen():
 def test_engine_generation_matches_oracle(spec):
     e = SoupEngine(spec, 400, PARAMS, seed=11)
     for g in range(3):
-        W0 = e.table[:, :spec.P].numpy().copy()
+        W0 = e.local_rows()[:, :spec.P].numpy().copy()
         uids = e.uid.numpy().astype(np.uint64).copy()
         e.evolve(1)
         W1, act, cp, loss, resp = O.soup_generation_sync(spec, W0, uids, g + 1, 11, PARAMS)
         keep = resp == 0
-        got = e.table[:, :spec.P].numpy()
+        got = e.local_rows()[:, :spec.P].numpy()
         ok = np.all(np.isfinite(W1), 1) & keep
         scale = np.max(np.abs(W1[ok]), 1, keepdims=True) + 1e-6
         # recurrent BPTT amplifies fp32 rounding-order differences (fma contraction)
