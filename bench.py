@@ -43,13 +43,18 @@ def main():
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--no-stats", action="store_true")
     ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--backend", default="nccl", help="nccl (= RCCL on ROCm) or gloo (rehearsal)")
+    ap.add_argument("--share-device", action="store_true",
+                    help="rehearsal on a 1-GPU box: every rank uses cuda:0")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if world != args.gpus:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
-    d = from_env(backend="nccl")
-    dev = torch.device("cuda", d.local_rank)
+    if args.share_device:
+        os.environ["SRNN_SHARE_DEVICE"] = "1"
+    d = from_env(backend=args.backend)
+    dev = torch.device("cuda", 0 if args.share_device else d.local_rank)
     torch.cuda.set_device(dev)
 
     spec = ArchSpec.weightwise(2, 2)

@@ -53,6 +53,7 @@ struct SrnnArgs {
   int64_t* uid_out;     // respawn: uid column to update
   const int64_t* uid_base;  // respawn: device scalar, first uid for this rank
   const int32_t* gen_ptr;   // soup: device scalar generation (graph replay); null -> gen
+  int64_t segment;          // soup: >0 -> independent sub-soups of this many slots (partners chosen inside)
   int8_t* action;       // soup: action code per local row
   int64_t* counterpart; // soup: counterpart slot per local row
   int8_t* respawn;      // soup: 0 none, 1 divergent_dead, 2 zweo_dead
@@ -79,7 +80,7 @@ enum SrnnOp {
   OP_VARY_RUN = 12,     // known-fixpoint variation run: nsteps = time to vergence, loss = time as fixpoint
 };
 
-int srnn_abi_version();  // 5
+int srnn_abi_version();  // 6
 int srnn_has_config(const SrnnCfg* cfg);
 int srnn_run(int op, const SrnnCfg* cfg, const SrnnArgs* args);
 const char* srnn_last_error();

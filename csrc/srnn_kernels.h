@@ -246,8 +246,11 @@ struct Item {
     U4 d = rng(a).draw((uint64_t)g, (uint32_t)gen, P_SOUP);
     at = -1;
     te = -1;
-    if (u01(d.x) < a.attacking_rate) at = (int32_t)(((uint64_t)d.y * (uint64_t)a.n_total) >> 32);
-    if (u01(d.z) < a.learn_from_rate) te = (int32_t)(((uint64_t)d.w * (uint64_t)a.n_total) >> 32);
+    // partners are drawn inside the slot's sub-soup (segment) or the whole population
+    const int64_t span = a.segment > 0 ? a.segment : a.n_total;
+    const int64_t base = a.segment > 0 ? (g / a.segment) * a.segment : 0;
+    if (u01(d.x) < a.attacking_rate) at = (int32_t)(base + (int64_t)(((uint64_t)d.y * (uint64_t)span) >> 32));
+    if (u01(d.z) < a.learn_from_rate) te = (int32_t)(base + (int64_t)(((uint64_t)d.w * (uint64_t)span) >> 32));
   }
   SRNN_HD static int32_t gen_of(const SrnnArgs& a) { return a.gen_ptr ? a.gen_ptr[0] : a.gen; }
 

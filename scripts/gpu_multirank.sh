@@ -1,0 +1,8 @@
+#!/bin/bash
+# Rehearse the sharded soup on ONE GPU: 2 ranks sharing cuda:0 (RCCL, then gloo fallback).
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-/root/repo}"
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+timeout -k 10 240 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29511 bench.py --gpus 2 --steps 10 --warmup 2 --share-device --backend gloo > gpurun_out/mr_gloo.log 2>&1; echo "gloo rc=$?"; grep metric gpurun_out/mr_gloo.log | cut -c1-250
+timeout -k 10 240 env NCCL_DEBUG=WARN python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29512 bench.py --gpus 2 --steps 10 --warmup 2 --share-device > gpurun_out/mr_nccl.log 2>&1; echo "nccl rc=$?"; grep -E "metric|Error|error" gpurun_out/mr_nccl.log | head -5 | cut -c1-300

@@ -19,7 +19,7 @@ import threading
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libsrnn.so")
 CSRC = os.path.normpath(os.path.join(_HERE, "..", "..", "csrc"))
-ABI_VERSION = 5
+ABI_VERSION = 6
 
 OP_INIT = 0
 OP_APPLY = 1
@@ -61,7 +61,7 @@ class SrnnArgs(ctypes.Structure):
         ("idx_f", _P), ("idx_t", _P), ("idx_o", _P), ("uid", _P),
         ("cls", _P), ("nsteps", _P), ("loss", _P), ("counts", _P),
         ("i32a", _P), ("i32b", _P), ("i32c", _P), ("i32d", _P), ("i32e", _P), ("i32f", _P),
-        ("uid_out", _P), ("uid_base", _P), ("gen_ptr", _P),
+        ("uid_out", _P), ("uid_base", _P), ("gen_ptr", _P), ("segment", ctypes.c_int64),
         ("action", _P), ("counterpart", _P), ("respawn", _P),
         ("temp", _P), ("temp_bytes", ctypes.c_int64),
         ("dev", ctypes.c_int32), ("pad1", ctypes.c_int32), ("stream", _P),

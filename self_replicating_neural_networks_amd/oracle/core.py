@@ -424,13 +424,15 @@ def perturb(w, e, seed, uids, ctr):
 
 
 # ------------------------------------------------------------------------------ soup (synchronous)
-def soup_decisions(seed, gen, n_total, attacking_rate, learn_from_rate):
+def soup_decisions(seed, gen, n_total, attacking_rate, learn_from_rate, segment=0):
     slots = np.arange(n_total, dtype=np.uint64)
     d = draw(seed, slots, gen, P_SOUP)
+    span = np.uint64(segment if segment > 0 else n_total)
+    base = (np.arange(n_total) // segment * segment) if segment > 0 else np.zeros(n_total, dtype=np.int64)
     att = np.where(u01(d[0]) < np.float32(attacking_rate),
-                   ((d[1].astype(np.uint64) * np.uint64(n_total)) >> np.uint64(32)).astype(np.int64), -1)
+                   base + ((d[1].astype(np.uint64) * span) >> np.uint64(32)).astype(np.int64), -1)
     te = np.where(u01(d[2]) < np.float32(learn_from_rate),
-                  ((d[3].astype(np.uint64) * np.uint64(n_total)) >> np.uint64(32)).astype(np.int64), -1)
+                  base + ((d[3].astype(np.uint64) * span) >> np.uint64(32)).astype(np.int64), -1)
     return att, te
 
 
@@ -438,7 +440,8 @@ def soup_generation_sync(spec, W0, uids, gen, seed, params, lr=0.01, shuffle=Tru
     """Synchronous (Jacobi) soup generation — the semantics of the fused kernel
     (csrc Item::soup_evolve).  Returns (W1, action, counterpart, loss, respawn)."""
     n = W0.shape[0]
-    att, te = soup_decisions(seed, gen, n, params["attacking_rate"], params["learn_from_rate"])
+    att, te = soup_decisions(seed, gen, n, params["attacking_rate"], params["learn_from_rate"],
+                             int(params.get("segment", 0)))
     W = np.array(W0, dtype=np.float32, copy=True)
     ctr = np.full(n, (gen * 1024) & M32, dtype=np.int64)
     with np.errstate(over="ignore", invalid="ignore"):

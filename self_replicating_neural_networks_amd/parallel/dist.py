@@ -98,8 +98,9 @@ def from_env(backend: Optional[str] = None, device_type: str = "cuda") -> Dist:
             backend = "nccl" if device_type == "cuda" else "gloo"
         kw = {}
         if backend == "nccl":
-            torch.cuda.set_device(local_rank)
-            kw["device_id"] = torch.device("cuda", local_rank)
+            dev_idx = 0 if os.environ.get("SRNN_SHARE_DEVICE") == "1" else local_rank
+            torch.cuda.set_device(dev_idx)
+            kw["device_id"] = torch.device("cuda", dev_idx)
         dist.init_process_group(backend=backend, **kw)
     return Dist(dist.get_rank(), dist.get_world_size(), local_rank, None)
 

@@ -65,6 +65,9 @@ class SoupEngine:
         self.n = self.hi - self.lo
         if self.n_total >= 2 ** 31 - 1:
             raise ValueError("soup slots are int32 on device")
+        seg = int(self.params.get("segment", 0) or 0)
+        if seg and self.n_total % seg:
+            raise ValueError("population size must be a multiple of the sub-soup segment")
         dev, PP = self.device, spec.PP
         i32 = dict(dtype=torch.int32, device=dev)
         if self.dist.enabled:
@@ -146,6 +149,7 @@ class SoupEngine:
         a.severity = int(self.params.get("learn_from_severity", 1))
         a.flags = self._flags()
         a.gen_ptr = _p(self.gen_dev)
+        a.segment = int(self.params.get("segment", 0) or 0)
         if self.device.type == "cuda":
             a.dev = 1
             a.stream = ctypes.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)

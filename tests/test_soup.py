@@ -121,3 +121,22 @@ def test_device_vs_sequential_statistics_training_soup():
     frac_other_or_fix = (c["fix_other"] + c["other"]) / 2000
     assert frac_other_or_fix > 0.9
     assert c["fix_other"] / 2000 > 0.3
+
+
+def test_segmented_soups_are_independent():
+    """segment=S: N/S independent sub-soups in one launch (partners never cross a segment)."""
+    spec = ArchSpec.weightwise(2, 2)
+    params = dict(PARAMS, segment=10, attacking_rate=0.5, learn_from_rate=0.5)
+    e = SoupEngine(spec, 200, params, seed=13)
+    att, te = O.soup_decisions(13, 1, 200, 0.5, 0.5, 10)
+    slots = np.arange(200)
+    assert np.all((att < 0) | (att // 10 == slots // 10)) and np.all((te < 0) | (te // 10 == slots // 10))
+    W0 = e.local_rows()[:, :spec.P].numpy().copy()
+    e.evolve(1)
+    W1, act, cp, _, resp = O.soup_generation_sync(spec, W0, e.uid.numpy().astype(np.uint64) * 0 + np.arange(200, dtype=np.uint64),
+                                                  1, 13, params)
+    keep = resp == 0
+    assert (e.counterpart.numpy() == cp).all()
+    got = e.local_rows()[:, :spec.P].numpy()
+    scale = np.max(np.abs(W1[keep]), 1, keepdims=True) + 1e-6
+    assert np.max(np.abs(got[keep] - W1[keep]) / scale) < 1e-3

@@ -1,0 +1,91 @@
+"""Golden statistical tests against the reference's published outcome numbers
+(code/results/**/log.txt).  Trials are population rows, so we use many
+more than the reference's 50 and compare with binomial / normal confidence bounds."""
+import numpy as np
+import pytest
+
+from self_replicating_neural_networks_amd.setups import experiments as E
+
+
+def within(p_hat, n, p_ref, n_ref, z=4.0):
+    """|p_hat - p_ref| within z standard errors of the combined binomial estimate."""
+    se = np.sqrt(p_hat * (1 - p_hat) / n + p_ref * (1 - p_ref) / n_ref) + 1e-9
+    return abs(p_hat - p_ref) <= z * se
+
+
+@pytest.fixture(scope="module")
+def applying(tmp_path_factory):
+    return E.applying_fixpoints(trials=4000, device="cpu", seed=1, root=str(tmp_path_factory.mktemp("a")))
+
+
+def test_applying_fixpoints_weightwise(applying):
+    c = applying["counters"][0]  # published 23 divergent / 27 fix_zero of 50
+    assert c["divergent"] + c["fix_zero"] == 4000
+    assert within(c["divergent"] / 4000, 4000, 23 / 50, 50)
+
+
+def test_applying_fixpoints_aggregating(applying):
+    c = applying["counters"][1]  # published 4 / 46
+    assert c["divergent"] + c["fix_zero"] == 4000
+    assert within(c["divergent"] / 4000, 4000, 4 / 50, 50)
+
+
+def test_applying_fixpoints_recurrent(applying):
+    c = applying["counters"][2]  # published 46 / 4
+    assert c["divergent"] + c["fix_zero"] == 4000
+    assert within(c["divergent"] / 4000, 4000, 46 / 50, 50)
+
+
+def test_training_fixpoints_ww_and_agg(tmp_path):
+    r = E.training_fixpoints(trials=200, device="cpu", seed=2, root=str(tmp_path),
+                             specs=(E.WW, E.AGG))
+    ww, agg = r["counters"]
+    assert ww["fix_other"] >= 196        # published 50/50 fix_other
+    assert agg["other"] >= 196           # published 50/50 other
+
+
+def test_known_fixpoint_variation_curve(tmp_path):
+    r = E.known_fixpoint_variation(trials=400, device="cpu", seed=3, root=str(tmp_path))
+    pub_y = [3.63, 5.02, 6.46, 8.04, 9.61, 11.23, 12.99, 14.58, 21.95, 26.45]
+    pub_z = [0, 0, 0, 0, 0.04, 1.38, 3.23, 4.84, 11.91, 16.47]
+    assert np.allclose(r["ys"], pub_y, atol=1.0, rtol=0.06)
+    assert np.allclose(r["zs"], pub_z, atol=0.6, rtol=0.08)
+    # the float32 jump between 1e-7 and 1e-8
+    assert r["ys"][8] - r["ys"][7] > 5
+
+
+def test_learn_from_soup_curve(tmp_path):
+    r = E.learn_from_soup(trials=100, device="cpu", seed=4, root=str(tmp_path))
+    zs = np.array(r["data"][0]["zs"])
+    pub = np.array([0, 1.2, 5.2, 7.4, 8.1, 9.1, 9.6, 9.8, 10.0, 9.9, 9.9])
+    assert zs[0] == 0 and np.all(np.array(r["data"][0]["ys"]) < 0.2)
+    assert np.max(np.abs(zs - pub)) < 1.6
+    assert np.all(np.diff(zs[:6]) > -0.3)  # monotone rise with severity
+
+
+def test_mixed_soup_curve(tmp_path):
+    r = E.mixed_soup(trials=100, device="cpu", seed=5, root=str(tmp_path))
+    ww, agg = r["data"]
+    pub = np.array([0, 0, 0.7, 1.9, 3.6, 4.3, 6.0, 6.1, 8.3, 7.7, 8.8])
+    assert np.max(np.abs(np.array(ww["zs"]) - pub)) < 1.6
+    assert np.all(np.array(agg["zs"]) == 0)  # aggregating soups never reach non-zero fixpoints
+
+
+def test_mixed_self_fixpoints_curve(tmp_path):
+    r = E.mixed_self_fixpoints(trials=200, device="cpu", seed=6, root=str(tmp_path),
+                               trains=[0, 250, 500])
+    ww, agg, rnn = (np.array(d["ys"]) for d in r["data"])
+    assert ww[0] < 0.45 and ww[2] > 0.8      # published 0.2 -> 1.0
+    assert np.all(agg > 0.75)                 # published 0.8 .. 1.0
+    assert np.all(rnn < 0.25)                 # published 0 .. 0.1
+
+
+def test_network_trajectorys_records(tmp_path):
+    r = E.network_trajectorys(trials=20, device="cpu", seed=7, root=str(tmp_path))
+    assert sum(r["counters"].values()) == 20
+    from self_replicating_neural_networks_amd.io import refpickle as R
+    import os
+    t = R.load(os.path.join(r["dir"], "trajectorys.dill"))
+    assert len(t.historical_particles) == 20
+    states = next(iter(t.historical_particles.values()))
+    assert states[0]["action"] == "init" and [s["time"] for s in states] == list(range(len(states)))
