@@ -24,7 +24,7 @@ struct SrnnArgs {
   int32_t epochs;       // train: epochs; soup: train count
   int32_t severity;     // soup: learn_from_severity
   int32_t early_exit;   // fixpoint run: stop at fixpoint / divergence
-  int32_t flags;        // bit0 shuffle, bit1 remove_divergent, bit2 remove_zero, bit3 fix_sec, bit4 per-row respawn flags
+  int32_t flags;        // bit0 shuffle, bit1 remove_divergent, bit2 remove_zero, bit3 fix_sec, bit4 per-row respawn flags, bit5 respawn inline, bit6 count respawns in counts[5]
   int32_t gen;          // soup generation (time)
   float eps;
   float lr;
@@ -54,6 +54,17 @@ struct SrnnArgs {
   const int64_t* uid_base;  // respawn: device scalar, first uid for this rank
   const int32_t* gen_ptr;   // soup: device scalar generation (graph replay); null -> gen
   int64_t segment;          // soup: >0 -> independent sub-soups of this many slots (partners chosen inside)
+  int32_t world;            // soup: ranks sharing the population (<= 1: unsharded)
+  int32_t rank;
+  int64_t cap;              // soup: rows per destination rank in the exchange buffers
+  float* sendbuf;           // [world][cap][pp + 4]: row, then (slot, generation) tags
+  const float* recvbuf;     // [world][cap][pp + 4]
+  int32_t* need;            // [n] bitmask of the ranks that need local row j this generation
+  int32_t* sendcnt;         // [world] rows packed per destination
+  int32_t* rmap;            // [n_total] received row index of a remote slot
+  int32_t* ovf;             // [1] exchange overflow flag
+  const int64_t* stats;     // [world][6] gathered (class counts[5], respawns) per rank
+  int64_t* census;          // [5] global class counts (written by OP_UID_ASSIGN)
   int8_t* action;       // soup: action code per local row
   int64_t* counterpart; // soup: counterpart slot per local row
   int8_t* respawn;      // soup: 0 none, 1 divergent_dead, 2 zweo_dead
@@ -78,9 +89,12 @@ enum SrnnOp {
   OP_SCAN = 10,         // i32d[0..n] = exclusive scan of i32c[0..n)
   OP_RESPAWN = 11,      // rows with respawn != 0: uid_out = *uid_base + i32d[i], fresh weights
   OP_VARY_RUN = 12,     // known-fixpoint variation run: nsteps = time to vergence, loss = time as fixpoint
+  OP_SOUP_PACK = 13,    // sharded soup: local rows needed by other ranks -> sendbuf (tagged)
+  OP_SOUP_UNPACK = 14,  // sharded soup: index the received rows (rmap), reset sendcnt
+  OP_UID_ASSIGN = 15,   // sharded soup: uids of respawned rows from the gathered per-rank stats
 };
 
-int srnn_abi_version();  // 6
+int srnn_abi_version();  // 7
 int srnn_has_config(const SrnnCfg* cfg);
 int srnn_run(int op, const SrnnCfg* cfg, const SrnnArgs* args);
 const char* srnn_last_error();

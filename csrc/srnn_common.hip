@@ -33,7 +33,7 @@ static int dispatch(int op, const SrnnCfg* c, const SrnnArgs* a) {
 
 extern "C" {
 
-int srnn_abi_version() { return 6; }
+int srnn_abi_version() { return 7; }
 
 const char* srnn_last_error() { return srnn::g_err.c_str(); }
 

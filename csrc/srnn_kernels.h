@@ -60,10 +60,39 @@ SRNN_HD int32_t atomic_add_i32(int32_t* p, int32_t v) {
 #define SAMP_STRIDE 1
 #endif
 
+SRNN_HD int32_t atomic_or_i32(int32_t* p, int32_t v) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return atomicOr(p, v);
+#else
+  return __atomic_fetch_or(p, v, __ATOMIC_RELAXED);
+#endif
+}
+
+// rank owning global slot g under the contiguous sharding lo_r = floor(r * N / R)
+SRNN_HD int32_t shard_of(int64_t g, int64_t n_total, int32_t world) {
+  int32_t r = (int32_t)((g * world) / n_total);
+  while (r + 1 < world && ((int64_t)(r + 1) * n_total) / world <= g) ++r;
+  while (r > 0 && ((int64_t)r * n_total) / world > g) --r;
+  return r;
+}
+
+// init key of the particle born in slot g at generation `gen` (rank-count invariant)
+SRNN_HD uint64_t respawn_key(int32_t gen, int64_t g) {
+  return (1ull << 62) | ((uint64_t)(uint32_t)gen << 32) | (uint64_t)g;
+}
+
 template <class Net>
 struct Item {
   static constexpr int P = Net::P;
   static constexpr int PP = Net::PP;
+  static constexpr int XW = PP + 4;  // exchange row: weights + (slot, gen, -, -)
+
+  // generation-start row of global slot g: local table (W2, this rank's rows) or the
+  // exchange receive buffer for slots of other ranks
+  SRNN_HD static const float* row_of(const SrnnArgs& a, int64_t g) {
+    if (a.world <= 1 || (g >= a.lo && g < a.lo + a.n)) return a.W2 + (g - a.lo) * PP;
+    return a.recvbuf + (int64_t)a.rmap[g] * XW;
+  }
 
   SRNN_HD static void load(const float* __restrict__ row, float* __restrict__ w) {
     const float4* r4 = reinterpret_cast<const float4*>(row);
@@ -262,13 +291,51 @@ struct Item {
     decision(a, i, gen_of(a), at, te);
     if (a.i32a) a.i32a[i] = at;
     if (a.i32b) a.i32b[i] = te;
+    const bool i_local = i >= a.lo && i < a.lo + a.n;
     if (at >= a.lo && at < a.lo + a.n) {
 #if defined(__HIP_DEVICE_COMPILE__)
       a.i32f[i] = atomicExch(a.i32e + (at - a.lo), (int32_t)i);
 #else
       a.i32f[i] = __atomic_exchange_n(a.i32e + (at - a.lo), (int32_t)i, __ATOMIC_RELAXED);
 #endif
+    } else if (a.world > 1 && at >= 0 && i_local) {
+      // my particle attacks a victim owned by another rank: ship my row there
+      atomic_or_i32(a.need + (i - a.lo), 1 << shard_of(at, a.n_total, a.world));
     }
+    if (a.world > 1 && te >= a.lo && te < a.lo + a.n && !i_local) {
+      // a remote learner picked one of my particles as teacher
+      atomic_or_i32(a.need + (te - a.lo), 1 << shard_of(i, a.n_total, a.world));
+    }
+  }
+
+  // sharded soup: copy local row j to every rank that needs it this generation
+  SRNN_HD static void soup_pack(const SrnnArgs& a, int64_t j) {
+    int32_t m = a.need[j];
+    if (!m) return;
+    a.need[j] = 0;
+    const int32_t gen = gen_of(a);
+    const float* src = a.W2 + j * PP;
+    while (m) {
+      const int r = __builtin_ctz((unsigned)m);
+      m &= m - 1;
+      const int32_t pos = atomic_add_i32(a.sendcnt + r, 1);
+      if (pos >= a.cap) {
+        atomic_or_i32(a.ovf, 1);
+        continue;
+      }
+      float* dst = a.sendbuf + ((int64_t)r * a.cap + pos) * XW;
+      const float4* s4 = reinterpret_cast<const float4*>(src);
+      float4* d4 = reinterpret_cast<float4*>(dst);
+#pragma unroll
+      for (int q = 0; q < PP / 4; ++q) d4[q] = s4[q];
+      int32_t tag[4] = {(int32_t)(a.lo + j), gen, 0, 0};
+      d4[PP / 4] = *reinterpret_cast<float4*>(tag);
+    }
+  }
+  // sharded soup: received row k -> rmap[slot]; rows of older generations are ignored
+  SRNN_HD static void soup_unpack(const SrnnArgs& a, int64_t k) {
+    const int32_t* tag = reinterpret_cast<const int32_t*>(a.recvbuf + k * XW + PP);
+    if (tag[1] == gen_of(a)) a.rmap[tag[0]] = (int32_t)k;
   }
 
   // Synchronous (Jacobi) generation for local row j: every read is from the
@@ -276,7 +343,7 @@ struct Item {
   SRNN_HD static void soup_evolve(const SrnnCfg& c, const SrnnArgs& a, int64_t j, float4* samp, uint8_t* perm) {
     const int64_t g = a.lo + j;
     float w[P], f[P], o[P];
-    load(a.W2 + g * PP, w);
+    load(a.W2 + j * PP, w);
     const uint64_t uid = uid_of(a, j);
     const int32_t gen = gen_of(a);
     ApplyCtx x = actx(a, c, uid, (uint32_t)gen * 1024u, perm);
@@ -289,7 +356,7 @@ struct Item {
       for (int32_t r = head; r >= 0; r = a.i32f[r]) best = (r > last && r < best) ? r : best;
       if (best == INT_MAX) break;
       last = best;
-      load(a.W2 + (int64_t)best * PP, f);
+      load(row_of(a, best), f);
       Net::apply(f, w, o, x);
       x.ctr += 1;
       copy(w, o);
@@ -314,7 +381,7 @@ struct Item {
     float loss = 0.f;
     // 2. learn_from a teacher (its generation-start weights)
     if (te >= 0) {
-      load(a.W2 + (int64_t)te * PP, f);
+      load(row_of(a, te), f);
       for (int e = 0; e < a.severity; ++e) loss = Net::train_epoch(w, f, tc);
       act = A_LEARN_FROM;
       cp = te;
@@ -330,6 +397,7 @@ struct Item {
     int8_t rs = 0;
     if ((a.flags & 2) && is_diverged<P>(w)) rs = 1;
     else if ((a.flags & 4) && is_zero<P>(w, a.eps)) rs = 2;
+    if (rs && (a.flags & 32)) Net::init(w, rng(a), respawn_key(gen, g));  // newborn, uid assigned later
     store(a.W + j * PP, w);
     if (a.action) a.action[j] = act;
     if (a.counterpart) a.counterpart[j] = cp;
@@ -347,10 +415,8 @@ struct Item {
 
   SRNN_HD static void respawn(const SrnnArgs& a, int64_t j) {
     if (a.respawn[j] == 0) return;
-    uint64_t uid = (uint64_t)(a.uid_base[0] + (int64_t)a.i32d[j]);
-    a.uid_out[j] = (int64_t)uid;
     float w[P];
-    Net::init(w, rng(a), uid);
+    Net::init(w, rng(a), respawn_key(gen_of(a), a.lo + j));
     store(a.W + j * PP, w);
   }
 };
@@ -374,6 +440,11 @@ __global__ __launch_bounds__(TB) void k_op(SrnnCfg c, SrnnArgs a) {
   if constexpr (OP == OP_SOUP_DECIDE) {
     if (i < a.n_total) I::soup_decide(a, i);
     return;
+  } else if constexpr (OP == OP_SOUP_UNPACK) {
+    if (i == 0)
+      for (int r = 0; r < a.world; ++r) a.sendcnt[r] = 0;  // packing of this generation is complete
+    if (i < (int64_t)a.world * a.cap) I::soup_unpack(a, i);
+    return;
   } else if constexpr (OP == OP_CLASSIFY) {
     if (i < a.n) I::classify(c, a, i, perm);  // histogram: k_classify_count
     return;
@@ -387,6 +458,7 @@ __global__ __launch_bounds__(TB) void k_op(SrnnCfg c, SrnnArgs a) {
     else if constexpr (OP == OP_PERTURB) I::perturb(c, a, i, samp, perm);
     else if constexpr (OP == OP_RESPAWN) I::respawn(a, i);
     else if constexpr (OP == OP_VARY_RUN) I::vary_run(c, a, i, samp, perm);
+    else if constexpr (OP == OP_SOUP_PACK) I::soup_pack(a, i);
   }
 }
 
@@ -439,11 +511,15 @@ __global__ __launch_bounds__(TBC) void k_classify_count(SrnnCfg c, SrnnArgs a) {
   }
   __syncthreads();
   if (threadIdx.x < 5 && s_cnt[threadIdx.x]) atomicAdd(a.counts + threadIdx.x, (uint64_t)s_cnt[threadIdx.x]);
+  if (a.flags & 64) {  // respawns of this generation (sharded soup: uid prefix)
+    unsigned long long m = __ballot(i < a.n && a.respawn[i] != 0);
+    if ((threadIdx.x & 63) == 0 && m) atomicAdd(a.counts + 5, (uint64_t)__popcll(m));
+  }
 }
 
 template <class Net, int OP>
 int launch(const SrnnCfg& c, const SrnnArgs& a) {
-  int64_t items = (OP == OP_SOUP_DECIDE) ? a.n_total : a.n;
+  int64_t items = (OP == OP_SOUP_DECIDE) ? a.n_total : (OP == OP_SOUP_UNPACK) ? (int64_t)a.world * a.cap : a.n;
   if (items <= 0) return 0;
   int64_t blocks = (items + TB - 1) / TB;
   if (blocks > 0x7fffffffLL) {
@@ -473,7 +549,9 @@ template <class Net, int OP>
 int host_run(const SrnnCfg& c, const SrnnArgs& a) {
   using I = Item<Net>;
   constexpr int P = Net::P;
-  int64_t items = (OP == OP_SOUP_DECIDE) ? a.n_total : a.n;
+  int64_t items = (OP == OP_SOUP_DECIDE) ? a.n_total : (OP == OP_SOUP_UNPACK) ? (int64_t)a.world * a.cap : a.n;
+  if (OP == OP_SOUP_UNPACK)
+    for (int r = 0; r < a.world; ++r) a.sendcnt[r] = 0;
   if (OP == OP_CLASSIFY && a.counts) {
     uint64_t local[5] = {0, 0, 0, 0, 0};
     std::vector<int8_t> ks((size_t)items);
@@ -483,6 +561,8 @@ int host_run(const SrnnCfg& c, const SrnnArgs& a) {
     });
     for (int64_t i = 0; i < items; ++i) local[ks[(size_t)i]]++;
     for (int q = 0; q < 5; ++q) a.counts[q] += local[q];
+    if (a.flags & 64)
+      for (int64_t i = 0; i < items; ++i) a.counts[5] += a.respawn[i] != 0;
     return 0;
   }
   host_parallel(items, [&](int64_t i) {
@@ -499,6 +579,8 @@ int host_run(const SrnnCfg& c, const SrnnArgs& a) {
     else if constexpr (OP == OP_SOUP_EVOLVE) I::soup_evolve(c, a, i, samp, perm);
     else if constexpr (OP == OP_RESPAWN) I::respawn(a, i);
     else if constexpr (OP == OP_VARY_RUN) I::vary_run(c, a, i, samp, perm);
+    else if constexpr (OP == OP_SOUP_PACK) I::soup_pack(a, i);
+    else if constexpr (OP == OP_SOUP_UNPACK) I::soup_unpack(a, i);
   });
   return 0;
 }
@@ -540,7 +622,7 @@ __global__ __launch_bounds__(TBR) void k_respawn_seq(SrnnCfg c, SrnnArgs a) {
         const int64_t r = b * TB + bit;
         a.uid_out[r] = k;
         float w[Net::P];
-        Net::init(w, I::rng(a), (uint64_t)k);
+        Net::init(w, I::rng(a), respawn_key(I::gen_of(a), a.lo + r));
         I::store(a.W + r * Net::PP, w);
         ++k;
       }
@@ -570,7 +652,7 @@ int respawn_seq(const SrnnCfg& c, const SrnnArgs& a) {
     if (a.respawn[i] == 0) continue;
     a.uid_out[i] = k;
     float w[Net::P];
-    Net::init(w, Item<Net>::rng(a), (uint64_t)k);
+    Net::init(w, Item<Net>::rng(a), respawn_key(Item<Net>::gen_of(a), a.lo + i));
     Item<Net>::store(a.W + i * Net::PP, w);
     ++k;
   }
@@ -578,6 +660,96 @@ int respawn_seq(const SrnnCfg& c, const SrnnArgs& a) {
   if (a.gen_ptr) ((int32_t*)a.gen_ptr)[0] += 1;
   if (a.counts)
     for (int q = 0; q < 5; ++q) a.counts[q] = 0;
+  return 0;
+}
+
+// Sharded soup: uids of this generation's newborns.  The gathered per-rank stats give
+// the respawn counts of lower ranks (globally sequential uids, reference S13) and the
+// global census; the 64-bit respawn ballots of the evolve waves give the local order.
+// Also advances next_uid (*uid_base), the generation counter and zeroes counts[0..5].
+template <class Net>
+__global__ __launch_bounds__(TBR) void k_uid_assign(SrnnCfg c, SrnnArgs a) {
+  __shared__ int32_t s_cnt[TBR];
+  __shared__ int64_t s_prefix, s_total;
+  if (threadIdx.x == 0) {
+    int64_t pre = 0, tot = 0;
+    for (int r = 0; r < a.world; ++r) {
+      const int64_t k = a.stats[r * 6 + 5];
+      if (r < a.rank) pre += k;
+      tot += k;
+    }
+    s_prefix = pre;
+    s_total = tot;
+    if (a.census)
+      for (int q = 0; q < 5; ++q) {
+        int64_t v = 0;
+        for (int r = 0; r < a.world; ++r) v += a.stats[r * 6 + q];
+        a.census[q] = v;
+      }
+  }
+  const unsigned long long* masks = reinterpret_cast<const unsigned long long*>(a.i32c);
+  const int64_t nb = (a.n + TB - 1) / TB;
+  const int64_t ch = (nb + TBR - 1) / TBR;
+  const int64_t b0 = (int64_t)threadIdx.x * ch;
+  const int64_t b1 = b0 + ch < nb ? b0 + ch : nb;
+  int32_t cnt = 0;
+  for (int64_t b = b0; b < b1; ++b) cnt += __popcll(masks[b]);
+  s_cnt[threadIdx.x] = cnt;
+  __syncthreads();
+  for (int off = 1; off < TBR; off <<= 1) {
+    int32_t v = threadIdx.x >= off ? s_cnt[threadIdx.x - off] : 0;
+    __syncthreads();
+    s_cnt[threadIdx.x] += v;
+    __syncthreads();
+  }
+  const int64_t base = *(volatile const int64_t*)a.uid_base;
+  int64_t k = base + s_prefix + s_cnt[threadIdx.x] - cnt;
+  for (int64_t b = b0; b < b1 && cnt; ++b) {
+    unsigned long long m = masks[b];
+    while (m) {
+      const int bit = __ffsll((long long)m) - 1;
+      m &= m - 1;
+      a.uid_out[b * TB + bit] = k++;
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    ((int64_t*)a.uid_base)[0] = base + s_total;
+    if (a.gen_ptr) ((int32_t*)a.gen_ptr)[0] += 1;
+  }
+  if (a.counts && threadIdx.x < 6) a.counts[threadIdx.x] = 0;
+}
+
+template <class Net>
+int uid_assign(const SrnnCfg& c, const SrnnArgs& a) {
+  if (a.dev) {
+    hipLaunchKernelGGL((k_uid_assign<Net>), dim3(1), dim3(TBR), 0, (hipStream_t)a.stream, c, a);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) {
+      set_error(hipGetErrorString(e));
+      return -3;
+    }
+    return 0;
+  }
+  int64_t pre = 0, tot = 0;
+  for (int r = 0; r < a.world; ++r) {
+    const int64_t k = a.stats[r * 6 + 5];
+    if (r < a.rank) pre += k;
+    tot += k;
+  }
+  if (a.census)
+    for (int q = 0; q < 5; ++q) {
+      int64_t v = 0;
+      for (int r = 0; r < a.world; ++r) v += a.stats[r * 6 + q];
+      a.census[q] = v;
+    }
+  int64_t k = a.uid_base[0] + pre;
+  for (int64_t i = 0; i < a.n; ++i)
+    if (a.respawn[i]) a.uid_out[i] = k++;
+  ((int64_t*)a.uid_base)[0] += tot;
+  if (a.gen_ptr) ((int32_t*)a.gen_ptr)[0] += 1;
+  if (a.counts)
+    for (int q = 0; q < 6; ++q) a.counts[q] = 0;
   return 0;
 }
 
@@ -598,6 +770,9 @@ int run_net_op(int op, const SrnnCfg& c, const SrnnArgs& a) {
     case OP_PERTURB: return run_one<Net, OP_PERTURB>(c, a);
     case OP_SOUP_DECIDE: return run_one<Net, OP_SOUP_DECIDE>(c, a);
     case OP_RESPAWN_SEQ: return respawn_seq<Net>(c, a);
+    case OP_SOUP_PACK: return run_one<Net, OP_SOUP_PACK>(c, a);
+    case OP_SOUP_UNPACK: return run_one<Net, OP_SOUP_UNPACK>(c, a);
+    case OP_UID_ASSIGN: return uid_assign<Net>(c, a);
     case OP_SOUP_EVOLVE: return run_one<Net, OP_SOUP_EVOLVE>(c, a);
     case OP_RESPAWN: return run_one<Net, OP_RESPAWN>(c, a);
     case OP_VARY_RUN: return run_one<Net, OP_VARY_RUN>(c, a);

@@ -19,7 +19,7 @@ import threading
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libsrnn.so")
 CSRC = os.path.normpath(os.path.join(_HERE, "..", "..", "csrc"))
-ABI_VERSION = 6
+ABI_VERSION = 7
 
 OP_INIT = 0
 OP_APPLY = 1
@@ -34,11 +34,17 @@ OP_SOUP_EVOLVE = 9
 OP_SCAN = 10
 OP_RESPAWN = 11
 OP_VARY_RUN = 12
+OP_SOUP_PACK = 13
+OP_SOUP_UNPACK = 14
+OP_UID_ASSIGN = 15
 
 FLAG_SHUFFLE = 1
 FLAG_REMOVE_DIVERGENT = 2
 FLAG_REMOVE_ZERO = 4
 FLAG_FIX_SEC = 8
+FLAG_ROW_FLAGS = 16
+FLAG_RESPAWN_INLINE = 32
+FLAG_COUNT_RESPAWNS = 64
 
 
 class SrnnCfg(ctypes.Structure):
@@ -62,6 +68,9 @@ class SrnnArgs(ctypes.Structure):
         ("cls", _P), ("nsteps", _P), ("loss", _P), ("counts", _P),
         ("i32a", _P), ("i32b", _P), ("i32c", _P), ("i32d", _P), ("i32e", _P), ("i32f", _P),
         ("uid_out", _P), ("uid_base", _P), ("gen_ptr", _P), ("segment", ctypes.c_int64),
+        ("world", ctypes.c_int32), ("rank", ctypes.c_int32), ("cap", ctypes.c_int64),
+        ("sendbuf", _P), ("recvbuf", _P), ("need", _P), ("sendcnt", _P), ("rmap", _P), ("ovf", _P),
+        ("stats", _P), ("census", _P),
         ("action", _P), ("counterpart", _P), ("respawn", _P),
         ("temp", _P), ("temp_bytes", ctypes.c_int64),
         ("dev", ctypes.c_int32), ("pad1", ctypes.c_int32), ("stream", _P),

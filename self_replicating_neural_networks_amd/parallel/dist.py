@@ -68,6 +68,21 @@ class Dist:
                 o += sz
         return out
 
+    def all_to_all(self, out: torch.Tensor, inp: torch.Tensor):
+        """Equal-split all-to-all (RCCL over xGMI for nccl: direct peer links)."""
+        if self.enabled:
+            dist.all_to_all_single(out, inp, group=self.group)
+        else:
+            out.copy_(inp)
+        return out
+
+    def all_gather_into(self, out: torch.Tensor, local: torch.Tensor):
+        if self.enabled:
+            dist.all_gather_into_tensor(out, local, group=self.group)
+        else:
+            out.copy_(local)
+        return out
+
     def all_reduce_sum(self, t: torch.Tensor):
         if self.enabled:
             dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group)

@@ -1,30 +1,32 @@
-"""Device soup engine: one fused generation pipeline over a sharded population.
+"""Device soup engine: one fused generation pipeline over a (sharded) population.
 
 Replaces the per-particle Python loop of ``Soup.evolve`` (reference code/soup.py:51-87)
-with a *synchronous* (Jacobi) generation, computed for every particle at once:
+with a *synchronous* (Jacobi) generation computed for every particle at once.
 
-1. ``decide``  — every rank draws the decisions of every *global* slot from Philox keyed
-   by (seed, slot, generation), so pairings are known everywhere without exchanging
-   indices; attacks on local victims are counted.
-2. ``scan`` + ``fill`` — CSR list of attackers per local victim.
-3. ``evolve`` (fused kernel, lane per particle) — received attacks in ascending attacker
-   slot order using generation-start attacker weights, then ``learn_from_severity``
-   epochs on the teacher's generation-start samples, then ``train`` self-train epochs,
-   then divergence / zero respawn flags (reference :77-86).
-4. ``scan`` + ``respawn`` — new uids are globally sequential (reference S13): rank r's
-   first new uid = next_uid + sum of the respawn counts of ranks < r.
-5. all-gather of the new local rows into the global generation-start table of the next
-   generation (RCCL over xGMI with ``nccl``; gloo on CPU).
-6. optional ``classify`` + all-reduce of the 5-bin class histogram (reference
-   code/soup.py:89-103).
+Single rank (4 kernels, captured as hipGraphs):
 
-Differences from the sequential reference (documented in docs and tested
-statistically): particle k does not see the effects of particles < k within the same
-generation; every read is from the generation-start table.  ``Soup(mode="sequential")``
-provides the exact reference order for small populations.
+1. ``decide`` -- every global slot draws its decisions from Philox keyed by
+   (seed, slot, generation); attacks on local victims are linked into per-victim lists.
+2. ``evolve`` (fused, lane per particle) -- received attacks in ascending attacker-slot
+   order with generation-start attacker weights, ``learn_from_severity`` epochs on the
+   teacher's generation-start samples, ``train`` self-train epochs, divergence / zero
+   respawn flags (reference :77-86); each wave publishes a 64-bit respawn ballot.
+3. ``respawn`` (one workgroup) -- scans the ballots, assigns globally sequential uids
+   (reference S13), re-initialises the rows (init keyed by (generation, slot)), advances
+   next_uid and the generation counter.
+4. ``classify`` -- the per-generation census (reference code/soup.py:89-103).
 
-The per-generation work is graph-capturable (device generation counter, no host syncs),
-so ``capture()`` records one generation into a HIP graph that is replayed per evolve().
+Sharded over R ranks (one process per GPU, RCCL over xGMI): every rank recomputes every
+slot's decisions, so it knows which of its rows other ranks need (attackers of their
+victims, teachers of their learners): those rows -- ~(attack+learn rate)/R of a shard per
+peer -- go through ONE fixed-capacity all-to-all; the census plus each rank's respawn
+count go through ONE 48-byte all-gather, from which the uid prefix is computed on device.
+No weight table is replicated.  Results are bitwise independent of R
+(tests/test_dist_gloo.py).
+
+Differences from the sequential reference (tested statistically): particle k does not see
+the effects of particles < k within the same generation; every read is from the
+generation-start weights.  ``Soup(mode="sequential")`` keeps the exact reference order.
 """
 from __future__ import annotations
 
@@ -70,14 +72,26 @@ class SoupEngine:
             raise ValueError("population size must be a multiple of the sub-soup segment")
         dev, PP = self.device, spec.PP
         i32 = dict(dtype=torch.int32, device=dev)
+        # this rank's rows, ping-pong: generation t reads buf[p], writes buf[1-p]
+        self._bufs = [torch.zeros((self.n, PP), dtype=torch.float32, device=dev) for _ in range(2)]
+        self._p = 0
         if self.dist.enabled:
-            # generation-start table of every global row + this rank's output rows
-            self.table = torch.zeros((self.n_total, PP), dtype=torch.float32, device=dev)
-            self.next_rows = torch.zeros((self.n, PP), dtype=torch.float32, device=dev)
-        else:
-            # ping-pong pair: generation t reads buf[p], writes buf[1-p]
-            self._bufs = [torch.zeros((self.n, PP), dtype=torch.float32, device=dev) for _ in range(2)]
-            self._p = 0
+            # exchange of the generation-start rows that other ranks need (attackers of
+            # their victims, teachers of their learners): fixed-capacity all-to-all
+            R = self.dist.world
+            ar = max(float(self.params.get("attacking_rate", 0.1)), 0.0)
+            lr_ = max(float(self.params.get("learn_from_rate", 0.1)), 0.0)
+            mean = self.n * min(ar + lr_, 2.0) / R
+            self.cap = int(min(max(mean * 1.2 + 6.0 * mean ** 0.5 + 32, 32), max(self.n, 32)))
+            self.need = torch.zeros(self.n, **i32)
+            self.sendcnt = torch.zeros(R, **i32)
+            self.rmap = torch.zeros(self.n_total, **i32)
+            self.ovf = torch.zeros(1, **i32)
+            xw = PP + 4
+            self.sendbuf = torch.full((R * self.cap, xw), -1, **i32).view(torch.float32)
+            self.recvbuf = torch.full((R * self.cap, xw), -1, **i32).view(torch.float32)
+            self.stats_all = torch.zeros(R * 6, dtype=torch.int64, device=dev)
+            self.census = torch.zeros(5, dtype=torch.int64, device=dev)
         self.uid = torch.arange(self.lo, self.hi, dtype=torch.int64, device=dev)
         self.next_uid = torch.full((1,), self.n_total, dtype=torch.int64, device=dev)
         self.uid_base = torch.zeros(1, dtype=torch.int64, device=dev)
@@ -91,10 +105,7 @@ class SoupEngine:
         self.counterpart = torch.full((self.n,), -1, dtype=torch.int64, device=dev)
         self.loss = torch.zeros(self.n, dtype=torch.float32, device=dev)
         self.respawn = torch.zeros(self.n, dtype=torch.int8, device=dev)
-        self.counts = torch.zeros(5, dtype=torch.int64, device=dev)
-        self.rank_totals = torch.zeros(self.dist.world, **i32)
-        tb = _lib.scan_temp_bytes(self.n) if dev.type == "cuda" and self.dist.enabled else 0
-        self.scan_temp = torch.empty(max(tb, 16), dtype=torch.uint8, device=dev)
+        self.counts = torch.zeros(6, dtype=torch.int64, device=dev)  # classes[5] + respawns
         self.cfg = _lib.make_cfg(spec)
         self.recorder = None
         self.stats = False          # classify + all-reduce every generation
@@ -108,23 +119,20 @@ class SoupEngine:
             local[:, : w.shape[1]] = w[self.lo:self.hi].to(dev)
         else:
             K.init_rows(spec, local, self.uid, self.seed)
-        if self.dist.enabled:
-            self.next_rows.copy_(local)
-            self.dist.all_gather_rows(self.table, self.next_rows, self.n_total)
 
     # ------------------------------------------------------------------ views
     @property
     def table_in(self) -> torch.Tensor:
-        """Generation-start table read by the next generation."""
-        return self.table if self.dist.enabled else self._bufs[self._p]
+        """This rank's generation-start rows read by the next generation."""
+        return self._bufs[self._p]
 
     @property
     def rows_out(self) -> torch.Tensor:
-        return self.next_rows if self.dist.enabled else self._bufs[1 - self._p]
+        return self._bufs[1 - self._p]
 
     def local_rows(self) -> torch.Tensor:
         """Current weights of this rank's particles ([n, PP])."""
-        return self.table[self.lo:self.hi] if self.dist.enabled else self._bufs[self._p]
+        return self._bufs[self._p]
 
     @property
     def eps(self) -> float:
@@ -163,37 +171,55 @@ class SoupEngine:
         a.W = _p(self.rows_out)
         a.uid = _p(self.uid)
         a.i32e, a.i32f = _p(self.head), _p(self.next_att)
-        a.i32c, a.i32d = _p(self.flags32), _p(self.off)
+        a.i32c = _p(self.flags32)
         a.action, a.counterpart, a.loss, a.respawn = _p(self.action), _p(self.counterpart), _p(self.loss), _p(self.respawn)
-        a.temp, a.temp_bytes = _p(self.scan_temp), self.scan_temp.numel()
         a.uid_out = _p(self.uid)
-        if self.dist.enabled:
-            a.flags |= 16  # per-row respawn flags for the scan (else per-block counts)
         # head[] is -1 on entry: set at construction, reset by the evolve kernel after use
-        _lib.run(_lib.OP_SOUP_DECIDE, spec, a, cfg)
-        _lib.run(_lib.OP_SOUP_EVOLVE, spec, a, cfg)
-        if record and self.recorder is not None:
-            self.recorder.on_evolved(self)
-        if self.dist.enabled:
-            # globally sequential uids: rank r starts after the respawns of ranks < r
-            _lib.run(_lib.OP_SCAN, spec, a, cfg)
-            self.dist.all_gather_scalar(self.rank_totals, self.off[self.n:self.n + 1])
-            prefix = self.rank_totals[: self.dist.rank].sum().to(torch.int64)
-            self.uid_base.copy_(self.next_uid + prefix)
-            self.next_uid.add_(self.rank_totals.sum().to(torch.int64))
-            a.uid_base = _p(self.uid_base)
-            _lib.run(_lib.OP_RESPAWN, spec, a, cfg)
-            self.gen_dev.add_(1)
-            self.dist.all_gather_rows(self.table, self.next_rows, self.n_total)
-        else:
+        if not self.dist.enabled:
+            _lib.run(_lib.OP_SOUP_DECIDE, spec, a, cfg)
+            _lib.run(_lib.OP_SOUP_EVOLVE, spec, a, cfg)
+            if record and self.recorder is not None:
+                self.recorder.on_evolved(self)
             a.uid_base = _p(self.next_uid)  # updated in place, gen_dev advanced by the kernel
             a.counts = _p(self.counts)       # zeroed by the kernel for the census below
             _lib.run(_lib.OP_RESPAWN_SEQ, spec, a, cfg)
             self._p = 1 - self._p
-        if self.stats:
-            # per-generation fixpoint-fraction statistics (reference Soup.count, code/soup.py:89-103)
-            self.classify_local(self.stats_with_sec, zero=self.dist.enabled)
-            self.dist.all_reduce_sum(self.counts)
+            if self.stats:
+                # per-generation fixpoint-fraction statistics (reference Soup.count, code/soup.py:89-103)
+                self.classify_local(self.stats_with_sec, zero=False)
+            return
+        # ---- sharded: decide -> pack -> all-to-all -> unpack -> evolve -> census+respawns -> all-gather -> uids
+        d = self.dist
+        a.world, a.rank, a.cap = d.world, d.rank, self.cap
+        a.need, a.sendcnt, a.rmap, a.ovf = _p(self.need), _p(self.sendcnt), _p(self.rmap), _p(self.ovf)
+        a.sendbuf, a.recvbuf = _p(self.sendbuf), _p(self.recvbuf)
+        a.stats, a.census = _p(self.stats_all), _p(self.census)
+        a.counts, a.uid_base = _p(self.counts), _p(self.next_uid)
+        _lib.run(_lib.OP_SOUP_DECIDE, spec, a, cfg)
+        _lib.run(_lib.OP_SOUP_PACK, spec, a, cfg)
+        d.all_to_all(self.recvbuf, self.sendbuf)
+        _lib.run(_lib.OP_SOUP_UNPACK, spec, a, cfg)
+        inline = not (record and self.recorder is not None)
+        if inline:
+            a.flags |= _lib.FLAG_RESPAWN_INLINE
+        _lib.run(_lib.OP_SOUP_EVOLVE, spec, a, cfg)
+        a.flags &= ~_lib.FLAG_RESPAWN_INLINE
+        if not inline:
+            self.recorder.on_evolved(self)
+            _lib.run(_lib.OP_RESPAWN, spec, a, cfg)
+        # census of the new generation + this rank's respawn count -> every rank
+        ca = self._args()
+        ca.n, ca.eps = self.n, self.eps
+        ca.flags = (_lib.FLAG_FIX_SEC if self.stats_with_sec else 0) | _lib.FLAG_COUNT_RESPAWNS
+        ca.W, ca.counts, ca.respawn, ca.uid = _p(self.rows_out), _p(self.counts), _p(self.respawn), _p(self.uid)
+        ca.ctr = 0x7FFFFFF0
+        _lib.run(_lib.OP_CLASSIFY, spec, ca, cfg)
+        d.all_gather_into(self.stats_all, self.counts)
+        _lib.run(_lib.OP_UID_ASSIGN, spec, a, cfg)
+        self._p = 1 - self._p
+
+    def exchange_overflowed(self) -> bool:
+        return bool(self.dist.enabled and int(self.ovf.item()) != 0)
 
     def classify_local(self, with_sec: bool = True, zero: bool = True):
         if zero:
@@ -204,9 +230,17 @@ class SoupEngine:
 
     def count(self, with_sec: bool = True) -> Dict[str, int]:
         """Global class histogram of the current particles (all-reduced)."""
+        if self.exchange_overflowed():
+            raise RuntimeError("soup row exchange overflowed its capacity: results are invalid")
         self.classify_local(with_sec)
-        self.dist.all_reduce_sum(self.counts)
-        return counts_dict(self.counts.cpu())
+        c = self.counts[:5].clone()
+        self.dist.all_reduce_sum(c)
+        return counts_dict(c.cpu())
+
+    def last_census(self) -> Dict[str, int]:
+        """Census recorded by the last generation (stats / sharded path)."""
+        c = self.census if self.dist.enabled else self.counts[:5]
+        return counts_dict(c.cpu())
 
     def evolve(self, iterations: int = 1, record: bool = False):
         for _ in range(iterations):

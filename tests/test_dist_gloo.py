@@ -36,13 +36,14 @@ def _worker(rank, world, port, spec_json, out_dir):
         e.stats = True
         e.evolve(GENS)
         counts = e.count()
+        assert not e.exchange_overflowed()
         np.savez(os.path.join(out_dir, f"r{rank}.npz"), W=e.local_rows().numpy(), uid=e.uid.numpy(),
                  next_uid=e.next_uid.numpy(), counts=np.array([counts[k] for k in sorted(counts)]))
     finally:
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("world", [2, 3, 4])
 def test_sharded_soup_equals_single_rank(tmp_path, world):
     spec = ArchSpec.weightwise(2, 2)
     ref = SoupEngine(spec, N_TOTAL, PARAMS, device="cpu", seed=21)
@@ -58,3 +59,25 @@ def test_sharded_soup_equals_single_rank(tmp_path, world):
     for p in parts:
         assert int(p["next_uid"][0]) == int(ref.next_uid[0])
         assert list(p["counts"]) == [ref_counts[k] for k in sorted(ref_counts)]
+
+
+def _worker_hi(rank, world, port, out_dir):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        p = dict(PARAMS, attacking_rate=0.9, learn_from_rate=0.9, learn_from_severity=2)
+        e = SoupEngine(ArchSpec.aggregating(4, 2, 2), 160, p, device="cpu", seed=5, dist=Dist(rank, world, 0, None))
+        e.evolve(4)
+        assert not e.exchange_overflowed()
+        np.save(os.path.join(out_dir, f"h{rank}.npy"), e.local_rows().numpy())
+    finally:
+        dist.destroy_process_group()
+
+
+def test_sharded_high_rates_aggregating(tmp_path):
+    p = dict(PARAMS, attacking_rate=0.9, learn_from_rate=0.9, learn_from_severity=2)
+    ref = SoupEngine(ArchSpec.aggregating(4, 2, 2), 160, p, device="cpu", seed=5)
+    ref.evolve(4)
+    mp.start_processes(_worker_hi, args=(4, _free_port(), str(tmp_path)), nprocs=4, start_method="spawn", join=True)
+    W = np.concatenate([np.load(os.path.join(tmp_path, f"h{r}.npy")) for r in range(4)])
+    assert np.array_equal(W, ref.local_rows().numpy(), equal_nan=True)
