@@ -81,8 +81,9 @@ class SoupEngine:
             R = self.dist.world
             ar = max(float(self.params.get("attacking_rate", 0.1)), 0.0)
             lr_ = max(float(self.params.get("learn_from_rate", 0.1)), 0.0)
-            mean = self.n * min(ar + lr_, 2.0) / R
-            self.cap = int(min(max(mean * 1.2 + 6.0 * mean ** 0.5 + 32, 32), max(self.n, 32)))
+            n_max = -(-self.n_total // R)  # identical on every rank (buffers must match)
+            mean = n_max * min(ar + lr_, 2.0) / R
+            self.cap = int(min(max(mean * 1.2 + 6.0 * mean ** 0.5 + 32, 32), max(n_max, 32)))
             self.need = torch.zeros(self.n, **i32)
             self.sendcnt = torch.zeros(R, **i32)
             self.rmap = torch.zeros(self.n_total, **i32)
