@@ -112,6 +112,7 @@ class SoupEngine:
         self.stats = False          # classify + all-reduce every generation
         self.stats_with_sec = True
         self._graphs = None
+        self._arg_cache = {}
         # initial particles: uids 0..n_total-1, keyed init (identical for any rank count)
         local = self.local_rows()
         if weights is not None:
@@ -165,8 +166,15 @@ class SoupEngine:
         return a
 
     # ------------------------------------------------------------------ one generation
-    def _generation(self, record: bool = False):
-        spec, cfg = self.spec, self.cfg
+    def _gen_args(self):
+        """Populated argument blocks of one generation (cached per parity / stream /
+        params: building ctypes structs every generation costs host time)."""
+        stream = torch.cuda.current_stream(self.device).cuda_stream if self.device.type == "cuda" else 0
+        key = (self._p, stream, tuple(sorted((k, str(v)) for k, v in self.params.items())), self.stats_with_sec,
+               self.lr, self.shuffle)
+        hit = self._arg_cache.get(key)
+        if hit is not None:
+            return hit
         a = self._args()
         a.W2 = _p(self.table_in)
         a.W = _p(self.rows_out)
@@ -175,14 +183,33 @@ class SoupEngine:
         a.i32c = _p(self.flags32)
         a.action, a.counterpart, a.loss, a.respawn = _p(self.action), _p(self.counterpart), _p(self.loss), _p(self.respawn)
         a.uid_out = _p(self.uid)
+        a.counts, a.uid_base = _p(self.counts), _p(self.next_uid)
+        ca = None
+        if self.dist.enabled:
+            d = self.dist
+            a.world, a.rank, a.cap = d.world, d.rank, self.cap
+            a.need, a.sendcnt, a.rmap, a.ovf = _p(self.need), _p(self.sendcnt), _p(self.rmap), _p(self.ovf)
+            a.sendbuf, a.recvbuf = _p(self.sendbuf), _p(self.recvbuf)
+            a.stats, a.census = _p(self.stats_all), _p(self.census)
+            ca = self._args()
+            ca.n, ca.eps = self.n, self.eps
+            ca.flags = (_lib.FLAG_FIX_SEC if self.stats_with_sec else 0) | _lib.FLAG_COUNT_RESPAWNS
+            ca.W, ca.counts, ca.respawn, ca.uid = _p(self.rows_out), _p(self.counts), _p(self.respawn), _p(self.uid)
+            ca.ctr = 0x7FFFFFF0
+        self._arg_cache[key] = (a, ca, a.flags)
+        return self._arg_cache[key]
+
+    def _generation(self, record: bool = False):
+        spec, cfg = self.spec, self.cfg
+        a, ca, flags = self._gen_args()
+        a.flags = flags
         # head[] is -1 on entry: set at construction, reset by the evolve kernel after use
         if not self.dist.enabled:
             _lib.run(_lib.OP_SOUP_DECIDE, spec, a, cfg)
             _lib.run(_lib.OP_SOUP_EVOLVE, spec, a, cfg)
             if record and self.recorder is not None:
                 self.recorder.on_evolved(self)
-            a.uid_base = _p(self.next_uid)  # updated in place, gen_dev advanced by the kernel
-            a.counts = _p(self.counts)       # zeroed by the kernel for the census below
+            # uids from next_uid (advanced in place), generation counter, census histogram zeroed
             _lib.run(_lib.OP_RESPAWN_SEQ, spec, a, cfg)
             self._p = 1 - self._p
             if self.stats:
@@ -191,29 +218,18 @@ class SoupEngine:
             return
         # ---- sharded: decide -> pack -> all-to-all -> unpack -> evolve -> census+respawns -> all-gather -> uids
         d = self.dist
-        a.world, a.rank, a.cap = d.world, d.rank, self.cap
-        a.need, a.sendcnt, a.rmap, a.ovf = _p(self.need), _p(self.sendcnt), _p(self.rmap), _p(self.ovf)
-        a.sendbuf, a.recvbuf = _p(self.sendbuf), _p(self.recvbuf)
-        a.stats, a.census = _p(self.stats_all), _p(self.census)
-        a.counts, a.uid_base = _p(self.counts), _p(self.next_uid)
         _lib.run(_lib.OP_SOUP_DECIDE, spec, a, cfg)
         _lib.run(_lib.OP_SOUP_PACK, spec, a, cfg)
         d.all_to_all(self.recvbuf, self.sendbuf)
         _lib.run(_lib.OP_SOUP_UNPACK, spec, a, cfg)
         inline = not (record and self.recorder is not None)
-        if inline:
-            a.flags |= _lib.FLAG_RESPAWN_INLINE
+        a.flags = flags | (_lib.FLAG_RESPAWN_INLINE if inline else 0)
         _lib.run(_lib.OP_SOUP_EVOLVE, spec, a, cfg)
-        a.flags &= ~_lib.FLAG_RESPAWN_INLINE
+        a.flags = flags
         if not inline:
             self.recorder.on_evolved(self)
             _lib.run(_lib.OP_RESPAWN, spec, a, cfg)
         # census of the new generation + this rank's respawn count -> every rank
-        ca = self._args()
-        ca.n, ca.eps = self.n, self.eps
-        ca.flags = (_lib.FLAG_FIX_SEC if self.stats_with_sec else 0) | _lib.FLAG_COUNT_RESPAWNS
-        ca.W, ca.counts, ca.respawn, ca.uid = _p(self.rows_out), _p(self.counts), _p(self.respawn), _p(self.uid)
-        ca.ctr = 0x7FFFFFF0
         _lib.run(_lib.OP_CLASSIFY, spec, ca, cfg)
         d.all_gather_into(self.stats_all, self.counts)
         _lib.run(_lib.OP_UID_ASSIGN, spec, a, cfg)
