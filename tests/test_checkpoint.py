@@ -1,0 +1,71 @@
+"""Native checkpoint / exact resume / re-sharding."""
+import os
+import socket
+
+import numpy as np
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from self_replicating_neural_networks_amd.arch import ArchSpec
+from self_replicating_neural_networks_amd.io import checkpoint as C
+from self_replicating_neural_networks_amd.parallel.dist import Dist
+from self_replicating_neural_networks_amd.population import Population
+from self_replicating_neural_networks_amd.soup_engine import SoupEngine
+
+PARAMS = dict(attacking_rate=0.2, learn_from_rate=0.2, train=2, remove_divergent=True, remove_zero=True, epsilon=1e-4)
+
+
+def test_soup_resume_is_exact(tmp_path):
+    spec = ArchSpec.weightwise(2, 2)
+    a = SoupEngine(spec, 300, PARAMS, seed=9)
+    a.evolve(6)
+    b = SoupEngine(spec, 300, PARAMS, seed=9)
+    b.evolve(3)
+    C.save_engine(b, str(tmp_path / "ck"))
+    c = C.load_engine(str(tmp_path / "ck"))
+    c.evolve(3)
+    assert torch.equal(a.uid, c.uid) and int(a.next_uid) == int(c.next_uid)
+    assert torch.equal(a.local_rows(), c.local_rows())
+    assert c.time == 6
+
+
+def test_population_roundtrip(tmp_path):
+    p = Population(ArchSpec.recurrent(2, 2), 50, seed=3)
+    p.train(3)
+    C.save_population(p, str(tmp_path / "p"))
+    q = C.load_population(str(tmp_path / "p"))
+    assert np.array_equal(p.W.numpy(), q.W.numpy(), equal_nan=True)  # diverged rows hold NaN
+    assert torch.equal(p.uid, q.uid) and q.ctr == p.ctr
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _resume_worker(rank, world, port, ck, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        e = C.load_engine(ck, dist=Dist(rank, world, 0, None))
+        e.evolve(3)
+        np.save(os.path.join(out, f"r{rank}.npy"), e.local_rows().numpy())
+    finally:
+        dist.destroy_process_group()
+
+
+def test_checkpoint_reshards_1_to_2(tmp_path):
+    spec = ArchSpec.weightwise(2, 2)
+    a = SoupEngine(spec, 201, PARAMS, seed=4)
+    a.evolve(6)
+    b = SoupEngine(spec, 201, PARAMS, seed=4)
+    b.evolve(3)
+    ck = str(tmp_path / "ck")
+    C.save_engine(b, ck)
+    mp.start_processes(_resume_worker, args=(2, _port(), ck, str(tmp_path)), nprocs=2, start_method="spawn", join=True)
+    W = np.concatenate([np.load(os.path.join(tmp_path, f"r{r}.npy")) for r in range(2)])
+    assert np.array_equal(W, a.local_rows().numpy(), equal_nan=True)
