@@ -51,10 +51,11 @@ def main():
     ap.add_argument("--epochs", type=int, default=20)
     ap.add_argument("--only", default="")
     ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--big-n", type=int, default=1_000_000, help="population of the wave-per-particle nets")
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     specs = [ArchSpec.weightwise(2, 2), ArchSpec.aggregating(4, 2, 2), ArchSpec.recurrent(2, 2),
-             ArchSpec.fft(4, 2, 2), ArchSpec.weightwise(4, 3)]
+             ArchSpec.fft(4, 2, 2), ArchSpec.weightwise(4, 3), ArchSpec.aggregating(4, 10, 3)]
     res = []
     for spec in specs:
         name = f"{spec.kind}({spec.aggregates},{spec.width},{spec.depth})"
@@ -66,6 +67,14 @@ def main():
         K.init_rows(spec, W, uid, 1)
         W0 = W.clone()
         out = torch.zeros_like(W)
+        big = spec.P > 64
+        if big and args.big_n:
+            n = args.big_n
+            uid = torch.arange(n, dtype=torch.int64, device=dev)
+            W = torch.zeros(n, spec.PP, device=dev)
+            K.init_rows(spec, W, uid, 1)
+            W0 = W.clone()
+            out = torch.zeros_like(W)
         r = {"arch": name, "P": spec.P, "n": n}
         r["init_us"] = timeit(lambda: K.init_rows(spec, W, uid, 1), args.reps)
 
@@ -77,6 +86,8 @@ def main():
         r["self_apply_per_s"] = n * 100 / (t * 1e-6)
         r["self_apply_tflops"] = n * 100 * flops_apply(spec) / (t * 1e-6) / 1e12
         r["apply_attack_us"] = timeit(lambda: K.apply(spec, W0, out, idx_f=torch.roll(uid, 1)), args.reps)
+        # HBM traffic of one attack: attacker + target rows read, output row written
+        r["apply_attack_GBps"] = 3 * n * spec.PP * 4 / (r["apply_attack_us"] * 1e-6) / 1e9
         r["classify_us"] = timeit(lambda: K.classify(spec, W0, 1e-4), args.reps)
 
         def train():
@@ -86,6 +97,10 @@ def main():
         r["train_us"] = t
         steps = spec.P if spec.kind == "weightwise" else 1
         r["sgd_steps_per_s"] = n * args.epochs * steps / (t * 1e-6)
+        if big:
+            res.append(r)
+            print(json.dumps(r), flush=True)
+            continue
         eng = SoupEngine(spec, n, dict(train=args.epochs, remove_divergent=True, remove_zero=True, epsilon=1e-4),
                          device=dev, seed=5)
         r["soup_gen_us"] = timeit(lambda: eng.evolve(1), args.reps)

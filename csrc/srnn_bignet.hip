@@ -1,0 +1,483 @@
+// srnn_bignet.hip — wave-per-particle kernels for Aggregating nets too large for the
+// lane-per-particle register kernels (north-star config: Aggregating(4, 10, 3), P = 280,
+// 1M particles; reference code/network.py:292-439).
+//
+// One 64-lane wave owns one particle: the row is streamed HBM -> LDS with float4 loads
+// (coalesced, 1120 B per particle), chunk means are wave reductions (fp64, like the
+// reference's python-float sums), every dense layer is computed by lanes j < out reading
+// column j of the kernel from LDS, and the output row is written back coalesced.
+//
+// Self-application to convergence runs on a 4-number state: after one application an
+// aggregating net's weights are constant over each aggregation chunk (no shuffle), the
+// chunk means of such a vector are exactly those constants (double sums of identical
+// floats), so every further application is a function of the A chunk values only --
+// bit-identical to re-evaluating the expanded weights, with no memory traffic until the
+// final write.  MFMA does not apply: each particle is a GEMV chain with its own weights
+// (M = 1), see docs/kernels.md.
+#include "srnn_kernels.h"
+
+namespace srnn {
+
+constexpr int BW = 4;            // waves (particles) per block
+constexpr int TBB = 64 * BW;
+
+template <int A_, int W_, int D_>
+struct AggBig {
+  static constexpr int A = A_, W = W_, D = D_;
+  using Net = MLP<A, W, D, A>;
+  static constexpr int P = Net::P;
+  static constexpr int PP = (P + 3) & ~3;
+  static constexpr int NL = D + 1;
+  static constexpr int CS = P / A;
+  static_assert(P / CS == A, "invalid aggregation (SURVEY S4)");
+  static constexpr int MAXW = (A > W ? A : W);
+  static constexpr int rows(int l) { return l == 0 ? A : W; }
+  static constexpr int cols(int l) { return l == D ? A : W; }
+  static constexpr int off(int l) { return Net::off(l); }
+  __device__ static int chunk(int k) { int c = k / CS; return c < A ? c : A - 1; }
+};
+
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) {
+    float u = __shfl_xor(v, o, 64);
+    v = u > v ? u : v;
+  }
+  return v;
+}
+__device__ __forceinline__ bool wave_all(bool b) { return __ballot(!b) == 0ull; }
+
+// per-wave LDS scratch: weights [PP] + vectors for backprop
+template <class T>
+struct WaveLds {
+  float w[T::PP];
+  float act[T::NL][T::MAXW];  // input of every layer
+  float st[T::MAXW];          // propagated step
+  float st2[T::MAXW];
+};
+
+template <class T>
+__device__ void load_row(float* __restrict__ sw, const float* __restrict__ row, int lane) {
+  const float4* r4 = reinterpret_cast<const float4*>(row);
+  float4* s4 = reinterpret_cast<float4*>(sw);
+  for (int q = lane; q < T::PP / 4; q += 64) s4[q] = r4[q];
+}
+template <class T>
+__device__ void store_state(float* __restrict__ row, const float* s, int lane) {
+  // expand the chunk state into the full row
+  float4* r4 = reinterpret_cast<float4*>(row);
+  for (int q = lane; q < T::PP / 4; q += 64) {
+    float v[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int k = 4 * q + e;
+      float x = 0.f;
+#pragma unroll
+      for (int c = 0; c < T::A; ++c) x = (k < T::P && T::chunk(k) == c) ? s[c] : x;
+      v[e] = x;
+    }
+    r4[q] = make_float4(v[0], v[1], v[2], v[3]);
+  }
+}
+template <class T>
+__device__ void store_lds(float* __restrict__ row, const float* __restrict__ sw, int lane) {
+  float4* r4 = reinterpret_cast<float4*>(row);
+  const float4* s4 = reinterpret_cast<const float4*>(sw);
+  for (int q = lane; q < T::PP / 4; q += 64) r4[q] = s4[q];
+}
+
+// chunk aggregation of an LDS row (aggregator: 0 mean, 1 max, 2 max with the reference quirk)
+template <class T>
+__device__ void aggregate_lds(const float* __restrict__ sw, float* g, int lane, int aggregator) {
+#pragma unroll
+  for (int c = 0; c < T::A; ++c) {
+    const int b = c * T::CS, e = (c == T::A - 1) ? T::P : b + T::CS;
+    if (aggregator == 0) {
+      double acc = 0.0;
+      for (int k = b + lane; k < e; k += 64) acc += (double)sw[k];
+      g[c] = (float)(wave_sum(acc) / (double)(e - b));
+    } else {
+      // sequential semantics of the reference loop (first element seeds the max)
+      float m = sw[b];
+      if (lane == 0)
+        for (int k = b; k < e; ++k) {
+          const float v = sw[k];
+          m = (aggregator == 1) ? (v > m ? v : m) : ((v > m && v != 0.0f) ? v : m);
+        }
+      g[c] = __shfl(m, 0, 64);
+    }
+  }
+}
+
+// y = x . K for the layer at LDS offset `o` (rows I, cols O); x replicated in all lanes,
+// y returned replicated.  Lane j < O accumulates column j in the kernels' order.
+template <int I, int O>
+__device__ void dense_lds(const float* __restrict__ k, const float* x, float* y, int lane) {
+  float acc = 0.f;
+  if (lane < O) {
+    acc = x[0] * k[lane];
+#pragma unroll
+    for (int i = 1; i < I; ++i) acc = fmaf(x[i], k[i * O + lane], acc);
+  }
+#pragma unroll
+  for (int j = 0; j < O; ++j) y[j] = __shfl(acc, j, 64);
+}
+
+// same with piecewise-constant weights: K[i][j] = s[chunk(o + i*O + j)]
+template <class T, int I, int O>
+__device__ void dense_state(int o, const float* s, const float* x, float* y, int lane) {
+  float acc = 0.f;
+  if (lane < O) {
+    float kv = 0.f;
+    int f = o + lane;
+    int c = T::chunk(f);
+#pragma unroll
+    for (int q = 0; q < T::A; ++q) kv = (c == q) ? s[q] : kv;
+    acc = x[0] * kv;
+#pragma unroll
+    for (int i = 1; i < I; ++i) {
+      f = o + i * O + lane;
+      c = T::chunk(f);
+#pragma unroll
+      for (int q = 0; q < T::A; ++q) kv = (c == q) ? s[q] : kv;
+      acc = fmaf(x[i], kv, acc);
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < O; ++j) y[j] = __shfl(acc, j, 64);
+}
+
+template <class T>
+__device__ void mlp_lds(const float* __restrict__ sw, const float* g, float* h, int lane) {
+  float x[T::MAXW], y[T::MAXW];
+#pragma unroll
+  for (int i = 0; i < T::A; ++i) x[i] = g[i];
+  dense_lds<T::A, T::W>(sw + T::off(0), x, y, lane);
+#pragma unroll
+  for (int l = 1; l < T::D; ++l) {
+#pragma unroll
+    for (int i = 0; i < T::W; ++i) x[i] = y[i];
+    dense_lds<T::W, T::W>(sw + T::off(l), x, y, lane);
+  }
+#pragma unroll
+  for (int i = 0; i < T::W; ++i) x[i] = y[i];
+  dense_lds<T::W, T::A>(sw + T::off(T::D), x, h, lane);
+}
+
+template <class T>
+__device__ void mlp_state(const float* s, const float* g, float* h, int lane) {
+  float x[T::MAXW], y[T::MAXW];
+#pragma unroll
+  for (int i = 0; i < T::A; ++i) x[i] = g[i];
+  dense_state<T, T::A, T::W>(T::off(0), s, x, y, lane);
+#pragma unroll
+  for (int l = 1; l < T::D; ++l) {
+#pragma unroll
+    for (int i = 0; i < T::W; ++i) x[i] = y[i];
+    dense_state<T, T::W, T::W>(T::off(l), s, x, y, lane);
+  }
+#pragma unroll
+  for (int i = 0; i < T::W; ++i) x[i] = y[i];
+  dense_state<T, T::W, T::A>(T::off(T::D), s, x, h, lane);
+}
+
+template <class T>
+__device__ bool finite_all(const float* v) {
+  bool ok = true;
+#pragma unroll
+  for (int i = 0; i < T::A; ++i) ok &= finitef(v[i]);
+  return ok;
+}
+template <class T>
+__device__ bool close_all(const float* a, const float* b, float eps) {
+  bool ok = true;
+#pragma unroll
+  for (int i = 0; i < T::A; ++i) ok &= !(fabsf(a[i] - b[i]) >= eps);
+  return ok;
+}
+template <class T>
+__device__ bool lds_finite(const float* sw, int lane) {
+  bool ok = true;
+  for (int k = lane; k < T::P; k += 64) ok &= finitef(sw[k]);
+  return wave_all(ok);
+}
+// |state-expanded(s) - lds weights| < eps for every weight
+template <class T>
+__device__ bool lds_close_state(const float* sw, const float* s, float eps, int lane) {
+  bool ok = true;
+  for (int k = lane; k < T::P; k += 64) {
+    const int c = T::chunk(k);
+    float v = 0.f;
+#pragma unroll
+    for (int q = 0; q < T::A; ++q) v = (c == q) ? s[q] : v;
+    ok &= !(fabsf(v - sw[k]) >= eps);
+  }
+  return wave_all(ok);
+}
+template <class T>
+__device__ bool lds_zero(const float* sw, float eps, int lane) {
+  bool ok = true;
+  for (int k = lane; k < T::P; k += 64) ok &= (-eps <= sw[k]) && (sw[k] <= eps);
+  return wave_all(ok);
+}
+
+// classification of general (LDS) weights: f = f_W(W) = expand(h1), f2 = expand(h2)
+template <class T>
+__device__ int8_t classify_lds(const float* sw, float eps, bool with_sec, int aggregator, int lane) {
+  if (!lds_finite<T>(sw, lane)) return C_DIVERGENT;
+  float g[T::A], h1[T::A], h2[T::A];
+  aggregate_lds<T>(sw, g, lane, aggregator);
+  mlp_lds<T>(sw, g, h1, lane);
+  if (finite_all<T>(h1) && lds_close_state<T>(sw, h1, eps, lane))
+    return lds_zero<T>(sw, eps, lane) ? C_FIX_ZERO : C_FIX_OTHER;
+  if (with_sec) {
+    mlp_lds<T>(sw, h1, h2, lane);  // aggregate(expand(h1)) == h1 exactly
+    if (finite_all<T>(h2) && lds_close_state<T>(sw, h2, eps, lane)) return C_FIX_SEC;
+  }
+  return C_OTHER;
+}
+// classification of chunk-constant weights expand(s)
+template <class T>
+__device__ int8_t classify_state(const float* s, float eps, bool with_sec, int lane) {
+  if (!finite_all<T>(s)) return C_DIVERGENT;
+  float h1[T::A], h2[T::A];
+  mlp_state<T>(s, s, h1, lane);
+  if (finite_all<T>(h1) && close_all<T>(h1, s, eps)) {
+    bool zero = true;
+#pragma unroll
+    for (int i = 0; i < T::A; ++i) zero &= (-eps <= s[i]) && (s[i] <= eps);
+    return zero ? C_FIX_ZERO : C_FIX_OTHER;
+  }
+  if (with_sec) {
+    mlp_state<T>(s, h1, h2, lane);
+    if (finite_all<T>(h2) && close_all<T>(h2, s, eps)) return C_FIX_SEC;
+  }
+  return C_OTHER;
+}
+
+// one SGD step on x = y = aggregate(own or teacher weights); weights in LDS (updated)
+template <class T>
+__device__ float train_step_lds(float* sw, WaveLds<T>& L, const float* g, float lr, int lane) {
+  // forward keeping every layer input
+  float x[T::MAXW], y[T::MAXW];
+#pragma unroll
+  for (int i = 0; i < T::A; ++i) x[i] = g[i];
+#pragma unroll
+  for (int l = 0; l <= T::D; ++l) {
+    if (lane < T::rows(l)) {
+      float v = x[0];
+#pragma unroll
+      for (int i = 1; i < T::MAXW; ++i) v = (lane == i) ? x[i] : v;
+      L.act[l][lane] = v;
+    }
+    if (l == 0) dense_lds<T::A, T::W>(sw + T::off(0), x, y, lane);
+    else if (l < T::D) dense_lds<T::W, T::W>(sw + T::off(l), x, y, lane);
+    else dense_lds<T::W, T::A>(sw + T::off(T::D), x, y, lane);
+#pragma unroll
+    for (int i = 0; i < T::MAXW; ++i) x[i] = y[i];
+  }
+  // loss mean over A, step = -lr * dL/dh
+  float loss = 0.f;
+  float st = 0.f;
+#pragma unroll
+  for (int k = 0; k < T::A; ++k) {
+    const float e = x[k] - g[k];
+    loss += e * e;
+    if (lane == k) st = -lr * (2.0f * e / (float)T::A);
+  }
+  if (lane < T::A) L.st[lane] = st;
+  __builtin_amdgcn_wave_barrier();
+  // backward: st_in = K . st_out (pre-update K), K += act (x) st_out
+#pragma unroll
+  for (int l = T::D; l >= 0; --l) {
+    const int R = T::rows(l), Cc = T::cols(l);
+    float* k = sw + T::off(l);
+    if (l > 0 && lane < R) {
+      float acc = k[lane * Cc] * L.st[0];
+      for (int j = 1; j < Cc; ++j) acc = fmaf(k[lane * Cc + j], L.st[j], acc);
+      L.st2[lane] = acc;
+    }
+    __builtin_amdgcn_wave_barrier();
+    for (int f = lane; f < R * Cc; f += 64) {
+      const int i = f / Cc, j = f - i * Cc;
+      k[f] = fmaf(L.act[l][i], L.st[j], k[f]);
+    }
+    __builtin_amdgcn_wave_barrier();
+    if (l > 0 && lane < R) L.st[lane] = L.st2[lane];
+    __builtin_amdgcn_wave_barrier();
+  }
+  return loss / (float)T::A;
+}
+
+// ------------------------------------------------------------------------------ kernel
+template <class T, int OP>
+__global__ __launch_bounds__(TBB) void k_big(SrnnCfg c, SrnnArgs a) {
+  __shared__ WaveLds<T> lds[BW];
+  __shared__ uint32_t s_cnt[5];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int64_t p = (int64_t)blockIdx.x * BW + wv;  // particle (wave-uniform)
+  WaveLds<T>& L = lds[wv];
+  if (OP == OP_CLASSIFY && threadIdx.x < 5) s_cnt[threadIdx.x] = 0;
+  __syncthreads();
+  int8_t cls = -1;
+  if (p < a.n) {
+    if constexpr (OP == OP_APPLY) {
+      const int64_t fi = a.idx_f ? a.idx_f[p] : p, ti = a.idx_t ? a.idx_t[p] : p, oi = a.idx_o ? a.idx_o[p] : p;
+      // aggregate the target, run the attacker's net
+      load_row<T>(L.w, a.W + ti * T::PP, lane);
+      __builtin_amdgcn_wave_barrier();
+      float g[T::A], h[T::A];
+      aggregate_lds<T>(L.w, g, lane, c.aggregator);
+      __builtin_amdgcn_wave_barrier();
+      load_row<T>(L.w, a.W + fi * T::PP, lane);
+      __builtin_amdgcn_wave_barrier();
+      mlp_lds<T>(L.w, g, h, lane);
+      store_state<T>(a.W2 + oi * T::PP, h, lane);
+    } else if constexpr (OP == OP_RUN_FIXPOINT || OP == OP_CLASSIFY) {
+      load_row<T>(L.w, a.W + p * T::PP, lane);
+      __builtin_amdgcn_wave_barrier();
+      const bool with_sec = (a.flags & 8) != 0;
+      int s = 0;
+      float st[T::A];
+      bool compressed = false;
+      if constexpr (OP == OP_RUN_FIXPOINT) {
+        float g[T::A], h[T::A];
+        for (; s < a.steps; ++s) {
+          if (!compressed) {
+            if (a.early_exit && !lds_finite<T>(L.w, lane)) break;
+            aggregate_lds<T>(L.w, g, lane, c.aggregator);
+            mlp_lds<T>(L.w, g, h, lane);
+            if (a.early_exit && finite_all<T>(h) && lds_close_state<T>(L.w, h, a.eps, lane)) break;
+          } else {
+            if (a.early_exit && !finite_all<T>(st)) break;
+            mlp_state<T>(st, st, h, lane);
+            if (a.early_exit && finite_all<T>(h) && close_all<T>(h, st, a.eps)) break;
+          }
+#pragma unroll
+          for (int i = 0; i < T::A; ++i) st[i] = h[i];
+          compressed = true;
+        }
+        if (compressed) store_state<T>(a.W + p * T::PP, st, lane);
+        if (a.nsteps && lane == 0) a.nsteps[p] = s;
+      }
+      cls = compressed ? classify_state<T>(st, a.eps, with_sec, lane)
+                       : classify_lds<T>(L.w, a.eps, with_sec, c.aggregator, lane);
+      if (a.cls && lane == 0) a.cls[p] = cls;
+    } else if constexpr (OP == OP_TRAIN || OP == OP_LEARN) {
+      load_row<T>(L.w, a.W + p * T::PP, lane);
+      float g[T::A];
+      if constexpr (OP == OP_LEARN) {
+        // teacher samples are fixed: aggregate the teacher row once (through L.act as scratch)
+        const float* tr = a.W2 + (a.idx_t ? a.idx_t[p] : p) * T::PP;
+        double acc[T::A];
+#pragma unroll
+        for (int q = 0; q < T::A; ++q) acc[q] = 0.0;
+        for (int k = lane; k < T::P; k += 64) {
+          const int ch = T::chunk(k);
+#pragma unroll
+          for (int q = 0; q < T::A; ++q) acc[q] += (ch == q) ? (double)tr[k] : 0.0;
+        }
+#pragma unroll
+        for (int q = 0; q < T::A; ++q) {
+          const int b = q * T::CS, e = (q == T::A - 1) ? T::P : b + T::CS;
+          g[q] = (float)(wave_sum(acc[q]) / (double)(e - b));
+        }
+      }
+      __builtin_amdgcn_wave_barrier();
+      float loss = 0.f;
+      for (int e = 0; e < a.epochs; ++e) {
+        if constexpr (OP == OP_TRAIN) aggregate_lds<T>(L.w, g, lane, c.aggregator);
+        loss = train_step_lds<T>(L.w, L, g, a.lr, lane);
+      }
+      __builtin_amdgcn_wave_barrier();
+      store_lds<T>(a.W + p * T::PP, L.w, lane);
+      if (a.loss && lane == 0) a.loss[p] = loss;
+    }
+  }
+  if constexpr (OP == OP_CLASSIFY) {
+    if (a.counts && lane == 0 && cls >= 0) atomicAdd(&s_cnt[cls], 1u);
+    __syncthreads();
+    if (a.counts && threadIdx.x < 5 && s_cnt[threadIdx.x]) atomicAdd(a.counts + threadIdx.x, (uint64_t)s_cnt[threadIdx.x]);
+  }
+}
+
+// lane-per-particle ops writing straight to global memory (init, perturb)
+template <class T, int OP>
+__global__ __launch_bounds__(256) void k_big_lane(SrnnCfg c, SrnnArgs a) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= a.n) return;
+  float* row = a.W + i * T::PP;
+  const Rng rng{(uint32_t)a.seed, (uint32_t)(a.seed >> 32)};
+  const uint64_t uid = a.uid ? (uint64_t)a.uid[i] : (uint64_t)i;
+  if constexpr (OP == OP_INIT) {
+    glorot_fill(row, 0, T::A, T::W, rng, uid);
+    for (int l = 1; l < T::D; ++l) glorot_fill(row, T::off(l), T::W, T::W, rng, uid);
+    glorot_fill(row, T::off(T::D), T::W, T::A, rng, uid);
+    for (int k = T::P; k < T::PP; ++k) row[k] = 0.f;
+  } else {
+    for (int k = 0; k < T::P; ++k) {
+      U4 u = rng.draw(uid, a.ctr * 1024u + (uint32_t)k, P_PERTURB);
+      double mag = (double)u01(u.y) * (double)a.eps;
+      row[k] = u01(u.x) < 0.5f ? (float)((double)row[k] + mag) : (float)((double)row[k] - mag);
+    }
+  }
+}
+
+template <class T>
+int big_run(int op, const SrnnCfg& c, const SrnnArgs& a) {
+  if (!a.dev) {
+    set_error("wave-per-particle nets run on the GPU only (use a smaller shape on the host)");
+    return -5;
+  }
+  if (c.shuffler != 0 && op != OP_INIT && op != OP_PERTURB && op != OP_TRAIN && op != OP_LEARN) {
+    set_error("wave-per-particle aggregating nets: shuffle_random is not supported");
+    return -5;
+  }
+  hipStream_t st = (hipStream_t)a.stream;
+  if (a.n <= 0) return 0;
+  const unsigned gw = (unsigned)((a.n + BW - 1) / BW), gl = (unsigned)((a.n + 255) / 256);
+  switch (op) {
+    case OP_INIT: hipLaunchKernelGGL((k_big_lane<T, OP_INIT>), dim3(gl), dim3(256), 0, st, c, a); break;
+    case OP_PERTURB: hipLaunchKernelGGL((k_big_lane<T, OP_PERTURB>), dim3(gl), dim3(256), 0, st, c, a); break;
+    case OP_APPLY: hipLaunchKernelGGL((k_big<T, OP_APPLY>), dim3(gw), dim3(TBB), 0, st, c, a); break;
+    case OP_RUN_FIXPOINT: hipLaunchKernelGGL((k_big<T, OP_RUN_FIXPOINT>), dim3(gw), dim3(TBB), 0, st, c, a); break;
+    case OP_CLASSIFY: hipLaunchKernelGGL((k_big<T, OP_CLASSIFY>), dim3(gw), dim3(TBB), 0, st, c, a); break;
+    case OP_TRAIN: hipLaunchKernelGGL((k_big<T, OP_TRAIN>), dim3(gw), dim3(TBB), 0, st, c, a); break;
+    case OP_LEARN: hipLaunchKernelGGL((k_big<T, OP_LEARN>), dim3(gw), dim3(TBB), 0, st, c, a); break;
+    default: set_error("op not supported for wave-per-particle nets"); return -5;
+  }
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) {
+    set_error(hipGetErrorString(e));
+    return -3;
+  }
+  return 0;
+}
+
+}  // namespace srnn
+
+using AGGB_4_10_3 = srnn::AggBig<4, 10, 3>;
+using AGGB_4_8_2 = srnn::AggBig<4, 8, 2>;
+using AGGB_4_16_2 = srnn::AggBig<4, 16, 2>;
+
+#define SRNN_TRY_BIG(T, W_, D_, A_)                                              \
+  if (c->width == (W_) && c->depth == (D_) && c->aggregates == (A_)) {           \
+    if (c->p != T::P || c->pp != T::PP) {                                        \
+      srnn::set_error("layout mismatch (p/pp) for instantiated shape");          \
+      return -4;                                                                 \
+    }                                                                            \
+    if (op < 0) return 0;                                                        \
+    return srnn::big_run<T>(op, *c, *a);                                         \
+  }
+
+extern "C" int srnn_dispatch_aggbig(int op, const SrnnCfg* c, const SrnnArgs* a) {
+  SRNN_TRY_BIG(AGGB_4_10_3, 10, 3, 4)
+  SRNN_TRY_BIG(AGGB_4_8_2, 8, 2, 4)
+  SRNN_TRY_BIG(AGGB_4_16_2, 16, 2, 4)
+  return 1;
+}

@@ -13,6 +13,7 @@ extern "C" int srnn_dispatch_ww(int op, const SrnnCfg* c, const SrnnArgs* a);
 extern "C" int srnn_dispatch_agg(int op, const SrnnCfg* c, const SrnnArgs* a);
 extern "C" int srnn_dispatch_rnn(int op, const SrnnCfg* c, const SrnnArgs* a);
 extern "C" int srnn_dispatch_fft(int op, const SrnnCfg* c, const SrnnArgs* a);
+extern "C" int srnn_dispatch_aggbig(int op, const SrnnCfg* c, const SrnnArgs* a);
 
 __global__ void k_scan_tail(int32_t* out, const int32_t* in, int64_t n) {
   // out[0] = 0 (inclusive scan was written to out+1)
@@ -24,7 +25,10 @@ __global__ void k_scan_tail(int32_t* out, const int32_t* in, int64_t n) {
 static int dispatch(int op, const SrnnCfg* c, const SrnnArgs* a) {
   switch (c->kind) {
     case 0: return srnn_dispatch_ww(op, c, a);
-    case 1: return srnn_dispatch_agg(op, c, a);
+    case 1: {
+      int r = srnn_dispatch_agg(op, c, a);
+      return r == 1 ? srnn_dispatch_aggbig(op, c, a) : r;
+    }
     case 2: return srnn_dispatch_rnn(op, c, a);
     case 3: return srnn_dispatch_fft(op, c, a);
     default: srnn::set_error("unknown network kind"); return -1;

@@ -356,6 +356,7 @@ struct TrainCtx {
   uint8_t* perm;     // >= P bytes (only for P > 16)
   bool shuffle;
   int stride;        // device: threads per block (slot-major, lane fastest: conflict-free b128)
+  int aggregator;    // aggregating nets: samples come from the configured aggregator
 };
 
 struct ApplyCtx {
@@ -524,7 +525,7 @@ struct Aggregating {
   // one sample x = y = aggregated weights (reference :414-417); loss mean over A outputs
   SRNN_HD static float train_epoch(float* __restrict__ w, const float* __restrict__ s, TrainCtx& c) {
     float g[A], acts[Net::NACT], h[A], gy[A];
-    aggregate<P, A>(s, g, 0);
+    aggregate<P, A>(s, g, c.aggregator);  // compute_samples -> get_aggregated_weights (network.py:414)
     Net::forward(w, g, acts, h);
     float loss = 0.f;
 #pragma unroll

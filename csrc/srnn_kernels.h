@@ -237,7 +237,7 @@ struct Item {
   }
 
   // ---------------------------------------------------------------- train / learn_from
-  SRNN_HD static void train(const SrnnCfg&, const SrnnArgs& a, int64_t i, float4* samp, uint8_t* perm, bool learn) {
+  SRNN_HD static void train(const SrnnCfg& c, const SrnnArgs& a, int64_t i, float4* samp, uint8_t* perm, bool learn) {
     float w[P], s[P];
     load(a.W + i * PP, w);
     if (learn) load(a.W2 + (a.idx_t ? a.idx_t[i] : i) * PP, s);
@@ -250,6 +250,7 @@ struct Item {
     tc.perm = perm;
     tc.shuffle = (a.flags & 1) != 0;
     tc.stride = SAMP_STRIDE;
+    tc.aggregator = c.aggregator;
     float loss = 0.f;
     for (int e = 0; e < a.epochs; ++e) {
       if (!learn) copy(s, w);
@@ -378,6 +379,7 @@ struct Item {
     tc.perm = perm;
     tc.shuffle = (a.flags & 1) != 0;
     tc.stride = SAMP_STRIDE;
+    tc.aggregator = c.aggregator;
     float loss = 0.f;
     // 2. learn_from a teacher (its generation-start weights)
     if (te >= 0) {

@@ -318,7 +318,7 @@ def train_epoch(spec: ArchSpec, w, s, lr=0.01, shuffle=True, seed=0, uids=None, 
             _mlp_backward_update(mats, acts, (np.float32(2.0) * e)[:, None], lr)
         return _flat(spec, mats), loss / np.float32(spec.P)
     if spec.kind in ("aggregating", "fft"):
-        g = aggregate(spec, s, "mean") if spec.kind == "aggregating" else fft_reduce(spec, s)
+        g = aggregate(spec, s, spec.aggregator) if spec.kind == "aggregating" else fft_reduce(spec, s)
         h, acts = _mlp_forward(mats, g)
         e = h - g
         loss = np.sum(e * e, axis=1) / np.float32(spec.aggregates)

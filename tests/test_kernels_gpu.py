@@ -118,3 +118,51 @@ def test_soup_graph_replay_matches_eager(cuda):
     torch.cuda.synchronize()
     assert torch.equal(a.uid, b.uid)
     assert torch.allclose(a.local_rows(), b.local_rows(), equal_nan=True)
+
+
+BIG = [ArchSpec.aggregating(4, 10, 3), ArchSpec.aggregating(4, 8, 2, aggregator="max")]
+
+
+@pytest.mark.parametrize("spec", BIG, ids=lambda s: f"agg-{s.aggregates}-{s.width}-{s.depth}-{s.aggregator}")
+def test_wave_per_particle_aggregating_vs_oracle(cuda, spec):
+    """Aggregating(4, 10, 3) (P = 280, north-star config) runs wave-per-particle."""
+    n, seed = 3000, 21
+    uid = torch.arange(n, dtype=torch.int64, device=cuda)
+    W = torch.zeros(n, spec.PP, device=cuda)
+    K.init_rows(spec, W, uid, seed)
+    ow = O.init(spec, uid.cpu().numpy(), seed)
+    assert _rel(W[:, :spec.P].cpu().numpy(), ow) < 1e-5
+    out = torch.zeros_like(W)
+    idx_f = torch.roll(torch.arange(n, device=cuda), 1).contiguous()
+    K.apply(spec, W, out, idx_f=idx_f)
+    oo = O.apply(spec, np.roll(ow, 1, axis=0), ow)
+    assert _rel(out[:, :spec.P].cpu().numpy(), oo) < 1e-5
+    # multi-step self-application on the chunk state == step-by-step oracle
+    W5 = W.clone()
+    cls, nsteps, _ = K.run_fixpoint(spec, W5, 5, 1e-4, early_exit=False)
+    w = ow.copy()
+    with np.errstate(all="ignore"):
+        for _ in range(5):
+            w = O.apply(spec, w, w)
+    assert _rel(W5[:, :spec.P].cpu().numpy(), w) < 1e-4
+    assert (cls.cpu().numpy() == O.classify(spec, w, 1e-4)).mean() > 0.99
+    c2, counts = K.classify(spec, W, 1e-4)
+    assert (c2.cpu().numpy() == O.classify(spec, ow, 1e-4)).mean() > 0.99 and int(counts.sum()) == n
+    W2 = W.clone()
+    loss = K.train(spec, W2, epochs=3, lr=0.01)
+    tw = ow.copy()
+    for _ in range(3):
+        tw, tl = O.train_epoch(spec, tw, tw, 0.01, False)
+    assert _rel(W2[:, :spec.P].cpu().numpy(), tw) < 1e-4
+    assert _rel(loss.cpu().numpy(), tl) < 1e-4
+
+
+def test_big_aggregating_applying_statistics(cuda):
+    """applying-fixpoints on the north-star shape: the chunk-state kernel runs 100 steps."""
+    spec = ArchSpec.aggregating(4, 10, 3)
+    n = 100_000
+    W = torch.zeros(n, spec.PP, device=cuda)
+    K.init_rows(spec, W, torch.arange(n, dtype=torch.int64, device=cuda), 3)
+    cls, _, _ = K.run_fixpoint(spec, W, 100, 1e-4, early_exit=False)
+    c = np.bincount(cls.cpu().numpy(), minlength=5)
+    assert c.sum() == n and c[0] + c[1] > 0.9 * n  # divergent or collapsed to zero
