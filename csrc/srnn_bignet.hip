@@ -35,6 +35,7 @@ struct AggBig {
   static constexpr int cols(int l) { return l == D ? A : W; }
   static constexpr int off(int l) { return Net::off(l); }
   __device__ static int chunk(int k) { int c = k / CS; return c < A ? c : A - 1; }
+  static constexpr int chunk_c(int k) { return k / CS < A ? k / CS : A - 1; }
 };
 
 __device__ __forceinline__ double wave_sum(double v) {
@@ -56,6 +57,7 @@ __device__ __forceinline__ bool wave_all(bool b) { return __ballot(!b) == 0ull; 
 template <class T>
 struct WaveLds {
   float w[T::PP];
+  float t[T::PP];             // second row (attack target)
   float act[T::NL][T::MAXW];  // input of every layer
   float st[T::MAXW];          // propagated step
   float st2[T::MAXW];
@@ -328,14 +330,21 @@ __global__ __launch_bounds__(TBB) void k_big(SrnnCfg c, SrnnArgs a) {
   if (p < a.n) {
     if constexpr (OP == OP_APPLY) {
       const int64_t fi = a.idx_f ? a.idx_f[p] : p, ti = a.idx_t ? a.idx_t[p] : p, oi = a.idx_o ? a.idx_o[p] : p;
-      // aggregate the target, run the attacker's net
-      load_row<T>(L.w, a.W + ti * T::PP, lane);
+      // both rows in flight at once, then aggregate the target and run the attacker's net
+      {
+        const float4* f4 = reinterpret_cast<const float4*>(a.W + fi * T::PP);
+        const float4* t4 = reinterpret_cast<const float4*>(a.W + ti * T::PP);
+        float4* sw4 = reinterpret_cast<float4*>(L.w);
+        float4* st4 = reinterpret_cast<float4*>(L.t);
+        for (int q = lane; q < T::PP / 4; q += 64) {
+          const float4 x = f4[q], y = t4[q];
+          sw4[q] = x;
+          st4[q] = y;
+        }
+      }
       __builtin_amdgcn_wave_barrier();
       float g[T::A], h[T::A];
-      aggregate_lds<T>(L.w, g, lane, c.aggregator);
-      __builtin_amdgcn_wave_barrier();
-      load_row<T>(L.w, a.W + fi * T::PP, lane);
-      __builtin_amdgcn_wave_barrier();
+      aggregate_lds<T>(L.t, g, lane, c.aggregator);
       mlp_lds<T>(L.w, g, h, lane);
       store_state<T>(a.W2 + oi * T::PP, h, lane);
     } else if constexpr (OP == OP_RUN_FIXPOINT || OP == OP_CLASSIFY) {
@@ -406,6 +415,138 @@ __global__ __launch_bounds__(TBB) void k_big(SrnnCfg c, SrnnArgs a) {
   }
 }
 
+// ------------------------------------------------------------------ run_fixpoint, 3 phases
+// phase 1 (wave per particle): step-0 checks and the first application on the full row;
+// phase 2 (lane per particle): every further step on the A-float chunk state, with the
+//   chunk index of every weight a compile-time constant (fully unrolled MLP);
+// phase 3 (wave per particle): expand the final state into the row, coalesced.
+// temp = state float[n][A] followed by flags int8[n] (1 = continues in phase 2).
+
+template <class T, int L>
+__device__ __forceinline__ void dense_state_lane(const float* s, const float* x, float* y) {
+  constexpr int I = T::rows(L), O = T::cols(L), OFF = T::off(L);
+#pragma unroll
+  for (int j = 0; j < O; ++j) {
+    float acc = x[0] * s[T::chunk_c(OFF + j)];
+#pragma unroll
+    for (int i = 1; i < I; ++i) acc = fmaf(x[i], s[T::chunk_c(OFF + i * O + j)], acc);
+    y[j] = acc;
+  }
+}
+template <class T, int L>
+__device__ __forceinline__ void mlp_state_lane_rec(const float* s, float* x) {
+  float y[T::MAXW];
+  dense_state_lane<T, L>(s, x, y);
+#pragma unroll
+  for (int j = 0; j < T::cols(L); ++j) x[j] = y[j];
+  if constexpr (L < T::D) mlp_state_lane_rec<T, L + 1>(s, x);
+}
+template <class T>
+__device__ __forceinline__ void mlp_state_lane(const float* s, const float* g, float* h) {
+  float x[T::MAXW];
+#pragma unroll
+  for (int i = 0; i < T::A; ++i) x[i] = g[i];
+  mlp_state_lane_rec<T, 0>(s, x);
+#pragma unroll
+  for (int i = 0; i < T::A; ++i) h[i] = x[i];
+}
+
+template <class T>
+__global__ __launch_bounds__(TBB) void k_big_fix1(SrnnCfg c, SrnnArgs a) {
+  __shared__ WaveLds<T> lds[BW];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int64_t p = (int64_t)blockIdx.x * BW + wv;
+  if (p >= a.n) return;
+  WaveLds<T>& L = lds[wv];
+  float* state = reinterpret_cast<float*>(a.temp);
+  int8_t* flag = reinterpret_cast<int8_t*>(state + a.n * T::A);
+  load_row<T>(L.w, a.W + p * T::PP, lane);
+  __builtin_amdgcn_wave_barrier();
+  const bool with_sec = (a.flags & 8) != 0;
+  bool stop = a.steps <= 0;
+  float g[T::A], h[T::A];
+  if (!stop && a.early_exit && !lds_finite<T>(L.w, lane)) stop = true;
+  if (!stop) {
+    aggregate_lds<T>(L.w, g, lane, c.aggregator);
+    mlp_lds<T>(L.w, g, h, lane);
+    if (a.early_exit && finite_all<T>(h) && lds_close_state<T>(L.w, h, a.eps, lane)) stop = true;
+  }
+  if (stop) {  // no step taken: the row is unchanged, classify the general weights
+    const int8_t k = classify_lds<T>(L.w, a.eps, with_sec, c.aggregator, lane);
+    if (lane == 0) {
+      flag[p] = 0;
+      if (a.nsteps) a.nsteps[p] = 0;
+      if (a.cls) a.cls[p] = k;
+    }
+  } else if (lane < T::A) {
+    float v = h[0];
+#pragma unroll
+    for (int q = 1; q < T::A; ++q) v = (lane == q) ? h[q] : v;
+    state[p * T::A + lane] = v;
+    if (lane == 0) flag[p] = 1;
+  }
+}
+
+template <class T>
+__global__ __launch_bounds__(256) void k_big_fix2(SrnnCfg c, SrnnArgs a) {
+  const int64_t p = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (p >= a.n) return;
+  float* state = reinterpret_cast<float*>(a.temp);
+  const int8_t* flag = reinterpret_cast<const int8_t*>(state + a.n * T::A);
+  if (!flag[p]) return;
+  float st[T::A], h[T::A];
+#pragma unroll
+  for (int i = 0; i < T::A; ++i) st[i] = state[p * T::A + i];
+  int taken = 1;
+  for (int k = 1; k < a.steps; ++k) {
+    if (a.early_exit && !finite_all<T>(st)) break;
+    mlp_state_lane<T>(st, st, h);
+    if (a.early_exit && finite_all<T>(h) && close_all<T>(h, st, a.eps)) break;
+#pragma unroll
+    for (int i = 0; i < T::A; ++i) st[i] = h[i];
+    ++taken;
+  }
+#pragma unroll
+  for (int i = 0; i < T::A; ++i) state[p * T::A + i] = st[i];
+  if (a.nsteps) a.nsteps[p] = taken;
+  if (a.cls) {
+    // classify the chunk-constant weights expand(st)
+    int8_t k;
+    if (!finite_all<T>(st)) k = C_DIVERGENT;
+    else {
+      float h1[T::A], h2[T::A];
+      mlp_state_lane<T>(st, st, h1);
+      if (finite_all<T>(h1) && close_all<T>(h1, st, a.eps)) {
+        bool zero = true;
+#pragma unroll
+        for (int i = 0; i < T::A; ++i) zero &= (-a.eps <= st[i]) && (st[i] <= a.eps);
+        k = zero ? C_FIX_ZERO : C_FIX_OTHER;
+      } else {
+        k = C_OTHER;
+        if (a.flags & 8) {
+          mlp_state_lane<T>(st, h1, h2);
+          if (finite_all<T>(h2) && close_all<T>(h2, st, a.eps)) k = C_FIX_SEC;
+        }
+      }
+    }
+    a.cls[p] = k;
+  }
+}
+
+template <class T>
+__global__ __launch_bounds__(TBB) void k_big_fix3(SrnnCfg c, SrnnArgs a) {
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int64_t p = (int64_t)blockIdx.x * BW + wv;
+  if (p >= a.n) return;
+  const float* state = reinterpret_cast<const float*>(a.temp);
+  const int8_t* flag = reinterpret_cast<const int8_t*>(state + a.n * T::A);
+  if (!flag[p]) return;
+  float st[T::A];
+#pragma unroll
+  for (int i = 0; i < T::A; ++i) st[i] = state[p * T::A + i];
+  store_state<T>(a.W + p * T::PP, st, lane);
+}
+
 // lane-per-particle ops writing straight to global memory (init, perturb)
 template <class T, int OP>
 __global__ __launch_bounds__(256) void k_big_lane(SrnnCfg c, SrnnArgs a) {
@@ -445,7 +586,15 @@ int big_run(int op, const SrnnCfg& c, const SrnnArgs& a) {
     case OP_INIT: hipLaunchKernelGGL((k_big_lane<T, OP_INIT>), dim3(gl), dim3(256), 0, st, c, a); break;
     case OP_PERTURB: hipLaunchKernelGGL((k_big_lane<T, OP_PERTURB>), dim3(gl), dim3(256), 0, st, c, a); break;
     case OP_APPLY: hipLaunchKernelGGL((k_big<T, OP_APPLY>), dim3(gw), dim3(TBB), 0, st, c, a); break;
-    case OP_RUN_FIXPOINT: hipLaunchKernelGGL((k_big<T, OP_RUN_FIXPOINT>), dim3(gw), dim3(TBB), 0, st, c, a); break;
+    case OP_RUN_FIXPOINT:
+      if (!a.temp || a.temp_bytes < a.n * (T::A * 4 + 1)) {
+        set_error("run_fixpoint on wave-per-particle nets needs temp >= n*(4*aggregates+1) bytes");
+        return -5;
+      }
+      hipLaunchKernelGGL((k_big_fix1<T>), dim3(gw), dim3(TBB), 0, st, c, a);
+      hipLaunchKernelGGL((k_big_fix2<T>), dim3(gl), dim3(256), 0, st, c, a);
+      hipLaunchKernelGGL((k_big_fix3<T>), dim3(gw), dim3(TBB), 0, st, c, a);
+      break;
     case OP_CLASSIFY: hipLaunchKernelGGL((k_big<T, OP_CLASSIFY>), dim3(gw), dim3(TBB), 0, st, c, a); break;
     case OP_TRAIN: hipLaunchKernelGGL((k_big<T, OP_TRAIN>), dim3(gw), dim3(TBB), 0, st, c, a); break;
     case OP_LEARN: hipLaunchKernelGGL((k_big<T, OP_LEARN>), dim3(gw), dim3(TBB), 0, st, c, a); break;

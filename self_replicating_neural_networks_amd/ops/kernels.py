@@ -49,6 +49,11 @@ def _check_idx(idx: Optional[torch.Tensor], n_items: int, n_rows: int, dev, name
             raise IndexError(f"{name} out of range [0, {n_rows}): min {lo} max {hi}")
 
 
+def is_wave_per_particle(spec) -> bool:
+    """Nets too large for the register kernels run wave-per-particle (csrc/srnn_bignet.hip)."""
+    return spec.kind == "aggregating" and spec.P > 64
+
+
 def _base_args(W: torch.Tensor, seed: int = 0, ctr: int = 0) -> SrnnArgs:
     a = SrnnArgs()
     a.seed = int(seed) & 0xFFFFFFFFFFFFFFFF
@@ -114,6 +119,12 @@ def run_fixpoint(spec, W: torch.Tensor, steps: int, eps: float, early_exit: bool
     a.flags = _lib.FLAG_FIX_SEC if with_sec else 0
     a.W, a.cls, a.nsteps, a.traj = _p(W), _p(cls), _p(nsteps), _p(traj)
     a.uid = _p(_uid(uid, n, W.device))
+    temp = None
+    if is_wave_per_particle(spec):
+        if record:
+            raise NotImplementedError("trajectory recording is not supported for wave-per-particle nets")
+        temp = torch.empty(n * (4 * spec.aggregates + 1), dtype=torch.uint8, device=W.device)
+        a.temp, a.temp_bytes = _p(temp), temp.numel()
     _lib.run(_lib.OP_RUN_FIXPOINT, spec, a)
     return cls, nsteps, traj
 
