@@ -51,11 +51,13 @@ def main():
     ap.add_argument("--epochs", type=int, default=20)
     ap.add_argument("--only", default="")
     ap.add_argument("--reps", type=int, default=5)
-    ap.add_argument("--big-n", type=int, default=1_000_000, help="population of the wave-per-particle nets")
+    ap.add_argument("--big-n", type=int, default=1_000_000, help="population of the big aggregating nets")
+    ap.add_argument("--wide-n", type=int, default=100_000, help="population of the MFMA weightwise nets")
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     specs = [ArchSpec.weightwise(2, 2), ArchSpec.aggregating(4, 2, 2), ArchSpec.recurrent(2, 2),
-             ArchSpec.fft(4, 2, 2), ArchSpec.weightwise(4, 3), ArchSpec.aggregating(4, 10, 3)]
+             ArchSpec.fft(4, 2, 2), ArchSpec.weightwise(4, 3), ArchSpec.aggregating(4, 10, 3),
+             ArchSpec.weightwise(16, 2), ArchSpec.weightwise(32, 2)]
     res = []
     for spec in specs:
         name = f"{spec.kind}({spec.aggregates},{spec.width},{spec.depth})"
@@ -67,9 +69,13 @@ def main():
         K.init_rows(spec, W, uid, 1)
         W0 = W.clone()
         out = torch.zeros_like(W)
-        big = spec.P > 64
+        big = K.is_wave_per_particle(spec)
         if big and args.big_n:
-            n = args.big_n
+            if spec.kind == "weightwise":
+                args_n = args.wide_n
+            else:
+                args_n = args.big_n
+            n = args_n
             uid = torch.arange(n, dtype=torch.int64, device=dev)
             W = torch.zeros(n, spec.PP, device=dev)
             K.init_rows(spec, W, uid, 1)
@@ -93,6 +99,10 @@ def main():
         def train():
             W.copy_(W0)
             K.train(spec, W, epochs=args.epochs, uid=uid, seed=3)
+        if spec.kind == "weightwise" and big:
+            res.append(r)
+            print(json.dumps(r), flush=True)
+            continue
         t = timeit(train, args.reps)
         r["train_us"] = t
         steps = spec.P if spec.kind == "weightwise" else 1

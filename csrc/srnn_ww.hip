@@ -2,6 +2,8 @@
 // code/network.py:222-230).  Add a line to support another (width, depth).
 #include "srnn_kernels.h"
 
+extern "C" int srnn_dispatch_wwwide(int op, const SrnnCfg* c, const SrnnArgs* a);
+
 using WW_1_1 = srnn::Weightwise<1, 1>;
 using WW_2_1 = srnn::Weightwise<2, 1>;
 using WW_2_2 = srnn::Weightwise<2, 2>;
@@ -20,5 +22,5 @@ extern "C" int srnn_dispatch_ww(int op, const SrnnCfg* c, const SrnnArgs* a) {
   SRNN_TRY(WW_4_2, 4, 2, 0)
   SRNN_TRY(WW_4_3, 4, 3, 0)
   SRNN_TRY(WW_8_2, 8, 2, 0)
-  return 1;
+  return srnn_dispatch_wwwide(op, c, a);  // width 16/32: MFMA wave-per-particle path
 }

@@ -50,7 +50,13 @@ def _check_idx(idx: Optional[torch.Tensor], n_items: int, n_rows: int, dev, name
 
 
 def is_wave_per_particle(spec) -> bool:
-    """Nets too large for the register kernels run wave-per-particle (csrc/srnn_bignet.hip)."""
+    """Nets too large for the register kernels run wave-per-particle: aggregating nets
+    (csrc/srnn_bignet.hip, chunk-state multi-step) and width >= 16 weightwise nets
+    (csrc/srnn_wide.hip, MFMA)."""
+    return (spec.kind == "aggregating" and spec.P > 64) or (spec.kind == "weightwise" and spec.width >= 16)
+
+
+def needs_chunk_state_temp(spec) -> bool:
     return spec.kind == "aggregating" and spec.P > 64
 
 
@@ -120,7 +126,9 @@ def run_fixpoint(spec, W: torch.Tensor, steps: int, eps: float, early_exit: bool
     a.W, a.cls, a.nsteps, a.traj = _p(W), _p(cls), _p(nsteps), _p(traj)
     a.uid = _p(_uid(uid, n, W.device))
     temp = None
-    if is_wave_per_particle(spec):
+    if is_wave_per_particle(spec) and record:
+        raise NotImplementedError("trajectory recording is not supported for wave-per-particle nets")
+    if needs_chunk_state_temp(spec):
         if record:
             raise NotImplementedError("trajectory recording is not supported for wave-per-particle nets")
         temp = torch.empty(n * (4 * spec.aggregates + 1), dtype=torch.uint8, device=W.device)

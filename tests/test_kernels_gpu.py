@@ -167,3 +167,46 @@ def test_big_aggregating_applying_statistics(cuda):
     cls, _, _ = K.run_fixpoint(spec, W, 100, 1e-4, early_exit=False)
     c = np.bincount(cls.cpu().numpy(), minlength=5)
     assert c.sum() == n and c[0] + c[1] > 0.9 * n  # divergent or collapsed to zero
+
+
+WIDE = [ArchSpec.weightwise(16, 2), ArchSpec.weightwise(16, 3), ArchSpec.weightwise(32, 2)]
+
+
+@pytest.mark.parametrize("spec", WIDE, ids=lambda s: f"ww-{s.width}-{s.depth}")
+def test_mfma_weightwise_vs_oracle(cuda, spec):
+    """Wide Weightwise nets: all P weight-points of a target through one MLP = a GEMM
+    chain on v_mfma_f32_16x16x4_f32 (wave per particle)."""
+    n, seed = 512, 8
+    uid = torch.arange(n, dtype=torch.int64, device=cuda)
+    W = torch.zeros(n, spec.PP, device=cuda)
+    K.init_rows(spec, W, uid, seed)
+    ow = O.init(spec, uid.cpu().numpy(), seed)
+    assert _rel(W[:, :spec.P].cpu().numpy(), ow) < 1e-5
+    assert torch.all(W[:, spec.P:] == 0)
+    out = torch.zeros_like(W)
+    idx_f = torch.roll(torch.arange(n, device=cuda), 1).contiguous()
+    K.apply(spec, W, out, idx_f=idx_f)
+    oo = O.apply(spec, np.roll(ow, 1, axis=0), ow)
+    assert _rel(out[:, :spec.P].cpu().numpy(), oo) < 1e-4
+    W3 = W.clone()
+    cls, nsteps, _ = K.run_fixpoint(spec, W3, 3, 1e-4, early_exit=False)
+    w = ow.copy()
+    with np.errstate(all="ignore"):
+        for _ in range(3):
+            w = O.apply(spec, w, w)
+    assert _rel(W3[:, :spec.P].cpu().numpy(), w) < 1e-2
+    assert (cls.cpu().numpy() == O.classify(spec, w, 1e-4)).mean() > 0.98
+    c0, counts = K.classify(spec, W, 1e-4)
+    assert (c0.cpu().numpy() == O.classify(spec, ow, 1e-4)).mean() > 0.99 and int(counts.sum()) == n
+
+
+def test_mfma_weightwise_identity_fixpoint(cuda):
+    """The identity fixpoint generalises to any width: f(x) = x[0] stays put exactly."""
+    spec = ArchSpec.weightwise(16, 2)
+    W = torch.zeros(4, spec.PP, device=cuda)
+    W[:, 0] = 1.0                      # A0[0][0]
+    W[:, spec.offsets[1]] = 1.0        # A1[0][0]
+    W[:, spec.offsets[2]] = 1.0        # A2[0][0]
+    before = W.clone()
+    cls, _, _ = K.run_fixpoint(spec, W, 5, 1e-4, early_exit=False)
+    assert torch.equal(W, before) and cls.tolist() == [O.C_FIX_OTHER] * 4
