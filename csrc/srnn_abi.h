@@ -14,6 +14,7 @@ struct SrnnCfg {
   int32_t shuffler;    // 0 none, 1 random
   int32_t pp;          // padded row stride (floats)
   int32_t p;           // weights per particle
+  int32_t dtype;       // weight-table storage: 0 fp32, 1 bf16, 2 fp16 (arithmetic is fp32)
 };
 
 struct SrnnArgs {
@@ -24,7 +25,7 @@ struct SrnnArgs {
   int32_t epochs;       // train: epochs; soup: train count
   int32_t severity;     // soup: learn_from_severity
   int32_t early_exit;   // fixpoint run: stop at fixpoint / divergence
-  int32_t flags;        // bit0 shuffle, bit1 remove_divergent, bit2 remove_zero, bit3 fix_sec, bit4 per-row respawn flags, bit5 respawn inline, bit6 count respawns in counts[5]
+  int32_t flags;        // bit0 shuffle, bit1 remove_divergent, bit2 remove_zero, bit3 fix_sec, bit4 per-row respawn flags, bit5 respawn inline, bit6 count respawns in counts[5], bit7 recvbuf is the all-gathered table
   int32_t gen;          // soup generation (time)
   float eps;
   float lr;
@@ -94,7 +95,7 @@ enum SrnnOp {
   OP_UID_ASSIGN = 15,   // sharded soup: uids of respawned rows from the gathered per-rank stats
 };
 
-int srnn_abi_version();  // 7
+int srnn_abi_version();  // 8
 int srnn_has_config(const SrnnCfg* cfg);
 int srnn_run(int op, const SrnnCfg* cfg, const SrnnArgs* args);
 const char* srnn_last_error();

@@ -14,6 +14,7 @@ extern "C" int srnn_dispatch_agg(int op, const SrnnCfg* c, const SrnnArgs* a);
 extern "C" int srnn_dispatch_rnn(int op, const SrnnCfg* c, const SrnnArgs* a);
 extern "C" int srnn_dispatch_fft(int op, const SrnnCfg* c, const SrnnArgs* a);
 extern "C" int srnn_dispatch_aggbig(int op, const SrnnCfg* c, const SrnnArgs* a);
+extern "C" int srnn_dispatch_lowp(int op, const SrnnCfg* c, const SrnnArgs* a);
 
 __global__ void k_scan_tail(int32_t* out, const int32_t* in, int64_t n) {
   // out[0] = 0 (inclusive scan was written to out+1)
@@ -23,6 +24,13 @@ __global__ void k_scan_tail(int32_t* out, const int32_t* in, int64_t n) {
 }
 
 static int dispatch(int op, const SrnnCfg* c, const SrnnArgs* a) {
+  if (c->dtype != 0) {
+    if (c->dtype != 1 && c->dtype != 2) {
+      srnn::set_error("unknown weight-table dtype");
+      return -1;
+    }
+    return srnn_dispatch_lowp(op, c, a);
+  }
   switch (c->kind) {
     case 0: return srnn_dispatch_ww(op, c, a);
     case 1: {
@@ -37,7 +45,7 @@ static int dispatch(int op, const SrnnCfg* c, const SrnnArgs* a) {
 
 extern "C" {
 
-int srnn_abi_version() { return 7; }
+int srnn_abi_version() { return 8; }
 
 const char* srnn_last_error() { return srnn::g_err.c_str(); }
 
@@ -48,7 +56,7 @@ int srnn_has_config(const SrnnCfg* cfg) {
 
 int64_t srnn_scan_temp_bytes(int64_t n) {
   size_t bytes = 0;
-  hipcub::DeviceScan::InclusiveSum(nullptr, bytes, (const int32_t*)nullptr, (int32_t*)nullptr, (int)n);
+  (void)hipcub::DeviceScan::InclusiveSum(nullptr, bytes, (const int32_t*)nullptr, (int32_t*)nullptr, (int)n);
   return (int64_t)bytes;
 }
 

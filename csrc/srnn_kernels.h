@@ -81,40 +81,123 @@ SRNN_HD uint64_t respawn_key(int32_t gen, int64_t g) {
   return (1ull << 62) | ((uint64_t)(uint32_t)gen << 32) | (uint64_t)g;
 }
 
-template <class Net>
+// ----------------------------------------------------------------------------------
+// Storage precision of the weight tables.  Arithmetic is always fp32 in
+// registers; a 16-bit table holds every *stored* weight state in that format, and the
+// multi-step operators round after each application (so a K-step launch equals K
+// one-step launches and fixpoint tests compare what would be stored).
+// ----------------------------------------------------------------------------------
+SRNN_HD float bits_f(uint32_t u) {
+  union { uint32_t u; float f; } x;
+  x.u = u;
+  return x.f;
+}
+SRNN_HD uint32_t f_bits(float f) {
+  union { uint32_t u; float f; } x;
+  x.f = f;
+  return x.u;
+}
+struct StF32 {
+  static constexpr int ID = 0, BYTES = 4;
+  SRNN_HD static float q(float x) { return x; }
+};
+struct StBF16 {  // round-to-nearest-even, NaN kept quiet
+  static constexpr int ID = 1, BYTES = 2;
+  SRNN_HD static uint16_t enc(float x) {
+    uint32_t u = f_bits(x);
+    if ((u & 0x7fffffffu) > 0x7f800000u) return (uint16_t)((u >> 16) | 0x40u);
+    u += 0x7fffu + ((u >> 16) & 1u);
+    return (uint16_t)(u >> 16);
+  }
+  SRNN_HD static float dec(uint16_t h) { return bits_f((uint32_t)h << 16); }
+  SRNN_HD static float q(float x) { return dec(enc(x)); }
+};
+struct StF16 {  // IEEE binary16, round-to-nearest-even (overflow -> inf = divergent)
+  static constexpr int ID = 2, BYTES = 2;
+  SRNN_HD static uint16_t enc(float x) {
+    _Float16 h = (_Float16)x;
+    uint16_t u;
+    __builtin_memcpy(&u, &h, 2);
+    return u;
+  }
+  SRNN_HD static float dec(uint16_t u) {
+    _Float16 h;
+    __builtin_memcpy(&h, &u, 2);
+    return (float)h;
+  }
+  SRNN_HD static float q(float x) { return dec(enc(x)); }
+};
+
+template <class Net, class S = StF32>
 struct Item {
   static constexpr int P = Net::P;
   static constexpr int PP = Net::PP;
-  static constexpr int XW = PP + 4;  // exchange row: weights + (slot, gen, -, -)
+  static constexpr int RB = PP * S::BYTES;  // bytes per table row
+  static constexpr int XB = RB + 16;        // exchange row: weights + (slot, gen, -, -) int32 tags
+
+  SRNN_HD static char* rowp(float* base, int64_t i) { return reinterpret_cast<char*>(base) + i * RB; }
+  SRNN_HD static const char* rowp(const float* base, int64_t i) { return reinterpret_cast<const char*>(base) + i * RB; }
 
   // generation-start row of global slot g: local table (W2, this rank's rows) or the
   // exchange receive buffer for slots of other ranks
-  SRNN_HD static const float* row_of(const SrnnArgs& a, int64_t g) {
-    if (a.world <= 1 || (g >= a.lo && g < a.lo + a.n)) return a.W2 + (g - a.lo) * PP;
-    return a.recvbuf + (int64_t)a.rmap[g] * XW;
+  // (flag 128: recvbuf is the all-gathered [n_total] table of every rank's rows)
+  SRNN_HD static const char* row_of(const SrnnArgs& a, int64_t g) {
+    if (a.world <= 1 || (g >= a.lo && g < a.lo + a.n)) return rowp(a.W2, g - a.lo);
+    if (a.flags & 128) return rowp(a.recvbuf, g);
+    return reinterpret_cast<const char*>(a.recvbuf) + (int64_t)a.rmap[g] * XB;
   }
 
-  SRNN_HD static void load(const float* __restrict__ row, float* __restrict__ w) {
-    const float4* r4 = reinterpret_cast<const float4*>(row);
+  SRNN_HD static void q(float* w) {
+    if constexpr (S::ID != 0) {
 #pragma unroll
-    for (int q = 0; q < PP / 4; ++q) {
-      float4 v = r4[q];
-      if (4 * q + 0 < P) w[4 * q + 0] = v.x;
-      if (4 * q + 1 < P) w[4 * q + 1] = v.y;
-      if (4 * q + 2 < P) w[4 * q + 2] = v.z;
-      if (4 * q + 3 < P) w[4 * q + 3] = v.w;
+      for (int k = 0; k < P; ++k) w[k] = S::q(w[k]);
     }
   }
-  SRNN_HD static void store(float* __restrict__ row, const float* __restrict__ w) {
-    float4* r4 = reinterpret_cast<float4*>(row);
+
+  SRNN_HD static void load(const char* __restrict__ row, float* __restrict__ w) {
+    if constexpr (S::ID == 0) {
+      const float4* r4 = reinterpret_cast<const float4*>(row);
 #pragma unroll
-    for (int q = 0; q < PP / 4; ++q) {
-      float4 v;
-      v.x = 4 * q + 0 < P ? w[4 * q + 0] : 0.f;
-      v.y = 4 * q + 1 < P ? w[4 * q + 1] : 0.f;
-      v.z = 4 * q + 2 < P ? w[4 * q + 2] : 0.f;
-      v.w = 4 * q + 3 < P ? w[4 * q + 3] : 0.f;
-      r4[q] = v;
+      for (int q = 0; q < PP / 4; ++q) {
+        float4 v = r4[q];
+        if (4 * q + 0 < P) w[4 * q + 0] = v.x;
+        if (4 * q + 1 < P) w[4 * q + 1] = v.y;
+        if (4 * q + 2 < P) w[4 * q + 2] = v.z;
+        if (4 * q + 3 < P) w[4 * q + 3] = v.w;
+      }
+    } else {
+      const uint2* r2 = reinterpret_cast<const uint2*>(row);  // 4 x 16 bit
+#pragma unroll
+      for (int q = 0; q < PP / 4; ++q) {
+        uint2 v = r2[q];
+        if (4 * q + 0 < P) w[4 * q + 0] = S::dec((uint16_t)(v.x & 0xffffu));
+        if (4 * q + 1 < P) w[4 * q + 1] = S::dec((uint16_t)(v.x >> 16));
+        if (4 * q + 2 < P) w[4 * q + 2] = S::dec((uint16_t)(v.y & 0xffffu));
+        if (4 * q + 3 < P) w[4 * q + 3] = S::dec((uint16_t)(v.y >> 16));
+      }
+    }
+  }
+  SRNN_HD static void store(char* __restrict__ row, const float* __restrict__ w) {
+    if constexpr (S::ID == 0) {
+      float4* r4 = reinterpret_cast<float4*>(row);
+#pragma unroll
+      for (int q = 0; q < PP / 4; ++q) {
+        float4 v;
+        v.x = 4 * q + 0 < P ? w[4 * q + 0] : 0.f;
+        v.y = 4 * q + 1 < P ? w[4 * q + 1] : 0.f;
+        v.z = 4 * q + 2 < P ? w[4 * q + 2] : 0.f;
+        v.w = 4 * q + 3 < P ? w[4 * q + 3] : 0.f;
+        r4[q] = v;
+      }
+    } else {
+      uint2* r2 = reinterpret_cast<uint2*>(row);
+#pragma unroll
+      for (int q = 0; q < PP / 4; ++q) {
+        uint32_t e[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) e[k] = 4 * q + k < P ? S::enc(w[4 * q + k]) : 0u;
+        r2[q] = make_uint2(e[0] | (e[1] << 16), e[2] | (e[3] << 16));
+      }
     }
   }
   SRNN_HD static void copy(float* __restrict__ d, const float* __restrict__ s) {
@@ -138,7 +221,7 @@ struct Item {
   SRNN_HD static void init(const SrnnCfg&, const SrnnArgs& a, int64_t i, float4*, uint8_t*) {
     float w[P];
     Net::init(w, rng(a), uid_of(a, i));
-    store(a.W + i * PP, w);
+    store(rowp(a.W, i), w);
   }
 
   // ---------------------------------------------------------------- apply (attack)
@@ -147,11 +230,12 @@ struct Item {
     int64_t ti = a.idx_t ? a.idx_t[i] : i;
     int64_t oi = a.idx_o ? a.idx_o[i] : i;
     float f[P], t[P], o[P];
-    load(a.W + fi * PP, f);
-    load(a.W + ti * PP, t);
+    load(rowp(a.W, fi), f);
+    load(rowp(a.W, ti), t);
     uint64_t ouid = a.uid ? (uint64_t)a.uid[ti] : (uint64_t)ti;
     Net::apply(f, t, o, actx(a, c, ouid, a.ctr, perm));
-    store(a.W2 + oi * PP, o);
+    q(o);
+    store(rowp(a.W2, oi), o);
   }
 
   // classification of the current weights (reference code/experiment.py:79-91)
@@ -159,10 +243,12 @@ struct Item {
     if (is_diverged<P>(w)) return C_DIVERGENT;
     float f1[P];
     Net::apply(w, w, f1, x);
+    q(f1);
     if (!is_diverged<P>(f1) && within_eps<P>(f1, w, eps)) return is_zero<P>(w, eps) ? C_FIX_ZERO : C_FIX_OTHER;
     if (with_sec) {
       float f2[P];
       Net::apply(w, f1, f2, x);
+      q(f2);
       if (!is_diverged<P>(f2) && within_eps<P>(f2, w, eps)) return C_FIX_SEC;
     }
     return C_OTHER;
@@ -172,24 +258,26 @@ struct Item {
   // reference code/experiment.py:70-77: while i < limit and not diverged and not fixpoint: self_attack
   SRNN_HD static void run_fixpoint(const SrnnCfg& c, const SrnnArgs& a, int64_t i, float4*, uint8_t* perm) {
     float w[P], nw[P];
-    load(a.W + i * PP, w);
+    load(rowp(a.W, i), w);
     uint64_t uid = uid_of(a, i);
     ApplyCtx x = actx(a, c, uid, a.ctr, perm);
-    if (a.traj) store(a.traj + i * PP, w);
+    if (a.traj) store(rowp(a.traj, i), w);
     int s = 0;
     for (; s < a.steps; ++s) {
       if (a.early_exit) {
         if (is_diverged<P>(w)) break;
         Net::apply(w, w, nw, x);
+        q(nw);
         if (!is_diverged<P>(nw) && within_eps<P>(nw, w, a.eps)) break;  // is_fixpoint()
       } else {
         Net::apply(w, w, nw, x);
+        q(nw);
       }
       copy(w, nw);
       x.ctr += 1;
-      if (a.traj) store(a.traj + ((int64_t)(s + 1) * a.n + i) * PP, w);
+      if (a.traj) store(rowp(a.traj, (int64_t)(s + 1) * a.n + i), w);
     }
-    store(a.W + i * PP, w);
+    store(rowp(a.W, i), w);
     if (a.nsteps) a.nsteps[i] = s;
     if (a.cls) a.cls[i] = classify_w(w, a.eps, (a.flags & 8) != 0, x);
   }
@@ -198,15 +286,17 @@ struct Item {
   // reference code/setups/known-fixpoint-variation.py:66-83
   SRNN_HD static void vary_run(const SrnnCfg& c, const SrnnArgs& a, int64_t i, float4*, uint8_t* perm) {
     float w[P], nw[P];
-    load(a.W + i * PP, w);
+    load(rowp(a.W, i), w);
     ApplyCtx x = actx(a, c, uid_of(a, i), a.ctr, perm);
     int tts = 0, taf = 0;
     bool still = true;
     for (int s = 0; s < a.steps; ++s) {
       Net::apply(w, w, nw, x);
+      q(nw);
       copy(w, nw);
       if (is_zero<P>(w, a.eps) || is_diverged<P>(w)) break;
       Net::apply(w, w, nw, x);
+      q(nw);
       bool fix = !is_diverged<P>(nw) && within_eps<P>(nw, w, a.eps);
       if (fix) {
         if (still) ++taf;
@@ -216,7 +306,7 @@ struct Item {
       }
       ++tts;
     }
-    store(a.W + i * PP, w);
+    store(rowp(a.W, i), w);
     a.nsteps[i] = tts;
     a.loss[i] = (float)taf;
   }
@@ -224,7 +314,7 @@ struct Item {
   // ---------------------------------------------------------------- perturb (vary)
   SRNN_HD static void perturb(const SrnnCfg&, const SrnnArgs& a, int64_t i, float4*, uint8_t*) {
     float w[P];
-    load(a.W + i * PP, w);
+    load(rowp(a.W, i), w);
     Rng r = rng(a);
     uint64_t uid = uid_of(a, i);
 #pragma unroll
@@ -233,14 +323,14 @@ struct Item {
       double mag = (double)u01(u.y) * (double)a.eps;
       w[k] = u01(u.x) < 0.5f ? (float)((double)w[k] + mag) : (float)((double)w[k] - mag);
     }
-    store(a.W + i * PP, w);
+    store(rowp(a.W, i), w);
   }
 
   // ---------------------------------------------------------------- train / learn_from
   SRNN_HD static void train(const SrnnCfg& c, const SrnnArgs& a, int64_t i, float4* samp, uint8_t* perm, bool learn) {
     float w[P], s[P];
-    load(a.W + i * PP, w);
-    if (learn) load(a.W2 + (a.idx_t ? a.idx_t[i] : i) * PP, s);
+    load(rowp(a.W, i), w);
+    if (learn) load(rowp(a.W2, a.idx_t ? a.idx_t[i] : i), s);
     TrainCtx tc;
     tc.lr = a.lr;
     tc.rng = rng(a);
@@ -256,14 +346,14 @@ struct Item {
       if (!learn) copy(s, w);
       loss = Net::train_epoch(w, s, tc);
     }
-    store(a.W + i * PP, w);
+    store(rowp(a.W, i), w);
     if (a.loss) a.loss[i] = loss;
   }
 
   // ---------------------------------------------------------------- classify
   SRNN_HD static int8_t classify(const SrnnCfg& c, const SrnnArgs& a, int64_t i, uint8_t* perm) {
     float w[P];
-    load(a.W + i * PP, w);
+    load(rowp(a.W, i), w);
     int8_t k = classify_w(w, a.eps, (a.flags & 8) != 0, actx(a, c, uid_of(a, i), a.ctr, perm));
     if (a.cls) a.cls[i] = k;
     return k;
@@ -299,11 +389,11 @@ struct Item {
 #else
       a.i32f[i] = __atomic_exchange_n(a.i32e + (at - a.lo), (int32_t)i, __ATOMIC_RELAXED);
 #endif
-    } else if (a.world > 1 && at >= 0 && i_local) {
+    } else if (a.need && a.world > 1 && at >= 0 && i_local) {
       // my particle attacks a victim owned by another rank: ship my row there
       atomic_or_i32(a.need + (i - a.lo), 1 << shard_of(at, a.n_total, a.world));
     }
-    if (a.world > 1 && te >= a.lo && te < a.lo + a.n && !i_local) {
+    if (a.need && a.world > 1 && te >= a.lo && te < a.lo + a.n && !i_local) {
       // a remote learner picked one of my particles as teacher
       atomic_or_i32(a.need + (te - a.lo), 1 << shard_of(i, a.n_total, a.world));
     }
@@ -315,7 +405,7 @@ struct Item {
     if (!m) return;
     a.need[j] = 0;
     const int32_t gen = gen_of(a);
-    const float* src = a.W2 + j * PP;
+    const char* src = rowp(a.W2, j);
     while (m) {
       const int r = __builtin_ctz((unsigned)m);
       m &= m - 1;
@@ -324,18 +414,18 @@ struct Item {
         atomic_or_i32(a.ovf, 1);
         continue;
       }
-      float* dst = a.sendbuf + ((int64_t)r * a.cap + pos) * XW;
-      const float4* s4 = reinterpret_cast<const float4*>(src);
-      float4* d4 = reinterpret_cast<float4*>(dst);
+      char* dst = reinterpret_cast<char*>(a.sendbuf) + ((int64_t)r * a.cap + pos) * XB;
+      const uint2* s2 = reinterpret_cast<const uint2*>(src);
+      uint2* d2 = reinterpret_cast<uint2*>(dst);
 #pragma unroll
-      for (int q = 0; q < PP / 4; ++q) d4[q] = s4[q];
-      int32_t tag[4] = {(int32_t)(a.lo + j), gen, 0, 0};
-      d4[PP / 4] = *reinterpret_cast<float4*>(tag);
+      for (int q = 0; q < RB / 8; ++q) d2[q] = s2[q];
+      d2[RB / 8] = make_uint2((uint32_t)(a.lo + j), (uint32_t)gen);
+      d2[RB / 8 + 1] = make_uint2(0u, 0u);
     }
   }
   // sharded soup: received row k -> rmap[slot]; rows of older generations are ignored
   SRNN_HD static void soup_unpack(const SrnnArgs& a, int64_t k) {
-    const int32_t* tag = reinterpret_cast<const int32_t*>(a.recvbuf + k * XW + PP);
+    const int32_t* tag = reinterpret_cast<const int32_t*>(reinterpret_cast<const char*>(a.recvbuf) + k * XB + RB);
     if (tag[1] == gen_of(a)) a.rmap[tag[0]] = (int32_t)k;
   }
 
@@ -344,7 +434,7 @@ struct Item {
   SRNN_HD static void soup_evolve(const SrnnCfg& c, const SrnnArgs& a, int64_t j, float4* samp, uint8_t* perm) {
     const int64_t g = a.lo + j;
     float w[P], f[P], o[P];
-    load(a.W2 + j * PP, w);
+    load(rowp(a.W2, j), w);
     const uint64_t uid = uid_of(a, j);
     const int32_t gen = gen_of(a);
     ApplyCtx x = actx(a, c, uid, (uint32_t)gen * 1024u, perm);
@@ -359,6 +449,7 @@ struct Item {
       last = best;
       load(row_of(a, best), f);
       Net::apply(f, w, o, x);
+      q(o);
       x.ctr += 1;
       copy(w, o);
     }
@@ -396,11 +487,12 @@ struct Item {
       cp = -1;
     }
     // 4. respawn flags (reference code/soup.py:77-86; zero test on the old particle)
+    q(w);  // the stored state decides respawn
     int8_t rs = 0;
     if ((a.flags & 2) && is_diverged<P>(w)) rs = 1;
     else if ((a.flags & 4) && is_zero<P>(w, a.eps)) rs = 2;
     if (rs && (a.flags & 32)) Net::init(w, rng(a), respawn_key(gen, g));  // newborn, uid assigned later
-    store(a.W + j * PP, w);
+    store(rowp(a.W, j), w);
     if (a.action) a.action[j] = act;
     if (a.counterpart) a.counterpart[j] = cp;
     if (a.loss) a.loss[j] = loss;
@@ -419,16 +511,16 @@ struct Item {
     if (a.respawn[j] == 0) return;
     float w[P];
     Net::init(w, rng(a), respawn_key(gen_of(a), a.lo + j));
-    store(a.W + j * PP, w);
+    store(rowp(a.W, j), w);
   }
 };
 
 // ==================================================================================
 // Device kernels
 // ==================================================================================
-template <class Net, int OP>
+template <class Net, int OP, class S>
 __global__ __launch_bounds__(TB) void k_op(SrnnCfg c, SrnnArgs a) {
-  using I = Item<Net>;
+  using I = Item<Net, S>;
   constexpr int P = Net::P;
   constexpr bool NEED_SAMP = (OP == OP_TRAIN || OP == OP_LEARN || OP == OP_SOUP_EVOLVE) && Net::KIND == 0;
   constexpr int SAMP = NEED_SAMP ? P : 1;  // slot-major [P][TB]: lane fastest
@@ -467,9 +559,9 @@ __global__ __launch_bounds__(TB) void k_op(SrnnCfg c, SrnnArgs a) {
 // Fused soup generation body: one wave per block; after the per-particle work the wave
 // publishes its 64-bit respawn ballot (i32c as u64[block]) for the single-rank respawn scan, or per-row
 // flags (i32c[row]) when OP_SCAN follows (sharded path, a.i32d != null flags that mode).
-template <class Net>
+template <class Net, class S>
 __global__ __launch_bounds__(TB) void k_soup_evolve(SrnnCfg c, SrnnArgs a) {
-  using I = Item<Net>;
+  using I = Item<Net, S>;
   constexpr int P = Net::P;
   constexpr int SAMP = Net::KIND == 0 ? P : 1;
   constexpr int PERM = (P + 4) & ~3;
@@ -495,9 +587,9 @@ __global__ __launch_bounds__(TB) void k_soup_evolve(SrnnCfg c, SrnnArgs a) {
 // at most one atomic per (block, non-empty class) -- per-wave atomics on 5 addresses
 // serialised at L2 (39 us for 100k particles in the first profile).
 constexpr int TBC = 256;
-template <class Net>
+template <class Net, class S>
 __global__ __launch_bounds__(TBC) void k_classify_count(SrnnCfg c, SrnnArgs a) {
-  using I = Item<Net>;
+  using I = Item<Net, S>;
   constexpr int PERM = (Net::P + 4) & ~3;
   __shared__ uint8_t s_perm[TBC * PERM];
   __shared__ uint32_t s_cnt[5];
@@ -519,7 +611,7 @@ __global__ __launch_bounds__(TBC) void k_classify_count(SrnnCfg c, SrnnArgs a) {
   }
 }
 
-template <class Net, int OP>
+template <class Net, int OP, class S>
 int launch(const SrnnCfg& c, const SrnnArgs& a) {
   int64_t items = (OP == OP_SOUP_DECIDE) ? a.n_total : (OP == OP_SOUP_UNPACK) ? (int64_t)a.world * a.cap : a.n;
   if (items <= 0) return 0;
@@ -530,11 +622,11 @@ int launch(const SrnnCfg& c, const SrnnArgs& a) {
   }
   hipStream_t st = (hipStream_t)a.stream;
   if (OP == OP_SOUP_EVOLVE) {
-    hipLaunchKernelGGL((k_soup_evolve<Net>), dim3((unsigned)blocks), dim3(TB), 0, st, c, a);
+    hipLaunchKernelGGL((k_soup_evolve<Net, S>), dim3((unsigned)blocks), dim3(TB), 0, st, c, a);
   } else if (OP == OP_CLASSIFY && a.counts) {
-    hipLaunchKernelGGL((k_classify_count<Net>), dim3((unsigned)((items + TBC - 1) / TBC)), dim3(TBC), 0, st, c, a);
+    hipLaunchKernelGGL((k_classify_count<Net, S>), dim3((unsigned)((items + TBC - 1) / TBC)), dim3(TBC), 0, st, c, a);
   } else {
-    hipLaunchKernelGGL((k_op<Net, OP>), dim3((unsigned)blocks), dim3(TB), 0, st, c, a);
+    hipLaunchKernelGGL((k_op<Net, OP, S>), dim3((unsigned)blocks), dim3(TB), 0, st, c, a);
   }
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) {
@@ -547,9 +639,9 @@ int launch(const SrnnCfg& c, const SrnnArgs& a) {
 // ==================================================================================
 // Host execution of the same per-item code (CPU tensors)
 // ==================================================================================
-template <class Net, int OP>
+template <class Net, int OP, class S>
 int host_run(const SrnnCfg& c, const SrnnArgs& a) {
-  using I = Item<Net>;
+  using I = Item<Net, S>;
   constexpr int P = Net::P;
   int64_t items = (OP == OP_SOUP_DECIDE) ? a.n_total : (OP == OP_SOUP_UNPACK) ? (int64_t)a.world * a.cap : a.n;
   if (OP == OP_SOUP_UNPACK)
@@ -592,9 +684,9 @@ int host_run(const SrnnCfg& c, const SrnnArgs& a) {
 // advances next_uid and the generation counter -- replacing scan + torch bookkeeping
 // kernels with one launch (the flags are sparse; each thread walks a contiguous chunk).
 constexpr int TBR = 1024;
-template <class Net>
+template <class Net, class S>
 __global__ __launch_bounds__(TBR) void k_respawn_seq(SrnnCfg c, SrnnArgs a) {
-  using I = Item<Net>;
+  using I = Item<Net, S>;
   __shared__ int32_t s_cnt[TBR];
   // i32c as u64[b] = respawn ballot of evolve block b (64 rows); thread t owns blocks
   // [t*ch, (t+1)*ch): no per-row memory traffic, bits give the rows in slot order.
@@ -625,7 +717,7 @@ __global__ __launch_bounds__(TBR) void k_respawn_seq(SrnnCfg c, SrnnArgs a) {
         a.uid_out[r] = k;
         float w[Net::P];
         Net::init(w, I::rng(a), respawn_key(I::gen_of(a), a.lo + r));
-        I::store(a.W + r * Net::PP, w);
+        I::store(I::rowp(a.W, r), w);
         ++k;
       }
     }
@@ -638,10 +730,11 @@ __global__ __launch_bounds__(TBR) void k_respawn_seq(SrnnCfg c, SrnnArgs a) {
   if (a.counts && threadIdx.x < 5) a.counts[threadIdx.x] = 0;  // fresh histogram for the census
 }
 
-template <class Net>
+template <class Net, class S>
 int respawn_seq(const SrnnCfg& c, const SrnnArgs& a) {
+  using I = Item<Net, S>;
   if (a.dev) {
-    hipLaunchKernelGGL((k_respawn_seq<Net>), dim3(1), dim3(TBR), 0, (hipStream_t)a.stream, c, a);
+    hipLaunchKernelGGL((k_respawn_seq<Net, S>), dim3(1), dim3(TBR), 0, (hipStream_t)a.stream, c, a);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) {
       set_error(hipGetErrorString(e));
@@ -654,8 +747,8 @@ int respawn_seq(const SrnnCfg& c, const SrnnArgs& a) {
     if (a.respawn[i] == 0) continue;
     a.uid_out[i] = k;
     float w[Net::P];
-    Net::init(w, Item<Net>::rng(a), respawn_key(Item<Net>::gen_of(a), a.lo + i));
-    Item<Net>::store(a.W + i * Net::PP, w);
+    Net::init(w, I::rng(a), respawn_key(I::gen_of(a), a.lo + i));
+    I::store(I::rowp(a.W, i), w);
     ++k;
   }
   ((int64_t*)a.uid_base)[0] = k;
@@ -755,29 +848,29 @@ int uid_assign(const SrnnCfg& c, const SrnnArgs& a) {
   return 0;
 }
 
-template <class Net, int OP>
+template <class Net, int OP, class S>
 int run_one(const SrnnCfg& c, const SrnnArgs& a) {
-  return a.dev ? launch<Net, OP>(c, a) : host_run<Net, OP>(c, a);
+  return a.dev ? launch<Net, OP, S>(c, a) : host_run<Net, OP, S>(c, a);
 }
 
-template <class Net>
+template <class Net, class S = StF32>
 int run_net_op(int op, const SrnnCfg& c, const SrnnArgs& a) {
   switch (op) {
-    case OP_INIT: return run_one<Net, OP_INIT>(c, a);
-    case OP_APPLY: return run_one<Net, OP_APPLY>(c, a);
-    case OP_RUN_FIXPOINT: return run_one<Net, OP_RUN_FIXPOINT>(c, a);
-    case OP_TRAIN: return run_one<Net, OP_TRAIN>(c, a);
-    case OP_LEARN: return run_one<Net, OP_LEARN>(c, a);
-    case OP_CLASSIFY: return run_one<Net, OP_CLASSIFY>(c, a);
-    case OP_PERTURB: return run_one<Net, OP_PERTURB>(c, a);
-    case OP_SOUP_DECIDE: return run_one<Net, OP_SOUP_DECIDE>(c, a);
-    case OP_RESPAWN_SEQ: return respawn_seq<Net>(c, a);
-    case OP_SOUP_PACK: return run_one<Net, OP_SOUP_PACK>(c, a);
-    case OP_SOUP_UNPACK: return run_one<Net, OP_SOUP_UNPACK>(c, a);
+    case OP_INIT: return run_one<Net, OP_INIT, S>(c, a);
+    case OP_APPLY: return run_one<Net, OP_APPLY, S>(c, a);
+    case OP_RUN_FIXPOINT: return run_one<Net, OP_RUN_FIXPOINT, S>(c, a);
+    case OP_TRAIN: return run_one<Net, OP_TRAIN, S>(c, a);
+    case OP_LEARN: return run_one<Net, OP_LEARN, S>(c, a);
+    case OP_CLASSIFY: return run_one<Net, OP_CLASSIFY, S>(c, a);
+    case OP_PERTURB: return run_one<Net, OP_PERTURB, S>(c, a);
+    case OP_SOUP_DECIDE: return run_one<Net, OP_SOUP_DECIDE, S>(c, a);
+    case OP_RESPAWN_SEQ: return respawn_seq<Net, S>(c, a);
+    case OP_SOUP_PACK: return run_one<Net, OP_SOUP_PACK, S>(c, a);
+    case OP_SOUP_UNPACK: return run_one<Net, OP_SOUP_UNPACK, S>(c, a);
     case OP_UID_ASSIGN: return uid_assign<Net>(c, a);
-    case OP_SOUP_EVOLVE: return run_one<Net, OP_SOUP_EVOLVE>(c, a);
-    case OP_RESPAWN: return run_one<Net, OP_RESPAWN>(c, a);
-    case OP_VARY_RUN: return run_one<Net, OP_VARY_RUN>(c, a);
+    case OP_SOUP_EVOLVE: return run_one<Net, OP_SOUP_EVOLVE, S>(c, a);
+    case OP_RESPAWN: return run_one<Net, OP_RESPAWN, S>(c, a);
+    case OP_VARY_RUN: return run_one<Net, OP_VARY_RUN, S>(c, a);
     default: set_error("unknown op"); return -1;
   }
 }
@@ -793,6 +886,20 @@ int run_net_op(int op, const SrnnCfg& c, const SrnnArgs& a) {
       srnn::set_error("layout mismatch (p/pp) for instantiated shape");                \
       return -4;                                                                       \
     }                                                                                  \
+    if (c->dtype != 0) return 1; /* 16-bit tables: srnn_lowp.hip */                    \
     if (op < 0) return 0;                                                              \
     return srnn::run_net_op<NETTYPE>(op, *c, *a);                                      \
+  }
+
+// 16-bit weight tables (bf16 / fp16 storage, fp32 arithmetic) for a shape
+#define SRNN_TRY_LOWP(NETTYPE, W_, D_, A_)                                             \
+  if (c->width == (W_) && c->depth == (D_) && c->aggregates == (A_)) {                 \
+    if (c->p != NETTYPE::P || c->pp != NETTYPE::PP) {                                  \
+      srnn::set_error("layout mismatch (p/pp) for instantiated shape");                \
+      return -4;                                                                       \
+    }                                                                                  \
+    if (c->dtype != 1 && c->dtype != 2) return 1;                                      \
+    if (op < 0) return 0;                                                              \
+    if (c->dtype == 1) return srnn::run_net_op<NETTYPE, srnn::StBF16>(op, *c, *a);     \
+    return srnn::run_net_op<NETTYPE, srnn::StF16>(op, *c, *a);                         \
   }

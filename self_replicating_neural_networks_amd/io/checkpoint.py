@@ -5,6 +5,9 @@ Layout of a checkpoint directory::
     manifest.json        spec, population size, params, seed, lr, generation, next uid, ...
     shard-<lo>-<hi>.pt   {"W": float32[hi-lo, P], "uid": int64[hi-lo]}  (one per writing rank)
 
+16-bit tables (bf16 / fp16) are written widened to fp32 (exact) and narrowed again on load;
+the manifest records the storage dtype.
+
 Every random stream of the engine is a pure function of (seed, slot/uid, generation), so a
 resumed soup continues bit-for-bit.  Shards are keyed by their global row range, so a
 checkpoint written by R ranks can be loaded by any number of ranks (re-sharding).  Files
@@ -24,19 +27,21 @@ from ..arch import ArchSpec
 from ..parallel.dist import Dist
 
 FORMAT = "srnn-checkpoint-v1"
+_DTYPE_NAMES = {torch.float32: "float32", torch.bfloat16: "bfloat16", torch.float16: "float16"}
+_DTYPES = {v: k for k, v in _DTYPE_NAMES.items()}
 
 
 def save_engine(eng, path: str) -> str:
     """Write this rank's shard (+ the manifest on rank 0). Collective when sharded."""
     os.makedirs(path, exist_ok=True)
     P = eng.spec.P
-    torch.save({"W": eng.local_rows()[:, :P].detach().cpu().contiguous(), "uid": eng.uid.detach().cpu().clone()},
+    torch.save({"W": eng.local_rows()[:, :P].detach().float().cpu().contiguous(), "uid": eng.uid.detach().cpu().clone()},
                os.path.join(path, f"shard-{eng.lo:012d}-{eng.hi:012d}.pt"))
     if eng.dist.rank == 0:
         manifest = dict(format=FORMAT, kind="soup", spec=json.loads(eng.spec.to_json()), n_total=eng.n_total,
                         params={k: v for k, v in eng.params.items()}, seed=eng.seed, lr=eng.lr, shuffle=eng.shuffle,
                         time=eng.time, gen=int(eng.gen_dev.item()), next_uid=int(eng.next_uid.item()),
-                        world=eng.dist.world)
+                        world=eng.dist.world, dtype=_DTYPE_NAMES[eng.dtype], exchange=eng.exchange)
         with open(os.path.join(path, "manifest.json"), "w") as f:
             json.dump(manifest, f, indent=1, sort_keys=True)
     eng.dist.barrier()
@@ -76,7 +81,8 @@ def load_engine(path: str, device="cpu", dist: Optional[Dist] = None):
     full = np.zeros((m["n_total"], spec.P), dtype=np.float32)
     full[lo:hi] = W
     eng = SoupEngine(spec, m["n_total"], m["params"], device=device, seed=m["seed"], lr=m["lr"],
-                     shuffle=m["shuffle"], dist=d, weights=full)
+                     shuffle=m["shuffle"], dist=d, weights=full, dtype=_DTYPES[m.get("dtype", "float32")],
+                     exchange=m.get("exchange", "alltoall"))
     eng.uid.copy_(torch.from_numpy(uid))
     eng.next_uid.fill_(m["next_uid"])
     eng.gen_dev.fill_(m["gen"])
@@ -86,11 +92,12 @@ def load_engine(path: str, device="cpu", dist: Optional[Dist] = None):
 
 def save_population(pop, path: str) -> str:
     os.makedirs(path, exist_ok=True)
-    torch.save({"W": pop.weights().detach().cpu().contiguous(), "uid": pop.uid.detach().cpu().clone()},
+    torch.save({"W": pop.weights().detach().float().cpu().contiguous(), "uid": pop.uid.detach().cpu().clone()},
                os.path.join(path, f"shard-{0:012d}-{pop.n:012d}.pt"))
     with open(os.path.join(path, "manifest.json"), "w") as f:
         json.dump(dict(format=FORMAT, kind="population", spec=json.loads(pop.spec.to_json()), n_total=pop.n,
-                       seed=pop.seed, lr=pop.lr, ctr=pop.ctr), f, indent=1, sort_keys=True)
+                       seed=pop.seed, lr=pop.lr, ctr=pop.ctr, dtype=_DTYPE_NAMES[pop.W.dtype]), f, indent=1,
+                  sort_keys=True)
     return path
 
 
@@ -103,7 +110,8 @@ def load_population(path: str, device="cpu"):
         raise ValueError(f"{path}: not a population checkpoint")
     spec = ArchSpec(**m["spec"])
     W, uid = _read_rows(path, 0, m["n_total"], spec.P)
-    pop = Population(spec, m["n_total"], device=device, seed=m["seed"], weights=W, lr=m["lr"])
+    pop = Population(spec, m["n_total"], device=device, seed=m["seed"], weights=W, lr=m["lr"],
+                     dtype=_DTYPES[m.get("dtype", "float32")])
     pop.uid.copy_(torch.from_numpy(uid))
     pop.ctr = m["ctr"]
     return pop

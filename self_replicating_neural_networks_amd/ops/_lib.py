@@ -19,7 +19,7 @@ import threading
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libsrnn.so")
 CSRC = os.path.normpath(os.path.join(_HERE, "..", "..", "csrc"))
-ABI_VERSION = 7
+ABI_VERSION = 8
 
 OP_INIT = 0
 OP_APPLY = 1
@@ -45,11 +45,12 @@ FLAG_FIX_SEC = 8
 FLAG_ROW_FLAGS = 16
 FLAG_RESPAWN_INLINE = 32
 FLAG_COUNT_RESPAWNS = 64
+FLAG_FULL_TABLE = 128
 
 
 class SrnnCfg(ctypes.Structure):
     _fields_ = [(n, ctypes.c_int32) for n in
-                ("kind", "width", "depth", "aggregates", "aggregator", "shuffler", "pp", "p")]
+                ("kind", "width", "depth", "aggregates", "aggregator", "shuffler", "pp", "p", "dtype")]
 
 
 _P = ctypes.c_void_p
@@ -123,17 +124,20 @@ def lib():
         return _lib
 
 
-def make_cfg(spec) -> SrnnCfg:
-    return SrnnCfg(*spec.native_cfg_tuple())
+DTYPE_FP32, DTYPE_BF16, DTYPE_FP16 = 0, 1, 2
 
 
-def has_config(spec) -> bool:
-    return bool(lib().srnn_has_config(ctypes.byref(make_cfg(spec))))
+def make_cfg(spec, dtype: int = DTYPE_FP32) -> SrnnCfg:
+    return SrnnCfg(*spec.native_cfg_tuple(), int(dtype))
 
 
-def run(op: int, spec, args: SrnnArgs, cfg: SrnnCfg = None) -> None:
+def has_config(spec, dtype: int = DTYPE_FP32) -> bool:
+    return bool(lib().srnn_has_config(ctypes.byref(make_cfg(spec, dtype))))
+
+
+def run(op: int, spec, args: SrnnArgs, cfg: SrnnCfg = None, dtype: int = DTYPE_FP32) -> None:
     L = lib()
-    cfg = cfg if cfg is not None else make_cfg(spec)
+    cfg = cfg if cfg is not None else make_cfg(spec, dtype)
     r = L.srnn_run(op, ctypes.byref(cfg), ctypes.byref(args))
     if r != 0:
         msg = L.srnn_last_error().decode(errors="replace")

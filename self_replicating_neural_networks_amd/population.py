@@ -1,7 +1,9 @@
 """Device-resident particle populations.
 
 ``Population`` is the unit of computation of the framework: a weight table
-``W[N, spec.PP]`` (fp32, one particle per row, Keras flat order) plus a uid per row.
+``W[N, spec.PP]`` (one particle per row, Keras flat order) plus a uid per row.  The table
+is fp32 by default; ``dtype=torch.bfloat16`` / ``torch.float16`` stores every weight state
+in 16 bits (half the HBM per particle, arithmetic still fp32 -- SURVEY §7.7).
 Reference-style objects (``WeightwiseNeuralNetwork``, ``ParticleDecorator``, ``Soup``) are
 views of rows of a population; the batched methods here replace the reference's
 per-object Python loops (``code/experiment.py:70-91``, ``code/setups/*.py`` trial loops).
@@ -27,14 +29,15 @@ class Population:
     """N particles of one architecture on one device."""
 
     def __init__(self, spec: ArchSpec, n: int, device="cpu", seed: int = 0, uid_start: int = 0,
-                 weights: Optional[torch.Tensor] = None, lr: float = 0.01):
+                 weights: Optional[torch.Tensor] = None, lr: float = 0.01, dtype: torch.dtype = torch.float32):
         self.spec = spec
         self.device = torch.device(device)
         self.seed = int(seed)
         self.lr = float(lr)
         self.ctr = 0  # op counter: keys the per-particle random streams of shuffles etc.
         self.uid = torch.arange(uid_start, uid_start + n, dtype=torch.int64, device=self.device)
-        self.W = torch.zeros((n, spec.PP), dtype=torch.float32, device=self.device)
+        K.dtype_code(dtype)
+        self.W = torch.zeros((n, spec.PP), dtype=dtype, device=self.device)
         if weights is None:
             K.init_rows(spec, self.W, self.uid, self.seed)
         else:
@@ -64,7 +67,7 @@ class Population:
         if w.shape[0] != self.n or w.shape[1] not in (self.spec.P, self.spec.PP):
             raise ValueError(f"weights must be [{self.n}, {self.spec.P}], got {tuple(w.shape)}")
         self.W.zero_()
-        self.W[:, : w.shape[1]] = w.to(self.device)
+        self.W[:, : w.shape[1]] = w.to(self.device, self.W.dtype)
         if w.shape[1] == self.spec.PP:
             self.W[:, self.spec.P:] = 0
 

@@ -22,7 +22,12 @@ victims, teachers of their learners): those rows -- ~(attack+learn rate)/R of a 
 peer -- go through ONE fixed-capacity all-to-all; the census plus each rank's respawn
 count go through ONE 48-byte all-gather, from which the uid prefix is computed on device.
 No weight table is replicated.  Results are bitwise independent of R
-(tests/test_dist_gloo.py).
+(tests/test_dist_gloo.py).  ``exchange="allgather"`` instead all-gathers every rank's rows
+each generation (the X01 pattern of SURVEY §2.5: one collective, no decide-dependent
+packing, but every rank holds the whole table) -- same results, bitwise.
+
+``dtype`` selects the storage of the weight tables and exchange rows (fp32, bf16, fp16;
+arithmetic is fp32 -- SURVEY §7.7).
 
 Differences from the sequential reference (tested statistically): particle k does not see
 the effects of particles < k within the same generation; every read is from the
@@ -49,11 +54,38 @@ def _p(t):
     return ctypes.c_void_p(t.data_ptr()) if t is not None else None
 
 
+MAX_SLOTS = 2 ** 31 - 2  # soup slots are int32 on the device
+
+
+def plan_population(spec: ArchSpec, dtype=torch.float32, exchange: str = "alltoall", world: int = 1,
+                    hbm_bytes: int = 288 * 10 ** 9, fill: float = 0.9, attacking_rate: float = 0.1,
+                    learn_from_rate: float = 0.1) -> Dict:
+    """Device bytes per particle of a SoupEngine and the largest population that fits
+    ``fill`` of each GPU's HBM (288 GB HBM3E per MI355X).  Per local row: two ping-pong
+    table rows + uid/flags/action/counterpart/loss/respawn (34 B); per global slot: the
+    attacker link (+ the received-row map for all-to-all); exchange: the gathered table
+    (all-gather) or the capacity-bounded send/recv rows (all-to-all)."""
+    rb = spec.PP * torch.empty((), dtype=dtype).element_size()
+    per_local = 2 * rb + 34
+    if exchange == "allgather":
+        per_slot = 4 + (rb if world > 1 else 0)
+        per_local_x = 0.0
+    else:
+        per_slot = 4 + (4 if world > 1 else 0)
+        per_local_x = (2 * 1.2 * min(attacking_rate + learn_from_rate, 2.0) * (rb + 16)) if world > 1 else 0.0
+    per_particle = per_slot + (per_local + per_local_x) / world  # bytes per GPU per global particle
+    n_fit = int(fill * hbm_bytes / per_particle)
+    return dict(row_bytes=rb, bytes_per_particle_per_gpu=per_particle, n_total_fit=n_fit,
+                n_total=min(n_fit, MAX_SLOTS), limited_by="hbm" if n_fit <= MAX_SLOTS else "int32 slots",
+                world=world, exchange=exchange, dtype=str(dtype).replace("torch.", ""))
+
+
 class SoupEngine:
     """Population-sharded soup on one device per rank."""
 
     def __init__(self, spec: ArchSpec, n_total: int, params: Dict, device="cpu", seed: int = 0,
-                 lr: float = 0.01, shuffle: bool = True, dist: Optional[Dist] = None, weights=None):
+                 lr: float = 0.01, shuffle: bool = True, dist: Optional[Dist] = None, weights=None,
+                 dtype: torch.dtype = torch.float32, exchange: str = "alltoall"):
         self.spec = spec
         self.n_total = int(n_total)
         self.params = dict(attacking_rate=0.1, learn_from_rate=0.1, train=0, learn_from_severity=1)
@@ -65,17 +97,27 @@ class SoupEngine:
         self.dist = dist or Dist()
         self.lo, self.hi = self.dist.shard(self.n_total)
         self.n = self.hi - self.lo
-        if self.n_total >= 2 ** 31 - 1:
+        if self.n_total > MAX_SLOTS:
             raise ValueError("soup slots are int32 on device")
         seg = int(self.params.get("segment", 0) or 0)
         if seg and self.n_total % seg:
             raise ValueError("population size must be a multiple of the sub-soup segment")
+        if exchange not in ("alltoall", "allgather"):
+            raise ValueError(f"exchange must be 'alltoall' or 'allgather', got {exchange!r}")
+        self.exchange = exchange
+        self.dtype = dtype
+        self.dtype_code = K.dtype_code(dtype)
         dev, PP = self.device, spec.PP
         i32 = dict(dtype=torch.int32, device=dev)
         # this rank's rows, ping-pong: generation t reads buf[p], writes buf[1-p]
-        self._bufs = [torch.zeros((self.n, PP), dtype=torch.float32, device=dev) for _ in range(2)]
+        self._bufs = [torch.zeros((self.n, PP), dtype=dtype, device=dev) for _ in range(2)]
         self._p = 0
-        if self.dist.enabled:
+        if self.dist.enabled and exchange == "allgather":
+            # every rank's generation-start rows, gathered each generation
+            self.full = torch.zeros((self.n_total, PP), dtype=dtype, device=dev)
+            self.stats_all = torch.zeros(self.dist.world * 6, dtype=torch.int64, device=dev)
+            self.census = torch.zeros(5, dtype=torch.int64, device=dev)
+        elif self.dist.enabled:
             # exchange of the generation-start rows that other ranks need (attackers of
             # their victims, teachers of their learners): fixed-capacity all-to-all
             R = self.dist.world
@@ -88,7 +130,7 @@ class SoupEngine:
             self.sendcnt = torch.zeros(R, **i32)
             self.rmap = torch.zeros(self.n_total, **i32)
             self.ovf = torch.zeros(1, **i32)
-            xw = PP + 4
+            xw = PP * self._bufs[0].element_size() // 4 + 4  # row bytes + 16 tag bytes, in fp32 units
             self.sendbuf = torch.full((R * self.cap, xw), -1, **i32).view(torch.float32)
             self.recvbuf = torch.full((R * self.cap, xw), -1, **i32).view(torch.float32)
             self.stats_all = torch.zeros(R * 6, dtype=torch.int64, device=dev)
@@ -107,7 +149,7 @@ class SoupEngine:
         self.loss = torch.zeros(self.n, dtype=torch.float32, device=dev)
         self.respawn = torch.zeros(self.n, dtype=torch.int8, device=dev)
         self.counts = torch.zeros(6, dtype=torch.int64, device=dev)  # classes[5] + respawns
-        self.cfg = _lib.make_cfg(spec)
+        self.cfg = _lib.make_cfg(spec, self.dtype_code)
         self.recorder = None
         self.stats = False          # classify + all-reduce every generation
         self.stats_with_sec = True
@@ -118,7 +160,7 @@ class SoupEngine:
         if weights is not None:
             w = torch.as_tensor(weights, dtype=torch.float32)
             local.zero_()
-            local[:, : w.shape[1]] = w[self.lo:self.hi].to(dev)
+            local[:, : w.shape[1]] = w[self.lo:self.hi].to(dev, dtype)
         else:
             K.init_rows(spec, local, self.uid, self.seed)
 
@@ -187,9 +229,14 @@ class SoupEngine:
         ca = None
         if self.dist.enabled:
             d = self.dist
-            a.world, a.rank, a.cap = d.world, d.rank, self.cap
-            a.need, a.sendcnt, a.rmap, a.ovf = _p(self.need), _p(self.sendcnt), _p(self.rmap), _p(self.ovf)
-            a.sendbuf, a.recvbuf = _p(self.sendbuf), _p(self.recvbuf)
+            a.world, a.rank = d.world, d.rank
+            if self.exchange == "allgather":
+                a.recvbuf = _p(self.full)
+                a.flags |= _lib.FLAG_FULL_TABLE
+            else:
+                a.cap = self.cap
+                a.need, a.sendcnt, a.rmap, a.ovf = _p(self.need), _p(self.sendcnt), _p(self.rmap), _p(self.ovf)
+                a.sendbuf, a.recvbuf = _p(self.sendbuf), _p(self.recvbuf)
             a.stats, a.census = _p(self.stats_all), _p(self.census)
             ca = self._args()
             ca.n, ca.eps = self.n, self.eps
@@ -219,9 +266,13 @@ class SoupEngine:
         # ---- sharded: decide -> pack -> all-to-all -> unpack -> evolve -> census+respawns -> all-gather -> uids
         d = self.dist
         _lib.run(_lib.OP_SOUP_DECIDE, spec, a, cfg)
-        _lib.run(_lib.OP_SOUP_PACK, spec, a, cfg)
-        d.all_to_all(self.recvbuf, self.sendbuf)
-        _lib.run(_lib.OP_SOUP_UNPACK, spec, a, cfg)
+        if self.exchange == "allgather":
+            # raw 32-bit view: the collective moves bytes whatever the storage dtype
+            d.all_gather_rows(self.full.view(torch.int32), self.table_in.view(torch.int32), self.n_total)
+        else:
+            _lib.run(_lib.OP_SOUP_PACK, spec, a, cfg)
+            d.all_to_all(self.recvbuf, self.sendbuf)
+            _lib.run(_lib.OP_SOUP_UNPACK, spec, a, cfg)
         inline = not (record and self.recorder is not None)
         a.flags = flags | (_lib.FLAG_RESPAWN_INLINE if inline else 0)
         _lib.run(_lib.OP_SOUP_EVOLVE, spec, a, cfg)
@@ -236,7 +287,7 @@ class SoupEngine:
         self._p = 1 - self._p
 
     def exchange_overflowed(self) -> bool:
-        return bool(self.dist.enabled and int(self.ovf.item()) != 0)
+        return bool(self.dist.enabled and self.exchange == "alltoall" and int(self.ovf.item()) != 0)
 
     def classify_local(self, with_sec: bool = True, zero: bool = True):
         if zero:

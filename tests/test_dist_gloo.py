@@ -26,36 +26,41 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, spec_json, out_dir):
+DTYPES = {"float32": torch.float32, "bfloat16": torch.bfloat16, "float16": torch.float16}
+
+
+def _worker(rank, world, port, spec_json, out_dir, dtype="float32", exchange="alltoall"):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         d = Dist(rank, world, 0, None)
         spec = ArchSpec.from_json(spec_json)
-        e = SoupEngine(spec, N_TOTAL, PARAMS, device="cpu", seed=21, dist=d)
+        e = SoupEngine(spec, N_TOTAL, PARAMS, device="cpu", seed=21, dist=d, dtype=DTYPES[dtype], exchange=exchange)
         e.stats = True
         e.evolve(GENS)
         counts = e.count()
         assert not e.exchange_overflowed()
-        np.savez(os.path.join(out_dir, f"r{rank}.npz"), W=e.local_rows().numpy(), uid=e.uid.numpy(),
+        np.savez(os.path.join(out_dir, f"r{rank}.npz"), W=e.local_rows().float().numpy(), uid=e.uid.numpy(),
                  next_uid=e.next_uid.numpy(), counts=np.array([counts[k] for k in sorted(counts)]))
     finally:
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 3, 4])
-def test_sharded_soup_equals_single_rank(tmp_path, world):
+@pytest.mark.parametrize("world,dtype,exchange", [(2, "float32", "alltoall"), (3, "float32", "alltoall"),
+                                                  (4, "float32", "alltoall"), (2, "float32", "allgather"),
+                                                  (2, "bfloat16", "alltoall"), (3, "float16", "allgather")])
+def test_sharded_soup_equals_single_rank(tmp_path, world, dtype, exchange):
     spec = ArchSpec.weightwise(2, 2)
-    ref = SoupEngine(spec, N_TOTAL, PARAMS, device="cpu", seed=21)
+    ref = SoupEngine(spec, N_TOTAL, PARAMS, device="cpu", seed=21, dtype=DTYPES[dtype])
     ref.evolve(GENS)
     ref_counts = ref.count()
-    mp.start_processes(_worker, args=(world, _free_port(), spec.to_json(), str(tmp_path)), nprocs=world,
-                       start_method="spawn", join=True)
+    mp.start_processes(_worker, args=(world, _free_port(), spec.to_json(), str(tmp_path), dtype, exchange),
+                       nprocs=world, start_method="spawn", join=True)
     parts = [np.load(os.path.join(tmp_path, f"r{r}.npz")) for r in range(world)]
     W = np.concatenate([p["W"] for p in parts])
     uid = np.concatenate([p["uid"] for p in parts])
     assert np.array_equal(uid, ref.uid.numpy())
-    assert np.array_equal(W, ref.local_rows().numpy(), equal_nan=True)  # bitwise: per-row math is identical
+    assert np.array_equal(W, ref.local_rows().float().numpy(), equal_nan=True)  # bitwise: per-row math is identical
     for p in parts:
         assert int(p["next_uid"][0]) == int(ref.next_uid[0])
         assert list(p["counts"]) == [ref_counts[k] for k in sorted(ref_counts)]

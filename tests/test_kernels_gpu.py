@@ -210,3 +210,47 @@ def test_mfma_weightwise_identity_fixpoint(cuda):
     before = W.clone()
     cls, _, _ = K.run_fixpoint(spec, W, 5, 1e-4, early_exit=False)
     assert torch.equal(W, before) and cls.tolist() == [O.C_FIX_OTHER] * 4
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16], ids=["bf16", "fp16"])
+@pytest.mark.parametrize("spec", [ArchSpec.weightwise(2, 2), ArchSpec.aggregating(4, 2, 2)], ids=["ww", "agg"])
+def test_lowp_device_equals_rounded_fp32(cuda, spec, dtype):
+    """16-bit tables on the GPU: K fused self-applications == K rounded fp32 steps (bitwise)."""
+    n = 5000
+    uid = torch.arange(n, dtype=torch.int64, device=cuda)
+    W = torch.zeros(n, spec.PP, dtype=dtype, device=cuda)
+    K.init_rows(spec, W, uid, 2)
+    W32 = torch.zeros(n, spec.PP, device=cuda)
+    K.init_rows(spec, W32, uid, 2)
+    assert torch.equal(W, W32.to(dtype))
+    Wk = W.clone()
+    K.run_fixpoint(spec, Wk, 4, 1e-4, early_exit=False)
+    ref = W.clone()
+    for _ in range(4):
+        r = ref.float()
+        K.run_fixpoint(spec, r, 1, 1e-4, early_exit=False)
+        ref = r.to(dtype)
+    nan = lambda t: t.float().nan_to_num(7.0, 9.0, -9.0)
+    assert torch.equal(nan(Wk), nan(ref))
+    Wt, Wt32 = W.clone(), W.float()
+    K.train(spec, Wt, epochs=2, uid=uid, seed=1)
+    K.train(spec, Wt32, epochs=2, uid=uid, seed=1)
+    assert torch.equal(nan(Wt), nan(Wt32.to(dtype)))
+    # device == host path of the same 16-bit kernels
+    Wc = W.cpu()
+    K.run_fixpoint(spec, Wc, 4, 1e-4, early_exit=False)
+    assert (nan(Wc) == nan(Wk.cpu())).float().mean() > 0.999
+
+
+def test_lowp_soup_graph_on_device(cuda):
+    spec = ArchSpec.weightwise(2, 2)
+    params = dict(attacking_rate=0.1, learn_from_rate=0.1, train=5, remove_divergent=True, remove_zero=True)
+    a = SoupEngine(spec, 20_000, params, device=cuda, seed=4, dtype=torch.float16, exchange="allgather")
+    b = SoupEngine(spec, 20_000, params, device=cuda, seed=4, dtype=torch.float16)
+    assert a.capture(warmup=1)
+    b.evolve(1)
+    a.evolve(5)
+    b.evolve(5)
+    assert torch.equal(a.local_rows(), b.local_rows()) and torch.equal(a.uid, b.uid)
+    c = a.count()
+    assert sum(c.values()) == 20_000
