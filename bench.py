@@ -12,6 +12,11 @@ scaling: the population is sharded, every rank owns 100k particles; at N=1 this 
 100k-particle soup).  Random-init weights, fp32 (the reference's dtype; bf16 would make
 the 1e-4 fixpoint test meaningless).
 
+Multi-GPU (N>1): every rank owns 100k particles; one generation is decide -> pack -> ONE
+RCCL all-to-all (partner rows + per-rank stats rows, over xGMI) -> unpack/uids -> evolve
+-> census, captured with the collective inside a hipGraph (validated bitwise against the
+eager path on every rank before use; falls back to eager generations otherwise).
+
 value = particles x generations / second over the whole job (max time over ranks).
 
 Usage: python bench.py --gpus N --steps K --warmup W
@@ -46,7 +51,11 @@ def main():
     ap.add_argument("--backend", default="nccl", help="nccl (= RCCL on ROCm) or gloo (rehearsal)")
     ap.add_argument("--share-device", action="store_true",
                     help="rehearsal on a 1-GPU box: every rank uses cuda:0")
+    ap.add_argument("--force-sharded", action="store_true",
+                    help="rehearsal: run the multi-GPU generation (RCCL all-to-all) even with one rank")
     args = ap.parse_args()
+    if args.force_sharded:
+        os.environ["SRNN_FORCE_SHARDED"] = "1"
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if world != args.gpus:
@@ -102,6 +111,7 @@ def main():
                        "parallelism": f"population-dp{d.world}", "hip_graph": graphed,
                        "census_every_step": eng.stats, "final_census": census},
         }), flush=True)
+    eng.release_graphs()  # graph executables reference the RCCL communicator
     if d.enabled:
         dist.destroy_process_group()
 

@@ -45,7 +45,7 @@ static int dispatch(int op, const SrnnCfg* c, const SrnnArgs* a) {
 
 extern "C" {
 
-int srnn_abi_version() { return 8; }
+int srnn_abi_version() { return 9; }
 
 const char* srnn_last_error() { return srnn::g_err.c_str(); }
 

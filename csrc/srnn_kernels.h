@@ -134,6 +134,24 @@ struct Item {
   static constexpr int PP = Net::PP;
   static constexpr int RB = PP * S::BYTES;  // bytes per table row
   static constexpr int XB = RB + 16;        // exchange row: weights + (slot, gen, -, -) int32 tags
+  // the first SR rows of every destination block of the all-to-all carry the sender's
+  // int64[6] stats (census of its previous generation + respawn count): the per-rank
+  // stats all-gather rides on the row exchange (one collective per generation)
+  static constexpr int SR = (48 + XB - 1) / XB;
+
+  // stats word q of rank r: from the exchange receive buffer (flag 256) or the gathered
+  // [world][6] array
+  SRNN_HD static int64_t stat(const SrnnArgs& a, int r, int q) {
+    if (a.flags & 256)
+      return reinterpret_cast<const int64_t*>(reinterpret_cast<const char*>(a.recvbuf) + (int64_t)r * a.cap * XB)[q];
+    return a.stats[r * 6 + q];
+  }
+  SRNN_HD static void pack_stats(const SrnnArgs& a) {
+    for (int r = 0; r < a.world; ++r) {
+      int64_t* d = reinterpret_cast<int64_t*>(reinterpret_cast<char*>(a.sendbuf) + (int64_t)r * a.cap * XB);
+      for (int q = 0; q < 6; ++q) d[q] = (int64_t)a.counts[q];
+    }
+  }
 
   SRNN_HD static char* rowp(float* base, int64_t i) { return reinterpret_cast<char*>(base) + i * RB; }
   SRNN_HD static const char* rowp(const float* base, int64_t i) { return reinterpret_cast<const char*>(base) + i * RB; }
@@ -425,6 +443,7 @@ struct Item {
   }
   // sharded soup: received row k -> rmap[slot]; rows of older generations are ignored
   SRNN_HD static void soup_unpack(const SrnnArgs& a, int64_t k) {
+    if (k % a.cap < SR) return;  // stats rows
     const int32_t* tag = reinterpret_cast<const int32_t*>(reinterpret_cast<const char*>(a.recvbuf) + k * XB + RB);
     if (tag[1] == gen_of(a)) a.rmap[tag[0]] = (int32_t)k;
   }
@@ -535,9 +554,13 @@ __global__ __launch_bounds__(TB) void k_op(SrnnCfg c, SrnnArgs a) {
     if (i < a.n_total) I::soup_decide(a, i);
     return;
   } else if constexpr (OP == OP_SOUP_UNPACK) {
-    if (i == 0)
-      for (int r = 0; r < a.world; ++r) a.sendcnt[r] = 0;  // packing of this generation is complete
+    if (i == 0)  // packing of this generation is complete; data rows follow the stats rows
+      for (int r = 0; r < a.world; ++r) a.sendcnt[r] = I::SR;
     if (i < (int64_t)a.world * a.cap) I::soup_unpack(a, i);
+    return;
+  } else if constexpr (OP == OP_SOUP_PACK) {
+    if (i == 0) I::pack_stats(a);
+    if (i < a.n) I::soup_pack(a, i);
     return;
   } else if constexpr (OP == OP_CLASSIFY) {
     if (i < a.n) I::classify(c, a, i, perm);  // histogram: k_classify_count
@@ -552,7 +575,6 @@ __global__ __launch_bounds__(TB) void k_op(SrnnCfg c, SrnnArgs a) {
     else if constexpr (OP == OP_PERTURB) I::perturb(c, a, i, samp, perm);
     else if constexpr (OP == OP_RESPAWN) I::respawn(a, i);
     else if constexpr (OP == OP_VARY_RUN) I::vary_run(c, a, i, samp, perm);
-    else if constexpr (OP == OP_SOUP_PACK) I::soup_pack(a, i);
   }
 }
 
@@ -609,11 +631,15 @@ __global__ __launch_bounds__(TBC) void k_classify_count(SrnnCfg c, SrnnArgs a) {
     unsigned long long m = __ballot(i < a.n && a.respawn[i] != 0);
     if ((threadIdx.x & 63) == 0 && m) atomicAdd(a.counts + 5, (uint64_t)__popcll(m));
   }
+  // sharded soup: the census closes the generation (no later kernel of this generation
+  // reads the counter)
+  if ((a.flags & 512) && blockIdx.x == 0 && threadIdx.x == 0) ((int32_t*)a.gen_ptr)[0] += 1;
 }
 
 template <class Net, int OP, class S>
 int launch(const SrnnCfg& c, const SrnnArgs& a) {
   int64_t items = (OP == OP_SOUP_DECIDE) ? a.n_total : (OP == OP_SOUP_UNPACK) ? (int64_t)a.world * a.cap : a.n;
+  if (OP == OP_SOUP_PACK && items < 1) items = 1;  // the stats rows are always written
   if (items <= 0) return 0;
   int64_t blocks = (items + TB - 1) / TB;
   if (blocks > 0x7fffffffLL) {
@@ -645,7 +671,7 @@ int host_run(const SrnnCfg& c, const SrnnArgs& a) {
   constexpr int P = Net::P;
   int64_t items = (OP == OP_SOUP_DECIDE) ? a.n_total : (OP == OP_SOUP_UNPACK) ? (int64_t)a.world * a.cap : a.n;
   if (OP == OP_SOUP_UNPACK)
-    for (int r = 0; r < a.world; ++r) a.sendcnt[r] = 0;
+    for (int r = 0; r < a.world; ++r) a.sendcnt[r] = I::SR;
   if (OP == OP_CLASSIFY && a.counts) {
     uint64_t local[5] = {0, 0, 0, 0, 0};
     std::vector<int8_t> ks((size_t)items);
@@ -657,6 +683,12 @@ int host_run(const SrnnCfg& c, const SrnnArgs& a) {
     for (int q = 0; q < 5; ++q) a.counts[q] += local[q];
     if (a.flags & 64)
       for (int64_t i = 0; i < items; ++i) a.counts[5] += a.respawn[i] != 0;
+    if (a.flags & 512) ((int32_t*)a.gen_ptr)[0] += 1;
+    return 0;
+  }
+  if (OP == OP_SOUP_PACK) {
+    I::pack_stats(a);
+    host_parallel(a.n, [&](int64_t i) { I::soup_pack(a, i); });
     return 0;
   }
   host_parallel(items, [&](int64_t i) {
@@ -758,31 +790,32 @@ int respawn_seq(const SrnnCfg& c, const SrnnArgs& a) {
   return 0;
 }
 
-// Sharded soup: uids of this generation's newborns.  The gathered per-rank stats give
-// the respawn counts of lower ranks (globally sequential uids, reference S13) and the
-// global census; the 64-bit respawn ballots of the evolve waves give the local order.
-// Also advances next_uid (*uid_base), the generation counter and zeroes counts[0..5].
-template <class Net>
+// Sharded soup: uids of the newborns of the previous generation.  The per-rank stats
+// (the exchange's stats rows, flag 256, or the gathered [world][6] array) give the
+// respawn counts of lower ranks (globally sequential uids, reference S13) and the global
+// census; the 64-bit respawn ballots of the evolve waves give the local order.  Consumes
+// the ballots (zeroed), advances next_uid (*uid_base) and zeroes counts[0..5]; with no
+// stats pending (all zero) it is a no-op apart from that.
+template <class Net, class S>
 __global__ __launch_bounds__(TBR) void k_uid_assign(SrnnCfg c, SrnnArgs a) {
+  using I = Item<Net, S>;
   __shared__ int32_t s_cnt[TBR];
   __shared__ int64_t s_prefix, s_total;
   if (threadIdx.x == 0) {
-    int64_t pre = 0, tot = 0;
+    int64_t pre = 0, tot = 0, cen[5] = {0, 0, 0, 0, 0}, all = 0;
     for (int r = 0; r < a.world; ++r) {
-      const int64_t k = a.stats[r * 6 + 5];
+      const int64_t k = I::stat(a, r, 5);
       if (r < a.rank) pre += k;
       tot += k;
+      for (int q = 0; q < 5; ++q) cen[q] += I::stat(a, r, q);
     }
+    for (int q = 0; q < 5; ++q) all += cen[q];
     s_prefix = pre;
     s_total = tot;
-    if (a.census)
-      for (int q = 0; q < 5; ++q) {
-        int64_t v = 0;
-        for (int r = 0; r < a.world; ++r) v += a.stats[r * 6 + q];
-        a.census[q] = v;
-      }
+    if (a.census && all > 0)
+      for (int q = 0; q < 5; ++q) a.census[q] = cen[q];
   }
-  const unsigned long long* masks = reinterpret_cast<const unsigned long long*>(a.i32c);
+  unsigned long long* masks = reinterpret_cast<unsigned long long*>(a.i32c);
   const int64_t nb = (a.n + TB - 1) / TB;
   const int64_t ch = (nb + TBR - 1) / TBR;
   const int64_t b0 = (int64_t)threadIdx.x * ch;
@@ -801,6 +834,7 @@ __global__ __launch_bounds__(TBR) void k_uid_assign(SrnnCfg c, SrnnArgs a) {
   int64_t k = base + s_prefix + s_cnt[threadIdx.x] - cnt;
   for (int64_t b = b0; b < b1 && cnt; ++b) {
     unsigned long long m = masks[b];
+    masks[b] = 0ull;
     while (m) {
       const int bit = __ffsll((long long)m) - 1;
       m &= m - 1;
@@ -808,17 +842,15 @@ __global__ __launch_bounds__(TBR) void k_uid_assign(SrnnCfg c, SrnnArgs a) {
     }
   }
   __syncthreads();
-  if (threadIdx.x == 0) {
-    ((int64_t*)a.uid_base)[0] = base + s_total;
-    if (a.gen_ptr) ((int32_t*)a.gen_ptr)[0] += 1;
-  }
+  if (threadIdx.x == 0) ((int64_t*)a.uid_base)[0] = base + s_total;
   if (a.counts && threadIdx.x < 6) a.counts[threadIdx.x] = 0;
 }
 
-template <class Net>
+template <class Net, class S>
 int uid_assign(const SrnnCfg& c, const SrnnArgs& a) {
+  using I = Item<Net, S>;
   if (a.dev) {
-    hipLaunchKernelGGL((k_uid_assign<Net>), dim3(1), dim3(TBR), 0, (hipStream_t)a.stream, c, a);
+    hipLaunchKernelGGL((k_uid_assign<Net, S>), dim3(1), dim3(TBR), 0, (hipStream_t)a.stream, c, a);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) {
       set_error(hipGetErrorString(e));
@@ -826,23 +858,24 @@ int uid_assign(const SrnnCfg& c, const SrnnArgs& a) {
     }
     return 0;
   }
-  int64_t pre = 0, tot = 0;
+  int64_t pre = 0, tot = 0, cen[5] = {0, 0, 0, 0, 0}, all = 0;
   for (int r = 0; r < a.world; ++r) {
-    const int64_t k = a.stats[r * 6 + 5];
+    const int64_t k = I::stat(a, r, 5);
     if (r < a.rank) pre += k;
     tot += k;
+    for (int q = 0; q < 5; ++q) cen[q] += I::stat(a, r, q);
   }
-  if (a.census)
-    for (int q = 0; q < 5; ++q) {
-      int64_t v = 0;
-      for (int r = 0; r < a.world; ++r) v += a.stats[r * 6 + q];
-      a.census[q] = v;
-    }
+  for (int q = 0; q < 5; ++q) all += cen[q];
+  if (a.census && all > 0)
+    for (int q = 0; q < 5; ++q) a.census[q] = cen[q];
+  // host path: per-row respawn flags in i32c (evolve with flag 16), consumed here
   int64_t k = a.uid_base[0] + pre;
   for (int64_t i = 0; i < a.n; ++i)
-    if (a.respawn[i]) a.uid_out[i] = k++;
+    if (a.i32c[i]) {
+      a.uid_out[i] = k++;
+      a.i32c[i] = 0;
+    }
   ((int64_t*)a.uid_base)[0] += tot;
-  if (a.gen_ptr) ((int32_t*)a.gen_ptr)[0] += 1;
   if (a.counts)
     for (int q = 0; q < 6; ++q) a.counts[q] = 0;
   return 0;
@@ -867,7 +900,7 @@ int run_net_op(int op, const SrnnCfg& c, const SrnnArgs& a) {
     case OP_RESPAWN_SEQ: return respawn_seq<Net, S>(c, a);
     case OP_SOUP_PACK: return run_one<Net, OP_SOUP_PACK, S>(c, a);
     case OP_SOUP_UNPACK: return run_one<Net, OP_SOUP_UNPACK, S>(c, a);
-    case OP_UID_ASSIGN: return uid_assign<Net>(c, a);
+    case OP_UID_ASSIGN: return uid_assign<Net, S>(c, a);
     case OP_SOUP_EVOLVE: return run_one<Net, OP_SOUP_EVOLVE, S>(c, a);
     case OP_RESPAWN: return run_one<Net, OP_RESPAWN, S>(c, a);
     case OP_VARY_RUN: return run_one<Net, OP_VARY_RUN, S>(c, a);

@@ -19,7 +19,7 @@ import threading
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libsrnn.so")
 CSRC = os.path.normpath(os.path.join(_HERE, "..", "..", "csrc"))
-ABI_VERSION = 8
+ABI_VERSION = 9
 
 OP_INIT = 0
 OP_APPLY = 1
@@ -46,6 +46,8 @@ FLAG_ROW_FLAGS = 16
 FLAG_RESPAWN_INLINE = 32
 FLAG_COUNT_RESPAWNS = 64
 FLAG_FULL_TABLE = 128
+FLAG_STATS_X = 256
+FLAG_GEN_ADVANCE = 512
 
 
 class SrnnCfg(ctypes.Structure):

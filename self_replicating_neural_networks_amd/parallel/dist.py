@@ -25,11 +25,14 @@ class Dist:
     world: int = 1
     local_rank: int = 0
     group: Optional[object] = None
+    # run the sharded code path (collectives included) even with one rank: rehearses the
+    # multi-GPU generation -- and its hipGraph capture with RCCL -- on a one-GPU box
+    force: bool = False
     _pad_bufs: dict = dataclasses.field(default_factory=dict, repr=False)
 
     @property
     def enabled(self) -> bool:
-        return self.world > 1
+        return self.world > 1 or self.force
 
     def shard(self, n_total: int):
         """Contiguous [lo, hi) rows of this rank (sizes differ by at most one)."""
@@ -106,8 +109,14 @@ def from_env(backend: Optional[str] = None, device_type: str = "cuda") -> Dist:
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    if world <= 1:
+    force = os.environ.get("SRNN_FORCE_SHARDED") == "1"
+    if world <= 1 and not force:
         return Dist(0, 1, 0, None)
+    if world <= 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29533")
+        os.environ.setdefault("RANK", "0")
+        os.environ.setdefault("WORLD_SIZE", "1")
     if not dist.is_initialized():
         if backend is None:
             backend = "nccl" if device_type == "cuda" else "gloo"
@@ -117,7 +126,7 @@ def from_env(backend: Optional[str] = None, device_type: str = "cuda") -> Dist:
             torch.cuda.set_device(dev_idx)
             kw["device_id"] = torch.device("cuda", dev_idx)
         dist.init_process_group(backend=backend, **kw)
-    return Dist(dist.get_rank(), dist.get_world_size(), local_rank, None)
+    return Dist(dist.get_rank(), dist.get_world_size(), local_rank, None, force=force)
 
 
 def current() -> Dist:

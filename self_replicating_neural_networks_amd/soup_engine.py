@@ -125,12 +125,15 @@ class SoupEngine:
             lr_ = max(float(self.params.get("learn_from_rate", 0.1)), 0.0)
             n_max = -(-self.n_total // R)  # identical on every rank (buffers must match)
             mean = n_max * min(ar + lr_, 2.0) / R
-            self.cap = int(min(max(mean * 1.2 + 6.0 * mean ** 0.5 + 32, 32), max(n_max, 32)))
+            xw = PP * self._bufs[0].element_size() // 4 + 4  # row bytes + 16 tag bytes, in fp32 units
+            # the first `stat_rows` rows of each destination block carry the sender's
+            # int64[6] stats (previous census + respawns): one collective per generation
+            self.stat_rows = -(-48 // (4 * xw))
+            self.cap = self.stat_rows + int(min(max(mean * 1.2 + 6.0 * mean ** 0.5 + 32, 32), max(n_max, 32)))
             self.need = torch.zeros(self.n, **i32)
-            self.sendcnt = torch.zeros(R, **i32)
+            self.sendcnt = torch.full((R,), self.stat_rows, **i32)
             self.rmap = torch.zeros(self.n_total, **i32)
             self.ovf = torch.zeros(1, **i32)
-            xw = PP * self._bufs[0].element_size() // 4 + 4  # row bytes + 16 tag bytes, in fp32 units
             self.sendbuf = torch.full((R * self.cap, xw), -1, **i32).view(torch.float32)
             self.recvbuf = torch.full((R * self.cap, xw), -1, **i32).view(torch.float32)
             self.stats_all = torch.zeros(R * 6, dtype=torch.int64, device=dev)
@@ -142,7 +145,9 @@ class SoupEngine:
         self.time = 0
         self.head = torch.full((self.n,), -1, **i32)       # first attacker of each local victim
         self.next_att = torch.full((self.n_total,), -1, **i32)  # attacker -> next attacker of its victim
-        self.flags32 = torch.zeros(self.n, **i32)
+        # per-row respawn flags (host) or 64-bit respawn ballots per 64-row wave (device)
+        self.flags32 = torch.zeros(max(self.n, 2 * (-(-self.n // 64))), **i32)
+        self._pending = False  # sharded: uids of the last generation's newborns not yet assigned
         self.off = torch.zeros(self.n + 1, **i32)
         self.action = torch.zeros(self.n, dtype=torch.int8, device=dev)
         self.counterpart = torch.full((self.n,), -1, dtype=torch.int64, device=dev)
@@ -240,7 +245,8 @@ class SoupEngine:
             a.stats, a.census = _p(self.stats_all), _p(self.census)
             ca = self._args()
             ca.n, ca.eps = self.n, self.eps
-            ca.flags = (_lib.FLAG_FIX_SEC if self.stats_with_sec else 0) | _lib.FLAG_COUNT_RESPAWNS
+            ca.flags = ((_lib.FLAG_FIX_SEC if self.stats_with_sec else 0) | _lib.FLAG_COUNT_RESPAWNS
+                        | _lib.FLAG_GEN_ADVANCE)
             ca.W, ca.counts, ca.respawn, ca.uid = _p(self.rows_out), _p(self.counts), _p(self.respawn), _p(self.uid)
             ca.ctr = 0x7FFFFFF0
         self._arg_cache[key] = (a, ca, a.flags)
@@ -263,7 +269,12 @@ class SoupEngine:
                 # per-generation fixpoint-fraction statistics (reference Soup.count, code/soup.py:89-103)
                 self.classify_local(self.stats_with_sec, zero=False)
             return
-        # ---- sharded: decide -> pack -> all-to-all -> unpack -> evolve -> census+respawns -> all-gather -> uids
+        # ---- sharded (all-to-all, ONE collective per generation):
+        #   decide -> pack (stats rows of the previous generation + rows other ranks need)
+        #   -> all-to-all -> unpack + uids of the previous generation's newborns
+        #   -> evolve -> census + respawn count (+ generation counter)
+        # ---- sharded (all-gather): decide -> all-gather rows -> evolve -> census
+        #   -> all-gather stats -> uids
         d = self.dist
         _lib.run(_lib.OP_SOUP_DECIDE, spec, a, cfg)
         if self.exchange == "allgather":
@@ -273,6 +284,8 @@ class SoupEngine:
             _lib.run(_lib.OP_SOUP_PACK, spec, a, cfg)
             d.all_to_all(self.recvbuf, self.sendbuf)
             _lib.run(_lib.OP_SOUP_UNPACK, spec, a, cfg)
+            a.flags = flags | _lib.FLAG_STATS_X
+            _lib.run(_lib.OP_UID_ASSIGN, spec, a, cfg)
         inline = not (record and self.recorder is not None)
         a.flags = flags | (_lib.FLAG_RESPAWN_INLINE if inline else 0)
         _lib.run(_lib.OP_SOUP_EVOLVE, spec, a, cfg)
@@ -280,11 +293,25 @@ class SoupEngine:
         if not inline:
             self.recorder.on_evolved(self)
             _lib.run(_lib.OP_RESPAWN, spec, a, cfg)
-        # census of the new generation + this rank's respawn count -> every rank
+        # census of the new generation + this rank's respawn count; advances the generation
         _lib.run(_lib.OP_CLASSIFY, spec, ca, cfg)
-        d.all_gather_into(self.stats_all, self.counts)
-        _lib.run(_lib.OP_UID_ASSIGN, spec, a, cfg)
         self._p = 1 - self._p
+        if self.exchange == "allgather":
+            self._pending = True
+            self._flush()
+        else:
+            self._pending = True
+
+    def _flush(self):
+        """Sharded: assign the uids of the last generation's newborns now (all-gather of
+        the per-rank stats) instead of with the next generation's row exchange."""
+        if not (self.dist.enabled and self._pending):
+            return
+        a, _, flags = self._gen_args()
+        a.flags = flags
+        self.dist.all_gather_into(self.stats_all, self.counts)
+        _lib.run(_lib.OP_UID_ASSIGN, self.spec, a, self.cfg)
+        self._pending = False
 
     def exchange_overflowed(self) -> bool:
         return bool(self.dist.enabled and self.exchange == "alltoall" and int(self.ovf.item()) != 0)
@@ -316,12 +343,15 @@ class SoupEngine:
             if record and self.recorder is not None:
                 slot_uid = self.global_uids()  # uid of every slot at generation start
                 self._generation(record=True)
+                self._flush()
                 self.recorder.on_generation_end(self, self.time, slot_uid)
             elif self._graphs is not None:
                 self._graphs[self._p].replay()
                 self._p = 1 - self._p
+                self._pending = self.dist.enabled
             else:
                 self._generation()
+        self._flush()  # uids / census consistent between evolve calls
         return self
 
     def global_uids(self):
@@ -333,28 +363,104 @@ class SoupEngine:
         return out.cpu().numpy()
 
     # ------------------------------------------------------------------ HIP graphs
-    def capture(self, warmup: int = 1) -> bool:
-        """Capture the generation for both ping-pong parities in two hipGraphs (single
-        rank, ROCm device).  Everything that changes per generation lives in device
-        memory (generation counter, next uid), so replays advance the soup exactly like
-        the eager path."""
-        if self.device.type != "cuda" or self.dist.enabled:
+    def _state(self):
+        """Every device tensor a generation reads or writes (graph validation)."""
+        names = ["_bufs", "uid", "next_uid", "gen_dev", "head", "next_att", "flags32", "action", "counterpart",
+                 "loss", "respawn", "counts", "census", "need", "sendcnt", "rmap", "ovf", "sendbuf", "recvbuf",
+                 "full", "stats_all"]
+        out = []
+        for k in names:
+            v = getattr(self, k, None)
+            if isinstance(v, list):
+                out.extend(v)
+            elif isinstance(v, torch.Tensor):
+                out.append(v)
+        return out
+
+    def capture(self, warmup: int = 1, validate: bool = True) -> bool:
+        """Capture the generation for both ping-pong parities in two hipGraphs (ROCm
+        device).  Everything that changes per generation lives in device memory
+        (generation counter, next uid), so replays advance the soup exactly like the
+        eager path.  Sharded engines capture their RCCL collective inside the graph (one
+        all-to-all per generation, exchange="alltoall" only); ``validate`` then replays
+        two generations from a saved state, compares them bitwise with the eager path on
+        every rank and keeps the graphs only if all ranks agree."""
+        if self.device.type != "cuda":
+            return False
+        if self.dist.enabled and self.exchange != "alltoall":
+            return False
+        if self.dist.enabled and torch.distributed.get_backend() != "nccl":
             return False
         s = torch.cuda.Stream(self.device)
         s.wait_stream(torch.cuda.current_stream(self.device))
         with torch.cuda.stream(s):
-            for _ in range(max(warmup, 0)):
+            for _ in range(max(warmup, 1 if self.dist.enabled else 0)):
                 self.time += 1
                 self._generation()
         torch.cuda.current_stream(self.device).wait_stream(s)
         graphs = []
         p0 = self._p
-        for _ in range(2):
-            g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g, stream=s):
-                self._generation()  # flips self._p during capture (nothing ran)
-            graphs.append(g)
+        pend0 = self._pending
+        ok = True
+        try:
+            for _ in range(2):
+                g = torch.cuda.CUDAGraph()
+                # thread_local: the process group's watchdog thread keeps querying events
+                with torch.cuda.graph(g, stream=s, capture_error_mode="thread_local"):
+                    self._generation()  # flips self._p during capture (nothing ran)
+                graphs.append(g)
+        except Exception as e:  # noqa: BLE001 -- any capture failure -> eager generations
+            import sys
+            print(f"soup graph capture failed ({type(e).__name__}: {e}); running eagerly", file=sys.stderr)
+            ok = False
         self._p = p0
+        self._pending = pend0
+        if ok and self.dist.enabled and validate:
+            ok = self._validate_graphs(graphs if p0 == 0 else graphs[::-1])
+        if self.dist.enabled:
+            flag = torch.tensor([1 if ok else 0], dtype=torch.int32, device=self.device)
+            torch.distributed.all_reduce(flag, op=torch.distributed.ReduceOp.MIN)
+            ok = bool(flag.item())
+        if not ok:
+            self._graphs = None
+            return False
         # graphs[k] was captured with parity p0 ^ k; index them by parity
         self._graphs = graphs if p0 == 0 else graphs[::-1]
         return True
+
+    def release_graphs(self):
+        """Drop the captured graphs (before tearing down the process group: an RCCL
+        communicator must not be destroyed while graph executables still reference it)."""
+        if self._graphs is not None:
+            torch.cuda.synchronize(self.device)
+            for g in self._graphs:
+                g.reset()
+            self._graphs = None
+
+    def _validate_graphs(self, graphs) -> bool:
+        state = self._state()
+        saved = [t.clone() for t in state]
+        p0, pend0, t0 = self._p, self._pending, self.time
+        for _ in range(2):
+            self._generation()
+        torch.cuda.synchronize(self.device)
+        eager = [t.clone() for t in state]
+        for t, v in zip(state, saved):
+            t.copy_(v)
+        self._p, self._pending = p0, pend0
+        for _ in range(2):
+            graphs[self._p].replay()
+            self._p = 1 - self._p
+        torch.cuda.synchronize(self.device)
+        # compare the semantic state only: exchange-buffer row order and the attack
+        # lists' link order follow atomics and legitimately differ between runs
+        keep = {id(t) for t in self._bufs} | {id(getattr(self, k)) for k in (
+            "uid", "next_uid", "gen_dev", "counts", "census", "loss", "respawn", "action", "counterpart",
+            "flags32", "ovf") if isinstance(getattr(self, k, None), torch.Tensor)}
+        same = all(torch.equal(x.view(torch.uint8), y.view(torch.uint8))
+                   for x, y in zip(state, eager) if id(x) in keep)
+        for t, v in zip(state, saved):
+            t.copy_(v)
+        self._p, self._pending, self.time = p0, pend0, t0
+        torch.cuda.synchronize(self.device)
+        return same

@@ -29,15 +29,16 @@ def _free_port():
 DTYPES = {"float32": torch.float32, "bfloat16": torch.bfloat16, "float16": torch.float16}
 
 
-def _worker(rank, world, port, spec_json, out_dir, dtype="float32", exchange="alltoall"):
+def _worker(rank, world, port, spec_json, out_dir, dtype="float32", exchange="alltoall", chunks=(GENS,)):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        d = Dist(rank, world, 0, None)
+        d = Dist(rank, world, 0, None, force=world == 1)
         spec = ArchSpec.from_json(spec_json)
         e = SoupEngine(spec, N_TOTAL, PARAMS, device="cpu", seed=21, dist=d, dtype=DTYPES[dtype], exchange=exchange)
         e.stats = True
-        e.evolve(GENS)
+        for k in chunks:  # uids of the newborns are settled between evolve calls
+            e.evolve(k)
         counts = e.count()
         assert not e.exchange_overflowed()
         np.savez(os.path.join(out_dir, f"r{rank}.npz"), W=e.local_rows().float().numpy(), uid=e.uid.numpy(),
@@ -46,15 +47,17 @@ def _worker(rank, world, port, spec_json, out_dir, dtype="float32", exchange="al
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,dtype,exchange", [(2, "float32", "alltoall"), (3, "float32", "alltoall"),
-                                                  (4, "float32", "alltoall"), (2, "float32", "allgather"),
-                                                  (2, "bfloat16", "alltoall"), (3, "float16", "allgather")])
-def test_sharded_soup_equals_single_rank(tmp_path, world, dtype, exchange):
+@pytest.mark.parametrize("world,dtype,exchange,chunks", [
+    (2, "float32", "alltoall", (GENS,)), (3, "float32", "alltoall", (1, 2, 3)), (4, "float32", "alltoall", (GENS,)),
+    (2, "float32", "allgather", (2, 4)), (2, "bfloat16", "alltoall", (GENS,)), (3, "float16", "allgather", (GENS,)),
+    (1, "float32", "alltoall", (2, 1, 3))])
+def test_sharded_soup_equals_single_rank(tmp_path, world, dtype, exchange, chunks):
+    """world 1 = the forced sharded path (collectives over a one-rank group)."""
     spec = ArchSpec.weightwise(2, 2)
     ref = SoupEngine(spec, N_TOTAL, PARAMS, device="cpu", seed=21, dtype=DTYPES[dtype])
     ref.evolve(GENS)
     ref_counts = ref.count()
-    mp.start_processes(_worker, args=(world, _free_port(), spec.to_json(), str(tmp_path), dtype, exchange),
+    mp.start_processes(_worker, args=(world, _free_port(), spec.to_json(), str(tmp_path), dtype, exchange, chunks),
                        nprocs=world, start_method="spawn", join=True)
     parts = [np.load(os.path.join(tmp_path, f"r{r}.npz")) for r in range(world)]
     W = np.concatenate([p["W"] for p in parts])
