@@ -2,7 +2,9 @@
 #include "srnn_kernels.h"
 #include <hipcub/hipcub.hpp>
 #include <cstring>
+#include <cstdlib>
 #include <string>
+#include <dlfcn.h>
 
 namespace srnn {
 static thread_local std::string g_err;
@@ -22,6 +24,50 @@ __global__ void k_scan_tail(int32_t* out, const int32_t* in, int64_t n) {
   (void)in;
   (void)n;
 }
+
+// ---- tracing / checking hooks, read once from the environment:
+//   SRNN_ROCTX=1       one roctx range per operator launch (rocprofv3 --marker-trace),
+//                      roctx resolved with dlopen (no link dependency)
+//   SRNN_SYNC_CHECK=1  synchronise the stream after every device operator and report a
+//                      fault at the operator that caused it (like HIP_LAUNCH_BLOCKING)
+namespace {
+typedef int (*push_fn)(const char*);
+typedef int (*pop_fn)();
+struct Hooks {
+  push_fn push = nullptr;
+  pop_fn pop = nullptr;
+  bool sync = false;
+  Hooks() {
+    const char* r = std::getenv("SRNN_ROCTX");
+    if (r && r[0] == '1') {
+      const char* libs[] = {"librocprofiler-sdk-roctx.so.1", "librocprofiler-sdk-roctx.so", "libroctx64.so.4",
+                            "libroctx64.so"};
+      for (const char* l : libs) {
+        void* h = dlopen(l, RTLD_NOW | RTLD_LOCAL);
+        if (!h) continue;
+        push = (push_fn)dlsym(h, "roctxRangePushA");
+        pop = (pop_fn)dlsym(h, "roctxRangePop");
+        if (push && pop) break;
+        push = nullptr;
+        pop = nullptr;
+      }
+    }
+    const char* sc = std::getenv("SRNN_SYNC_CHECK");
+    sync = sc && sc[0] == '1';
+  }
+};
+const Hooks& hooks() {
+  static Hooks h;
+  return h;
+}
+const char* op_name(int op) {
+  static const char* names[] = {"srnn:init",       "srnn:apply",        "srnn:run_fixpoint", "srnn:train",
+                                "srnn:learn",      "srnn:classify",     "srnn:perturb",      "srnn:soup_decide",
+                                "srnn:respawn_seq", "srnn:soup_evolve", "srnn:scan",         "srnn:respawn",
+                                "srnn:vary_run",   "srnn:soup_pack",    "srnn:soup_unpack",  "srnn:uid_assign"};
+  return (op >= 0 && op < (int)(sizeof(names) / sizeof(names[0]))) ? names[op] : "srnn:op";
+}
+}  // namespace
 
 static int dispatch(int op, const SrnnCfg* c, const SrnnArgs* a) {
   if (c->dtype != 0) {
@@ -90,8 +136,24 @@ int srnn_run(int op, const SrnnCfg* cfg, const SrnnArgs* a) {
     }
     return 0;
   }
+  const Hooks& h = hooks();
+  if (h.push) h.push(op_name(op));
   int r = dispatch(op, cfg, a);
   if (r == 1) srnn::set_error("network shape not instantiated in libsrnn (add it to csrc/srnn_<kind>.hip)");
+  if (r == 0 && h.sync && a->dev) {
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    (void)hipStreamIsCapturing((hipStream_t)a->stream, &cs);
+    if (cs == hipStreamCaptureStatusNone) {
+      hipError_t e = hipStreamSynchronize((hipStream_t)a->stream);
+      if (e == hipSuccess) e = hipGetLastError();
+      if (e != hipSuccess) {
+        std::string m = std::string(op_name(op)) + ": " + hipGetErrorString(e);
+        srnn::set_error(m.c_str());
+        r = -5;
+      }
+    }
+  }
+  if (h.pop) h.pop();
   return r;
 }
 

@@ -1,0 +1,211 @@
+// host_selftest.cpp — native self-test of libsrnn's host path through the C ABI, built
+// under AddressSanitizer+UBSan (`make -C csrc asan`) or ThreadSanitizer (`make -C csrc
+// tsan`) (sanitizers on host code; GPU sanitizers are not available on the
+// pool).  It exercises every operator on host tables with the host thread pool, and
+// rehearses the sharded soup generation for R = 2 and 3 in one process (the all-to-all is
+// a memcpy between the ranks' buffers), checking bitwise equality with the single-rank
+// generation (the R-invariance the multi-GPU path relies on).
+#include "../srnn_abi.h"
+
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <vector>
+
+static int g_fail = 0;
+#define CHECK(c)                                                   \
+  do {                                                             \
+    if (!(c)) {                                                    \
+      std::fprintf(stderr, "CHECK failed %s:%d: %s\n", __FILE__, __LINE__, #c); \
+      ++g_fail;                                                    \
+    }                                                              \
+  } while (0)
+
+static void run(int op, const SrnnCfg& c, const SrnnArgs& a) {
+  int r = srnn_run(op, &c, &a);
+  if (r != 0) {
+    std::fprintf(stderr, "srnn_run(%d) = %d: %s\n", op, r, srnn_last_error());
+    ++g_fail;
+  }
+}
+
+static SrnnCfg ww22() {
+  SrnnCfg c{};
+  c.kind = 0, c.width = 2, c.depth = 2, c.aggregates = 0, c.aggregator = 0, c.shuffler = 0, c.pp = 16, c.p = 14;
+  c.dtype = 0;
+  return c;
+}
+static SrnnCfg agg422() {
+  SrnnCfg c{};
+  c.kind = 1, c.width = 2, c.depth = 2, c.aggregates = 4, c.aggregator = 0, c.shuffler = 0, c.pp = 20, c.p = 20;
+  c.dtype = 0;
+  return c;
+}
+
+static void ops_smoke(const SrnnCfg& c, int64_t n) {
+  const int PP = c.pp;
+  std::vector<float> W((size_t)(n * PP), 0.f), O((size_t)(n * PP), 0.f);
+  std::vector<int64_t> uid((size_t)n), idx((size_t)n);
+  for (int64_t i = 0; i < n; ++i) uid[(size_t)i] = i + 7, idx[(size_t)i] = (i + 1) % n;
+  std::vector<int8_t> cls((size_t)n);
+  std::vector<int32_t> nsteps((size_t)n);
+  std::vector<float> loss((size_t)n);
+  uint64_t counts[6] = {0, 0, 0, 0, 0, 0};
+  SrnnArgs a{};
+  a.n = n, a.seed = 11, a.W = W.data(), a.uid = uid.data(), a.dev = 0, a.lr = 0.01f, a.eps = 1e-4f;
+  run(OP_INIT, c, a);
+  bool finite = true;
+  for (int64_t i = 0; i < n; ++i)
+    for (int k = 0; k < c.p; ++k) finite &= std::isfinite(W[(size_t)(i * PP + k)]);
+  CHECK(finite);
+  SrnnArgs b = a;
+  b.W2 = O.data(), b.idx_f = idx.data();
+  run(OP_APPLY, c, b);
+  SrnnArgs t = a;
+  t.epochs = 3, t.flags = 1, t.loss = loss.data();
+  run(OP_TRAIN, c, t);
+  SrnnArgs l = t;
+  l.W2 = O.data(), l.idx_t = idx.data();
+  run(OP_LEARN, c, l);
+  SrnnArgs f = a;
+  f.steps = 20, f.early_exit = 1, f.flags = 8, f.cls = cls.data(), f.nsteps = nsteps.data();
+  run(OP_RUN_FIXPOINT, c, f);
+  SrnnArgs k = a;
+  k.flags = 8, k.cls = cls.data(), k.counts = counts;
+  run(OP_CLASSIFY, c, k);
+  CHECK((int64_t)(counts[0] + counts[1] + counts[2] + counts[3] + counts[4]) == n);
+  SrnnArgs p = a;
+  p.eps = 1e-3f;
+  run(OP_PERTURB, c, p);
+}
+
+// ---- one soup over R ranks (R = 1: the single-rank pipeline) --------------------------
+struct RankSoup {
+  int64_t lo, hi, n;
+  std::vector<float> buf[2];
+  std::vector<int64_t> uid;
+  std::vector<int32_t> head, next_att, flags, need, sendcnt, rmap, ovf;
+  std::vector<int8_t> action, respawn;
+  std::vector<int64_t> counterpart, census, next_uid, stats;
+  std::vector<float> loss, sendbuf, recvbuf;
+  std::vector<int32_t> gen;
+  std::vector<uint64_t> counts;
+};
+
+static std::vector<float> soup(int R, int64_t N, int gens, std::vector<int64_t>* uids_out, int64_t* next_out) {
+  const SrnnCfg c = ww22();
+  const int PP = c.pp;
+  const int XB = PP * 4 + 16, SR = (48 + XB - 1) / XB, XW = XB / 4;
+  const int64_t cap = SR + N;  // generous: no overflow
+  std::vector<RankSoup> rk((size_t)R);
+  for (int r = 0; r < R; ++r) {
+    RankSoup& s = rk[(size_t)r];
+    s.lo = r * N / R, s.hi = (r + 1) * N / R, s.n = s.hi - s.lo;
+    s.buf[0].assign((size_t)(s.n * PP), 0.f), s.buf[1].assign((size_t)(s.n * PP), 0.f);
+    s.uid.resize((size_t)s.n);
+    for (int64_t j = 0; j < s.n; ++j) s.uid[(size_t)j] = s.lo + j;
+    s.head.assign((size_t)s.n, -1), s.next_att.assign((size_t)N, -1), s.flags.assign((size_t)(s.n + 2), 0);
+    s.need.assign((size_t)s.n, 0), s.sendcnt.assign((size_t)R, SR), s.rmap.assign((size_t)N, 0), s.ovf.assign(1, 0);
+    s.action.assign((size_t)s.n, 0), s.respawn.assign((size_t)s.n, 0), s.counterpart.assign((size_t)s.n, -1);
+    s.census.assign(5, 0), s.next_uid.assign(1, N), s.stats.assign((size_t)(6 * R), 0), s.loss.assign((size_t)s.n, 0.f);
+    s.sendbuf.assign((size_t)(R * cap * XW), 0.f), s.recvbuf.assign((size_t)(R * cap * XW), 0.f);
+    s.gen.assign(1, 1), s.counts.assign(6, 0);
+    SrnnArgs a{};
+    a.n = s.n, a.seed = 5, a.W = s.buf[0].data(), a.uid = s.uid.data();
+    run(OP_INIT, c, a);
+  }
+  int p = 0;
+  auto args = [&](RankSoup& s) {
+    SrnnArgs a{};
+    a.n = s.n, a.n_total = N, a.lo = s.lo, a.seed = 5, a.lr = 0.01f, a.eps = 1e-4f;
+    a.attacking_rate = 0.3f, a.learn_from_rate = 0.3f, a.epochs = 2, a.severity = 1;
+    a.flags = 1 | 2 | 4;
+    a.gen_ptr = s.gen.data();
+    a.W2 = s.buf[p].data(), a.W = s.buf[1 - p].data(), a.uid = s.uid.data();
+    a.i32e = s.head.data(), a.i32f = s.next_att.data(), a.i32c = s.flags.data();
+    a.action = s.action.data(), a.counterpart = s.counterpart.data(), a.loss = s.loss.data();
+    a.respawn = s.respawn.data(), a.uid_out = s.uid.data(), a.counts = s.counts.data(), a.uid_base = s.next_uid.data();
+    return a;
+  };
+  for (int g = 0; g < gens; ++g) {
+    if (R == 1) {
+      RankSoup& s = rk[0];
+      SrnnArgs a = args(s);
+      run(OP_SOUP_DECIDE, c, a);
+      run(OP_SOUP_EVOLVE, c, a);
+      run(OP_RESPAWN_SEQ, c, a);
+    } else {
+      for (int r = 0; r < R; ++r) {
+        RankSoup& s = rk[(size_t)r];
+        SrnnArgs a = args(s);
+        a.world = R, a.rank = r, a.cap = cap, a.need = s.need.data(), a.sendcnt = s.sendcnt.data();
+        a.rmap = s.rmap.data(), a.ovf = s.ovf.data(), a.sendbuf = s.sendbuf.data(), a.recvbuf = s.recvbuf.data();
+        run(OP_SOUP_DECIDE, c, a);
+        run(OP_SOUP_PACK, c, a);
+      }
+      // all-to-all: block d of rank s's sendbuf -> block s of rank d's recvbuf
+      for (int src = 0; src < R; ++src)
+        for (int dst = 0; dst < R; ++dst)
+          std::memcpy(rk[(size_t)dst].recvbuf.data() + (size_t)src * cap * XW,
+                      rk[(size_t)src].sendbuf.data() + (size_t)dst * cap * XW, (size_t)cap * XB);
+      for (int r = 0; r < R; ++r) {
+        RankSoup& s = rk[(size_t)r];
+        SrnnArgs a = args(s);
+        a.world = R, a.rank = r, a.cap = cap, a.need = s.need.data(), a.sendcnt = s.sendcnt.data();
+        a.rmap = s.rmap.data(), a.ovf = s.ovf.data(), a.sendbuf = s.sendbuf.data(), a.recvbuf = s.recvbuf.data();
+        a.census = s.census.data();
+        run(OP_SOUP_UNPACK, c, a);
+        SrnnArgs u = a;
+        u.flags |= 256;
+        run(OP_UID_ASSIGN, c, u);
+        SrnnArgs e = a;
+        e.flags |= 32;
+        run(OP_SOUP_EVOLVE, c, e);
+        SrnnArgs k = a;
+        k.W = s.buf[1 - p].data(), k.flags = 8 | 64 | 512, k.ctr = 0x7FFFFFF0;
+        run(OP_CLASSIFY, c, k);
+        CHECK(s.ovf[0] == 0);
+      }
+    }
+    p = 1 - p;
+  }
+  if (R > 1) {  // flush: uids of the last generation's newborns (stats all-gather)
+    std::vector<int64_t> all((size_t)(6 * R));
+    for (int r = 0; r < R; ++r)
+      for (int q = 0; q < 6; ++q) all[(size_t)(r * 6 + q)] = (int64_t)rk[(size_t)r].counts[(size_t)q];
+    for (int r = 0; r < R; ++r) {
+      RankSoup& s = rk[(size_t)r];
+      SrnnArgs a = args(s);
+      a.world = R, a.rank = r, a.stats = all.data(), a.census = s.census.data();
+      run(OP_UID_ASSIGN, c, a);
+    }
+  }
+  std::vector<float> W;
+  uids_out->clear();
+  for (int r = 0; r < R; ++r) {
+    W.insert(W.end(), rk[(size_t)r].buf[p].begin(), rk[(size_t)r].buf[p].end());
+    uids_out->insert(uids_out->end(), rk[(size_t)r].uid.begin(), rk[(size_t)r].uid.end());
+  }
+  *next_out = rk[0].next_uid[0];
+  for (int r = 1; r < R; ++r) CHECK(rk[(size_t)r].next_uid[0] == *next_out);
+  return W;
+}
+
+int main() {
+  CHECK(srnn_abi_version() == 9);
+  ops_smoke(ww22(), 1000);
+  ops_smoke(agg422(), 777);
+  std::vector<int64_t> u1, u2, u3;
+  int64_t n1 = 0, n2 = 0, n3 = 0;
+  const int64_t N = 301;
+  std::vector<float> w1 = soup(1, N, 5, &u1, &n1);
+  std::vector<float> w2 = soup(2, N, 5, &u2, &n2);
+  std::vector<float> w3 = soup(3, N, 5, &u3, &n3);
+  CHECK(w1.size() == w2.size() && std::memcmp(w1.data(), w2.data(), w1.size() * 4) == 0);
+  CHECK(w1.size() == w3.size() && std::memcmp(w1.data(), w3.data(), w1.size() * 4) == 0);
+  CHECK(u1 == u2 && u1 == u3);
+  CHECK(n1 == n2 && n1 == n3);
+  std::printf("host_selftest: %s (next_uid %lld)\n", g_fail ? "FAILED" : "ok", (long long)n1);
+  return g_fail ? 1 : 0;
+}

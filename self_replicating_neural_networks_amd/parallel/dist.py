@@ -104,8 +104,10 @@ class Dist:
             dist.barrier(group=self.group)
 
 
-def from_env(backend: Optional[str] = None, device_type: str = "cuda") -> Dist:
-    """Initialise the default process group from torchrun's env (RANK/WORLD_SIZE/...)."""
+def from_env(backend: Optional[str] = None, device_type: str = "cuda", timeout_s: Optional[float] = None) -> Dist:
+    """Initialise the default process group from torchrun's env (RANK/WORLD_SIZE/...).
+    ``timeout_s`` bounds every collective: a dead or hung peer makes the others raise
+    instead of waiting forever (failure detection)."""
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
@@ -121,6 +123,9 @@ def from_env(backend: Optional[str] = None, device_type: str = "cuda") -> Dist:
         if backend is None:
             backend = "nccl" if device_type == "cuda" else "gloo"
         kw = {}
+        if timeout_s:
+            import datetime
+            kw["timeout"] = datetime.timedelta(seconds=float(timeout_s))
         if backend == "nccl":
             dev_idx = 0 if os.environ.get("SRNN_SHARE_DEVICE") == "1" else local_rank
             torch.cuda.set_device(dev_idx)

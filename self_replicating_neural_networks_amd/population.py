@@ -120,6 +120,12 @@ class Population:
         _, counts = self.classify(eps, with_sec)
         return counts_dict(counts.cpu())
 
+    def inject_nan(self, rows) -> "Population":
+        """Fault injection: NaN into the first weight of ``rows``."""
+        rows = torch.as_tensor(rows, dtype=torch.int64, device=self.W.device)
+        self.W[rows, 0] = float("nan")
+        return self
+
     def perturb(self, e: float) -> "Population":
         K.perturb(self.spec, self.W, e, uid=self.uid, seed=self.seed, ctr=self._next_ctr())
         return self

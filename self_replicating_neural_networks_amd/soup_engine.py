@@ -155,7 +155,10 @@ class SoupEngine:
         self.respawn = torch.zeros(self.n, dtype=torch.int8, device=dev)
         self.counts = torch.zeros(6, dtype=torch.int64, device=dev)  # classes[5] + respawns
         self.cfg = _lib.make_cfg(spec, self.dtype_code)
-        self.recorder = None
+        self.recorder = None        # full reference-schema state recorder (compat Soup)
+        self.trajectory = None      # sampled TrajectoryRecorder (large soups)
+        self.metrics = None         # MetricsWriter (JSONL per-generation metrics)
+        self._metrics_uid = None
         self.stats = False          # classify + all-reduce every generation
         self.stats_with_sec = True
         self._graphs = None
@@ -351,8 +354,35 @@ class SoupEngine:
                 self._pending = self.dist.enabled
             else:
                 self._generation()
+            self._hooks()
         self._flush()  # uids / census consistent between evolve calls
         return self
+
+    def _hooks(self):
+        """Per-generation observers (host work only when one is due)."""
+        t = self.time
+        if self.trajectory is not None and self.trajectory.due(t):
+            self._flush()
+            self.trajectory.snapshot(self, t)
+        if self.metrics is not None and self.metrics.due(t):
+            self._flush()
+            census = self.last_census() if (self.stats or self.dist.enabled) else self.count()
+            nu = int(self.next_uid.item())
+            resp = None if self._metrics_uid is None else nu - self._metrics_uid
+            self._metrics_uid = nu
+            ls = torch.stack([torch.nan_to_num(self.loss.double(), nan=0.0).sum(),
+                              torch.tensor(float(self.n), dtype=torch.float64, device=self.device)])
+            self.dist.all_reduce_sum(ls)
+            self.metrics.log(t, census, self.n_total, respawns=resp, mean_loss=float(ls[0] / ls[1]), next_uid=nu)
+
+    # ------------------------------------------------------------------ fault injection
+    def inject_nan(self, rows) -> None:
+        """Fault injection: poison local rows with NaN so the divergence
+        test / respawn path runs on them (reference code/network.py:44-52, soup.py:77-86)."""
+        rows = torch.as_tensor(rows, dtype=torch.int64, device=self.device)
+        if rows.numel() and (int(rows.min()) < 0 or int(rows.max()) >= self.n):
+            raise IndexError("inject_nan rows out of this rank's range")
+        self.local_rows()[rows, 0] = float("nan")
 
     def global_uids(self):
         """uid of every global slot (host numpy); all-gathered when sharded."""
