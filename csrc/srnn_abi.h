@@ -26,7 +26,8 @@ struct SrnnArgs {
   int32_t severity;     // soup: learn_from_severity
   int32_t early_exit;   // fixpoint run: stop at fixpoint / divergence
   int32_t flags;        // bit0 shuffle, bit1 remove_divergent, bit2 remove_zero, bit3 fix_sec, bit4 per-row respawn flags, bit5 respawn inline, bit6 count respawns in counts[5], bit7 recvbuf is the all-gathered table,
-                        // bit8 uid_assign reads the per-rank stats from the exchange's stats rows, bit9 classify advances *gen_ptr
+                        // bit8 uid_assign reads the per-rank stats from the exchange's stats rows, bit9 classify advances *gen_ptr,
+                        // bit10 fused generation computes the census
   int32_t gen;          // soup generation (time)
   float eps;
   float lr;
@@ -93,10 +94,11 @@ enum SrnnOp {
   OP_VARY_RUN = 12,     // known-fixpoint variation run: nsteps = time to vergence, loss = time as fixpoint
   OP_SOUP_PACK = 13,    // sharded soup: stats rows + local rows needed by other ranks -> sendbuf (tagged)
   OP_SOUP_UNPACK = 14,  // sharded soup: index the received rows (rmap), reset sendcnt
+  OP_SOUP_GEN = 16,     // single rank, fused: evolve + next decisions + census + uids (one launch)
   OP_UID_ASSIGN = 15,   // sharded soup: uids of the previous generation's newborns from the per-rank stats
 };
 
-int srnn_abi_version();  // 9
+int srnn_abi_version();  // 10
 int srnn_has_config(const SrnnCfg* cfg);
 int srnn_run(int op, const SrnnCfg* cfg, const SrnnArgs* args);
 const char* srnn_last_error();

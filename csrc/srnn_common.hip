@@ -64,7 +64,8 @@ const char* op_name(int op) {
   static const char* names[] = {"srnn:init",       "srnn:apply",        "srnn:run_fixpoint", "srnn:train",
                                 "srnn:learn",      "srnn:classify",     "srnn:perturb",      "srnn:soup_decide",
                                 "srnn:respawn_seq", "srnn:soup_evolve", "srnn:scan",         "srnn:respawn",
-                                "srnn:vary_run",   "srnn:soup_pack",    "srnn:soup_unpack",  "srnn:uid_assign"};
+                                "srnn:vary_run",   "srnn:soup_pack",    "srnn:soup_unpack",  "srnn:uid_assign",
+                                "srnn:soup_gen"};
   return (op >= 0 && op < (int)(sizeof(names) / sizeof(names[0]))) ? names[op] : "srnn:op";
 }
 }  // namespace
@@ -91,7 +92,7 @@ static int dispatch(int op, const SrnnCfg* c, const SrnnArgs* a) {
 
 extern "C" {
 
-int srnn_abi_version() { return 9; }
+int srnn_abi_version() { return 10; }
 
 const char* srnn_last_error() { return srnn::g_err.c_str(); }
 

@@ -438,6 +438,64 @@ struct Weightwise {
     return loss / (float)P;
   }
 
+  // E epochs (samples = the weights at each epoch start when SELF, else the fixed
+  // teacher row `t`), arithmetic identical to E calls of train_epoch.  Latency-hiding
+  // schedule for the nibble-permutation nets (P <= 16, lane per particle, 1-2 waves per
+  // SIMD at the 100k-particle soup): the coordinates go to LDS once, each epoch writes
+  // only the sample values, all P samples of an epoch are read ahead of its SGD chain in
+  // permuted order, and the next epoch's permutation (Philox + Fisher-Yates, independent
+  // of the weights) is computed inside the current epoch's block for the scheduler to
+  // interleave with the dependent SGD chain.
+  template <bool SELF>
+  SRNN_HD static float train_epochs(float* __restrict__ w, const float* __restrict__ t, int E, TrainCtx& c) {
+    if constexpr (P > 16) {
+      float s[P], loss = 0.f;
+#pragma unroll
+      for (int k = 0; k < P; ++k) s[k] = SELF ? w[k] : t[k];
+      for (int e = 0; e < E; ++e) {
+        if (SELF && e > 0)
+#pragma unroll
+          for (int k = 0; k < P; ++k) s[k] = w[k];
+        loss = train_epoch(w, s, c);
+      }
+      return loss;
+    } else {
+      if (E <= 0) return 0.f;
+#pragma unroll
+      for (int k = 0; k < P; ++k)
+        c.samp[k * c.stride] = make_float4(SELF ? w[k] : t[k], coords.c[k][0], coords.c[k][1], coords.c[k][2]);
+      uint64_t ident = 0;
+#pragma unroll
+      for (int k = 0; k < P; ++k) ident |= (uint64_t)k << (4 * k);
+      uint64_t pn = c.shuffle ? shuffle16<P>(c.rng, c.uid, c.ctr, P_SHUFFLE) : ident;
+      float loss = 0.f;
+      for (int e = 0; e < E; ++e) {
+        if (SELF && e > 0)
+#pragma unroll
+          for (int k = 0; k < P; ++k) reinterpret_cast<float*>(&c.samp[k * c.stride])[0] = w[k];
+        const uint64_t pn_next = c.shuffle ? shuffle16<P>(c.rng, c.uid, c.ctr + 1u, P_SHUFFLE) : ident;
+        float4 smp[P];
+#pragma unroll
+        for (int q = 0; q < P; ++q) smp[q] = c.samp[(int)((pn >> (4 * q)) & 15u) * c.stride];
+        float acc = 0.f;
+#pragma unroll
+        for (int q = 0; q < P; ++q) {
+          float x[4] = {smp[q].x, smp[q].y, smp[q].z, smp[q].w};
+          float acts[Net::NACT], y[1];
+          Net::forward(w, x, acts, y);
+          float err = y[0] - smp[q].x;
+          acc += err * err;
+          float gy[1] = {2.0f * err};
+          Net::backward_update(w, acts, gy, c.lr);
+        }
+        loss = acc / (float)P;
+        c.ctr += 1;
+        pn = pn_next;
+      }
+      return loss;
+    }
+  }
+
   SRNN_HD static void init(float* w, const Rng& rng, uint64_t uid) {
     constexpr ShapeTable<NL> t = shapes();
 #pragma unroll

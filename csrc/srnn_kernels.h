@@ -360,9 +360,14 @@ struct Item {
     tc.stride = SAMP_STRIDE;
     tc.aggregator = c.aggregator;
     float loss = 0.f;
-    for (int e = 0; e < a.epochs; ++e) {
-      if (!learn) copy(s, w);
-      loss = Net::train_epoch(w, s, tc);
+    if constexpr (Net::KIND == 0) {
+      loss = learn ? Net::template train_epochs<false>(w, s, a.epochs, tc)
+                   : Net::template train_epochs<true>(w, s, a.epochs, tc);
+    } else {
+      for (int e = 0; e < a.epochs; ++e) {
+        if (!learn) copy(s, w);
+        loss = Net::train_epoch(w, s, tc);
+      }
     }
     store(rowp(a.W, i), w);
     if (a.loss) a.loss[i] = loss;
@@ -494,14 +499,24 @@ struct Item {
     // 2. learn_from a teacher (its generation-start weights)
     if (te >= 0) {
       load(row_of(a, te), f);
-      for (int e = 0; e < a.severity; ++e) loss = Net::train_epoch(w, f, tc);
+      if constexpr (Net::KIND == 0) {
+        if (a.severity > 0) loss = Net::template train_epochs<false>(w, f, a.severity, tc);
+      } else {
+        for (int e = 0; e < a.severity; ++e) loss = Net::train_epoch(w, f, tc);
+      }
       act = A_LEARN_FROM;
       cp = te;
     }
     // 3. self-train
-    for (int e = 0; e < a.epochs; ++e) {
-      copy(f, w);
-      loss = Net::train_epoch(w, f, tc);
+    if (a.epochs > 0) {
+      if constexpr (Net::KIND == 0) {
+        loss = Net::template train_epochs<true>(w, f, a.epochs, tc);
+      } else {
+        for (int e = 0; e < a.epochs; ++e) {
+          copy(f, w);
+          loss = Net::train_epoch(w, f, tc);
+        }
+      }
       act = A_TRAIN_SELF;
       cp = -1;
     }
@@ -603,6 +618,254 @@ __global__ __launch_bounds__(TB) void k_soup_evolve(SrnnCfg c, SrnnArgs a) {
       if (threadIdx.x == 0) reinterpret_cast<unsigned long long*>(a.i32c)[blockIdx.x] = m;
     }
   }
+}
+
+// ----------------------------------------------------------------------------------
+// Fused single-rank soup generation (OP_SOUP_GEN): ONE launch per generation instead of
+// decide -> evolve -> respawn -> classify.  Per lane: the generation (attacks received,
+// learn_from, self-train, respawn + inline re-init), then the NEXT generation's decision
+// for its slot linked into the other list buffer (i32a = head, i32b = next; the decisions
+// are a pure function of (seed, slot, generation)), then the census class of the stored
+// row.  Each wave publishes its respawn ballot + class counts (temp: u64[4] per block)
+// and bumps a done counter (i32d[0]) with an agent-scope atomic; the LAST wave to
+// finish (no waiting anywhere: every wave exits) scans the ballots in slot order, assigns
+// the globally sequential uids of the newborns, writes the census (counts[0..4]),
+// advances next_uid and the generation counter and re-arms the done counter.
+// flags: 1024 = census on (FIX_SEC bit 8 = with second-order fixpoints).
+// ----------------------------------------------------------------------------------
+template <class Net, class S>
+__global__ __launch_bounds__(TB) void k_soup_gen(SrnnCfg c, SrnnArgs a) {
+  using I = Item<Net, S>;
+  constexpr int P = Net::P;
+  constexpr int SAMP = Net::KIND == 0 ? P : 1;
+  constexpr int PERM = (P + 4) & ~3;
+  __shared__ float4 s_samp[TB * SAMP];
+  __shared__ uint8_t s_perm[TB * PERM];
+  const int64_t i = (int64_t)blockIdx.x * TB + threadIdx.x;
+  const int lane = threadIdx.x;
+  uint8_t* perm = s_perm + lane * PERM;
+  const int32_t gen = I::gen_of(a);
+  const bool census = (a.flags & 1024) != 0;
+  bool rs = false;
+  int8_t k = -1;
+  if (i < a.n) {
+    I::soup_evolve(c, a, i, s_samp + lane, perm);
+    rs = a.respawn[i] != 0;
+    int32_t at, te;
+    I::decision(a, i, gen + 1, at, te);
+    if (at >= 0) a.i32b[i] = atomicExch(a.i32a + at, (int32_t)i);
+    if (census) {
+      float w[P];
+      I::load(I::rowp(a.W, i), w);
+      k = I::classify_w(w, a.eps, (a.flags & 8) != 0, I::actx(a, c, I::uid_of(a, i), 0x7FFFFFF0u, perm));
+    }
+  }
+  const unsigned long long m = __ballot(rs);
+  uint32_t cnt[5];
+#pragma unroll
+  for (int q = 0; q < 5; ++q) cnt[q] = (uint32_t)__popcll(__ballot(k == q));
+  // Hand-off to the last wave without an agent-scope release per wave (a release writes
+  // back the XCD's whole L2: ~+30 us over 1563 waves).  The block stats are 8-byte
+  // agent-scope atomic stores (memory-side, coherent across XCDs), drained with
+  // s_waitcnt vmcnt(0) before the relaxed ticket add; the last wave acquires once and
+  // reads them with agent-scope atomic loads (MI355X_MICROARCH "Valid forms").
+  unsigned long long* bs = reinterpret_cast<unsigned long long*>(a.temp);
+  if (a.flags & 2048) {  // two-phase: plain stores, k_gen_finish reads them after the kernel boundary
+    if (lane == 0) {
+      unsigned long long* mine = bs + (int64_t)blockIdx.x * 4;
+      mine[0] = m;
+      mine[1] = (unsigned long long)cnt[0] | ((unsigned long long)cnt[1] << 32);
+      mine[2] = (unsigned long long)cnt[2] | ((unsigned long long)cnt[3] << 32);
+      mine[3] = (unsigned long long)cnt[4];
+    }
+    return;
+  }
+  int32_t prev = 0;
+  if (lane == 0) {
+    unsigned long long* mine = bs + (int64_t)blockIdx.x * 4;
+    __hip_atomic_store(mine + 0, m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(mine + 1, (unsigned long long)cnt[0] | ((unsigned long long)cnt[1] << 32), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(mine + 2, (unsigned long long)cnt[2] | ((unsigned long long)cnt[3] << 32), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(mine + 3, (unsigned long long)cnt[4], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    prev = __hip_atomic_fetch_add(a.i32d, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  prev = __shfl(prev, 0);
+  const int32_t nb = (int32_t)gridDim.x;
+  if (prev != nb - 1) return;
+  // ---- last wave: census + sequential uids of the newborns (blocks in slot order)
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  const int32_t ch = (nb + TB - 1) / TB;
+  const int32_t b0 = lane * ch, b1 = b0 + ch < nb ? b0 + ch : nb;
+  int32_t born = 0;
+  uint64_t cs[5] = {0, 0, 0, 0, 0};
+  for (int32_t b = b0; b < b1; ++b) {
+    const unsigned long long* st = bs + (int64_t)b * 4;
+    born += __popcll(__hip_atomic_load(st + 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    const unsigned long long c01 = __hip_atomic_load(st + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned long long c23 = __hip_atomic_load(st + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned long long c4 = __hip_atomic_load(st + 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    cs[0] += (uint32_t)c01;
+    cs[1] += (uint32_t)(c01 >> 32);
+    cs[2] += (uint32_t)c23;
+    cs[3] += (uint32_t)(c23 >> 32);
+    cs[4] += (uint32_t)c4;
+  }
+  // wave inclusive scan of `born` (64 lanes)
+  int32_t incl = born;
+#pragma unroll
+  for (int off = 1; off < TB; off <<= 1) {
+    int32_t v = __shfl_up(incl, off);
+    if (lane >= off) incl += v;
+  }
+  const int32_t total = __shfl(incl, TB - 1);
+#pragma unroll
+  for (int q = 0; q < 5; ++q)
+#pragma unroll
+    for (int off = TB / 2; off > 0; off >>= 1) cs[q] += __shfl_xor(cs[q], off);
+  const int64_t base = *(volatile const int64_t*)a.uid_base;
+  int64_t u = base + incl - born;
+  for (int32_t b = b0; b < b1 && born; ++b) {
+    unsigned long long mm = __hip_atomic_load(bs + (int64_t)b * 4, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    while (mm) {
+      const int bit = __ffsll((long long)mm) - 1;
+      mm &= mm - 1;
+      a.uid_out[(int64_t)b * TB + bit] = u++;
+    }
+  }
+  if (lane == 0) {
+    ((int64_t*)a.uid_base)[0] = base + total;
+    ((int32_t*)a.gen_ptr)[0] = gen + 1;
+    if (a.counts) {
+#pragma unroll
+      for (int q = 0; q < 5; ++q) a.counts[q] = census ? cs[q] : 0ull;
+      a.counts[5] = (uint64_t)total;
+    }
+    __hip_atomic_store(a.i32d, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // re-armed for the next launch
+  }
+}
+
+// Second phase of the two-phase fused generation: one 1024-thread workgroup reduces the
+// per-wave census counts, scans the respawn ballots in slot order, assigns the newborns'
+// uids and advances next_uid / the generation counter.
+template <int NT>
+__global__ __launch_bounds__(NT) void k_gen_finish(SrnnArgs a, int32_t nb) {
+  __shared__ int32_t s_scan[1024];
+  __shared__ unsigned long long s_cs[5];
+  const int t = threadIdx.x;
+  if (t < 5) s_cs[t] = 0;
+  const unsigned long long* bs = reinterpret_cast<const unsigned long long*>(a.temp);
+  const int32_t ch = (nb + 1023) / 1024;
+  const int32_t b0 = t * ch, b1 = b0 + ch < nb ? b0 + ch : nb;
+  int32_t born = 0;
+  unsigned long long cs[5] = {0, 0, 0, 0, 0};
+  for (int32_t b = b0; b < b1; ++b) {
+    const unsigned long long* st = bs + (int64_t)b * 4;
+    born += __popcll(st[0]);
+    cs[0] += (uint32_t)st[1];
+    cs[1] += (uint32_t)(st[1] >> 32);
+    cs[2] += (uint32_t)st[2];
+    cs[3] += (uint32_t)(st[2] >> 32);
+    cs[4] += (uint32_t)st[3];
+  }
+  s_scan[t] = born;
+  __syncthreads();
+#pragma unroll
+  for (int q = 0; q < 5; ++q) {
+    unsigned long long v = cs[q];
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+    if ((t & 63) == 0 && v) atomicAdd(&s_cs[q], v);
+  }
+  for (int off = 1; off < 1024; off <<= 1) {
+    int32_t v = t >= off ? s_scan[t - off] : 0;
+    __syncthreads();
+    s_scan[t] += v;
+    __syncthreads();
+  }
+  const int64_t base = *(volatile const int64_t*)a.uid_base;
+  int64_t u = base + s_scan[t] - born;
+  for (int32_t b = b0; b < b1 && born; ++b) {
+    unsigned long long mm = bs[(int64_t)b * 4];
+    while (mm) {
+      const int bit = __ffsll((long long)mm) - 1;
+      mm &= mm - 1;
+      a.uid_out[(int64_t)b * TB + bit] = u++;
+    }
+  }
+  __syncthreads();
+  if (t == 0) {
+    const int32_t total = s_scan[1023];
+    ((int64_t*)a.uid_base)[0] = base + total;
+    ((int32_t*)a.gen_ptr)[0] += 1;
+    if (a.counts) {
+      for (int q = 0; q < 5; ++q) a.counts[q] = (a.flags & 1024) ? s_cs[q] : 0ull;
+      a.counts[5] = (uint64_t)total;
+    }
+  }
+}
+
+template <class Net, class S>
+int soup_gen(const SrnnCfg& c, const SrnnArgs& a) {
+  using I = Item<Net, S>;
+  if (!a.dev) {
+    // host: the same steps in order (evolve all rows, link next decisions, census, uids)
+    const int32_t gen = I::gen_of(a);
+    host_parallel(a.n, [&](int64_t i) {
+      float4 samp[Net::P + 1];
+      uint8_t perm[Net::P + 4];
+      I::soup_evolve(c, a, i, samp, perm);
+    });
+    for (int64_t i = 0; i < a.n; ++i) {
+      int32_t at, te;
+      I::decision(a, i, gen + 1, at, te);
+      if (at >= 0) {
+        a.i32b[i] = a.i32a[at];
+        a.i32a[at] = (int32_t)i;
+      }
+    }
+    uint64_t cs[5] = {0, 0, 0, 0, 0};
+    if (a.flags & 1024) {
+      std::vector<int8_t> ks((size_t)a.n);
+      host_parallel(a.n, [&](int64_t i) {
+        float w[Net::P];
+        uint8_t perm[Net::P + 4];
+        I::load(I::rowp(a.W, i), w);
+        ks[(size_t)i] = I::classify_w(w, a.eps, (a.flags & 8) != 0, I::actx(a, c, I::uid_of(a, i), 0x7FFFFFF0u, perm));
+      });
+      for (int64_t i = 0; i < a.n; ++i) cs[ks[(size_t)i]]++;
+    }
+    int64_t u = a.uid_base[0], total = 0;
+    for (int64_t i = 0; i < a.n; ++i)
+      if (a.respawn[i]) {
+        a.uid_out[i] = u++;
+        ++total;
+      }
+    ((int64_t*)a.uid_base)[0] = u;
+    ((int32_t*)a.gen_ptr)[0] = gen + 1;
+    if (a.counts) {
+      for (int q = 0; q < 5; ++q) a.counts[q] = cs[q];
+      a.counts[5] = (uint64_t)total;
+    }
+    return 0;
+  }
+  const int64_t blocks = (a.n + TB - 1) / TB;
+  if (blocks <= 0) return 0;
+  if (blocks > 0x7fffffffLL) {
+    set_error("grid too large");
+    return -2;
+  }
+  hipLaunchKernelGGL((k_soup_gen<Net, S>), dim3((unsigned)blocks), dim3(TB), 0, (hipStream_t)a.stream, c, a);
+  if (a.flags & 2048)
+    hipLaunchKernelGGL(k_gen_finish<1024>, dim3(1), dim3(1024), 0, (hipStream_t)a.stream, a, (int32_t)blocks);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) {
+    set_error(hipGetErrorString(e));
+    return -3;
+  }
+  return 0;
 }
 
 // Classification + 5-bin histogram: 256-thread blocks, per-wave ballots reduced in LDS,
@@ -904,6 +1167,7 @@ int run_net_op(int op, const SrnnCfg& c, const SrnnArgs& a) {
     case OP_SOUP_EVOLVE: return run_one<Net, OP_SOUP_EVOLVE, S>(c, a);
     case OP_RESPAWN: return run_one<Net, OP_RESPAWN, S>(c, a);
     case OP_VARY_RUN: return run_one<Net, OP_VARY_RUN, S>(c, a);
+    case OP_SOUP_GEN: return soup_gen<Net, S>(c, a);
     default: set_error("unknown op"); return -1;
   }
 }

@@ -19,7 +19,7 @@ import threading
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libsrnn.so")
 CSRC = os.path.normpath(os.path.join(_HERE, "..", "..", "csrc"))
-ABI_VERSION = 9
+ABI_VERSION = 10
 
 OP_INIT = 0
 OP_APPLY = 1
@@ -37,6 +37,7 @@ OP_VARY_RUN = 12
 OP_SOUP_PACK = 13
 OP_SOUP_UNPACK = 14
 OP_UID_ASSIGN = 15
+OP_SOUP_GEN = 16
 
 FLAG_SHUFFLE = 1
 FLAG_REMOVE_DIVERGENT = 2
@@ -48,6 +49,8 @@ FLAG_COUNT_RESPAWNS = 64
 FLAG_FULL_TABLE = 128
 FLAG_STATS_X = 256
 FLAG_GEN_ADVANCE = 512
+FLAG_FUSED_CENSUS = 1024
+FLAG_TWO_PHASE = 2048
 
 
 class SrnnCfg(ctypes.Structure):

@@ -36,6 +36,7 @@ generation-start weights.  ``Soup(mode="sequential")`` keeps the exact reference
 from __future__ import annotations
 
 import ctypes
+import os
 from typing import Dict, Optional
 
 import torch
@@ -143,8 +144,16 @@ class SoupEngine:
         self.uid_base = torch.zeros(1, dtype=torch.int64, device=dev)
         self.gen_dev = torch.ones(1, dtype=torch.int32, device=dev)  # generation about to run
         self.time = 0
-        self.head = torch.full((self.n,), -1, **i32)       # first attacker of each local victim
-        self.next_att = torch.full((self.n_total,), -1, **i32)  # attacker -> next attacker of its victim
+        # attack lists, one buffer per ping-pong parity: the fused single-rank generation
+        # links the NEXT generation's attacks into the other parity's buffer
+        self.heads = [torch.full((self.n,), -1, **i32) for _ in range(2)]       # first attacker of each local victim
+        self.nexts = [torch.full((self.n_total,), -1, **i32) for _ in range(2)]  # attacker -> next attacker
+        self._lists_ready = False   # heads[_p] already holds this generation's attacks
+        self.fused = not self.dist.enabled  # one launch per generation (OP_SOUP_GEN)
+        self.two_phase = os.environ.get("SRNN_GEN_TWO_PHASE", "1") == "1"  # + a 1-workgroup finish kernel
+        nb = -(-self.n // 64)
+        self._blockstat = torch.zeros(max(nb, 1) * 8, **i32)
+        self._done = torch.zeros(1, **i32)
         # per-row respawn flags (host) or 64-bit respawn ballots per 64-row wave (device)
         self.flags32 = torch.zeros(max(self.n, 2 * (-(-self.n // 64))), **i32)
         self._pending = False  # sharded: uids of the last generation's newborns not yet assigned
@@ -221,7 +230,7 @@ class SoupEngine:
         params: building ctypes structs every generation costs host time)."""
         stream = torch.cuda.current_stream(self.device).cuda_stream if self.device.type == "cuda" else 0
         key = (self._p, stream, tuple(sorted((k, str(v)) for k, v in self.params.items())), self.stats_with_sec,
-               self.lr, self.shuffle)
+               self.lr, self.shuffle, self.stats, self.two_phase)
         hit = self._arg_cache.get(key)
         if hit is not None:
             return hit
@@ -229,7 +238,7 @@ class SoupEngine:
         a.W2 = _p(self.table_in)
         a.W = _p(self.rows_out)
         a.uid = _p(self.uid)
-        a.i32e, a.i32f = _p(self.head), _p(self.next_att)
+        a.i32e, a.i32f = _p(self.heads[self._p]), _p(self.nexts[self._p])
         a.i32c = _p(self.flags32)
         a.action, a.counterpart, a.loss, a.respawn = _p(self.action), _p(self.counterpart), _p(self.loss), _p(self.respawn)
         a.uid_out = _p(self.uid)
@@ -252,6 +261,18 @@ class SoupEngine:
                         | _lib.FLAG_GEN_ADVANCE)
             ca.W, ca.counts, ca.respawn, ca.uid = _p(self.rows_out), _p(self.counts), _p(self.respawn), _p(self.uid)
             ca.ctr = 0x7FFFFFF0
+        if not self.dist.enabled:
+            # fused generation: next generation's lists, block stats, done counter, census
+            fa = self._args()
+            ctypes.pointer(fa)[0] = a
+            fa.i32a, fa.i32b = _p(self.heads[1 - self._p]), _p(self.nexts[1 - self._p])
+            fa.i32c = None
+            fa.temp, fa.temp_bytes = _p(self._blockstat), self._blockstat.numel() * 4
+            fa.i32d = _p(self._done)
+            fa.flags = a.flags | _lib.FLAG_RESPAWN_INLINE | (_lib.FLAG_TWO_PHASE if self.two_phase else 0)
+            if self.stats and self.spec.shuffler == "none":
+                fa.flags |= _lib.FLAG_FUSED_CENSUS | (_lib.FLAG_FIX_SEC if self.stats_with_sec else 0)
+            ca = fa
         self._arg_cache[key] = (a, ca, a.flags)
         return self._arg_cache[key]
 
@@ -261,8 +282,20 @@ class SoupEngine:
         a.flags = flags
         # head[] is -1 on entry: set at construction, reset by the evolve kernel after use
         if not self.dist.enabled:
-            _lib.run(_lib.OP_SOUP_DECIDE, spec, a, cfg)
+            if self.fused and not (record and self.recorder is not None):
+                # ONE launch: evolve + next generation's attack lists + census + uids
+                if not self._lists_ready:
+                    _lib.run(_lib.OP_SOUP_DECIDE, spec, a, cfg)
+                _lib.run(_lib.OP_SOUP_GEN, spec, ca, cfg)
+                self._lists_ready = True
+                self._p = 1 - self._p
+                if self.stats and not (ca.flags & _lib.FLAG_FUSED_CENSUS):
+                    self.classify_local(self.stats_with_sec, zero=False)
+                return
+            if not self._lists_ready:
+                _lib.run(_lib.OP_SOUP_DECIDE, spec, a, cfg)
             _lib.run(_lib.OP_SOUP_EVOLVE, spec, a, cfg)
+            self._lists_ready = False
             if record and self.recorder is not None:
                 self.recorder.on_evolved(self)
             # uids from next_uid (advanced in place), generation counter, census histogram zeroed
@@ -395,9 +428,9 @@ class SoupEngine:
     # ------------------------------------------------------------------ HIP graphs
     def _state(self):
         """Every device tensor a generation reads or writes (graph validation)."""
-        names = ["_bufs", "uid", "next_uid", "gen_dev", "head", "next_att", "flags32", "action", "counterpart",
+        names = ["_bufs", "uid", "next_uid", "gen_dev", "heads", "nexts", "flags32", "action", "counterpart",
                  "loss", "respawn", "counts", "census", "need", "sendcnt", "rmap", "ovf", "sendbuf", "recvbuf",
-                 "full", "stats_all"]
+                 "full", "stats_all", "_blockstat", "_done"]
         out = []
         for k in names:
             v = getattr(self, k, None)
@@ -424,7 +457,7 @@ class SoupEngine:
         s = torch.cuda.Stream(self.device)
         s.wait_stream(torch.cuda.current_stream(self.device))
         with torch.cuda.stream(s):
-            for _ in range(max(warmup, 1 if self.dist.enabled else 0)):
+            for _ in range(max(warmup, 1 if (self.dist.enabled or self.fused) else 0)):
                 self.time += 1
                 self._generation()
         torch.cuda.current_stream(self.device).wait_stream(s)

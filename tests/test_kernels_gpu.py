@@ -254,3 +254,33 @@ def test_lowp_soup_graph_on_device(cuda):
     assert torch.equal(a.local_rows(), b.local_rows()) and torch.equal(a.uid, b.uid)
     c = a.count()
     assert sum(c.values()) == 20_000
+
+
+@pytest.mark.parametrize("spec", [ArchSpec.weightwise(2, 2), ArchSpec.aggregating(4, 2, 2), ArchSpec.recurrent(2, 2)],
+                         ids=lambda s: s.kind)
+def test_fused_generation_equals_unfused(cuda, spec):
+    """OP_SOUP_GEN (one launch: evolve + next attack lists + census + last-wave uid scan
+    across all XCDs) == decide -> evolve -> respawn -> classify, bitwise, every generation;
+    n not a multiple of 64 and enough waves to span every XCD."""
+    params = dict(attacking_rate=0.2, learn_from_rate=0.2, train=3, remove_divergent=True, remove_zero=True,
+                  epsilon=1e-4)
+    n = 70001
+    a = SoupEngine(spec, n, params, device=cuda, seed=13)
+    b = SoupEngine(spec, n, params, device=cuda, seed=13)
+    b.fused = False
+    a.stats = b.stats = True
+    for g in range(6):
+        a.evolve(1)
+        b.evolve(1)
+        assert torch.equal(a.local_rows(), b.local_rows()), g
+        assert torch.equal(a.uid, b.uid), g
+        assert int(a.next_uid) == int(b.next_uid), g
+        assert a.last_census() == b.last_census(), g
+    assert int(a.gen_dev) == int(b.gen_dev)
+    assert int(a._done) == 0
+    a.capture(warmup=1)
+    b.evolve(1)
+    a.evolve(3)
+    b.evolve(3)
+    assert torch.equal(a.local_rows(), b.local_rows())
+    assert a.last_census() == b.last_census()
