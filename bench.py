@@ -109,9 +109,13 @@ def main():
                                 "learn_from 0.1, remove divergent/zero",
                        "global_batch": n_total, "particles_per_gpu": args.particles_per_gpu, "seq_len": None,
                        "parallelism": f"population-dp{d.world}", "hip_graph": graphed,
+                       "multi_generation_graph": eng._chunk is not None,
+                       "collectives": ("native RCCL communicator (" + d.native.library + ")") if d.native
+                       else ("torch.distributed" if d.enabled else None),
                        "census_every_step": eng.stats, "final_census": census},
         }), flush=True)
     eng.release_graphs()  # graph executables reference the RCCL communicator
+    d.close()
     if d.enabled:
         dist.destroy_process_group()
 

@@ -86,6 +86,7 @@ def main():
         torch.cuda.synchronize()
         stage("graphs released")
     if mode.endswith("destroy"):
+        d.close()
         torch.distributed.destroy_process_group()
         stage("process group destroyed")
     ok = res["eager_bitwise_equal"] and res["graph_bitwise_equal"] and res["census_equal"]

@@ -405,12 +405,18 @@ struct Item {
     decision(a, i, gen_of(a), at, te);
     if (a.i32a) a.i32a[i] = at;
     if (a.i32b) a.i32b[i] = te;
+    link_decision(a, i, at, te, a.i32e, a.i32f);
+  }
+  // attacks on this rank's victims -> lists (head, next); rows other ranks will need ->
+  // need masks (sharded)
+  SRNN_HD static void link_decision(const SrnnArgs& a, int64_t i, int32_t at, int32_t te, int32_t* head,
+                                    int32_t* next) {
     const bool i_local = i >= a.lo && i < a.lo + a.n;
     if (at >= a.lo && at < a.lo + a.n) {
 #if defined(__HIP_DEVICE_COMPILE__)
-      a.i32f[i] = atomicExch(a.i32e + (at - a.lo), (int32_t)i);
+      next[i] = atomicExch(head + (at - a.lo), (int32_t)i);
 #else
-      a.i32f[i] = __atomic_exchange_n(a.i32e + (at - a.lo), (int32_t)i, __ATOMIC_RELAXED);
+      next[i] = __atomic_exchange_n(head + (at - a.lo), (int32_t)i, __ATOMIC_RELAXED);
 #endif
     } else if (a.need && a.world > 1 && at >= 0 && i_local) {
       // my particle attacks a victim owned by another rank: ship my row there
@@ -651,9 +657,19 @@ __global__ __launch_bounds__(TB) void k_soup_gen(SrnnCfg c, SrnnArgs a) {
   if (i < a.n) {
     I::soup_evolve(c, a, i, s_samp + lane, perm);
     rs = a.respawn[i] != 0;
-    int32_t at, te;
-    I::decision(a, i, gen + 1, at, te);
-    if (at >= 0) a.i32b[i] = atomicExch(a.i32a + at, (int32_t)i);
+    if (a.flags & 4096) {
+      // sharded: the next generation's decisions of EVERY global slot (this lane takes
+      // slots i, i + n, ...): attack lists of local victims + need masks for the pack
+      for (int64_t g = i; g < a.n_total; g += a.n) {
+        int32_t at, te;
+        I::decision(a, g, gen + 1, at, te);
+        I::link_decision(a, g, at, te, a.i32a, a.i32b);
+      }
+    } else {
+      int32_t at, te;
+      I::decision(a, i, gen + 1, at, te);
+      if (at >= 0) a.i32b[i] = atomicExch(a.i32a + at, (int32_t)i);
+    }
     if (census) {
       float w[P];
       I::load(I::rowp(a.W, i), w);
@@ -750,9 +766,11 @@ __global__ __launch_bounds__(TB) void k_soup_gen(SrnnCfg c, SrnnArgs a) {
 
 // Second phase of the two-phase fused generation: one 1024-thread workgroup reduces the
 // per-wave census counts, scans the respawn ballots in slot order, assigns the newborns'
-// uids and advances next_uid / the generation counter.
-template <int NT>
+// uids and advances next_uid / the generation counter.  Sharded (flag 4096): only the
+// counts (census + respawns, sent with the next exchange); uids wait for k_uid_assign.
+template <class Net, class S, int NT>
 __global__ __launch_bounds__(NT) void k_gen_finish(SrnnArgs a, int32_t nb) {
+  using I = Item<Net, S>;
   __shared__ int32_t s_scan[1024];
   __shared__ unsigned long long s_cs[5];
   const int t = threadIdx.x;
@@ -785,9 +803,10 @@ __global__ __launch_bounds__(NT) void k_gen_finish(SrnnArgs a, int32_t nb) {
     s_scan[t] += v;
     __syncthreads();
   }
+  const bool sharded = (a.flags & 4096) != 0;  // uids come after the exchange (k_uid_assign)
   const int64_t base = *(volatile const int64_t*)a.uid_base;
   int64_t u = base + s_scan[t] - born;
-  for (int32_t b = b0; b < b1 && born; ++b) {
+  for (int32_t b = b0; b < b1 && born && !sharded; ++b) {
     unsigned long long mm = bs[(int64_t)b * 4];
     while (mm) {
       const int bit = __ffsll((long long)mm) - 1;
@@ -796,10 +815,11 @@ __global__ __launch_bounds__(NT) void k_gen_finish(SrnnArgs a, int32_t nb) {
     }
   }
   __syncthreads();
+  const int32_t gen = I::gen_of(a);
   if (t == 0) {
     const int32_t total = s_scan[1023];
-    ((int64_t*)a.uid_base)[0] = base + total;
-    ((int32_t*)a.gen_ptr)[0] += 1;
+    if (!sharded) ((int64_t*)a.uid_base)[0] = base + total;
+    ((int32_t*)a.gen_ptr)[0] = gen + 1;
     if (a.counts) {
       for (int q = 0; q < 5; ++q) a.counts[q] = (a.flags & 1024) ? s_cs[q] : 0ull;
       a.counts[5] = (uint64_t)total;
@@ -818,12 +838,20 @@ int soup_gen(const SrnnCfg& c, const SrnnArgs& a) {
       uint8_t perm[Net::P + 4];
       I::soup_evolve(c, a, i, samp, perm);
     });
-    for (int64_t i = 0; i < a.n; ++i) {
-      int32_t at, te;
-      I::decision(a, i, gen + 1, at, te);
-      if (at >= 0) {
-        a.i32b[i] = a.i32a[at];
-        a.i32a[at] = (int32_t)i;
+    if (a.flags & 4096) {
+      for (int64_t g = 0; g < a.n_total; ++g) {
+        int32_t at, te;
+        I::decision(a, g, gen + 1, at, te);
+        I::link_decision(a, g, at, te, a.i32a, a.i32b);
+      }
+    } else {
+      for (int64_t i = 0; i < a.n; ++i) {
+        int32_t at, te;
+        I::decision(a, i, gen + 1, at, te);
+        if (at >= 0) {
+          a.i32b[i] = a.i32a[at];
+          a.i32a[at] = (int32_t)i;
+        }
       }
     }
     uint64_t cs[5] = {0, 0, 0, 0, 0};
@@ -838,12 +866,23 @@ int soup_gen(const SrnnCfg& c, const SrnnArgs& a) {
       for (int64_t i = 0; i < a.n; ++i) cs[ks[(size_t)i]]++;
     }
     int64_t u = a.uid_base[0], total = 0;
-    for (int64_t i = 0; i < a.n; ++i)
-      if (a.respawn[i]) {
-        a.uid_out[i] = u++;
-        ++total;
-      }
-    ((int64_t*)a.uid_base)[0] = u;
+    if (a.flags & 4096) {
+      // sharded: respawn ballots per 64-row block for k_uid_assign after the next exchange
+      unsigned long long* bs = reinterpret_cast<unsigned long long*>(a.temp);
+      for (int64_t b = 0; b < (a.n + TB - 1) / TB; ++b) bs[b * 4] = 0ull;
+      for (int64_t i = 0; i < a.n; ++i)
+        if (a.respawn[i]) {
+          bs[(i / TB) * 4] |= 1ull << (i % TB);
+          ++total;
+        }
+    } else {
+      for (int64_t i = 0; i < a.n; ++i)
+        if (a.respawn[i]) {
+          a.uid_out[i] = u++;
+          ++total;
+        }
+      ((int64_t*)a.uid_base)[0] = u;
+    }
     ((int32_t*)a.gen_ptr)[0] = gen + 1;
     if (a.counts) {
       for (int q = 0; q < 5; ++q) a.counts[q] = cs[q];
@@ -859,7 +898,7 @@ int soup_gen(const SrnnCfg& c, const SrnnArgs& a) {
   }
   hipLaunchKernelGGL((k_soup_gen<Net, S>), dim3((unsigned)blocks), dim3(TB), 0, (hipStream_t)a.stream, c, a);
   if (a.flags & 2048)
-    hipLaunchKernelGGL(k_gen_finish<1024>, dim3(1), dim3(1024), 0, (hipStream_t)a.stream, a, (int32_t)blocks);
+    hipLaunchKernelGGL((k_gen_finish<Net, S, 1024>), dim3(1), dim3(1024), 0, (hipStream_t)a.stream, a, (int32_t)blocks);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) {
     set_error(hipGetErrorString(e));
@@ -1078,13 +1117,16 @@ __global__ __launch_bounds__(TBR) void k_uid_assign(SrnnCfg c, SrnnArgs a) {
     if (a.census && all > 0)
       for (int q = 0; q < 5; ++q) a.census[q] = cen[q];
   }
-  unsigned long long* masks = reinterpret_cast<unsigned long long*>(a.i32c);
+  // 64-bit respawn ballot of evolve wave b: i32c as u64[b], or the fused generation's
+  // block stats (flag 8192: u64[4] per block, ballot first)
+  unsigned long long* masks = reinterpret_cast<unsigned long long*>((a.flags & 8192) ? a.temp : (void*)a.i32c);
+  const int mstride = (a.flags & 8192) ? 4 : 1;
   const int64_t nb = (a.n + TB - 1) / TB;
   const int64_t ch = (nb + TBR - 1) / TBR;
   const int64_t b0 = (int64_t)threadIdx.x * ch;
   const int64_t b1 = b0 + ch < nb ? b0 + ch : nb;
   int32_t cnt = 0;
-  for (int64_t b = b0; b < b1; ++b) cnt += __popcll(masks[b]);
+  for (int64_t b = b0; b < b1; ++b) cnt += __popcll(masks[b * mstride]);
   s_cnt[threadIdx.x] = cnt;
   __syncthreads();
   for (int off = 1; off < TBR; off <<= 1) {
@@ -1096,8 +1138,8 @@ __global__ __launch_bounds__(TBR) void k_uid_assign(SrnnCfg c, SrnnArgs a) {
   const int64_t base = *(volatile const int64_t*)a.uid_base;
   int64_t k = base + s_prefix + s_cnt[threadIdx.x] - cnt;
   for (int64_t b = b0; b < b1 && cnt; ++b) {
-    unsigned long long m = masks[b];
-    masks[b] = 0ull;
+    unsigned long long m = masks[b * mstride];
+    masks[b * mstride] = 0ull;
     while (m) {
       const int bit = __ffsll((long long)m) - 1;
       m &= m - 1;
@@ -1131,13 +1173,27 @@ int uid_assign(const SrnnCfg& c, const SrnnArgs& a) {
   for (int q = 0; q < 5; ++q) all += cen[q];
   if (a.census && all > 0)
     for (int q = 0; q < 5; ++q) a.census[q] = cen[q];
-  // host path: per-row respawn flags in i32c (evolve with flag 16), consumed here
+  // host path: per-row respawn flags in i32c (evolve with flag 16) or the fused
+  // generation's block ballots (flag 8192), consumed here
   int64_t k = a.uid_base[0] + pre;
-  for (int64_t i = 0; i < a.n; ++i)
-    if (a.i32c[i]) {
-      a.uid_out[i] = k++;
-      a.i32c[i] = 0;
+  if (a.flags & 8192) {
+    unsigned long long* bs = reinterpret_cast<unsigned long long*>(a.temp);
+    for (int64_t b = 0; b < (a.n + TB - 1) / TB; ++b) {
+      unsigned long long m = bs[b * 4];
+      bs[b * 4] = 0ull;
+      while (m) {
+        const int bit = __builtin_ctzll(m);
+        m &= m - 1;
+        a.uid_out[b * TB + bit] = k++;
+      }
     }
+  } else {
+    for (int64_t i = 0; i < a.n; ++i)
+      if (a.i32c[i]) {
+        a.uid_out[i] = k++;
+        a.i32c[i] = 0;
+      }
+  }
   ((int64_t*)a.uid_base)[0] += tot;
   if (a.counts)
     for (int q = 0; q < 6; ++q) a.counts[q] = 0;

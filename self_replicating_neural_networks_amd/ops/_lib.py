@@ -51,6 +51,8 @@ FLAG_STATS_X = 256
 FLAG_GEN_ADVANCE = 512
 FLAG_FUSED_CENSUS = 1024
 FLAG_TWO_PHASE = 2048
+FLAG_SHARDED_DECIDE = 4096
+FLAG_MASKS_BS = 8192
 
 
 class SrnnCfg(ctypes.Structure):
@@ -122,6 +124,18 @@ def lib():
         L.srnn_last_error.restype = ctypes.c_char_p
         L.srnn_scan_temp_bytes.argtypes = [ctypes.c_int64]
         L.srnn_scan_temp_bytes.restype = ctypes.c_int64
+        vp, i64, cp = ctypes.c_void_p, ctypes.c_int64, ctypes.c_char_p
+        for name, args in (("srnn_comm_available", [cp]), ("srnn_comm_unique_id", [cp, vp, ctypes.c_int]),
+                           ("srnn_comm_init", [cp, vp, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                               ctypes.POINTER(ctypes.c_void_p)]),
+                           ("srnn_comm_destroy", [vp, ctypes.c_int]), ("srnn_comm_async_error", [vp]),
+                           ("srnn_comm_all_to_all", [vp, vp, vp, i64, vp]),
+                           ("srnn_comm_all_gather", [vp, vp, vp, i64, vp]),
+                           ("srnn_comm_all_reduce_i64", [vp, vp, vp, i64, vp])):
+            f = getattr(L, name)
+            f.argtypes = args
+            f.restype = ctypes.c_int
+        L.srnn_comm_library.restype = ctypes.c_char_p
         v = L.srnn_abi_version()
         if v != ABI_VERSION:
             raise NativeLibraryError(f"libsrnn ABI {v} != expected {ABI_VERSION}: rebuild with `make -C csrc`")
@@ -151,3 +165,7 @@ def run(op: int, spec, args: SrnnArgs, cfg: SrnnCfg = None, dtype: int = DTYPE_F
 
 def scan_temp_bytes(n: int) -> int:
     return int(lib().srnn_scan_temp_bytes(int(n)))
+
+
+def last_error() -> str:
+    return lib().srnn_last_error().decode(errors="replace")

@@ -19,6 +19,83 @@ import torch
 import torch.distributed as dist
 
 
+def _torch_rccl_path() -> Optional[str]:
+    p = os.path.join(os.path.dirname(torch.__file__), "lib", "librccl.so")
+    return p if os.path.exists(p) else None
+
+
+class NativeComm:
+    """The soup's own RCCL communicator (csrc/srnn_comm.cpp): collectives are
+    enqueued on the caller's HIP stream straight into RCCL, so they can be captured in a
+    hipGraph with the kernels of a generation.  torch.distributed only carries rank 0's
+    ncclUniqueId to the other ranks (rendezvous)."""
+
+    def __init__(self, world: int, rank: int, device: "torch.device"):
+        import ctypes
+        from ..ops import _lib
+        self._ct = ctypes
+        self.L = _lib.lib()
+        self.hint = (_torch_rccl_path() or "").encode()
+        self.world, self.rank, self.device = world, rank, device
+        if not self.L.srnn_comm_available(self.hint):
+            raise RuntimeError("RCCL not available: " + _lib.last_error())
+        buf = ctypes.create_string_buffer(256)
+        uid = None
+        if rank == 0:
+            n = self.L.srnn_comm_unique_id(self.hint, buf, 256)
+            if n <= 0:
+                raise RuntimeError("ncclGetUniqueId failed: " + _lib.last_error())
+            uid = bytes(buf.raw[:n])
+        if world > 1 or dist.is_initialized():
+            obj = [uid]
+            dist.broadcast_object_list(obj, src=0)
+            uid = obj[0]
+        h = ctypes.c_void_p()
+        r = self.L.srnn_comm_init(self.hint, ctypes.create_string_buffer(uid, len(uid)), world, rank,
+                                  device.index or 0, ctypes.byref(h))
+        if r != 0:
+            raise RuntimeError(f"ncclCommInitRank failed ({r}): " + _lib.last_error())
+        self.comm = h
+        self.library = self.L.srnn_comm_library().decode()
+
+    def _stream(self):
+        return self._ct.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
+
+    def _ok(self, r, what):
+        if r != 0:
+            from ..ops import _lib
+            raise RuntimeError(f"{what} failed ({r}): " + _lib.last_error())
+
+    def all_to_all(self, out: torch.Tensor, inp: torch.Tensor):
+        nb = inp.numel() * inp.element_size()
+        if nb % self.world or out.numel() * out.element_size() != nb:
+            raise ValueError("all-to-all buffers must split evenly over the ranks")
+        self._ok(self.L.srnn_comm_all_to_all(self.comm, inp.data_ptr(), out.data_ptr(), nb // self.world,
+                                             self._stream()), "all-to-all")
+
+    def all_gather(self, out: torch.Tensor, inp: torch.Tensor):
+        nb = inp.numel() * inp.element_size()
+        if out.numel() * out.element_size() != nb * self.world:
+            raise ValueError("all-gather output must be world x input")
+        self._ok(self.L.srnn_comm_all_gather(self.comm, inp.data_ptr(), out.data_ptr(), nb, self._stream()),
+                 "all-gather")
+
+    def all_reduce_sum_i64(self, t: torch.Tensor):
+        if t.dtype != torch.int64:
+            raise TypeError("int64 only")
+        self._ok(self.L.srnn_comm_all_reduce_i64(self.comm, t.data_ptr(), t.data_ptr(), t.numel(), self._stream()),
+                 "all-reduce")
+
+    def check(self):
+        """Raise if RCCL reported an asynchronous error (peer died, network failure)."""
+        self._ok(self.L.srnn_comm_async_error(self.comm), "RCCL async error")
+
+    def close(self, abort: bool = False):
+        if self.comm:
+            self.L.srnn_comm_destroy(self.comm, 1 if abort else 0)
+            self.comm = None
+
+
 @dataclasses.dataclass
 class Dist:
     rank: int = 0
@@ -28,7 +105,28 @@ class Dist:
     # run the sharded code path (collectives included) even with one rank: rehearses the
     # multi-GPU generation -- and its hipGraph capture with RCCL -- on a one-GPU box
     force: bool = False
+    native: Optional[NativeComm] = None   # own RCCL communicator (device collectives)
     _pad_bufs: dict = dataclasses.field(default_factory=dict, repr=False)
+
+    def enable_native_comm(self, device) -> bool:
+        """Create the soup's own RCCL communicator on ``device`` (collective over all
+        ranks).  No-op on CPU, without the nccl backend or with SRNN_NATIVE_COMM=0."""
+        if self.native is not None:
+            return True
+        device = torch.device(device)
+        if (not self.enabled or device.type != "cuda" or os.environ.get("SRNN_NATIVE_COMM", "1") != "1"
+                or dist.get_backend(self.group) != "nccl"):
+            return False
+        self.native = NativeComm(self.world, self.rank, device)
+        return True
+
+    def close(self):
+        if self.native is not None:
+            self.native.close()
+            self.native = None
+
+    def _use_native(self, *ts) -> bool:
+        return self.native is not None and all(t.is_cuda for t in ts)
 
     @property
     def enabled(self) -> bool:
@@ -51,7 +149,9 @@ class Dist:
                 out.copy_(local)
             return out
         sizes = self.shard_sizes(n_total)
-        if len(set(sizes)) == 1:
+        if len(set(sizes)) == 1 and self._use_native(out, local):
+            self.native.all_gather(out, local)
+        elif len(set(sizes)) == 1:
             dist.all_gather_into_tensor(out, local, group=self.group)
         else:
             # uneven shards: gather max-size padded blocks, then compact
@@ -73,21 +173,27 @@ class Dist:
 
     def all_to_all(self, out: torch.Tensor, inp: torch.Tensor):
         """Equal-split all-to-all (RCCL over xGMI for nccl: direct peer links)."""
-        if self.enabled:
+        if self._use_native(out, inp):
+            self.native.all_to_all(out, inp)
+        elif self.enabled:
             dist.all_to_all_single(out, inp, group=self.group)
         else:
             out.copy_(inp)
         return out
 
     def all_gather_into(self, out: torch.Tensor, local: torch.Tensor):
-        if self.enabled:
+        if self._use_native(out, local):
+            self.native.all_gather(out, local)
+        elif self.enabled:
             dist.all_gather_into_tensor(out, local, group=self.group)
         else:
             out.copy_(local)
         return out
 
     def all_reduce_sum(self, t: torch.Tensor):
-        if self.enabled:
+        if self._use_native(t) and t.dtype == torch.int64:
+            self.native.all_reduce_sum_i64(t)
+        elif self.enabled:
             dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group)
         return t
 

@@ -123,6 +123,7 @@ def run(cfg: ExperimentConfig, resume: bool = False, log=print):
     if d.rank == 0:
         log(json.dumps(out))
     eng.release_graphs()
+    d.close()
     return eng, out
 
 

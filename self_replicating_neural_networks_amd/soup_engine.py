@@ -96,6 +96,9 @@ class SoupEngine:
         self.lr = float(lr)
         self.shuffle = bool(shuffle)
         self.dist = dist or Dist()
+        if self.device.type == "cuda" and self.dist.enabled:
+            # the soup's own RCCL communicator: its collectives can live inside hipGraphs
+            self.dist.enable_native_comm(self.device)
         self.lo, self.hi = self.dist.shard(self.n_total)
         self.n = self.hi - self.lo
         if self.n_total > MAX_SLOTS:
@@ -149,7 +152,11 @@ class SoupEngine:
         self.heads = [torch.full((self.n,), -1, **i32) for _ in range(2)]       # first attacker of each local victim
         self.nexts = [torch.full((self.n_total,), -1, **i32) for _ in range(2)]  # attacker -> next attacker
         self._lists_ready = False   # heads[_p] already holds this generation's attacks
-        self.fused = not self.dist.enabled  # one launch per generation (OP_SOUP_GEN)
+        # one launch (+ a one-workgroup finish) per generation: OP_SOUP_GEN; sharded engines
+        # with the all-to-all exchange fuse the evolve, census and next decisions too
+        self.fused = not self.dist.enabled or exchange == "alltoall"
+        self._mask_src = "i32c"   # where the pending respawn ballots live ("bs": block stats)
+        self._fused_census = False
         self.two_phase = os.environ.get("SRNN_GEN_TWO_PHASE", "1") == "1"  # + a 1-workgroup finish kernel
         nb = -(-self.n // 64)
         self._blockstat = torch.zeros(max(nb, 1) * 8, **i32)
@@ -171,6 +178,7 @@ class SoupEngine:
         self.stats = False          # classify + all-reduce every generation
         self.stats_with_sec = True
         self._graphs = None
+        self._chunk = None          # (graph of G generations, start parity, G)
         self._arg_cache = {}
         # initial particles: uids 0..n_total-1, keyed init (identical for any rank count)
         local = self.local_rows()
@@ -261,7 +269,7 @@ class SoupEngine:
                         | _lib.FLAG_GEN_ADVANCE)
             ca.W, ca.counts, ca.respawn, ca.uid = _p(self.rows_out), _p(self.counts), _p(self.respawn), _p(self.uid)
             ca.ctr = 0x7FFFFFF0
-        if not self.dist.enabled:
+        if not self.dist.enabled or self.exchange == "alltoall":
             # fused generation: next generation's lists, block stats, done counter, census
             fa = self._args()
             ctypes.pointer(fa)[0] = a
@@ -270,11 +278,25 @@ class SoupEngine:
             fa.temp, fa.temp_bytes = _p(self._blockstat), self._blockstat.numel() * 4
             fa.i32d = _p(self._done)
             fa.flags = a.flags | _lib.FLAG_RESPAWN_INLINE | (_lib.FLAG_TWO_PHASE if self.two_phase else 0)
-            if self.stats and self.spec.shuffler == "none":
+            census = self.stats and self.spec.shuffler == "none"
+            if self.dist.enabled:
+                # sharded: every global slot's next decisions; counts feed the next pack
+                fa.flags |= _lib.FLAG_TWO_PHASE | _lib.FLAG_SHARDED_DECIDE
+                census = self.spec.shuffler == "none"
+            if census:
                 fa.flags |= _lib.FLAG_FUSED_CENSUS | (_lib.FLAG_FIX_SEC if self.stats_with_sec else 0)
-            ca = fa
+            if self.dist.enabled:
+                self._fused_census = census
+                ca = (ca, fa)
+            else:
+                ca = fa
         self._arg_cache[key] = (a, ca, a.flags)
         return self._arg_cache[key]
+
+    def _uid_flags(self, flags: int) -> int:
+        """uid assignment reads the respawn ballots where the producing generation left
+        them: the fused generation's block stats or the evolve kernel's i32c ballots."""
+        return flags | (_lib.FLAG_MASKS_BS if self._mask_src == "bs" else 0)
 
     def _generation(self, record: bool = False):
         spec, cfg = self.spec, self.cfg
@@ -305,14 +327,48 @@ class SoupEngine:
                 # per-generation fixpoint-fraction statistics (reference Soup.count, code/soup.py:89-103)
                 self.classify_local(self.stats_with_sec, zero=False)
             return
-        # ---- sharded (all-to-all, ONE collective per generation):
-        #   decide -> pack (stats rows of the previous generation + rows other ranks need)
-        #   -> all-to-all -> unpack + uids of the previous generation's newborns
+        # ---- sharded (all-to-all, ONE collective per generation), fused:
+        #   pack (stats rows of the previous generation + rows other ranks need)
+        #   -> all-to-all -> unpack -> uids of the previous generation's newborns
+        #   -> OP_SOUP_GEN: evolve + census + next generation's decisions of every global
+        #      slot (lists + need masks) -> finish (counts, generation counter)
+        # ---- sharded, unfused / recording: decide -> pack -> all-to-all -> unpack -> uids
         #   -> evolve -> census + respawn count (+ generation counter)
         # ---- sharded (all-gather): decide -> all-gather rows -> evolve -> census
         #   -> all-gather stats -> uids
         d = self.dist
-        _lib.run(_lib.OP_SOUP_DECIDE, spec, a, cfg)
+        if self.exchange == "alltoall" and self.fused and not (record and self.recorder is not None):
+            ca0, fa = ca
+            if not self._lists_ready:
+                _lib.run(_lib.OP_SOUP_DECIDE, spec, a, cfg)
+            # full-grid pack / unpack: one-workgroup versions fused into the finish and
+            # uid kernels measured 36 us each (latency-bound loops over 100k rows)
+            _lib.run(_lib.OP_SOUP_PACK, spec, a, cfg)
+            d.all_to_all(self.recvbuf, self.sendbuf)
+            _lib.run(_lib.OP_SOUP_UNPACK, spec, a, cfg)
+            # uids of the previous generation's newborns (stats rows of the exchange)
+            a.flags = self._uid_flags(flags | _lib.FLAG_STATS_X)
+            a.temp, a.temp_bytes = _p(self._blockstat), self._blockstat.numel() * 4
+            _lib.run(_lib.OP_UID_ASSIGN, spec, a, cfg)
+            a.flags = flags
+            # generation (evolve + census + next decisions of every slot) + finish
+            _lib.run(_lib.OP_SOUP_GEN, spec, fa, cfg)
+            if not self._fused_census:
+                # random shuffler: census by the classify kernel (adds to counts[0..4])
+                cflags = ca0.flags
+                ca0.flags = _lib.FLAG_FIX_SEC if self.stats_with_sec else 0
+                _lib.run(_lib.OP_CLASSIFY, spec, ca0, cfg)
+                ca0.flags = cflags
+            self._lists_ready = True
+            self._mask_src = "bs"
+            self._p = 1 - self._p
+            self._pending = True
+            return
+        if isinstance(ca, tuple):
+            ca = ca[0]
+        if not self._lists_ready:
+            _lib.run(_lib.OP_SOUP_DECIDE, spec, a, cfg)
+
         if self.exchange == "allgather":
             # raw 32-bit view: the collective moves bytes whatever the storage dtype
             d.all_gather_rows(self.full.view(torch.int32), self.table_in.view(torch.int32), self.n_total)
@@ -320,8 +376,11 @@ class SoupEngine:
             _lib.run(_lib.OP_SOUP_PACK, spec, a, cfg)
             d.all_to_all(self.recvbuf, self.sendbuf)
             _lib.run(_lib.OP_SOUP_UNPACK, spec, a, cfg)
-            a.flags = flags | _lib.FLAG_STATS_X
+            a.flags = self._uid_flags(flags | _lib.FLAG_STATS_X)
+            a.temp, a.temp_bytes = _p(self._blockstat), self._blockstat.numel() * 4
             _lib.run(_lib.OP_UID_ASSIGN, spec, a, cfg)
+        self._lists_ready = False
+        self._mask_src = "i32c"
         inline = not (record and self.recorder is not None)
         a.flags = flags | (_lib.FLAG_RESPAWN_INLINE if inline else 0)
         _lib.run(_lib.OP_SOUP_EVOLVE, spec, a, cfg)
@@ -344,9 +403,11 @@ class SoupEngine:
         if not (self.dist.enabled and self._pending):
             return
         a, _, flags = self._gen_args()
-        a.flags = flags
+        a.flags = self._uid_flags(flags)
+        a.temp, a.temp_bytes = _p(self._blockstat), self._blockstat.numel() * 4
         self.dist.all_gather_into(self.stats_all, self.counts)
         _lib.run(_lib.OP_UID_ASSIGN, self.spec, a, self.cfg)
+        a.flags = flags
         self._pending = False
 
     def exchange_overflowed(self) -> bool:
@@ -374,7 +435,18 @@ class SoupEngine:
         return counts_dict(c.cpu())
 
     def evolve(self, iterations: int = 1, record: bool = False):
-        for _ in range(iterations):
+        left = int(iterations)
+        while left > 0:
+            ch = self._chunk
+            if (ch is not None and not (record and self.recorder is not None) and left >= ch[2]
+                    and self._p == ch[1] and self.trajectory is None and self.metrics is None):
+                # G generations in one graph launch (no inter-graph gaps)
+                ch[0].replay()
+                self.time += ch[2]
+                left -= ch[2]
+                self._pending = self.dist.enabled
+                continue
+            left -= 1
             self.time += 1
             if record and self.recorder is not None:
                 slot_uid = self.global_uids()  # uid of every slot at generation start
@@ -452,7 +524,9 @@ class SoupEngine:
             return False
         if self.dist.enabled and self.exchange != "alltoall":
             return False
-        if self.dist.enabled and torch.distributed.get_backend() != "nccl":
+        if self.dist.enabled and self.dist.native is None:
+            # torch's process-group collectives are not captured: their watchdog thread
+            # queries events recorded by the capturing stream
             return False
         s = torch.cuda.Stream(self.device)
         s.wait_stream(torch.cuda.current_stream(self.device))
@@ -489,31 +563,76 @@ class SoupEngine:
             return False
         # graphs[k] was captured with parity p0 ^ k; index them by parity
         self._graphs = graphs if p0 == 0 else graphs[::-1]
+        self._capture_chunk(s, p0, pend0)
         return True
+
+    def _capture_chunk(self, s, p0, pend0):
+        """A graph of G consecutive generations (G even: it starts and ends at parity
+        p0) replayed as one launch, removing the per-generation graph-launch gap;
+        validated bitwise against G eager generations (all ranks agree or none use it)."""
+        self._chunk = None
+        G = int(os.environ.get("SRNN_GRAPH_CHUNK", "8"))
+        if G < 2 or G % 2:
+            return
+        ok = True
+        gc = torch.cuda.CUDAGraph()
+        flags0 = (self._lists_ready, self._mask_src)
+        try:
+            with torch.cuda.graph(gc, stream=s, capture_error_mode="thread_local"):
+                for _ in range(G):
+                    self._generation()
+        except Exception as e:  # noqa: BLE001
+            import sys
+            print(f"multi-generation graph capture failed ({type(e).__name__}: {e})", file=sys.stderr)
+            ok = False
+        self._p, self._pending = p0, pend0
+        self._lists_ready, self._mask_src = flags0
+        if ok:
+            ok = self._validate_replay(lambda: gc.replay(), G, parity_after=p0)
+        if self.dist.enabled:
+            flag = torch.tensor([1 if ok else 0], dtype=torch.int32, device=self.device)
+            torch.distributed.all_reduce(flag, op=torch.distributed.ReduceOp.MIN)
+            ok = bool(flag.item())
+        if ok:
+            self._chunk = (gc, p0, G)
 
     def release_graphs(self):
         """Drop the captured graphs (before tearing down the process group: an RCCL
         communicator must not be destroyed while graph executables still reference it)."""
-        if self._graphs is not None:
+        if self._graphs is not None or self._chunk is not None:
             torch.cuda.synchronize(self.device)
-            for g in self._graphs:
+            for g in (self._graphs or []) + ([self._chunk[0]] if self._chunk else []):
                 g.reset()
             self._graphs = None
+            self._chunk = None
 
     def _validate_graphs(self, graphs) -> bool:
+        def replay():
+            for _ in range(2):
+                graphs[self._p].replay()
+                self._p = 1 - self._p
+        return self._validate_replay(replay, 2)
+
+    def _validate_replay(self, replay, gens: int, parity_after=None) -> bool:
+        """Run ``gens`` eager generations from the current state, restore it, run
+        ``replay`` (the captured equivalent), compare bitwise, restore again."""
         state = self._state()
         saved = [t.clone() for t in state]
         p0, pend0, t0 = self._p, self._pending, self.time
-        for _ in range(2):
+        flags0 = (self._lists_ready, self._mask_src)
+        for _ in range(gens):
             self._generation()
         torch.cuda.synchronize(self.device)
+        flags1 = (self._lists_ready, self._mask_src)
         eager = [t.clone() for t in state]
         for t, v in zip(state, saved):
             t.copy_(v)
         self._p, self._pending = p0, pend0
-        for _ in range(2):
-            graphs[self._p].replay()
-            self._p = 1 - self._p
+        self._lists_ready, self._mask_src = flags0
+        replay()
+        if parity_after is not None:
+            self._p = parity_after
+        self._lists_ready, self._mask_src = flags1
         torch.cuda.synchronize(self.device)
         # compare the semantic state only: exchange-buffer row order and the attack
         # lists' link order follow atomics and legitimately differ between runs
@@ -525,5 +644,6 @@ class SoupEngine:
         for t, v in zip(state, saved):
             t.copy_(v)
         self._p, self._pending, self.time = p0, pend0, t0
+        self._lists_ready, self._mask_src = flags0
         torch.cuda.synchronize(self.device)
         return same

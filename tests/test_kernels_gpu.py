@@ -284,3 +284,24 @@ def test_fused_generation_equals_unfused(cuda, spec):
     b.evolve(3)
     assert torch.equal(a.local_rows(), b.local_rows())
     assert a.last_census() == b.last_census()
+
+
+def test_multi_generation_graph_equals_eager(cuda):
+    """capture() also records a graph of 8 consecutive generations (one launch): 21
+    generations through it (+ single-generation graphs for the remainder) == eager."""
+    spec = ArchSpec.weightwise(2, 2)
+    params = dict(attacking_rate=0.1, learn_from_rate=0.1, train=4, remove_divergent=True, remove_zero=True,
+                  epsilon=1e-4)
+    a = SoupEngine(spec, 30000, params, device=cuda, seed=21)
+    b = SoupEngine(spec, 30000, params, device=cuda, seed=21)
+    a.stats = b.stats = True
+    assert a.capture(warmup=1)
+    assert a._chunk is not None and a._chunk[2] == 8
+    b.evolve(1)
+    a.evolve(21)
+    b.evolve(21)
+    assert a.time == b.time == 22
+    assert torch.equal(a.local_rows(), b.local_rows())
+    assert torch.equal(a.uid, b.uid)
+    assert a.last_census() == b.last_census()
+    a.release_graphs()
