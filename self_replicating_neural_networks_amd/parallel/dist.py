@@ -117,7 +117,14 @@ class Dist:
         if (not self.enabled or device.type != "cuda" or os.environ.get("SRNN_NATIVE_COMM", "1") != "1"
                 or dist.get_backend(self.group) != "nccl"):
             return False
-        self.native = NativeComm(self.world, self.rank, device)
+        try:
+            self.native = NativeComm(self.world, self.rank, device)
+        except (RuntimeError, OSError) as e:  # symmetric failures: every rank falls back
+            import sys
+            print(f"native RCCL communicator unavailable ({e}); using torch.distributed collectives",
+                  file=sys.stderr)
+            self.native = None
+            return False
         return True
 
     def close(self):
