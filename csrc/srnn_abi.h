@@ -76,6 +76,9 @@ struct SrnnArgs {
   int32_t dev;          // 0 host (CPU tensors), 1 device (HIP)
   int32_t pad1;
   void* stream;         // hipStream_t for dev == 1
+  int32_t* gen_out;     // soup: where "advance the generation" writes gen + 1 (null -> *gen_ptr in
+                        // place).  The engine keeps a 2-slot ring indexed by the ping-pong parity
+                        // so a kernel can advance the counter while its other blocks still read it.
 };
 
 enum SrnnOp {
@@ -94,11 +97,13 @@ enum SrnnOp {
   OP_VARY_RUN = 12,     // known-fixpoint variation run: nsteps = time to vergence, loss = time as fixpoint
   OP_SOUP_PACK = 13,    // sharded soup: stats rows + local rows needed by other ranks -> sendbuf (tagged)
   OP_SOUP_UNPACK = 14,  // sharded soup: index the received rows (rmap), reset sendcnt
-  OP_SOUP_GEN = 16,     // single rank, fused: evolve + next decisions + census + uids (one launch)
+  OP_SOUP_GEN = 16,     // fused generation: evolve + next decisions + census (+ finish; flag 32768: the
+                        // finish launch also packs the next all-to-all = OP_SOUP_PACK)
   OP_UID_ASSIGN = 15,   // sharded soup: uids of the previous generation's newborns from the per-rank stats
+                        // (flag 16384: the same launch also indexes the received rows = OP_SOUP_UNPACK)
 };
 
-int srnn_abi_version();  // 10
+int srnn_abi_version();  // 11
 int srnn_has_config(const SrnnCfg* cfg);
 int srnn_run(int op, const SrnnCfg* cfg, const SrnnArgs* args);
 const char* srnn_last_error();

@@ -92,7 +92,7 @@ static int dispatch(int op, const SrnnCfg* c, const SrnnArgs* a) {
 
 extern "C" {
 
-int srnn_abi_version() { return 10; }
+int srnn_abi_version() { return 11; }
 
 const char* srnn_last_error() { return srnn::g_err.c_str(); }
 

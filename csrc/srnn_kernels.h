@@ -396,6 +396,11 @@ struct Item {
     if (u01(d.z) < a.learn_from_rate) te = (int32_t)(base + (int64_t)(((uint64_t)d.w * (uint64_t)span) >> 32));
   }
   SRNN_HD static int32_t gen_of(const SrnnArgs& a) { return a.gen_ptr ? a.gen_ptr[0] : a.gen; }
+  // the next generation's counter: the other ring slot (gen_out) or in place
+  SRNN_HD static void set_gen(const SrnnArgs& a, int32_t g) {
+    if (a.gen_out) a.gen_out[0] = g;
+    else if (a.gen_ptr) ((int32_t*)a.gen_ptr)[0] = g;
+  }
 
   // Every global slot: link attacks on this rank's victims into per-victim lists
   // (head[victim] in i32e, pre-set to -1; next[attacker] in i32f).  Optional i32a/i32b
@@ -754,7 +759,7 @@ __global__ __launch_bounds__(TB) void k_soup_gen(SrnnCfg c, SrnnArgs a) {
   }
   if (lane == 0) {
     ((int64_t*)a.uid_base)[0] = base + total;
-    ((int32_t*)a.gen_ptr)[0] = gen + 1;
+    I::set_gen(a, gen + 1);
     if (a.counts) {
 #pragma unroll
       for (int q = 0; q < 5; ++q) a.counts[q] = census ? cs[q] : 0ull;
@@ -771,6 +776,18 @@ __global__ __launch_bounds__(TB) void k_soup_gen(SrnnCfg c, SrnnArgs a) {
 template <class Net, class S, int NT>
 __global__ __launch_bounds__(NT) void k_gen_finish(SrnnArgs a, int32_t nb) {
   using I = Item<Net, S>;
+  if (blockIdx.x > 0) {
+    // flag 32768, blocks >= 1: pack the next generation's all-to-all (rows other ranks
+    // need; generation-start rows of gen + 1 = this generation's output).  Block 0 only
+    // writes the OTHER ring slot of the counter, so the gen read here is stable.
+    SrnnArgs pa = a;
+    pa.W2 = a.W;
+    pa.gen_ptr = nullptr;
+    pa.gen = I::gen_of(a) + 1;
+    const int64_t j = (int64_t)(blockIdx.x - 1) * NT + threadIdx.x;
+    if (j < a.n) I::soup_pack(pa, j);
+    return;
+  }
   __shared__ int32_t s_scan[1024];
   __shared__ unsigned long long s_cs[5];
   const int t = threadIdx.x;
@@ -819,11 +836,12 @@ __global__ __launch_bounds__(NT) void k_gen_finish(SrnnArgs a, int32_t nb) {
   if (t == 0) {
     const int32_t total = s_scan[1023];
     if (!sharded) ((int64_t*)a.uid_base)[0] = base + total;
-    ((int32_t*)a.gen_ptr)[0] = gen + 1;
+    I::set_gen(a, gen + 1);
     if (a.counts) {
       for (int q = 0; q < 5; ++q) a.counts[q] = (a.flags & 1024) ? s_cs[q] : 0ull;
       a.counts[5] = (uint64_t)total;
     }
+    if (a.flags & 32768) I::pack_stats(a);  // this generation's stats ride on the next exchange
   }
 }
 
@@ -883,10 +901,18 @@ int soup_gen(const SrnnCfg& c, const SrnnArgs& a) {
         }
       ((int64_t*)a.uid_base)[0] = u;
     }
-    ((int32_t*)a.gen_ptr)[0] = gen + 1;
+    I::set_gen(a, gen + 1);
     if (a.counts) {
       for (int q = 0; q < 5; ++q) a.counts[q] = cs[q];
       a.counts[5] = (uint64_t)total;
+    }
+    if (a.flags & 32768) {
+      I::pack_stats(a);
+      SrnnArgs pa = a;
+      pa.W2 = a.W;
+      pa.gen_ptr = nullptr;
+      pa.gen = gen + 1;
+      for (int64_t j = 0; j < a.n; ++j) I::soup_pack(pa, j);
     }
     return 0;
   }
@@ -897,8 +923,11 @@ int soup_gen(const SrnnCfg& c, const SrnnArgs& a) {
     return -2;
   }
   hipLaunchKernelGGL((k_soup_gen<Net, S>), dim3((unsigned)blocks), dim3(TB), 0, (hipStream_t)a.stream, c, a);
-  if (a.flags & 2048)
-    hipLaunchKernelGGL((k_gen_finish<Net, S, 1024>), dim3(1), dim3(1024), 0, (hipStream_t)a.stream, a, (int32_t)blocks);
+  if (a.flags & 2048) {
+    const int64_t pack_blocks = (a.flags & 32768) ? (a.n + 1023) / 1024 : 0;
+    hipLaunchKernelGGL((k_gen_finish<Net, S, 1024>), dim3((unsigned)(1 + pack_blocks)), dim3(1024), 0,
+                       (hipStream_t)a.stream, a, (int32_t)blocks);
+  }
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) {
     set_error(hipGetErrorString(e));
@@ -935,7 +964,7 @@ __global__ __launch_bounds__(TBC) void k_classify_count(SrnnCfg c, SrnnArgs a) {
   }
   // sharded soup: the census closes the generation (no later kernel of this generation
   // reads the counter)
-  if ((a.flags & 512) && blockIdx.x == 0 && threadIdx.x == 0) ((int32_t*)a.gen_ptr)[0] += 1;
+  if ((a.flags & 512) && blockIdx.x == 0 && threadIdx.x == 0) I::set_gen(a, I::gen_of(a) + 1);
 }
 
 template <class Net, int OP, class S>
@@ -985,7 +1014,7 @@ int host_run(const SrnnCfg& c, const SrnnArgs& a) {
     for (int q = 0; q < 5; ++q) a.counts[q] += local[q];
     if (a.flags & 64)
       for (int64_t i = 0; i < items; ++i) a.counts[5] += a.respawn[i] != 0;
-    if (a.flags & 512) ((int32_t*)a.gen_ptr)[0] += 1;
+    if (a.flags & 512) I::set_gen(a, I::gen_of(a) + 1);
     return 0;
   }
   if (OP == OP_SOUP_PACK) {
@@ -1059,7 +1088,7 @@ __global__ __launch_bounds__(TBR) void k_respawn_seq(SrnnCfg c, SrnnArgs a) {
   __syncthreads();
   if (threadIdx.x == 0) {
     ((int64_t*)a.uid_base)[0] = base + s_cnt[TBR - 1];
-    if (a.gen_ptr) ((int32_t*)a.gen_ptr)[0] += 1;
+    I::set_gen(a, I::gen_of(a) + 1);
   }
   if (a.counts && threadIdx.x < 5) a.counts[threadIdx.x] = 0;  // fresh histogram for the census
 }
@@ -1086,7 +1115,7 @@ int respawn_seq(const SrnnCfg& c, const SrnnArgs& a) {
     ++k;
   }
   ((int64_t*)a.uid_base)[0] = k;
-  if (a.gen_ptr) ((int32_t*)a.gen_ptr)[0] += 1;
+  I::set_gen(a, I::gen_of(a) + 1);
   if (a.counts)
     for (int q = 0; q < 5; ++q) a.counts[q] = 0;
   return 0;
@@ -1103,6 +1132,14 @@ __global__ __launch_bounds__(TBR) void k_uid_assign(SrnnCfg c, SrnnArgs a) {
   using I = Item<Net, S>;
   __shared__ int32_t s_cnt[TBR];
   __shared__ int64_t s_prefix, s_total;
+  if (blockIdx.x > 0) {
+    // flag 16384, blocks >= 1: index the received rows (OP_SOUP_UNPACK); block 0 resets
+    // the send counters (the pack that used them ran in an earlier launch)
+    const int64_t k = (int64_t)(blockIdx.x - 1) * TBR + threadIdx.x;
+    if (k < (int64_t)a.world * a.cap) I::soup_unpack(a, k);
+    return;
+  }
+  if ((a.flags & 16384) && threadIdx.x < a.world) a.sendcnt[threadIdx.x] = I::SR;
   if (threadIdx.x == 0) {
     int64_t pre = 0, tot = 0, cen[5] = {0, 0, 0, 0, 0}, all = 0;
     for (int r = 0; r < a.world; ++r) {
@@ -1155,13 +1192,19 @@ template <class Net, class S>
 int uid_assign(const SrnnCfg& c, const SrnnArgs& a) {
   using I = Item<Net, S>;
   if (a.dev) {
-    hipLaunchKernelGGL((k_uid_assign<Net, S>), dim3(1), dim3(TBR), 0, (hipStream_t)a.stream, c, a);
+    const int64_t unpack_blocks = (a.flags & 16384) ? ((int64_t)a.world * a.cap + TBR - 1) / TBR : 0;
+    hipLaunchKernelGGL((k_uid_assign<Net, S>), dim3((unsigned)(1 + unpack_blocks)), dim3(TBR), 0,
+                       (hipStream_t)a.stream, c, a);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) {
       set_error(hipGetErrorString(e));
       return -3;
     }
     return 0;
+  }
+  if (a.flags & 16384) {  // post-exchange: index the received rows too
+    for (int64_t k = 0; k < (int64_t)a.world * a.cap; ++k) I::soup_unpack(a, k);
+    for (int r = 0; r < a.world; ++r) a.sendcnt[r] = I::SR;
   }
   int64_t pre = 0, tot = 0, cen[5] = {0, 0, 0, 0, 0}, all = 0;
   for (int r = 0; r < a.world; ++r) {

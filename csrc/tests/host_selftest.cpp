@@ -193,7 +193,7 @@ static std::vector<float> soup(int R, int64_t N, int gens, std::vector<int64_t>*
 }
 
 int main() {
-  CHECK(srnn_abi_version() == 10);
+  CHECK(srnn_abi_version() == 11);
   ops_smoke(ww22(), 1000);
   ops_smoke(agg422(), 777);
   std::vector<int64_t> u1, u2, u3;

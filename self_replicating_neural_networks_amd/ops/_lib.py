@@ -19,7 +19,7 @@ import threading
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libsrnn.so")
 CSRC = os.path.normpath(os.path.join(_HERE, "..", "..", "csrc"))
-ABI_VERSION = 10
+ABI_VERSION = 11
 
 OP_INIT = 0
 OP_APPLY = 1
@@ -53,6 +53,8 @@ FLAG_FUSED_CENSUS = 1024
 FLAG_TWO_PHASE = 2048
 FLAG_SHARDED_DECIDE = 4096
 FLAG_MASKS_BS = 8192
+FLAG_POST_UNPACK = 16384
+FLAG_FINISH_PACK = 32768
 
 
 class SrnnCfg(ctypes.Structure):
@@ -81,7 +83,7 @@ class SrnnArgs(ctypes.Structure):
         ("stats", _P), ("census", _P),
         ("action", _P), ("counterpart", _P), ("respawn", _P),
         ("temp", _P), ("temp_bytes", ctypes.c_int64),
-        ("dev", ctypes.c_int32), ("pad1", ctypes.c_int32), ("stream", _P),
+        ("dev", ctypes.c_int32), ("pad1", ctypes.c_int32), ("stream", _P), ("gen_out", _P),
     ]
 
 

@@ -145,7 +145,10 @@ class SoupEngine:
         self.uid = torch.arange(self.lo, self.hi, dtype=torch.int64, device=dev)
         self.next_uid = torch.full((1,), self.n_total, dtype=torch.int64, device=dev)
         self.uid_base = torch.zeros(1, dtype=torch.int64, device=dev)
-        self.gen_dev = torch.ones(1, dtype=torch.int32, device=dev)  # generation about to run
+        # generation counter as a 2-slot ring indexed by the ping-pong parity: a launch
+        # reads slot _p and the generation-closing kernel writes slot 1-_p, so blocks of
+        # one launch never race on it (gen_dev is the current slot)
+        self._gen_ring = torch.ones(2, dtype=torch.int32, device=dev)
         self.time = 0
         # attack lists, one buffer per ping-pong parity: the fused single-rank generation
         # links the NEXT generation's attacks into the other parity's buffer
@@ -156,6 +159,7 @@ class SoupEngine:
         # with the all-to-all exchange fuse the evolve, census and next decisions too
         self.fused = not self.dist.enabled or exchange == "alltoall"
         self._mask_src = "i32c"   # where the pending respawn ballots live ("bs": block stats)
+        self._packed = False      # sharded: the coming generation's send buffer is packed
         self._fused_census = False
         self.two_phase = os.environ.get("SRNN_GEN_TWO_PHASE", "1") == "1"  # + a 1-workgroup finish kernel
         nb = -(-self.n // 64)
@@ -190,6 +194,11 @@ class SoupEngine:
             K.init_rows(spec, local, self.uid, self.seed)
 
     # ------------------------------------------------------------------ views
+    @property
+    def gen_dev(self) -> torch.Tensor:
+        """Device scalar (1-element view): the generation about to run."""
+        return self._gen_ring[self._p:self._p + 1]
+
     @property
     def table_in(self) -> torch.Tensor:
         """This rank's generation-start rows read by the next generation."""
@@ -226,6 +235,7 @@ class SoupEngine:
         a.severity = int(self.params.get("learn_from_severity", 1))
         a.flags = self._flags()
         a.gen_ptr = _p(self.gen_dev)
+        a.gen_out = _p(self._gen_ring[1 - self._p:2 - self._p])
         a.segment = int(self.params.get("segment", 0) or 0)
         if self.device.type == "cuda":
             a.dev = 1
@@ -281,7 +291,7 @@ class SoupEngine:
             census = self.stats and self.spec.shuffler == "none"
             if self.dist.enabled:
                 # sharded: every global slot's next decisions; counts feed the next pack
-                fa.flags |= _lib.FLAG_TWO_PHASE | _lib.FLAG_SHARDED_DECIDE
+                fa.flags |= _lib.FLAG_TWO_PHASE | _lib.FLAG_SHARDED_DECIDE | _lib.FLAG_FINISH_PACK
                 census = self.spec.shuffler == "none"
             if census:
                 fa.flags |= _lib.FLAG_FUSED_CENSUS | (_lib.FLAG_FIX_SEC if self.stats_with_sec else 0)
@@ -341,18 +351,19 @@ class SoupEngine:
             ca0, fa = ca
             if not self._lists_ready:
                 _lib.run(_lib.OP_SOUP_DECIDE, spec, a, cfg)
-            # full-grid pack / unpack: one-workgroup versions fused into the finish and
-            # uid kernels measured 36 us each (latency-bound loops over 100k rows)
-            _lib.run(_lib.OP_SOUP_PACK, spec, a, cfg)
+            if not self._packed:
+                _lib.run(_lib.OP_SOUP_PACK, spec, a, cfg)
             d.all_to_all(self.recvbuf, self.sendbuf)
-            _lib.run(_lib.OP_SOUP_UNPACK, spec, a, cfg)
-            # uids of the previous generation's newborns (stats rows of the exchange)
-            a.flags = self._uid_flags(flags | _lib.FLAG_STATS_X)
+            # post-exchange launch: block 0 assigns the uids of the previous generation's
+            # newborns (stats rows of the exchange), the other blocks index the received rows
+            a.flags = self._uid_flags(flags | _lib.FLAG_STATS_X | _lib.FLAG_POST_UNPACK)
             a.temp, a.temp_bytes = _p(self._blockstat), self._blockstat.numel() * 4
             _lib.run(_lib.OP_UID_ASSIGN, spec, a, cfg)
             a.flags = flags
-            # generation (evolve + census + next decisions of every slot) + finish
+            # generation (evolve + census + next decisions of every slot); finish launch:
+            # block 0 closes the generation, the other blocks pack the next exchange
             _lib.run(_lib.OP_SOUP_GEN, spec, fa, cfg)
+            self._packed = True
             if not self._fused_census:
                 # random shuffler: census by the classify kernel (adds to counts[0..4])
                 cflags = ca0.flags
@@ -368,12 +379,13 @@ class SoupEngine:
             ca = ca[0]
         if not self._lists_ready:
             _lib.run(_lib.OP_SOUP_DECIDE, spec, a, cfg)
-
+        packed, self._packed = self._packed, False
         if self.exchange == "allgather":
             # raw 32-bit view: the collective moves bytes whatever the storage dtype
             d.all_gather_rows(self.full.view(torch.int32), self.table_in.view(torch.int32), self.n_total)
         else:
-            _lib.run(_lib.OP_SOUP_PACK, spec, a, cfg)
+            if not packed:
+                _lib.run(_lib.OP_SOUP_PACK, spec, a, cfg)
             d.all_to_all(self.recvbuf, self.sendbuf)
             _lib.run(_lib.OP_SOUP_UNPACK, spec, a, cfg)
             a.flags = self._uid_flags(flags | _lib.FLAG_STATS_X)
@@ -409,6 +421,9 @@ class SoupEngine:
         _lib.run(_lib.OP_UID_ASSIGN, self.spec, a, self.cfg)
         a.flags = flags
         self._pending = False
+        if self._packed:
+            # the packed send buffer carries these stats too: they are settled now
+            self.sendbuf.view(self.dist.world, -1)[:, :12].zero_()
 
     def exchange_overflowed(self) -> bool:
         return bool(self.dist.enabled and self.exchange == "alltoall" and int(self.ovf.item()) != 0)
@@ -461,6 +476,8 @@ class SoupEngine:
                 self._generation()
             self._hooks()
         self._flush()  # uids / census consistent between evolve calls
+        if self.dist.native is not None:
+            self.dist.native.check()  # RCCL asynchronous errors (peer failure) surface here
         return self
 
     def _hooks(self):
@@ -500,7 +517,7 @@ class SoupEngine:
     # ------------------------------------------------------------------ HIP graphs
     def _state(self):
         """Every device tensor a generation reads or writes (graph validation)."""
-        names = ["_bufs", "uid", "next_uid", "gen_dev", "heads", "nexts", "flags32", "action", "counterpart",
+        names = ["_bufs", "uid", "next_uid", "_gen_ring", "heads", "nexts", "flags32", "action", "counterpart",
                  "loss", "respawn", "counts", "census", "need", "sendcnt", "rmap", "ovf", "sendbuf", "recvbuf",
                  "full", "stats_all", "_blockstat", "_done"]
         out = []
@@ -576,7 +593,7 @@ class SoupEngine:
             return
         ok = True
         gc = torch.cuda.CUDAGraph()
-        flags0 = (self._lists_ready, self._mask_src)
+        flags0 = (self._lists_ready, self._mask_src, self._packed)
         try:
             with torch.cuda.graph(gc, stream=s, capture_error_mode="thread_local"):
                 for _ in range(G):
@@ -586,7 +603,7 @@ class SoupEngine:
             print(f"multi-generation graph capture failed ({type(e).__name__}: {e})", file=sys.stderr)
             ok = False
         self._p, self._pending = p0, pend0
-        self._lists_ready, self._mask_src = flags0
+        self._lists_ready, self._mask_src, self._packed = flags0
         if ok:
             ok = self._validate_replay(lambda: gc.replay(), G, parity_after=p0)
         if self.dist.enabled:
@@ -619,31 +636,31 @@ class SoupEngine:
         state = self._state()
         saved = [t.clone() for t in state]
         p0, pend0, t0 = self._p, self._pending, self.time
-        flags0 = (self._lists_ready, self._mask_src)
+        flags0 = (self._lists_ready, self._mask_src, self._packed)
         for _ in range(gens):
             self._generation()
         torch.cuda.synchronize(self.device)
-        flags1 = (self._lists_ready, self._mask_src)
+        flags1 = (self._lists_ready, self._mask_src, self._packed)
         eager = [t.clone() for t in state]
         for t, v in zip(state, saved):
             t.copy_(v)
         self._p, self._pending = p0, pend0
-        self._lists_ready, self._mask_src = flags0
+        self._lists_ready, self._mask_src, self._packed = flags0
         replay()
         if parity_after is not None:
             self._p = parity_after
-        self._lists_ready, self._mask_src = flags1
+        self._lists_ready, self._mask_src, self._packed = flags1
         torch.cuda.synchronize(self.device)
         # compare the semantic state only: exchange-buffer row order and the attack
         # lists' link order follow atomics and legitimately differ between runs
         keep = {id(t) for t in self._bufs} | {id(getattr(self, k)) for k in (
-            "uid", "next_uid", "gen_dev", "counts", "census", "loss", "respawn", "action", "counterpart",
+            "uid", "next_uid", "_gen_ring", "counts", "census", "loss", "respawn", "action", "counterpart",
             "flags32", "ovf") if isinstance(getattr(self, k, None), torch.Tensor)}
         same = all(torch.equal(x.view(torch.uint8), y.view(torch.uint8))
                    for x, y in zip(state, eager) if id(x) in keep)
         for t, v in zip(state, saved):
             t.copy_(v)
         self._p, self._pending, self.time = p0, pend0, t0
-        self._lists_ready, self._mask_src = flags0
+        self._lists_ready, self._mask_src, self._packed = flags0
         torch.cuda.synchronize(self.device)
         return same

@@ -305,3 +305,21 @@ def test_multi_generation_graph_equals_eager(cuda):
     assert torch.equal(a.uid, b.uid)
     assert a.last_census() == b.last_census()
     a.release_graphs()
+
+
+def test_soup_is_deterministic_run_to_run(cuda):
+    """Race detector for the atomics of the generation (attack-list links, need masks,
+    block stats): two identical soups stay bitwise equal."""
+    params = dict(attacking_rate=0.5, learn_from_rate=0.5, train=2, remove_divergent=True, remove_zero=True,
+                  epsilon=1e-4)
+    runs = []
+    for _ in range(2):
+        e = SoupEngine(ArchSpec.weightwise(2, 2), 50000, params, device=cuda, seed=77)
+        e.stats = True
+        e.capture(warmup=1)
+        e.evolve(12)
+        runs.append((e.local_rows().clone(), e.uid.clone(), e.last_census()))
+        e.release_graphs()
+    assert torch.equal(runs[0][0], runs[1][0])
+    assert torch.equal(runs[0][1], runs[1][1])
+    assert runs[0][2] == runs[1][2]
