@@ -72,29 +72,42 @@ SRNN_HD float u01_open0(uint32_t x) { return (float)((x >> 8) + 1u) * (1.0f / 16
 
 SRNN_HD bool finitef(float v) { return (__builtin_isfinite(v)) != 0; }
 
-// Permutation of [0, n) (n <= 16) packed as nibbles of a 64-bit register: Fisher-Yates
-// with the swap index j = (r16 * (i+1)) >> 16 from two Philox draws (15 x 16-bit chunks;
-// bias (i+1)/65536).  No memory traffic: replaces the LDS byte shuffle for small nets.
+// Permutation of [0, n) (n <= 16) packed as nibbles of a 64-bit register.  Fisher-Yates
+// whose swap indices j_i in [0, i] are the mixed-radix digits of ONE uniform 64-bit value
+// u (radices n, n-1, ..., 2): j = hi64(u * (i+1)), u = lo64(u * (i+1)).  log2(16!) = 44.3
+// bits are consumed, so every permutation's probability is off by < 16!/2^64 (~1e-6
+// relative): uniform for all practical purposes.  One Philox draw (128 bits) serves two
+// consecutive epochs (steps 2k and 2k+1).  No memory traffic.
+SRNN_HD uint64_t perm_bits(const U4& r, uint32_t step) {
+  return (step & 1u) ? (((uint64_t)r.w << 32) | r.z) : (((uint64_t)r.y << 32) | r.x);
+}
+SRNN_HD U4 perm_draw(const Rng& rng, uint64_t id, uint32_t step, uint32_t purpose) {
+  return rng.draw(id, (step >> 1) * 64u, purpose);
+}
 template <int N>
-SRNN_HD uint64_t shuffle16(const Rng& rng, uint64_t id, uint32_t step, uint32_t purpose) {
+SRNN_HD uint64_t perm_from_bits(uint64_t u) {
   static_assert(N <= 16, "nibble permutation holds at most 16 entries");
   uint64_t p = 0;
 #pragma unroll
   for (int k = 0; k < N; ++k) p |= (uint64_t)k << (4 * k);
-  U4 r0 = rng.draw(id, step * 64u, purpose);
-  U4 r1 = rng.draw(id, step * 64u + 1u, purpose);
-  const uint32_t words[8] = {r0.x, r0.y, r0.z, r0.w, r1.x, r1.y, r1.z, r1.w};
+  uint32_t ul = (uint32_t)u, uh = (uint32_t)(u >> 32);
 #pragma unroll
   for (int i = N - 1; i > 0; --i) {
-    const int c = N - 1 - i;  // chunk index (static)
-    const uint32_t r16 = (words[c >> 1] >> (16 * (c & 1))) & 0xFFFFu;
-    const uint32_t j = (r16 * (uint32_t)(i + 1)) >> 16;
+    const uint64_t lo = (uint64_t)ul * (uint32_t)(i + 1);
+    const uint64_t hi = (uint64_t)uh * (uint32_t)(i + 1) + (lo >> 32);
+    const uint32_t j = (uint32_t)(hi >> 32);
+    ul = (uint32_t)lo;
+    uh = (uint32_t)hi;
     const uint64_t ni = (p >> (4 * i)) & 15u;
     const uint64_t nj = (p >> (4 * j)) & 15u;
     const uint64_t x = ni ^ nj;
     p ^= (x << (4 * i)) | (x << (4 * j));
   }
   return p;
+}
+template <int N>
+SRNN_HD uint64_t shuffle16(const Rng& rng, uint64_t id, uint32_t step, uint32_t purpose) {
+  return perm_from_bits<N>(perm_bits(perm_draw(rng, id, step, purpose), step));
 }
 
 // ----------------------------------------------------------------------------------
@@ -467,13 +480,24 @@ struct Weightwise {
       uint64_t ident = 0;
 #pragma unroll
       for (int k = 0; k < P; ++k) ident |= (uint64_t)k << (4 * k);
-      uint64_t pn = c.shuffle ? shuffle16<P>(c.rng, c.uid, c.ctr, P_SHUFFLE) : ident;
+      // one Philox draw per pair of epochs (c.ctr is the same for every lane: uniform branch)
+      U4 rr = perm_draw(c.rng, c.uid, c.ctr, P_SHUFFLE);
+      uint32_t pair = c.ctr >> 1;
+      uint64_t pn = c.shuffle ? perm_from_bits<P>(perm_bits(rr, c.ctr)) : ident;
       float loss = 0.f;
       for (int e = 0; e < E; ++e) {
         if (SELF && e > 0)
 #pragma unroll
           for (int k = 0; k < P; ++k) reinterpret_cast<float*>(&c.samp[k * c.stride])[0] = w[k];
-        const uint64_t pn_next = c.shuffle ? shuffle16<P>(c.rng, c.uid, c.ctr + 1u, P_SHUFFLE) : ident;
+        uint64_t pn_next = ident;
+        if (c.shuffle) {
+          const uint32_t nx = c.ctr + 1u;
+          if ((nx >> 1) != pair) {
+            pair = nx >> 1;
+            rr = perm_draw(c.rng, c.uid, nx, P_SHUFFLE);
+          }
+          pn_next = perm_from_bits<P>(perm_bits(rr, nx));
+        }
         float4 smp[P];
 #pragma unroll
         for (int q = 0; q < P; ++q) smp[q] = c.samp[(int)((pn >> (4 * q)) & 15u) * c.stride];

@@ -77,18 +77,26 @@ def fisher_yates(n_items, seed, ids, step, purpose):
 
 
 def shuffle16(n_items, seed, ids, step, purpose):
-    """Nibble-register Fisher-Yates of csrc shuffle16 (n <= 16): j = (r16 * (i+1)) >> 16."""
+    """Nibble-register Fisher-Yates of csrc shuffle16 (n <= 16): the swap indices are the
+    mixed-radix digits of one uniform 64-bit value (j = hi64(u * (i+1)), u = lo64(...)),
+    taken from half of the Philox draw (step >> 1) (one draw per two epochs)."""
     ids = np.asarray(ids, dtype=np.uint64).reshape(-1)
     n = ids.shape[0]
     perm = np.tile(np.arange(n_items, dtype=np.int64), (n, 1))
     rows = np.arange(n)
-    r0 = draw(seed, ids, np.uint64((int(step) * 64) & M32), purpose)
-    r1 = draw(seed, ids, np.uint64((int(step) * 64 + 1) & M32), purpose)
-    words = list(r0) + list(r1)
+    step = int(step)
+    r = draw(seed, ids, np.uint64(((step >> 1) * 64) & M32), purpose)
+    lo_w, hi_w = (r[2], r[3]) if step & 1 else (r[0], r[1])
+    ul = lo_w.astype(np.uint64)
+    uh = hi_w.astype(np.uint64)
+    m32 = np.uint64(0xFFFFFFFF)
     for i in range(n_items - 1, 0, -1):
-        c = n_items - 1 - i
-        r16 = (words[c >> 1].astype(np.uint64) >> np.uint64(16 * (c & 1))) & np.uint64(0xFFFF)
-        j = ((r16 * np.uint64(i + 1)) >> np.uint64(16)).astype(np.int64)
+        k = np.uint64(i + 1)
+        lo = ul * k
+        hi = uh * k + (lo >> np.uint64(32))
+        j = (hi >> np.uint64(32)).astype(np.int64)
+        ul = lo & m32
+        uh = hi & m32
         a = perm[rows, i].copy()
         perm[rows, i] = perm[rows, j]
         perm[rows, j] = a
