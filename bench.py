@@ -12,10 +12,11 @@ scaling: the population is sharded, every rank owns 100k particles; at N=1 this 
 100k-particle soup).  Random-init weights, fp32 (the reference's dtype; bf16 would make
 the 1e-4 fixpoint test meaningless).
 
-Multi-GPU (N>1): every rank owns 100k particles; one generation is decide -> pack -> ONE
-RCCL all-to-all (partner rows + per-rank stats rows, over xGMI) -> unpack/uids -> evolve
--> census, captured with the collective inside a hipGraph (validated bitwise against the
-eager path on every rank before use; falls back to eager generations otherwise).
+Multi-GPU (N>1): every rank owns 100k particles; one generation is ONE all-to-all on the
+soup's own RCCL communicator (partner rows + per-rank stats rows, over xGMI) -> post-exchange
+launch (received-row index + newborn uids) -> generation kernel (evolve + census + the next
+generation's decisions of every global slot) -> finish launch (counts + packing the next
+exchange).  Single GPU: the generation kernel + finish, 8 generations per hipGraph.
 
 value = particles x generations / second over the whole job (max time over ranks).
 

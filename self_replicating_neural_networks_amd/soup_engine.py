@@ -545,6 +545,12 @@ class SoupEngine:
             # torch's process-group collectives are not captured: their watchdog thread
             # queries events recorded by the capturing stream
             return False
+        if self.dist.world > 1 and os.environ.get("SRNN_SHARDED_GRAPH", "0") != "1":
+            # multi-GPU generations run eagerly by default: a generation is ~0.1 ms of GPU
+            # work against ~0.04 ms of host enqueue, so the host stays ahead; capturing RCCL
+            # peer-to-peer collectives is validated with one rank only (opt in with
+            # SRNN_SHARDED_GRAPH=1)
+            return False
         s = torch.cuda.Stream(self.device)
         s.wait_stream(torch.cuda.current_stream(self.device))
         with torch.cuda.stream(s):
