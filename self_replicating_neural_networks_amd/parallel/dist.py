@@ -182,6 +182,11 @@ class Dist:
         """Equal-split all-to-all (RCCL over xGMI for nccl: direct peer links)."""
         if self._use_native(out, inp):
             self.native.all_to_all(out, inp)
+        elif self.enabled and inp.is_cuda and dist.get_backend(self.group) == "gloo":
+            # gloo rehearsal of device tensors (e.g. ranks sharing one GPU): stage on the host
+            o = torch.empty_like(out, device="cpu")
+            dist.all_to_all_single(o, inp.cpu(), group=self.group)
+            out.copy_(o)
         elif self.enabled:
             dist.all_to_all_single(out, inp, group=self.group)
         else:
