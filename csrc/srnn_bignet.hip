@@ -15,6 +15,7 @@
 // final write.  MFMA does not apply: each particle is a GEMV chain with its own weights
 // (M = 1), see docs/kernels.md.
 #include "srnn_kernels.h"
+#include <cstdlib>
 
 namespace srnn {
 
@@ -383,6 +384,11 @@ __global__ __launch_bounds__(TBB) void k_big(SrnnCfg c, SrnnArgs a) {
       if constexpr (OP == OP_LEARN) {
         // teacher samples are fixed: aggregate the teacher row once (through L.act as scratch)
         const float* tr = a.W2 + (a.idx_t ? a.idx_t[p] : p) * T::PP;
+        if (c.aggregator != 0) {  // max aggregators: stage the teacher row, sequential semantics
+          load_row<T>(L.t, tr, lane);
+          __builtin_amdgcn_wave_barrier();
+          aggregate_lds<T>(L.t, g, lane, c.aggregator);
+        }
         double acc[T::A];
 #pragma unroll
         for (int q = 0; q < T::A; ++q) acc[q] = 0.0;
@@ -394,7 +400,8 @@ __global__ __launch_bounds__(TBB) void k_big(SrnnCfg c, SrnnArgs a) {
 #pragma unroll
         for (int q = 0; q < T::A; ++q) {
           const int b = q * T::CS, e = (q == T::A - 1) ? T::P : b + T::CS;
-          g[q] = (float)(wave_sum(acc[q]) / (double)(e - b));
+          const float mean = (float)(wave_sum(acc[q]) / (double)(e - b));
+          if (c.aggregator == 0) g[q] = mean;
         }
       }
       __builtin_amdgcn_wave_barrier();
@@ -569,6 +576,305 @@ __global__ __launch_bounds__(256) void k_big_lane(SrnnCfg c, SrnnArgs a) {
   }
 }
 
+// ------------------------------------------------------------------ lane per particle
+// classify / attack / train with the particle's whole row in VGPRs (P = 280 floats:
+// ~360 VGPRs, one wave per SIMD): every lane does useful work instead of the 10 of 64
+// lanes of the wave-per-particle layers, and the kernels become HBM-bound (1.1 KB row per
+// particle).  Arithmetic in the same order as the wave kernels (dense: x[0]*k then fma
+// over the inputs; chunk means as double sums, here in index order).
+template <class T>
+__device__ __forceinline__ void lrow_load(const float* __restrict__ row, float (&w)[T::P]) {
+  const float4* r4 = reinterpret_cast<const float4*>(row);
+#pragma unroll
+  for (int q = 0; q < T::PP / 4; ++q) {
+    const float4 v = r4[q];
+    if (4 * q + 0 < T::P) w[4 * q + 0] = v.x;
+    if (4 * q + 1 < T::P) w[4 * q + 1] = v.y;
+    if (4 * q + 2 < T::P) w[4 * q + 2] = v.z;
+    if (4 * q + 3 < T::P) w[4 * q + 3] = v.w;
+  }
+}
+template <class T>
+__device__ __forceinline__ void lrow_store(float* __restrict__ row, const float (&w)[T::P]) {
+  float4* r4 = reinterpret_cast<float4*>(row);
+#pragma unroll
+  for (int q = 0; q < T::PP / 4; ++q) {
+    float v[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) v[e] = (4 * q + e < T::P) ? w[4 * q + e] : 0.f;
+    r4[q] = make_float4(v[0], v[1], v[2], v[3]);
+  }
+}
+template <class T>
+__device__ __forceinline__ void lrow_store_state(float* __restrict__ row, const float* h) {
+  float4* r4 = reinterpret_cast<float4*>(row);
+#pragma unroll
+  for (int q = 0; q < T::PP / 4; ++q) {
+    float v[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) v[e] = (4 * q + e < T::P) ? h[T::chunk_c(4 * q + e)] : 0.f;
+    r4[q] = make_float4(v[0], v[1], v[2], v[3]);
+  }
+}
+// chunk aggregation of a register row (reference: python-float sums / sequential max)
+template <class T>
+__device__ __forceinline__ void lrow_aggregate(const float (&w)[T::P], float* g, int aggregator) {
+#pragma unroll
+  for (int c = 0; c < T::A; ++c) {
+    constexpr int dummy = 0;
+    (void)dummy;
+    const int b = c * T::CS, e = (c == T::A - 1) ? T::P : b + T::CS;
+    if (aggregator == 0) {
+      double acc = 0.0;
+#pragma unroll
+      for (int k = 0; k < T::P; ++k)
+        if (k >= b && k < e) acc += (double)w[k];
+      g[c] = (float)(acc / (double)(e - b));
+    } else {
+      float m = w[b];
+#pragma unroll
+      for (int k = 0; k < T::P; ++k)
+        if (k >= b && k < e) m = (aggregator == 1) ? (w[k] > m ? w[k] : m) : ((w[k] > m && w[k] != 0.0f) ? w[k] : m);
+      g[c] = m;
+    }
+  }
+}
+// aggregation of a streamed row (attack target / teacher): float4 by float4 into the
+// chunk accumulators (same per-chunk order as lrow_aggregate), the row is never held
+template <class T>
+__device__ __forceinline__ void lstream_aggregate(const float* __restrict__ row, float* g, int aggregator) {
+  const float4* r4 = reinterpret_cast<const float4*>(row);
+  double acc[T::A];
+  float m[T::A];
+#pragma unroll
+  for (int c = 0; c < T::A; ++c) acc[c] = 0.0;
+#pragma unroll
+  for (int q = 0; q < T::PP / 4; ++q) {
+    const float4 v4 = r4[q];
+    const float v[4] = {v4.x, v4.y, v4.z, v4.w};
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int k = 4 * q + e;
+      if (k >= T::P) continue;
+      const int c = T::chunk_c(k);
+      if (aggregator == 0) {
+        acc[c] += (double)v[e];
+      } else if (k == c * T::CS) {
+        m[c] = v[e];
+      } else {
+        m[c] = (aggregator == 1) ? (v[e] > m[c] ? v[e] : m[c]) : ((v[e] > m[c] && v[e] != 0.0f) ? v[e] : m[c]);
+      }
+    }
+  }
+#pragma unroll
+  for (int c = 0; c < T::A; ++c) {
+    const int b = c * T::CS, e = (c == T::A - 1) ? T::P : b + T::CS;
+    g[c] = aggregator == 0 ? (float)(acc[c] / (double)(e - b)) : m[c];
+  }
+}
+template <class T, int L>
+__device__ __forceinline__ void lmlp_rec(const float (&w)[T::P], float* x) {
+  constexpr int I = T::rows(L), O = T::cols(L), OFF = T::off(L);
+  float y[T::MAXW];
+#pragma unroll
+  for (int j = 0; j < O; ++j) {
+    float acc = x[0] * w[OFF + j];
+#pragma unroll
+    for (int i = 1; i < I; ++i) acc = fmaf(x[i], w[OFF + i * O + j], acc);
+    y[j] = acc;
+  }
+#pragma unroll
+  for (int j = 0; j < O; ++j) x[j] = y[j];
+  if constexpr (L < T::D) lmlp_rec<T, L + 1>(w, x);
+}
+template <class T>
+__device__ __forceinline__ void lmlp(const float (&w)[T::P], const float* g, float* h) {
+  float x[T::MAXW];
+#pragma unroll
+  for (int i = 0; i < T::A; ++i) x[i] = g[i];
+  lmlp_rec<T, 0>(w, x);
+#pragma unroll
+  for (int i = 0; i < T::A; ++i) h[i] = x[i];
+}
+template <class T>
+__device__ __forceinline__ bool lrow_close_state(const float (&w)[T::P], const float* h, float eps) {
+  bool ok = true;
+#pragma unroll
+  for (int k = 0; k < T::P; ++k) ok &= !(fabsf(h[T::chunk_c(k)] - w[k]) >= eps);
+  return ok;
+}
+template <class T>
+__device__ __forceinline__ int8_t lclassify(const float (&w)[T::P], float eps, bool with_sec, int aggregator) {
+  bool fin = true;
+#pragma unroll
+  for (int k = 0; k < T::P; ++k) fin &= finitef(w[k]);
+  if (!fin) return C_DIVERGENT;
+  float g[T::A], h1[T::A], h2[T::A];
+  lrow_aggregate<T>(w, g, aggregator);
+  lmlp<T>(w, g, h1);
+  if (finite_all<T>(h1) && lrow_close_state<T>(w, h1, eps)) {
+    bool zero = true;
+#pragma unroll
+    for (int k = 0; k < T::P; ++k) zero &= (-eps <= w[k]) && (w[k] <= eps);
+    return zero ? C_FIX_ZERO : C_FIX_OTHER;
+  }
+  if (with_sec) {
+    lmlp<T>(w, h1, h2);  // aggregate(expand(h1)) == h1 exactly
+    if (finite_all<T>(h2) && lrow_close_state<T>(w, h2, eps)) return C_FIX_SEC;
+  }
+  return C_OTHER;
+}
+// one SGD step on x = y = g (same order as train_step_lds)
+template <class T>
+__device__ __forceinline__ float ltrain_step(float (&w)[T::P], const float* g, float lr) {
+  float act[T::NL][T::MAXW];
+  float x[T::MAXW];
+#pragma unroll
+  for (int i = 0; i < T::A; ++i) x[i] = g[i];
+#pragma unroll
+  for (int l = 0; l <= T::D; ++l) {
+#pragma unroll
+    for (int i = 0; i < T::MAXW; ++i) act[l][i] = x[i];
+    const int I = T::rows(l), O = T::cols(l), OFF = T::off(l);
+    float y[T::MAXW];
+#pragma unroll
+    for (int j = 0; j < T::MAXW; ++j) {
+      if (j < O) {
+        float acc = x[0] * w[OFF + j];
+#pragma unroll
+        for (int i = 1; i < T::MAXW; ++i)
+          if (i < I) acc = fmaf(x[i], w[OFF + i * O + j], acc);
+        y[j] = acc;
+      } else {
+        y[j] = 0.f;
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < T::MAXW; ++j) x[j] = y[j];
+  }
+  float loss = 0.f, st[T::MAXW], st2[T::MAXW];
+#pragma unroll
+  for (int k = 0; k < T::MAXW; ++k) st[k] = 0.f;
+#pragma unroll
+  for (int k = 0; k < T::A; ++k) {
+    const float e = x[k] - g[k];
+    loss += e * e;
+    st[k] = -lr * (2.0f * e / (float)T::A);
+  }
+#pragma unroll
+  for (int l = T::D; l >= 0; --l) {
+    const int R = T::rows(l), Cc = T::cols(l), OFF = T::off(l);
+    if (l > 0) {
+#pragma unroll
+      for (int i = 0; i < T::MAXW; ++i) {
+        if (i < R) {
+          float acc = w[OFF + i * Cc] * st[0];
+#pragma unroll
+          for (int j = 1; j < T::MAXW; ++j)
+            if (j < Cc) acc = fmaf(w[OFF + i * Cc + j], st[j], acc);
+          st2[i] = acc;
+        }
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < T::MAXW; ++i)
+#pragma unroll
+      for (int j = 0; j < T::MAXW; ++j)
+        if (i < R && j < Cc) w[OFF + i * Cc + j] = fmaf(act[l][i], st[j], w[OFF + i * Cc + j]);
+    if (l > 0) {
+#pragma unroll
+      for (int i = 0; i < T::MAXW; ++i) st[i] = (i < R) ? st2[i] : 0.f;
+    }
+  }
+  return loss / (float)T::A;
+}
+
+constexpr int TBROW = 256;  // 4 waves: one per SIMD at ~360 VGPRs
+
+// run_fixpoint phase 1 with the row in VGPRs (same decisions as k_big_fix1)
+template <class T>
+__global__ __launch_bounds__(TBROW) void k_big_fix1_row(SrnnCfg c, SrnnArgs a) {
+  const int64_t p = (int64_t)blockIdx.x * TBROW + threadIdx.x;
+  if (p >= a.n) return;
+  float* state = reinterpret_cast<float*>(a.temp);
+  int8_t* flag = reinterpret_cast<int8_t*>(state + a.n * T::A);
+  float w[T::P];
+  lrow_load<T>(a.W + p * T::PP, w);
+  bool stop = a.steps <= 0;
+  if (!stop && a.early_exit) {
+    bool fin = true;
+#pragma unroll
+    for (int k = 0; k < T::P; ++k) fin &= finitef(w[k]);
+    stop = !fin;
+  }
+  float g[T::A], h[T::A];
+  if (!stop) {
+    lrow_aggregate<T>(w, g, c.aggregator);
+    lmlp<T>(w, g, h);
+    if (a.early_exit && finite_all<T>(h) && lrow_close_state<T>(w, h, a.eps)) stop = true;
+  }
+  if (stop) {  // no step taken: the row is unchanged, classify the general weights
+    flag[p] = 0;
+    if (a.nsteps) a.nsteps[p] = 0;
+    if (a.cls) a.cls[p] = lclassify<T>(w, a.eps, (a.flags & 8) != 0, c.aggregator);
+  } else {
+#pragma unroll
+    for (int i = 0; i < T::A; ++i) state[p * T::A + i] = h[i];
+    flag[p] = 1;
+  }
+}
+template <class T, int OP>
+__global__ __launch_bounds__(TBROW) void k_big_row(SrnnCfg c, SrnnArgs a) {
+  const int64_t p = (int64_t)blockIdx.x * TBROW + threadIdx.x;
+  float w[T::P];
+  if constexpr (OP == OP_CLASSIFY) {
+    __shared__ uint32_t s_cnt[5];
+    if (threadIdx.x < 5) s_cnt[threadIdx.x] = 0;
+    __syncthreads();
+    int8_t k = -1;
+    if (p < a.n) {
+      lrow_load<T>(a.W + p * T::PP, w);
+      k = lclassify<T>(w, a.eps, (a.flags & 8) != 0, c.aggregator);
+      if (a.cls) a.cls[p] = k;
+    }
+    if (a.counts) {  // histogram: wave ballots -> LDS -> one atomic per (block, class)
+#pragma unroll
+      for (int q = 0; q < 5; ++q) {
+        const unsigned long long m = __ballot(k == q);
+        if ((threadIdx.x & 63) == 0 && m) atomicAdd(&s_cnt[q], (uint32_t)__popcll(m));
+      }
+      __syncthreads();
+      if (threadIdx.x < 5 && s_cnt[threadIdx.x]) atomicAdd(a.counts + threadIdx.x, (uint64_t)s_cnt[threadIdx.x]);
+    }
+    return;
+  }
+  if (p >= a.n) return;
+  if constexpr (OP == OP_APPLY) {
+    const int64_t fi = a.idx_f ? a.idx_f[p] : p, ti = a.idx_t ? a.idx_t[p] : p, oi = a.idx_o ? a.idx_o[p] : p;
+    float g[T::A], h[T::A];
+    {  // target row into registers (all 70 loads in flight), aggregated, then dropped
+      float t[T::P];
+      lrow_load<T>(a.W + ti * T::PP, t);
+      lrow_aggregate<T>(t, g, c.aggregator);
+    }
+    lrow_load<T>(a.W + fi * T::PP, w);
+    lmlp<T>(w, g, h);
+    lrow_store_state<T>(a.W2 + oi * T::PP, h);
+  } else {  // OP_TRAIN / OP_LEARN
+    float g[T::A];
+    // teacher samples first (its row dies after the aggregation: one row live at a time)
+    if constexpr (OP == OP_LEARN) lstream_aggregate<T>(a.W2 + (a.idx_t ? a.idx_t[p] : p) * T::PP, g, c.aggregator);
+    lrow_load<T>(a.W + p * T::PP, w);
+    float loss = 0.f;
+    for (int e = 0; e < a.epochs; ++e) {
+      if constexpr (OP == OP_TRAIN) lrow_aggregate<T>(w, g, c.aggregator);
+      loss = ltrain_step<T>(w, g, a.lr);
+    }
+    lrow_store<T>(a.W + p * T::PP, w);
+    if (a.loss) a.loss[p] = loss;
+  }
+}
+
 template <class T>
 int big_run(int op, const SrnnCfg& c, const SrnnArgs& a) {
   if (!a.dev) {
@@ -582,22 +888,39 @@ int big_run(int op, const SrnnCfg& c, const SrnnArgs& a) {
   hipStream_t st = (hipStream_t)a.stream;
   if (a.n <= 0) return 0;
   const unsigned gw = (unsigned)((a.n + BW - 1) / BW), gl = (unsigned)((a.n + 255) / 256);
+  const unsigned g64 = (unsigned)((a.n + TBROW - 1) / TBROW);
+  // lane-per-particle row kernels (default) or the wave-per-particle ones (SRNN_BIG_WAVE=1)
+  const char* wave_env = std::getenv("SRNN_BIG_WAVE");
+  const bool row_kernels = !(wave_env && wave_env[0] == '1');
   switch (op) {
     case OP_INIT: hipLaunchKernelGGL((k_big_lane<T, OP_INIT>), dim3(gl), dim3(256), 0, st, c, a); break;
     case OP_PERTURB: hipLaunchKernelGGL((k_big_lane<T, OP_PERTURB>), dim3(gl), dim3(256), 0, st, c, a); break;
-    case OP_APPLY: hipLaunchKernelGGL((k_big<T, OP_APPLY>), dim3(gw), dim3(TBB), 0, st, c, a); break;
+    case OP_APPLY:
+      if (row_kernels) hipLaunchKernelGGL((k_big_row<T, OP_APPLY>), dim3(g64), dim3(TBROW), 0, st, c, a);
+      else hipLaunchKernelGGL((k_big<T, OP_APPLY>), dim3(gw), dim3(TBB), 0, st, c, a);
+      break;
     case OP_RUN_FIXPOINT:
       if (!a.temp || a.temp_bytes < a.n * (T::A * 4 + 1)) {
         set_error("run_fixpoint on wave-per-particle nets needs temp >= n*(4*aggregates+1) bytes");
         return -5;
       }
-      hipLaunchKernelGGL((k_big_fix1<T>), dim3(gw), dim3(TBB), 0, st, c, a);
+      if (row_kernels) hipLaunchKernelGGL((k_big_fix1_row<T>), dim3(g64), dim3(TBROW), 0, st, c, a);
+      else hipLaunchKernelGGL((k_big_fix1<T>), dim3(gw), dim3(TBB), 0, st, c, a);
       hipLaunchKernelGGL((k_big_fix2<T>), dim3(gl), dim3(256), 0, st, c, a);
       hipLaunchKernelGGL((k_big_fix3<T>), dim3(gw), dim3(TBB), 0, st, c, a);
       break;
-    case OP_CLASSIFY: hipLaunchKernelGGL((k_big<T, OP_CLASSIFY>), dim3(gw), dim3(TBB), 0, st, c, a); break;
-    case OP_TRAIN: hipLaunchKernelGGL((k_big<T, OP_TRAIN>), dim3(gw), dim3(TBB), 0, st, c, a); break;
-    case OP_LEARN: hipLaunchKernelGGL((k_big<T, OP_LEARN>), dim3(gw), dim3(TBB), 0, st, c, a); break;
+    case OP_CLASSIFY:
+      if (row_kernels) hipLaunchKernelGGL((k_big_row<T, OP_CLASSIFY>), dim3(g64), dim3(TBROW), 0, st, c, a);
+      else hipLaunchKernelGGL((k_big<T, OP_CLASSIFY>), dim3(gw), dim3(TBB), 0, st, c, a);
+      break;
+    case OP_TRAIN:
+      if (row_kernels) hipLaunchKernelGGL((k_big_row<T, OP_TRAIN>), dim3(g64), dim3(TBROW), 0, st, c, a);
+      else hipLaunchKernelGGL((k_big<T, OP_TRAIN>), dim3(gw), dim3(TBB), 0, st, c, a);
+      break;
+    case OP_LEARN:
+      if (row_kernels) hipLaunchKernelGGL((k_big_row<T, OP_LEARN>), dim3(g64), dim3(TBROW), 0, st, c, a);
+      else hipLaunchKernelGGL((k_big<T, OP_LEARN>), dim3(gw), dim3(TBB), 0, st, c, a);
+      break;
     default: set_error("op not supported for wave-per-particle nets"); return -5;
   }
   hipError_t e = hipGetLastError();

@@ -323,3 +323,41 @@ def test_soup_is_deterministic_run_to_run(cuda):
     assert torch.equal(runs[0][0], runs[1][0])
     assert torch.equal(runs[0][1], runs[1][1])
     assert runs[0][2] == runs[1][2]
+
+
+@pytest.mark.parametrize("aggregator", ["mean", "max"])
+def test_big_aggregating_row_kernels_match_wave_kernels(cuda, aggregator, monkeypatch):
+    """Lane-per-particle row kernels (row in VGPRs, default) vs the wave-per-particle
+    kernels (SRNN_BIG_WAVE=1) for the P = 280 north-star net: attack, classify, train,
+    learn_from."""
+    spec = ArchSpec.aggregating(4, 10, 3, aggregator=aggregator)
+    n = 5000
+    uid = torch.arange(n, dtype=torch.int64, device=cuda)
+    W = torch.zeros(n, spec.PP, device=cuda)
+    K.init_rows(spec, W, uid, 4)
+    idx = torch.roll(torch.arange(n, device=cuda), 3).contiguous()
+    res = {}
+    for mode in ("wave", "row"):
+        if mode == "wave":
+            monkeypatch.setenv("SRNN_BIG_WAVE", "1")
+        else:
+            monkeypatch.delenv("SRNN_BIG_WAVE", raising=False)
+        out = torch.zeros_like(W)
+        K.apply(spec, W, out, idx_f=idx)
+        cls, counts = K.classify(spec, W, 1e-4)
+        Wt = W.clone()
+        lt = K.train(spec, Wt, epochs=3, uid=uid, seed=5)
+        Wl = W.clone()
+        ll = K.learn_from(spec, Wl, W, idx_t=idx, epochs=2, uid=uid, seed=5)
+        Wf = W.clone()
+        fc, fs, _ = K.run_fixpoint(spec, Wf, 30, 1e-4)
+        res[mode] = (out, cls, counts, Wt, lt, Wl, ll, Wf, fc, fs)
+    a, b = res["wave"], res["row"]
+    assert _rel(a[0][:, :spec.P].cpu().numpy(), b[0][:, :spec.P].cpu().numpy()) < 1e-5
+    assert (a[1] == b[1]).float().mean() > 0.999
+    assert torch.equal(a[2], b[2]) or (a[2] - b[2]).abs().sum() <= 2
+    for i in (3, 5):
+        assert _rel(a[i][:, :spec.P].cpu().numpy(), b[i][:, :spec.P].cpu().numpy()) < 1e-5
+    for i in (4, 6):
+        assert _rel(a[i].cpu().numpy(), b[i].cpu().numpy()) < 1e-4
+    assert torch.equal(a[7], b[7]) and torch.equal(a[8], b[8]) and torch.equal(a[9], b[9])  # run_fixpoint

@@ -79,5 +79,10 @@ def test_vary_is_the_identity_fixpoint():
 
 @pytest.mark.gpu
 def test_prototypes_on_device(cuda):
-    net = RecurrentNetwork(Network(2, 2, 2, recurrent=True), n=1000, device=cuda, seed=0)
-    assert torch.isfinite(net.fit(epochs=2)).all()
+    """Same population on the device and on the host (one step: the linear RNN dynamics
+    explode within a few)."""
+    a = RecurrentNetwork(Network(2, 2, 2, recurrent=True), n=256, device=cuda, seed=0)
+    b = RecurrentNetwork(Network(2, 2, 2, recurrent=True), n=256, device="cpu", seed=0)
+    la, lb = a.fit(epochs=1), b.fit(epochs=1)
+    torch.testing.assert_close(la.cpu(), lb, rtol=1e-4, atol=1e-5)
+    torch.testing.assert_close(a.get_weights_flat().cpu(), b.get_weights_flat(), rtol=1e-4, atol=1e-5)
