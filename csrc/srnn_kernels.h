@@ -769,6 +769,31 @@ __global__ __launch_bounds__(TB) void k_soup_gen(SrnnCfg c, SrnnArgs a) {
   }
 }
 
+// Inclusive scan over an NT-thread block: wave shuffles (no barrier) + one LDS pass over
+// the NT/64 wave totals (one barrier) instead of a log2(NT)-round Hillis-Steele scan with
+// two barriers per round.  *total receives the block sum.
+template <int NT>
+__device__ __forceinline__ int32_t block_incl_scan(int32_t v, int32_t* s_wave, int32_t* total) {
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  int32_t x = v;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const int32_t y = __shfl_up(x, off);
+    if (lane >= off) x += y;
+  }
+  if (lane == 63) s_wave[wv] = x;
+  __syncthreads();
+  int32_t pre = 0, tot = 0;
+#pragma unroll
+  for (int w = 0; w < NT / 64; ++w) {
+    const int32_t sw = s_wave[w];
+    pre += (w < wv) ? sw : 0;
+    tot += sw;
+  }
+  *total = tot;
+  return x + pre;
+}
+
 // Second phase of the two-phase fused generation: one 1024-thread workgroup reduces the
 // per-wave census counts, scans the respawn ballots in slot order, assigns the newborns'
 // uids and advances next_uid / the generation counter.  Sharded (flag 4096): only the
@@ -788,7 +813,7 @@ __global__ __launch_bounds__(NT) void k_gen_finish(SrnnArgs a, int32_t nb) {
     if (j < a.n) I::soup_pack(pa, j);
     return;
   }
-  __shared__ int32_t s_scan[1024];
+  __shared__ int32_t s_wave[NT / 64];
   __shared__ unsigned long long s_cs[5];
   const int t = threadIdx.x;
   if (t < 5) s_cs[t] = 0;
@@ -806,23 +831,17 @@ __global__ __launch_bounds__(NT) void k_gen_finish(SrnnArgs a, int32_t nb) {
     cs[3] += (uint32_t)(st[2] >> 32);
     cs[4] += (uint32_t)st[3];
   }
-  s_scan[t] = born;
-  __syncthreads();
+  int32_t total_born;
+  const int32_t incl = block_incl_scan<NT>(born, s_wave, &total_born);  // barrier inside
 #pragma unroll
   for (int q = 0; q < 5; ++q) {
     unsigned long long v = cs[q];
     for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
     if ((t & 63) == 0 && v) atomicAdd(&s_cs[q], v);
   }
-  for (int off = 1; off < 1024; off <<= 1) {
-    int32_t v = t >= off ? s_scan[t - off] : 0;
-    __syncthreads();
-    s_scan[t] += v;
-    __syncthreads();
-  }
   const bool sharded = (a.flags & 4096) != 0;  // uids come after the exchange (k_uid_assign)
   const int64_t base = *(volatile const int64_t*)a.uid_base;
-  int64_t u = base + s_scan[t] - born;
+  int64_t u = base + incl - born;
   for (int32_t b = b0; b < b1 && born && !sharded; ++b) {
     unsigned long long mm = bs[(int64_t)b * 4];
     while (mm) {
@@ -834,7 +853,7 @@ __global__ __launch_bounds__(NT) void k_gen_finish(SrnnArgs a, int32_t nb) {
   __syncthreads();
   const int32_t gen = I::gen_of(a);
   if (t == 0) {
-    const int32_t total = s_scan[1023];
+    const int32_t total = total_born;
     if (!sharded) ((int64_t*)a.uid_base)[0] = base + total;
     I::set_gen(a, gen + 1);
     if (a.counts) {
@@ -1050,7 +1069,7 @@ constexpr int TBR = 1024;
 template <class Net, class S>
 __global__ __launch_bounds__(TBR) void k_respawn_seq(SrnnCfg c, SrnnArgs a) {
   using I = Item<Net, S>;
-  __shared__ int32_t s_cnt[TBR];
+  __shared__ int32_t s_wave[TBR / 64];
   // i32c as u64[b] = respawn ballot of evolve block b (64 rows); thread t owns blocks
   // [t*ch, (t+1)*ch): no per-row memory traffic, bits give the rows in slot order.
   const unsigned long long* masks = reinterpret_cast<const unsigned long long*>(a.i32c);
@@ -1060,16 +1079,10 @@ __global__ __launch_bounds__(TBR) void k_respawn_seq(SrnnCfg c, SrnnArgs a) {
   const int64_t b1 = b0 + ch < nb ? b0 + ch : nb;
   int32_t cnt = 0;
   for (int64_t b = b0; b < b1; ++b) cnt += __popcll(masks[b]);
-  s_cnt[threadIdx.x] = cnt;
-  __syncthreads();
-  for (int off = 1; off < TBR; off <<= 1) {  // Hillis-Steele inclusive scan
-    int32_t v = threadIdx.x >= off ? s_cnt[threadIdx.x - off] : 0;
-    __syncthreads();
-    s_cnt[threadIdx.x] += v;
-    __syncthreads();
-  }
+  int32_t total;
+  const int32_t incl = block_incl_scan<TBR>(cnt, s_wave, &total);
   const int64_t base = *(volatile const int64_t*)a.uid_base;
-  int64_t k = base + s_cnt[threadIdx.x] - cnt;
+  int64_t k = base + incl - cnt;
   if (cnt) {
     for (int64_t b = b0; b < b1; ++b) {
       unsigned long long m = masks[b];
@@ -1087,7 +1100,7 @@ __global__ __launch_bounds__(TBR) void k_respawn_seq(SrnnCfg c, SrnnArgs a) {
   }
   __syncthreads();
   if (threadIdx.x == 0) {
-    ((int64_t*)a.uid_base)[0] = base + s_cnt[TBR - 1];
+    ((int64_t*)a.uid_base)[0] = base + total;
     I::set_gen(a, I::gen_of(a) + 1);
   }
   if (a.counts && threadIdx.x < 5) a.counts[threadIdx.x] = 0;  // fresh histogram for the census
@@ -1130,7 +1143,7 @@ int respawn_seq(const SrnnCfg& c, const SrnnArgs& a) {
 template <class Net, class S>
 __global__ __launch_bounds__(TBR) void k_uid_assign(SrnnCfg c, SrnnArgs a) {
   using I = Item<Net, S>;
-  __shared__ int32_t s_cnt[TBR];
+  __shared__ int32_t s_wave[TBR / 64];
   __shared__ int64_t s_prefix, s_total;
   if (blockIdx.x > 0) {
     // flag 16384, blocks >= 1: index the received rows (OP_SOUP_UNPACK); block 0 resets
@@ -1164,16 +1177,10 @@ __global__ __launch_bounds__(TBR) void k_uid_assign(SrnnCfg c, SrnnArgs a) {
   const int64_t b1 = b0 + ch < nb ? b0 + ch : nb;
   int32_t cnt = 0;
   for (int64_t b = b0; b < b1; ++b) cnt += __popcll(masks[b * mstride]);
-  s_cnt[threadIdx.x] = cnt;
-  __syncthreads();
-  for (int off = 1; off < TBR; off <<= 1) {
-    int32_t v = threadIdx.x >= off ? s_cnt[threadIdx.x - off] : 0;
-    __syncthreads();
-    s_cnt[threadIdx.x] += v;
-    __syncthreads();
-  }
+  int32_t total_local;
+  const int32_t incl = block_incl_scan<TBR>(cnt, s_wave, &total_local);  // barrier inside
   const int64_t base = *(volatile const int64_t*)a.uid_base;
-  int64_t k = base + s_prefix + s_cnt[threadIdx.x] - cnt;
+  int64_t k = base + s_prefix + incl - cnt;
   for (int64_t b = b0; b < b1 && cnt; ++b) {
     unsigned long long m = masks[b * mstride];
     masks[b * mstride] = 0ull;
