@@ -14,6 +14,7 @@
 #include <vector>
 #include <algorithm>
 #include <climits>
+#include <cstdlib>
 
 namespace srnn {
 
@@ -104,10 +105,16 @@ struct StF32 {
 struct StBF16 {  // round-to-nearest-even, NaN kept quiet
   static constexpr int ID = 1, BYTES = 2;
   SRNN_HD static uint16_t enc(float x) {
+#ifdef __HIP_DEVICE_COMPILE__
+    // gfx950 v_cvt_pk_bf16_f32: the same RNE rounding and NaN quieting as the host form
+    // (tests/test_kernels_gpu.py::test_bf16_encode_matches_host_rounding)
+    return __builtin_bit_cast(uint16_t, (__bf16)x);
+#else
     uint32_t u = f_bits(x);
     if ((u & 0x7fffffffu) > 0x7f800000u) return (uint16_t)((u >> 16) | 0x40u);
     u += 0x7fffu + ((u >> 16) & 1u);
     return (uint16_t)(u >> 16);
+#endif
   }
   SRNN_HD static float dec(uint16_t h) { return bits_f((uint32_t)h << 16); }
   SRNN_HD static float q(float x) { return dec(enc(x)); }
@@ -115,6 +122,11 @@ struct StBF16 {  // round-to-nearest-even, NaN kept quiet
 struct StF16 {  // IEEE binary16, round-to-nearest-even (overflow -> inf = divergent)
   static constexpr int ID = 2, BYTES = 2;
   SRNN_HD static uint16_t enc(float x) {
+#ifdef __HIP_DEVICE_COMPILE__
+    // keep the fp32 rounding of the producing fma: without the barrier the backend folds
+    // fptrunc(fma) into v_fma_mixlo_f16 (one rounding instead of fp32-then-fp16)
+    asm volatile("" : "+v"(x));
+#endif
     _Float16 h = (_Float16)x;
     uint16_t u;
     __builtin_memcpy(&u, &h, 2);
@@ -986,6 +998,95 @@ __global__ __launch_bounds__(TBC) void k_classify_count(SrnnCfg c, SrnnArgs a) {
   if ((a.flags & 512) && blockIdx.x == 0 && threadIdx.x == 0) I::set_gen(a, I::gen_of(a) + 1);
 }
 
+// ----------------------------------------------------------------------------------
+// Weightwise self-application runs (OP_RUN_FIXPOINT) for SMALL populations: 16 lanes per
+// particle.  Lane k owns point / weight k, every lane of the group holds the whole vector
+// (the applying net), computes its own point, and the new vector is gathered with
+// in-group shuffles; the predicates are group ballots.  A lane-per-particle launch of
+// n <= ~65k particles leaves SIMDs idle and each wave latency-bound; this spreads the
+// same work over 16x the lanes.  Same arithmetic per point as Item::run_fixpoint.
+// ----------------------------------------------------------------------------------
+// w[q] = v of lane q of this lane's 16-lane row, q < P (DPP row_newbcast, VALU only)
+template <int Q>
+__device__ __forceinline__ float row_bcast(float v) {
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x150 + Q, 0xF, 0xF, true));
+}
+template <int P, int Q = 0>
+__device__ __forceinline__ void row_bcast_all(float v, float* w) {
+  if constexpr (Q < P) {
+    w[Q] = row_bcast<Q>(v);
+    row_bcast_all<P, Q + 1>(v, w);
+  }
+}
+constexpr int TBG = 256;
+constexpr int64_t FIX_GROUP_MAX_N = 32768;  // measured crossover vs lane-per-particle (profiles/r1h)
+template <class Net, class S>
+__global__ __launch_bounds__(TBG) void k_fix_group(SrnnCfg c, SrnnArgs a) {
+  using I = Item<Net, S>;
+  constexpr int P = Net::P;
+  static_assert(P <= 16, "one 16-lane group per particle");
+  const int lane = threadIdx.x & 63;
+  const int k = lane & 15;
+  const int gbase = lane & ~15;
+  const int64_t i = ((int64_t)blockIdx.x * TBG + threadIdx.x) >> 4;
+  if (i >= a.n) return;  // whole groups leave together
+  const unsigned long long vmask = (((1ull << P) - 1ull) << gbase);
+  float c0 = 0.f, c1 = 0.f, c2 = 0.f;
+#pragma unroll
+  for (int q = 0; q < P; ++q)
+    if (k == q) {
+      c0 = Net::coords.c[q][0];
+      c1 = Net::coords.c[q][1];
+      c2 = Net::coords.c[q][2];
+    }
+  float w[P];
+  I::load(I::rowp(a.W, i), w);
+  float wk = 0.f;
+#pragma unroll
+  for (int q = 0; q < P; ++q) wk = (k == q) ? w[q] : wk;
+  if (a.traj && k == 0) I::store(I::rowp(a.traj, i), w);
+  auto all_of = [&](bool pred) { return (__ballot(pred || k >= P) & vmask) == vmask; };
+  int s = 0;
+  for (; s < a.steps; ++s) {
+    float x[4] = {wk, c0, c1, c2}, y[1];
+    Net::Net::forward_only(w, x, y);
+    const float nk = S::q(y[0]);
+    if (a.early_exit) {
+      if (!all_of(finitef(wk))) break;  // is_diverged(w)
+      if (all_of(finitef(nk) && !(fabsf(nk - wk) >= a.eps))) break;  // is_fixpoint()
+    }
+    row_bcast_all<P>(nk, w);
+    wk = nk;
+    if (a.traj && k == 0) I::store(I::rowp(a.traj, (int64_t)(s + 1) * a.n + i), w);
+  }
+  if (k == 0) {
+    I::store(I::rowp(a.W, i), w);
+    if (a.nsteps) a.nsteps[i] = s;
+  }
+  if (a.cls) {  // classify_w with the group: f1 = f_w(w), f2 = f_w(f1) -- own points only
+    int8_t cl;
+    if (!all_of(finitef(wk))) {
+      cl = C_DIVERGENT;
+    } else {
+      float x[4] = {wk, c0, c1, c2}, y[1];
+      Net::Net::forward_only(w, x, y);
+      const float f1 = S::q(y[0]);
+      if (all_of(finitef(f1) && !(fabsf(f1 - wk) >= a.eps))) {
+        cl = all_of((-a.eps <= wk) && (wk <= a.eps)) ? C_FIX_ZERO : C_FIX_OTHER;
+      } else {
+        cl = C_OTHER;
+        if (a.flags & 8) {
+          float x2[4] = {f1, c0, c1, c2};
+          Net::Net::forward_only(w, x2, y);
+          const float f2 = S::q(y[0]);
+          if (all_of(finitef(f2) && !(fabsf(f2 - wk) >= a.eps))) cl = C_FIX_SEC;
+        }
+      }
+    }
+    if (k == 0) a.cls[i] = cl;
+  }
+}
+
 template <class Net, int OP, class S>
 int launch(const SrnnCfg& c, const SrnnArgs& a) {
   int64_t items = (OP == OP_SOUP_DECIDE) ? a.n_total : (OP == OP_SOUP_UNPACK) ? (int64_t)a.world * a.cap : a.n;
@@ -997,6 +1098,21 @@ int launch(const SrnnCfg& c, const SrnnArgs& a) {
     return -2;
   }
   hipStream_t st = (hipStream_t)a.stream;
+  if constexpr (OP == OP_RUN_FIXPOINT && Net::KIND == 0 && Net::P <= 16) {
+    // small populations: 16 lanes per particle (SRNN_FIX_GROUP=0/1 forces either form)
+    const char* env = std::getenv("SRNN_FIX_GROUP");
+    const bool group = env ? env[0] == '1' : a.n <= FIX_GROUP_MAX_N;
+    if (group) {
+      hipLaunchKernelGGL((k_fix_group<Net, S>), dim3((unsigned)((a.n * 16 + TBG - 1) / TBG)), dim3(TBG), 0, st, c,
+                         a);
+      hipError_t e = hipGetLastError();
+      if (e != hipSuccess) {
+        set_error(hipGetErrorString(e));
+        return -3;
+      }
+      return 0;
+    }
+  }
   if (OP == OP_SOUP_EVOLVE) {
     hipLaunchKernelGGL((k_soup_evolve<Net, S>), dim3((unsigned)blocks), dim3(TB), 0, st, c, a);
   } else if (OP == OP_CLASSIFY && a.counts) {

@@ -361,3 +361,80 @@ def test_big_aggregating_row_kernels_match_wave_kernels(cuda, aggregator, monkey
     for i in (4, 6):
         assert _rel(a[i].cpu().numpy(), b[i].cpu().numpy()) < 1e-4
     assert torch.equal(a[7], b[7]) and torch.equal(a[8], b[8]) and torch.equal(a[9], b[9])  # run_fixpoint
+
+
+@pytest.mark.parametrize("width,depth,dtype", [(2, 2, torch.float32), (2, 2, torch.bfloat16),
+                                               (2, 1, torch.float32), (1, 1, torch.float32)])
+def test_group_fixpoint_kernel_matches_lane_kernel(cuda, dtype, width, depth, monkeypatch):
+    """Small-population run_fixpoint (16 lanes per particle, SRNN_FIX_GROUP=1) vs the
+    lane-per-particle kernel (SRNN_FIX_GROUP=0): bitwise equal weights, classes, step
+    counts and trajectories."""
+    spec = ArchSpec.weightwise(width, depth)
+    n = 3001
+    uid = torch.arange(n, dtype=torch.int64, device=cuda)
+    W0 = torch.zeros(n, spec.PP, dtype=dtype, device=cuda)
+    K.init_rows(spec, W0, uid, 7)
+    W0[:50] *= 40.0  # divergent
+    W0[50:100] *= 1e-3  # towards zero
+    res = {}
+    for mode in ("0", "1"):
+        monkeypatch.setenv("SRNN_FIX_GROUP", mode)
+        out = []
+        for early, sec, rec, steps in ((True, True, False, 100), (False, False, False, 37), (True, True, True, 12)):
+            W = W0.clone()
+            cls, ns, traj = K.run_fixpoint(spec, W, steps, 1e-4, early_exit=early, with_sec=sec, record=rec)
+            out.append((W, cls, ns, traj))
+        res[mode] = out
+    bits = torch.int32 if dtype == torch.float32 else torch.int16
+
+    def same(x, y):  # bitwise, so NaN rows compare equal
+        return torch.equal(x.contiguous().view(bits), y.contiguous().view(bits))
+
+    for a, b in zip(res["0"], res["1"]):
+        assert same(a[0][:, :spec.P], b[0][:, :spec.P])
+        assert torch.equal(a[1], b[1]) and torch.equal(a[2], b[2])
+        if a[3] is not None:
+            assert same(a[3][..., :spec.P], b[3][..., :spec.P])
+    cls = res["1"][0][1].cpu()
+    assert len(torch.unique(cls)) >= 2  # a mixture of outcomes was exercised
+
+
+def _bf16_host(u32: np.ndarray) -> np.ndarray:
+    """The host form of StBF16::enc (csrc/srnn_kernels.h): RNE, NaN kept quiet."""
+    u = u32.astype(np.uint64)
+    nan = (u & 0x7FFFFFFF) > 0x7F800000
+    r = ((u + 0x7FFF + ((u >> 16) & 1)) >> 16) & 0xFFFF
+    return np.where(nan, ((u >> 16) | 0x40) & 0xFFFF, r).astype(np.uint16)
+
+
+def test_bf16_encode_matches_host_rounding(cuda):
+    """The device bf16 storage rounding (gfx950 v_cvt_pk_bf16_f32) equals the host formula
+    bit for bit: ties, denormals, infinities and NaN payloads of both signs."""
+    import ctypes
+    from self_replicating_neural_networks_amd.ops import _lib
+    rng = np.random.default_rng(0)
+    bits = rng.integers(0, 2 ** 32, size=1 << 20, dtype=np.uint64).astype(np.uint32)
+    special = np.array([0, 0x80000000, 0x7F800000, 0xFF800000, 0x7FC00000, 0xFFC00000, 0x7F800001, 0xFF800001,
+                        0x7FBFFFFF, 0x7F808000, 0x00000001, 0x807FFFFF, 0x00018000, 0x00008000, 0x3F808000,
+                        0x3F818000, 0x3F80FFFF, 0x7F7FFFFF, 0x7F7F8000, 0xFF7F8000], dtype=np.uint32)
+    ties = (rng.integers(0, 2 ** 16, size=4096, dtype=np.uint64).astype(np.uint32) << 16) | 0x8000
+    u = np.concatenate([special, ties, bits])
+    x = torch.from_numpy(u.view(np.float32).copy()).to(cuda)
+    out = torch.empty(x.numel(), dtype=torch.int16, device=cuda)
+    st = torch.cuda.current_stream().cuda_stream
+    r = _lib.lib().srnn_storage_encode(ctypes.c_void_p(x.data_ptr()), ctypes.c_void_p(out.data_ptr()),
+                                       x.numel(), 1, ctypes.c_void_p(st))
+    assert r == 0
+    got = out.cpu().numpy().view(np.uint16)
+    want = _bf16_host(u)
+    bad = np.nonzero(got != want)[0]
+    assert bad.size == 0, [(hex(u[i]), hex(got[i]), hex(want[i])) for i in bad[:8]]
+    # fp16: IEEE RNE for every non-NaN value
+    r = _lib.lib().srnn_storage_encode(ctypes.c_void_p(x.data_ptr()), ctypes.c_void_p(out.data_ptr()),
+                                       x.numel(), 2, ctypes.c_void_p(st))
+    assert r == 0
+    f = u.view(np.float32)
+    ok = ~np.isnan(f)
+    with np.errstate(over="ignore"):
+        want16 = f.astype(np.float16).view(np.uint16)
+    assert np.array_equal(out.cpu().numpy().view(np.uint16)[ok], want16[ok])
