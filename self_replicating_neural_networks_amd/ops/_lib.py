@@ -17,7 +17,8 @@ import subprocess
 import threading
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libsrnn.so")
+# SRNN_LIB: load another build of the library (A/B of compiler flags on the GPU box)
+LIB_PATH = os.environ.get("SRNN_LIB") or os.path.join(_HERE, "libsrnn.so")
 CSRC = os.path.normpath(os.path.join(_HERE, "..", "..", "csrc"))
 ABI_VERSION = 11
 
