@@ -148,3 +148,53 @@ def test_recurrent_divergence_rate_matches_autograd_model():
     frac = got.float().mean().item()
     assert 0.35 < frac < 0.6, frac
     assert (got != refd).float().mean().item() < 0.02
+
+
+def _agg_forward(spec, mats, w):
+    """Chunk means -> Dense stack a -> w -> ... -> a; (code/network.py:359-386, mean aggregator)."""
+    agg = torch.stack([w[:, s:s + n].mean(1) for s, n in spec.chunks], 1)
+    h = agg[:, None, :]
+    for m in mats:
+        h = torch.bmm(h, m)
+    return agg, h[:, 0, :]
+
+
+def _check_agg(device):
+    for spec in (ArchSpec.aggregating(4, 2, 2), ArchSpec.aggregating(2, 2, 2), ArchSpec.aggregating(4, 2, 3),
+                 ArchSpec.aggregating(4, 4, 2)):
+        pop = _pop(spec, 64, device, 13)
+        w0 = pop.weights().detach().cpu().double()
+        # self-application: every weight of chunk k <- net(chunk means)[k]
+        sa = _pop(spec, 64, device, 13)
+        sa.set_weights(w0.float())
+        sa.self_apply(1)
+        _, out = _agg_forward(spec, _split(spec, w0), w0)
+        ref = torch.cat([out[:, k:k + 1].expand(-1, n) for k, (_, n) in enumerate(spec.chunks)], 1)
+        got = sa.weights().cpu().double()
+        assert torch.allclose(got, ref, rtol=1e-4, atol=1e-6), (spec, (got - ref).abs().max())
+        # self-training: one sample x = y = the aggregations (compute_samples :414-417)
+        for epochs in (1, 4):
+            p = _pop(spec, 64, device, 13)
+            p.set_weights(w0.float())
+            p.train(epochs=epochs)
+            w = w0.clone()
+            for _ in range(epochs):
+                x, _ = _agg_forward(spec, _split(spec, w), w)
+                wv = w.detach().requires_grad_(True)
+                h = x.detach()[:, None, :]
+                for m in _split(spec, wv):
+                    h = torch.bmm(h, m)
+                loss = ((h[:, 0, :] - x.detach()) ** 2).mean(1).sum()
+                (g,) = torch.autograd.grad(loss, wv)
+                w = (wv - 0.01 * g).detach()
+            got = p.weights().cpu().double()
+            assert torch.allclose(got, w, rtol=1e-4, atol=1e-6), (spec, epochs, (got - w).abs().max())
+
+
+def test_aggregating_matches_autograd_cpu():
+    _check_agg("cpu")
+
+
+@pytest.mark.gpu
+def test_aggregating_matches_autograd_gpu():
+    _check_agg("cuda")
