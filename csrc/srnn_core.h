@@ -87,9 +87,15 @@ SRNN_HD U4 perm_draw(const Rng& rng, uint64_t id, uint32_t step, uint32_t purpos
 template <int N>
 SRNN_HD uint64_t perm_from_bits(uint64_t u) {
   static_assert(N <= 16, "nibble permutation holds at most 16 entries");
-  uint64_t p = 0;
+  // nibbles 0-7 in plo, 8-15 in phi.  j <= i, so for i < 8 (i is a compile-time constant
+  // after unrolling) both nibbles live in plo and the swap is 32-bit (v_bfe_u32 + shifts)
+  // instead of variable 64-bit shifts; identical permutation.
+  uint32_t plo = 0, phi = 0;
 #pragma unroll
-  for (int k = 0; k < N; ++k) p |= (uint64_t)k << (4 * k);
+  for (int k = 0; k < N; ++k) {
+    if (k < 8) plo |= (uint32_t)k << (4 * k);
+    else phi |= (uint32_t)k << (4 * (k - 8));
+  }
   uint32_t ul = (uint32_t)u, uh = (uint32_t)(u >> 32);
 #pragma unroll
   for (int i = N - 1; i > 0; --i) {
@@ -98,12 +104,22 @@ SRNN_HD uint64_t perm_from_bits(uint64_t u) {
     const uint32_t j = (uint32_t)(hi >> 32);
     ul = (uint32_t)lo;
     uh = (uint32_t)hi;
-    const uint64_t ni = (p >> (4 * i)) & 15u;
-    const uint64_t nj = (p >> (4 * j)) & 15u;
-    const uint64_t x = ni ^ nj;
-    p ^= (x << (4 * i)) | (x << (4 * j));
+    if (i < 8) {
+      const uint32_t ni = (plo >> (4 * i)) & 15u;
+      const uint32_t nj = (plo >> (4 * j)) & 15u;
+      const uint32_t x = ni ^ nj;
+      plo ^= (x << (4 * i)) | (x << (4 * j));
+    } else {
+      uint64_t p = ((uint64_t)phi << 32) | plo;
+      const uint64_t ni = (p >> (4 * i)) & 15u;
+      const uint64_t nj = (p >> (4 * j)) & 15u;
+      const uint64_t x = ni ^ nj;
+      p ^= (x << (4 * i)) | (x << (4 * j));
+      plo = (uint32_t)p;
+      phi = (uint32_t)(p >> 32);
+    }
   }
-  return p;
+  return ((uint64_t)phi << 32) | plo;
 }
 template <int N>
 SRNN_HD uint64_t shuffle16(const Rng& rng, uint64_t id, uint32_t step, uint32_t purpose) {
