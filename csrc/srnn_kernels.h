@@ -830,6 +830,10 @@ __global__ __launch_bounds__(NT) void k_gen_finish(SrnnArgs a, int32_t nb) {
   const int t = threadIdx.x;
   if (t < 5) s_cs[t] = 0;
   const unsigned long long* bs = reinterpret_cast<const unsigned long long*>(a.temp);
+  // the uid base and the generation counter are only written by thread 0 after the last
+  // barrier: load them up front so their latency overlaps the per-block stats loads
+  const int64_t base = *(volatile const int64_t*)a.uid_base;
+  const int32_t gen = I::gen_of(a);
   const int32_t ch = (nb + 1023) / 1024;
   const int32_t b0 = t * ch, b1 = b0 + ch < nb ? b0 + ch : nb;
   int32_t born = 0;
@@ -852,7 +856,6 @@ __global__ __launch_bounds__(NT) void k_gen_finish(SrnnArgs a, int32_t nb) {
     if ((t & 63) == 0 && v) atomicAdd(&s_cs[q], v);
   }
   const bool sharded = (a.flags & 4096) != 0;  // uids come after the exchange (k_uid_assign)
-  const int64_t base = *(volatile const int64_t*)a.uid_base;
   int64_t u = base + incl - born;
   for (int32_t b = b0; b < b1 && born && !sharded; ++b) {
     unsigned long long mm = bs[(int64_t)b * 4];
@@ -863,7 +866,6 @@ __global__ __launch_bounds__(NT) void k_gen_finish(SrnnArgs a, int32_t nb) {
     }
   }
   __syncthreads();
-  const int32_t gen = I::gen_of(a);
   if (t == 0) {
     const int32_t total = total_born;
     if (!sharded) ((int64_t*)a.uid_base)[0] = base + total;
