@@ -90,6 +90,9 @@ def main():
     if d.enabled:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     dt = float(t.item())
+    if eng.exchange_overflowed():
+        # rows that did not fit the all-to-all capacity were dropped: the generation is invalid
+        raise SystemExit("soup row exchange overflowed its capacity: the measured generations are invalid")
     census = eng.count()
     value = n_total * args.steps / dt
     if d.rank == 0:

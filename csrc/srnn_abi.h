@@ -79,6 +79,8 @@ struct SrnnArgs {
   int32_t* gen_out;     // soup: where "advance the generation" writes gen + 1 (null -> *gen_ptr in
                         // place).  The engine keeps a 2-slot ring indexed by the ping-pong parity
                         // so a kernel can advance the counter while its other blocks still read it.
+  void* scratch;        // generic (runtime-shape) engine: per-lane vectors, element-major; null ->
+  int64_t scratch_bytes;  // the library's own cached device buffer (not inside a graph capture)
 };
 
 enum SrnnOp {
@@ -103,9 +105,12 @@ enum SrnnOp {
                         // (flag 16384: the same launch also indexes the received rows = OP_SOUP_UNPACK)
 };
 
-int srnn_abi_version();  // 11
+int srnn_abi_version();  // 12
 int srnn_has_config(const SrnnCfg* cfg);
 int srnn_run(int op, const SrnnCfg* cfg, const SrnnArgs* args);
 const char* srnn_last_error();
 int64_t srnn_scan_temp_bytes(int64_t n);
+int srnn_is_generic(const SrnnCfg* cfg, int op);
+void srnn_set_force_generic(int on);  // 1: this op of this config runs on the generic engine
+int64_t srnn_generic_scratch_bytes(const SrnnCfg* cfg, int64_t n, int64_t max_lanes);
 }

@@ -18,12 +18,7 @@ extern "C" int srnn_dispatch_fft(int op, const SrnnCfg* c, const SrnnArgs* a);
 extern "C" int srnn_dispatch_aggbig(int op, const SrnnCfg* c, const SrnnArgs* a);
 extern "C" int srnn_dispatch_lowp(int op, const SrnnCfg* c, const SrnnArgs* a);
 
-__global__ void k_scan_tail(int32_t* out, const int32_t* in, int64_t n) {
-  // out[0] = 0 (inclusive scan was written to out+1)
-  out[0] = 0;
-  (void)in;
-  (void)n;
-}
+extern "C" int srnn_dispatch_generic(int op, const SrnnCfg* c, const SrnnArgs* a);
 
 // ---- tracing / checking hooks, read once from the environment:
 //   SRNN_ROCTX=1       one roctx range per operator launch (rocprofv3 --marker-trace),
@@ -70,7 +65,9 @@ const char* op_name(int op) {
 }
 }  // namespace
 
-static int dispatch(int op, const SrnnCfg* c, const SrnnArgs* a) {
+// Specialised (templated) paths first; 1 = shape not instantiated, 2 = op / host execution
+// not provided by the specialised path: both fall through to the runtime-shape engine.
+static int dispatch_special(int op, const SrnnCfg* c, const SrnnArgs* a) {
   if (c->dtype != 0) {
     if (c->dtype != 1 && c->dtype != 2) {
       srnn::set_error("unknown weight-table dtype");
@@ -90,15 +87,112 @@ static int dispatch(int op, const SrnnCfg* c, const SrnnArgs* a) {
   }
 }
 
+// SRNN_FORCE_GENERIC=1 (or srnn_set_force_generic) routes every op to the runtime-shape
+// engine: the A/B switch of tests/test_generic.py
+static int g_force_generic = -1;
+static bool force_generic() {
+  if (g_force_generic < 0) {
+    const char* e = std::getenv("SRNN_FORCE_GENERIC");
+    g_force_generic = (e && e[0] == '1') ? 1 : 0;
+  }
+  return g_force_generic == 1;
+}
+
+// which engine serves (op, cfg, host/device): 0 specialised, 1 generic, -1 none
+static int route(int op, const SrnnCfg* c, const SrnnArgs* a) {
+  if (!force_generic()) {
+    SrnnArgs probe{};
+    probe.dev = a ? a->dev : 1;
+    const int r = dispatch_special(-1, c, &probe);
+    if (r == 0) {
+      // instantiated: does the specialised path provide this op (on this side)?
+      const int k = c->kind == 1 && c->p > 64 ? 1 : (c->kind == 0 && c->width >= 16 ? 2 : 0);
+      if (k == 0) return 0;  // lane-per-particle templates: every op, host and device
+      const bool host = a && !a->dev;
+      if (host) return 1;  // wave-per-particle paths are GPU only
+      if (k == 1 && (op == OP_INIT || op == OP_APPLY || op == OP_RUN_FIXPOINT || op == OP_CLASSIFY ||
+                     op == OP_TRAIN || op == OP_LEARN || op == OP_PERTURB) &&
+          (c->shuffler == 0 || op == OP_INIT || op == OP_PERTURB || op == OP_TRAIN || op == OP_LEARN))
+        return 0;
+      if (k == 2 && (op == OP_INIT || op == OP_APPLY || op == OP_RUN_FIXPOINT || op == OP_CLASSIFY)) return 0;
+      return 1;
+    }
+    if (r < 0 && r != -1) return -1;  // layout mismatch etc.
+  }
+  return srnn_dispatch_generic(-1, c, a) == 0 ? 1 : -1;
+}
+
+static int dispatch(int op, const SrnnCfg* c, const SrnnArgs* a) {
+  if (op < 0) return route(0, c, a) >= 0 ? 0 : 1;
+  const int r = route(op, c, a);
+  if (r == 0) return dispatch_special(op, c, a);
+  if (r == 1) {
+    const int g = srnn_dispatch_generic(op, c, a);
+    if (g == 2) {
+      srnn::set_error("op not supported for this network shape (fused soup generations need an instantiated shape)");
+      return -1;
+    }
+    return g;
+  }
+  return 1;
+}
+
+// Device scratch of the generic engine when the caller passes none: one grow-only buffer
+// per device (allocated outside graph captures: the first eager call sizes it).
+static void* g_scratch[64] = {nullptr};
+static int64_t g_scratch_bytes[64] = {0};
+
+static int with_scratch(int op, const SrnnCfg* c, const SrnnArgs* a) {
+  if (!a->dev || a->scratch || route(op, c, a) != 1 || op == OP_SOUP_DECIDE || op == OP_SOUP_PACK ||
+      op == OP_SOUP_UNPACK || op == OP_UID_ASSIGN)
+    return dispatch(op, c, a);
+  const int64_t want = srnn_generic_scratch_bytes(c, a->n, 65536);
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  if (dev < 0 || dev >= 64) dev = 0;
+  if (want > g_scratch_bytes[dev]) {
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    (void)hipStreamIsCapturing((hipStream_t)a->stream, &cs);
+    if (cs != hipStreamCaptureStatusNone) {
+      srnn::set_error("generic engine: scratch must be allocated before graph capture (pass SrnnArgs.scratch)");
+      return -5;
+    }
+    if (g_scratch[dev]) {
+      (void)hipDeviceSynchronize();
+      (void)hipFree(g_scratch[dev]);
+      g_scratch[dev] = nullptr;
+      g_scratch_bytes[dev] = 0;
+    }
+    if (hipMalloc(&g_scratch[dev], (size_t)want) != hipSuccess) {
+      srnn::set_error("generic engine: scratch allocation failed");
+      return -3;
+    }
+    g_scratch_bytes[dev] = want;
+  }
+  SrnnArgs b = *a;
+  b.scratch = g_scratch[dev];
+  b.scratch_bytes = g_scratch_bytes[dev];
+  return dispatch(op, c, &b);
+}
+
 extern "C" {
 
-int srnn_abi_version() { return 11; }
+int srnn_abi_version() { return 12; }
 
 const char* srnn_last_error() { return srnn::g_err.c_str(); }
 
 int srnn_has_config(const SrnnCfg* cfg) {
-  int r = dispatch(-1, cfg, nullptr);
-  return r == 0 ? 1 : 0;
+  SrnnArgs probe{};
+  probe.dev = 0;
+  return route(0, cfg, &probe) >= 0 ? 1 : 0;
+}
+
+void srnn_set_force_generic(int on) { g_force_generic = on ? 1 : 0; }
+
+int srnn_is_generic(const SrnnCfg* cfg, int op) {
+  SrnnArgs probe{};
+  probe.dev = 1;
+  return route(op, cfg, &probe) == 1 ? 1 : 0;
 }
 
 int64_t srnn_scan_temp_bytes(int64_t n) {
@@ -129,8 +223,9 @@ int srnn_run(int op, const SrnnCfg* cfg, const SrnnArgs* a) {
         return -3;
       }
     }
-    hipLaunchKernelGGL(k_scan_tail, dim3(1), dim3(1), 0, st, a->i32d, a->i32c, a->n);
-    hipError_t e = hipGetLastError();
+    // i32d[0] = 0 (the inclusive scan went to i32d + 1)
+    hipError_t e = hipMemsetAsync(a->i32d, 0, sizeof(int32_t), st);
+    if (e == hipSuccess) e = hipGetLastError();
     if (e != hipSuccess) {
       srnn::set_error(hipGetErrorString(e));
       return -3;
@@ -139,8 +234,8 @@ int srnn_run(int op, const SrnnCfg* cfg, const SrnnArgs* a) {
   }
   const Hooks& h = hooks();
   if (h.push) h.push(op_name(op));
-  int r = dispatch(op, cfg, a);
-  if (r == 1) srnn::set_error("network shape not instantiated in libsrnn (add it to csrc/srnn_<kind>.hip)");
+  int r = with_scratch(op, cfg, a);
+  if (r == 1) srnn::set_error("not a valid network shape for libsrnn");
   if (r == 0 && h.sync && a->dev) {
     hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
     (void)hipStreamIsCapturing((hipStream_t)a->stream, &cs);

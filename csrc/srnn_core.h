@@ -331,10 +331,12 @@ SRNN_HD void glorot_fill(float* w, int off, int r, int c, const Rng& rng, uint64
 }
 
 // orthogonal (n, n) kernel by modified Gram-Schmidt of a gaussian matrix with
-// sign(diag R) correction == QR with positive diagonal (Haar distributed).
+// sign(diag R) correction == QR with positive diagonal (Haar distributed).  The
+// orthogonalisation runs in double (Keras' initializer is a float64 numpy QR): in float32
+// a single MGS pass loses orthogonality ~ eps32 * cond(A), 1e-4 for unlucky draws.
 template <int N>
 SRNN_HD void orthogonal_fill(float* w, int off, const Rng& rng, uint64_t uid) {
-  float a[N][N];  // a[row][col]
+  double a[N][N];  // a[row][col]
   int cnt = 0;
   U4 u{0, 0, 0, 0};
   float nrm[4] = {0, 0, 0, 0};
@@ -353,23 +355,23 @@ SRNN_HD void orthogonal_fill(float* w, int off, const Rng& rng, uint64_t uid) {
         nrm[2] = r2 * cosf(t2);
         nrm[3] = r2 * sinf(t2);
       }
-      a[i][j] = nrm[cnt & 3];
+      a[i][j] = (double)nrm[cnt & 3];
       ++cnt;
     }
   // Gram-Schmidt on columns
   for (int j = 0; j < N; ++j) {
     for (int p = 0; p < j; ++p) {
-      float d = 0.f;
-      for (int i = 0; i < N; ++i) d += a[i][p] * a[i][j];
-      for (int i = 0; i < N; ++i) a[i][j] -= d * a[i][p];
+      double d = 0.0;
+      for (int i = 0; i < N; ++i) d = fma(a[i][p], a[i][j], d);
+      for (int i = 0; i < N; ++i) a[i][j] = fma(-d, a[i][p], a[i][j]);
     }
-    float s = 0.f;
-    for (int i = 0; i < N; ++i) s += a[i][j] * a[i][j];
-    float inv = 1.0f / sqrtf(s);
+    double s = 0.0;
+    for (int i = 0; i < N; ++i) s = fma(a[i][j], a[i][j], s);
+    const double inv = 1.0 / sqrt(s);
     for (int i = 0; i < N; ++i) a[i][j] *= inv;
   }
   for (int i = 0; i < N; ++i)
-    for (int j = 0; j < N; ++j) w[off + i * N + j] = a[i][j];
+    for (int j = 0; j < N; ++j) w[off + i * N + j] = (float)a[i][j];
 }
 
 // ----------------------------------------------------------------------------------

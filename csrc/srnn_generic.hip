@@ -1,0 +1,1212 @@
+// srnn_generic.hip — runtime-shape engine: every (kind, width, depth, aggregates) the
+// reference constructors accept (code/network.py:222-230 Weightwise, :324-333
+// Aggregating, :465-474 FFT, :526-535 Recurrent), on the host and on the GPU.
+//
+// The templated kernels (srnn_kernels.h, srnn_bignet.hip, srnn_wide.hip) keep a
+// particle's weights in VGPRs and are instantiated for a list of shapes; every other shape
+// -- and every operator a specialised path does not provide (e.g. soups of the P = 280
+// north-star net, shuffle_random on it, host execution of the GPU-only paths) -- runs
+// here.  The per-particle arithmetic is the same, in the same order (x[0]*k then fmaf over
+// the inputs, Keras SGD with the folded step, chunk means as double sums, BPTT of the
+// linear SimpleRNN stack), with the same Philox streams, so on the same device a generic
+// run is bitwise equal to the templated one (tests/test_generic.py).
+//
+// Execution: lane per particle with a grid-stride loop over rows.  The layer tables live
+// in the kernel argument (GShape), the weight-point coordinate table in LDS, and every
+// per-particle vector (weights, targets, activations, samples, BPTT states) in a scratch
+// buffer laid out element-major -- element e of lane L at scratch[e * lanes + L] -- so the
+// 64 lanes of a wave touch 64 consecutive floats (coalesced) on every access.
+#include "srnn_kernels.h"
+
+#include <cstring>
+#include <vector>
+
+namespace srnn {
+
+constexpr int GMAXL = 33;  // dense layers (depth <= 32) / SimpleRNN layers
+constexpr int GTB = 64;    // threads per block: one wave, the respawn ballot is per 64 rows
+
+struct GShape {
+  int kind, W, D, A, P, PP, NL;
+  int aggregator, shuffler, dtype;
+  int rows[GMAXL], cols[GMAXL], off[GMAXL];  // dense layers (Weightwise / Aggregating / FFT)
+  int in_[GMAXL], un[GMAXL], koff[GMAXL], roff[GMAXL];  // SimpleRNN layers
+  int IN, OUT, NACT, HS, MAXV, CS;
+  // scratch layout (float offsets of every per-item region)
+  int o_w, o_t, o_o, o_f, o_acts, o_v1, o_v2, o_v3, o_v4, o_samp, o_perm, o_hs, o_gw, o_orth, sfloats;
+  int orthd;  // doubles of lane-private orthogonal-init scratch (recurrent: W*W)
+};
+
+static inline int gmax(int a, int b) { return a > b ? a : b; }
+SRNN_HD int64_t g_lane_bytes(const struct GShape& s);
+
+// host: layer tables + scratch layout of a configuration; false if it is not a valid shape
+static bool make_gshape(const SrnnCfg& c, GShape& s, const char** why) {
+  std::memset(&s, 0, sizeof(s));
+  s.kind = c.kind, s.W = c.width, s.D = c.depth, s.A = c.aggregates;
+  s.aggregator = c.aggregator, s.shuffler = c.shuffler, s.dtype = c.dtype;
+  if (s.W < 1 || s.D < 1 || s.D + 1 > GMAXL) {
+    *why = "generic engine: width >= 1 and 1 <= depth <= 32 required";
+    return false;
+  }
+  int P = 0;
+  if (s.kind == 2) {  // recurrent: (1,w)+(w,w), (w,w)+(w,w) x (d-1), (w,1)+(1,1)
+    s.NL = s.D + 1;
+    for (int l = 0; l < s.NL; ++l) {
+      s.in_[l] = l == 0 ? 1 : s.W;
+      s.un[l] = l == s.D ? 1 : s.W;
+      s.koff[l] = P;
+      s.roff[l] = P + s.in_[l] * s.un[l];
+      P += s.in_[l] * s.un[l] + s.un[l] * s.un[l];
+    }
+    s.HS = s.D * s.W + 1;
+    s.IN = 1, s.OUT = 1;
+  } else if (s.kind == 0 || s.kind == 1 || s.kind == 3) {
+    s.IN = s.kind == 0 ? 4 : s.A;
+    s.OUT = s.kind == 0 ? 1 : s.A;
+    if (s.kind != 0 && s.A < 1) {
+      *why = "generic engine: aggregating / fft nets need aggregates >= 1";
+      return false;
+    }
+    s.NL = s.D + 1;
+    for (int l = 0; l < s.NL; ++l) {
+      s.rows[l] = l == 0 ? s.IN : s.W;
+      s.cols[l] = l == s.D ? s.OUT : s.W;
+      s.off[l] = P;
+      P += s.rows[l] * s.cols[l];
+    }
+  } else {
+    *why = "unknown network kind";
+    return false;
+  }
+  s.P = P;
+  s.PP = (P + 3) & ~3;
+  if (c.p != s.P || c.pp != s.PP) {
+    *why = "layout mismatch (p/pp) for the generic engine";
+    return false;
+  }
+  if (s.kind == 1) {
+    s.CS = P / s.A;
+    if (s.CS < 1 || P / s.CS != s.A) {
+      *why = "aggregating net cannot be cut into `aggregates` chunks (SURVEY S4)";
+      return false;
+    }
+  }
+  if (s.kind == 3 && s.A > P) {
+    *why = "fft aggregates must not exceed the number of weights";
+    return false;
+  }
+  s.NACT = s.IN + s.D * s.W;
+  s.MAXV = gmax(gmax(s.IN, s.OUT), gmax(s.W, s.HS)) + 1;
+  int o = 0;
+  auto take = [&](int n) { int r = o; o += n; return r; };
+  s.o_w = take(s.PP), s.o_t = take(s.PP), s.o_o = take(s.PP), s.o_f = take(s.PP);
+  s.o_acts = take(s.NACT + 1);
+  s.o_v1 = take(s.MAXV), s.o_v2 = take(s.MAXV), s.o_v3 = take(s.MAXV), s.o_v4 = take(s.MAXV);
+  s.o_samp = take(s.kind == 0 ? s.P : 0);            // sample values (coordinates from the table)
+  s.o_perm = take(s.P);                              // permutation (one index per float slot)
+  s.o_hs = take(s.kind == 2 ? s.P * s.HS + 3 * s.HS : 0);  // BPTT states + h / carry / zeros
+  s.o_gw = take(s.kind == 2 ? s.P : 0);
+  s.o_orth = 0;
+  s.sfloats = o;
+  s.orthd = s.kind == 2 ? s.W * s.W : 0;  // after the strided region: lane L at [L * orthd]
+  return true;
+}
+
+SRNN_HD int64_t g_lane_bytes(const GShape& s) { return (int64_t)s.sfloats * 4 + (int64_t)s.orthd * 8; }
+// lane-private doubles of lane L after the strided float region of `lanes` lanes
+SRNN_HD double* g_orth(const GShape& s, void* scratch, int64_t lanes, int64_t L) {
+  return reinterpret_cast<double*>(reinterpret_cast<char*>(scratch) + lanes * (int64_t)s.sfloats * 4) + L * s.orthd;
+}
+
+// ---------------------------------------------------------------------------------
+// Strided scratch vectors: element k at p[k * st] (st = lanes on the device, 1 on host)
+// ---------------------------------------------------------------------------------
+struct SV {
+  float* p;
+  int64_t st;
+  SRNN_HD float& operator[](int64_t k) const { return p[k * st]; }
+  SRNN_HD SV at(int64_t k) const { return SV{p + k * st, st}; }
+};
+
+struct GCtx {  // one item's view of the shape, its scratch and the coordinate table
+  const GShape* s;
+  float* base;
+  int64_t st;
+  const float* coords;  // [P][3] (Weightwise)
+  double* orth;         // recurrent init: un*un doubles, lane-private (contiguous)
+  SRNN_HD SV v(int off) const { return SV{base + (int64_t)off * st, st}; }
+};
+
+// ---------------------------------------------------------------- storage formats
+SRNN_HD float g_dec(const char* row, int k, int dtype) {
+  if (dtype == 0) return reinterpret_cast<const float*>(row)[k];
+  const uint16_t h = reinterpret_cast<const uint16_t*>(row)[k];
+  return dtype == 1 ? StBF16::dec(h) : StF16::dec(h);
+}
+SRNN_HD float g_q(float x, int dtype) { return dtype == 0 ? x : dtype == 1 ? StBF16::q(x) : StF16::q(x); }
+SRNN_HD void g_load(const GShape& s, const char* row, SV w) {
+  for (int k = 0; k < s.P; ++k) w[k] = g_dec(row, k, s.dtype);
+}
+SRNN_HD void g_store(const GShape& s, char* row, SV w) {
+  for (int k = 0; k < s.PP; ++k) {
+    const float v = k < s.P ? w[k] : 0.f;
+    if (s.dtype == 0) reinterpret_cast<float*>(row)[k] = v;
+    else reinterpret_cast<uint16_t*>(row)[k] = s.dtype == 1 ? StBF16::enc(v) : StF16::enc(v);
+  }
+}
+SRNN_HD void g_quant(const GShape& s, SV w) {
+  if (s.dtype != 0)
+    for (int k = 0; k < s.P; ++k) w[k] = g_q(w[k], s.dtype);
+}
+SRNN_HD int64_t g_rb(const GShape& s) { return (int64_t)s.PP * (s.dtype == 0 ? 4 : 2); }
+SRNN_HD void g_copy(const GShape& s, SV d, SV src) {
+  for (int k = 0; k < s.P; ++k) d[k] = src[k];
+}
+
+// ---------------------------------------------------------------- dense layers
+// y = x . K (row-major (I, O) kernel at k): acc = x[0]*k[j], then fma over the inputs
+SRNN_HD void g_dense(const SV& k, int I, int O, const SV& x, SV y) {
+  for (int j = 0; j < O; ++j) {
+    float acc = x[0] * k[j];
+    for (int i = 1; i < I; ++i) acc = fmaf(x[i], k[(int64_t)i * O + j], acc);
+    y[j] = acc;
+  }
+}
+// si = K . so (pre-update K); K += x (x) so  (MLP::step_layer)
+SRNN_HD void g_step_layer(SV k, int I, int O, const SV& x, const SV& so, SV si, bool want_in) {
+  if (want_in) {
+    for (int i = 0; i < I; ++i) {
+      float acc = k[(int64_t)i * O] * so[0];
+      for (int j = 1; j < O; ++j) acc = fmaf(k[(int64_t)i * O + j], so[j], acc);
+      si[i] = acc;
+    }
+  }
+  for (int i = 0; i < I; ++i)
+    for (int j = 0; j < O; ++j) k[(int64_t)i * O + j] = fmaf(x[i], so[j], k[(int64_t)i * O + j]);
+}
+// MLP forward keeping every layer's input in acts = [x][h1]...[hD]
+SRNN_HD void g_forward(const GShape& s, const SV& w, const SV& x, SV acts, SV y) {
+  for (int i = 0; i < s.IN; ++i) acts[i] = x[i];
+  g_dense(w.at(s.off[0]), s.IN, s.cols[0], acts, acts.at(s.IN));
+  for (int l = 1; l < s.D; ++l) g_dense(w.at(s.off[l]), s.W, s.W, acts.at(s.IN + (l - 1) * s.W), acts.at(s.IN + l * s.W));
+  g_dense(w.at(s.off[s.D]), s.W, s.OUT, acts.at(s.IN + (s.D - 1) * s.W), y);
+}
+// forward through the MLP with ping-pong vectors h, g (MLP::forward_only)
+SRNN_HD void g_forward_only(const GShape& s, const SV& w, const SV& x, SV h, SV g, SV y) {
+  g_dense(w.at(s.off[0]), s.IN, s.W, x, h);
+  for (int l = 1; l < s.D; ++l) {
+    g_dense(w.at(s.off[l]), s.W, s.W, h, g);
+    for (int j = 0; j < s.W; ++j) h[j] = g[j];
+  }
+  g_dense(w.at(s.off[s.D]), s.W, s.OUT, h, y);
+}
+// one SGD step given dL/dy (MLP::backward_update); so / si are MAXV vectors
+SRNN_HD void g_backward(const GShape& s, SV w, const SV& acts, const SV& gy, float lr, SV so, SV si) {
+  for (int j = 0; j < s.OUT; ++j) so[j] = -lr * gy[j];
+  g_step_layer(w.at(s.off[s.D]), s.W, s.OUT, acts.at(s.IN + (s.D - 1) * s.W), so, si, true);
+  for (int l = s.D - 1; l >= 1; --l) {
+    for (int j = 0; j < s.W; ++j) so[j] = si[j];
+    g_step_layer(w.at(s.off[l]), s.W, s.W, acts.at(s.IN + (l - 1) * s.W), so, si, true);
+  }
+  for (int j = 0; j < s.W; ++j) so[j] = si[j];
+  g_step_layer(w, s.IN, s.W, acts, so, si, false);
+}
+
+// ---------------------------------------------------------------- coordinates
+// (layer, cell, position) of every Weightwise weight (reference code/network.py:240-255)
+static void make_coords_host(const GShape& s, float* c) {
+  int k = 0;
+  for (int l = 0; l < s.NL; ++l)
+    for (int i = 0; i < s.rows[l]; ++i)
+      for (int j = 0; j < s.cols[l]; ++j) {
+        c[3 * k + 0] = norm_id(l, s.NL - 1);
+        c[3 * k + 1] = norm_id(i, s.rows[l] - 1);
+        c[3 * k + 2] = norm_id(j, s.cols[l] - 1);
+        ++k;
+      }
+}
+__device__ void make_coords_dev(const GShape& s, float* c) {  // whole block, then a barrier
+  for (int k = threadIdx.x; k < s.P; k += blockDim.x) {
+    int l = 0;
+    while (l + 1 < s.NL && s.off[l + 1] <= k) ++l;
+    const int q = k - s.off[l], i = q / s.cols[l], j = q - i * s.cols[l];
+    c[3 * k + 0] = norm_id(l, s.NL - 1);
+    c[3 * k + 1] = norm_id(i, s.rows[l] - 1);
+    c[3 * k + 2] = norm_id(j, s.cols[l] - 1);
+  }
+  __syncthreads();
+}
+
+// ---------------------------------------------------------------- permutations
+// nibble permutation of [0, n), n <= 16: the runtime-n form of perm_from_bits<N>
+SRNN_HD uint64_t g_perm_nibbles(int n, uint64_t u) {
+  uint64_t p = 0;
+  for (int k = 0; k < n; ++k) p |= (uint64_t)k << (4 * k);
+  uint32_t ul = (uint32_t)u, uh = (uint32_t)(u >> 32);
+  for (int i = n - 1; i > 0; --i) {
+    const uint64_t lo = (uint64_t)ul * (uint32_t)(i + 1);
+    const uint64_t hi = (uint64_t)uh * (uint32_t)(i + 1) + (lo >> 32);
+    const uint32_t j = (uint32_t)(hi >> 32);
+    ul = (uint32_t)lo;
+    uh = (uint32_t)hi;
+    const uint64_t ni = (p >> (4 * i)) & 15u, nj = (p >> (4 * j)) & 15u, x = ni ^ nj;
+    p ^= (x << (4 * i)) | (x << (4 * j));
+  }
+  return p;
+}
+// Fisher-Yates into a strided vector (fisher_yates of srnn_core.h, same draws)
+SRNN_HD void g_fisher_yates(SV perm, int n, const Rng& rng, uint64_t id, uint32_t step, uint32_t purpose) {
+  for (int i = 0; i < n; ++i) perm[i] = (float)i;
+  U4 r{0, 0, 0, 0};
+  int used = 4;
+  uint32_t blk = 0;
+  for (int i = n - 1; i > 0; --i) {
+    if (used == 4) {
+      r = rng.draw(id, step * 64u + blk, purpose);
+      ++blk;
+      used = 0;
+    }
+    uint32_t x = used == 0 ? r.x : used == 1 ? r.y : used == 2 ? r.z : r.w;
+    ++used;
+    int j = (int)(u01(x) * (float)(i + 1));
+    if (j > i) j = i;
+    const float t = perm[i];
+    perm[i] = perm[j];
+    perm[j] = t;
+  }
+}
+
+// ---------------------------------------------------------------- init
+SRNN_HD void g_glorot(SV w, int off, int r, int c, const Rng& rng, uint64_t uid) {
+  const float lim = sqrtf(6.0f / (float)(r + c));
+  const int n = r * c;
+  for (int b = 0; b < (n + 3) / 4; ++b) {
+    U4 u = rng.draw(uid, (uint32_t)off * 1024u + (uint32_t)b, P_INIT);
+    uint32_t xs[4] = {u.x, u.y, u.z, u.w};
+    for (int q = 0; q < 4; ++q) {
+      int k = b * 4 + q;
+      if (k < n) w[off + k] = -lim + 2.0f * lim * u01(xs[q]);
+    }
+  }
+}
+SRNN_HD void g_orthogonal(SV w, int off, int N, double* a, const Rng& rng, uint64_t uid) {
+  // orthogonal_fill of srnn_core.h with a runtime N; `a` is N*N doubles of scratch
+  int cnt = 0;
+  U4 u{0, 0, 0, 0};
+  float nrm[4] = {0, 0, 0, 0};
+  uint32_t blk = 0;
+  for (int i = 0; i < N; ++i)
+    for (int j = 0; j < N; ++j) {
+      if ((cnt & 3) == 0) {
+        u = rng.draw(uid, (uint32_t)off * 1024u + blk, P_NORMAL);
+        ++blk;
+        float r1 = sqrtf(-2.0f * logf(u01_open0(u.x)));
+        float t1 = 6.283185307179586f * u01(u.y);
+        float r2 = sqrtf(-2.0f * logf(u01_open0(u.z)));
+        float t2 = 6.283185307179586f * u01(u.w);
+        nrm[0] = r1 * cosf(t1);
+        nrm[1] = r1 * sinf(t1);
+        nrm[2] = r2 * cosf(t2);
+        nrm[3] = r2 * sinf(t2);
+      }
+      a[i * N + j] = (double)nrm[cnt & 3];
+      ++cnt;
+    }
+  for (int j = 0; j < N; ++j) {
+    for (int p = 0; p < j; ++p) {
+      double d = 0.0;
+      for (int i = 0; i < N; ++i) d = fma(a[i * N + p], a[i * N + j], d);
+      for (int i = 0; i < N; ++i) a[i * N + j] = fma(-d, a[i * N + p], a[i * N + j]);
+    }
+    double sq = 0.0;
+    for (int i = 0; i < N; ++i) sq = fma(a[i * N + j], a[i * N + j], sq);
+    const double inv = 1.0 / sqrt(sq);
+    for (int i = 0; i < N; ++i) a[i * N + j] *= inv;
+  }
+  for (int i = 0; i < N; ++i)
+    for (int j = 0; j < N; ++j) w[off + i * N + j] = (float)a[i * N + j];
+}
+SRNN_HD void g_init(const GCtx& x, SV w, const Rng& rng, uint64_t uid) {
+  const GShape& s = *x.s;
+  if (s.kind == 2) {
+    for (int l = 0; l < s.NL; ++l) {
+      g_glorot(w, s.koff[l], s.in_[l], s.un[l], rng, uid);
+      g_orthogonal(w, s.roff[l], s.un[l], x.orth, rng, uid);
+    }
+  } else {
+    for (int l = 0; l < s.NL; ++l) g_glorot(w, s.off[l], s.rows[l], s.cols[l], rng, uid);
+  }
+}
+
+// ---------------------------------------------------------------- aggregation / fft
+SRNN_HD int g_clen(const GShape& s, int k) { return k == s.A - 1 ? s.P - s.CS * (s.A - 1) : s.CS; }
+SRNN_HD void g_aggregate(const GShape& s, const SV& t, SV g, int aggregator) {
+  for (int k = 0; k < s.A; ++k) {
+    const int b = k * s.CS, len = g_clen(s, k);
+    if (aggregator == 0) {
+      double acc = 0.0;
+      for (int i = 0; i < len; ++i) acc += (double)t[b + i];
+      g[k] = (float)(acc / (double)len);
+    } else {
+      float m = t[b];
+      for (int i = 0; i < len; ++i) {
+        const float v = t[b + i];
+        if (aggregator == 1) m = (v > m) ? v : m;
+        else m = (v > m && v != 0.0f) ? v : m;
+      }
+      g[k] = m;
+    }
+  }
+}
+SRNN_HD void g_fft_reduce(const GShape& s, const SV& t, SV g) {
+  for (int k = 0; k < s.A; ++k) {
+    float acc = 0.f;
+    for (int n = 0; n < s.A; ++n)
+      acc = fmaf(t[n], cosf(6.283185307179586f * (float)((k * n) % s.A) / (float)s.A), acc);
+    g[k] = acc;
+  }
+}
+// shuffle_random (reference code/network.py:319-322): out[k] = out[perm[k]]
+SRNN_HD void g_shuffle_out(const GCtx& x, SV out, const ApplyCtx& c) {
+  const GShape& s = *x.s;
+  if (c.shuffler != 1) return;
+  SV perm = x.v(s.o_perm), tmp = x.v(s.o_f);
+  g_fisher_yates(perm, s.P, c.rng, c.uid, c.ctr, P_AGGSHUF);
+  for (int k = 0; k < s.P; ++k) tmp[k] = out[k];
+  for (int k = 0; k < s.P; ++k) out[k] = tmp[(int)perm[k]];
+}
+
+// ---------------------------------------------------------------- recurrent
+// one time step of every layer; h holds the hidden state of layer l at offset l*W
+SRNN_HD void g_rnn_step(const GShape& s, const SV& w, float x0, SV h, SV xk, SV hr) {
+  for (int L = 0; L < s.NL; ++L) {
+    const int I = s.in_[L], U = s.un[L];
+    // cell: hn = x . K + h_prev . R, x = the scalar input (L = 0) or layer L-1's new state
+    if (L == 0) {
+      for (int j = 0; j < U; ++j) xk[j] = x0 * w[s.koff[0] + j];
+    } else {
+      g_dense(w.at(s.koff[L]), I, U, h.at((L - 1) * s.W), xk);
+    }
+    g_dense(w.at(s.roff[L]), U, U, h.at(L * s.W), hr);
+    for (int j = 0; j < U; ++j) h[L * s.W + j] = xk[j] + hr[j];
+  }
+}
+
+// ---------------------------------------------------------------- apply (f_a(t))
+SRNN_HD void g_apply(const GCtx& x, const SV& a, const SV& t, SV out, const ApplyCtx& ac) {
+  const GShape& s = *x.s;
+  SV v1 = x.v(s.o_v1), v2 = x.v(s.o_v2), v3 = x.v(s.o_v3), v4 = x.v(s.o_v4);
+  if (s.kind == 0) {
+    for (int k = 0; k < s.P; ++k) {
+      v1[0] = t[k];
+      v1[1] = x.coords[3 * k + 0];
+      v1[2] = x.coords[3 * k + 1];
+      v1[3] = x.coords[3 * k + 2];
+      g_forward_only(s, a, v1, v2, v3, v4);
+      out[k] = v4[0];
+    }
+  } else if (s.kind == 1 || s.kind == 3) {
+    if (s.kind == 1) g_aggregate(s, t, v1, ac.aggregator);
+    else g_fft_reduce(s, t, v1);
+    SV h = x.v(s.o_acts);  // forward_only's output (A floats)
+    g_forward_only(s, a, v1, v2, v3, h);
+    if (s.kind == 1) {
+      for (int k = 0; k < s.A; ++k)
+        for (int i = 0; i < g_clen(s, k); ++i) out[k * s.CS + i] = h[k];
+    } else {
+      for (int m = 0; m < s.P; ++m) {
+        float acc = 0.f;
+        for (int k = 0; k < s.A; ++k)
+          acc = fmaf(h[k], cosf(6.283185307179586f * (float)((k * m) % s.P) / (float)s.P), acc);
+        out[m] = acc / (float)s.P;
+      }
+    }
+    g_shuffle_out(x, out, ac);
+  } else {
+    SV h = x.v(s.o_hs);
+    for (int q = 0; q < s.HS; ++q) h[q] = 0.f;
+    for (int st = 0; st < s.P; ++st) {
+      g_rnn_step(s, a, t[st], h, v1, v2);
+      out[st] = h[s.D * s.W];
+    }
+  }
+}
+
+// ---------------------------------------------------------------- one training epoch
+// Keras fit(batch_size=1) epoch on the samples of `smp` (frozen), in place on w.
+SRNN_HD float g_train_epoch(const GCtx& x, SV w, const SV& smp, TrainCtx& c) {
+  const GShape& s = *x.s;
+  SV v1 = x.v(s.o_v1), v2 = x.v(s.o_v2), v3 = x.v(s.o_v3), v4 = x.v(s.o_v4), acts = x.v(s.o_acts);
+  if (s.kind == 0) {
+    SV sv = x.v(s.o_samp), perm = x.v(s.o_perm);
+    for (int k = 0; k < s.P; ++k) sv[k] = smp[k];
+    uint64_t pn = 0;
+    if (s.P <= 16) {
+      if (c.shuffle) pn = g_perm_nibbles(s.P, perm_bits(perm_draw(c.rng, c.uid, c.ctr, P_SHUFFLE), c.ctr));
+      else
+        for (int k = 0; k < s.P; ++k) pn |= (uint64_t)k << (4 * k);
+    } else if (c.shuffle) {
+      g_fisher_yates(perm, s.P, c.rng, c.uid, c.ctr, P_SHUFFLE);
+    }
+    float loss = 0.f;
+    for (int q = 0; q < s.P; ++q) {
+      int idx;
+      if (s.P <= 16) idx = (int)((pn >> (4 * q)) & 15u);
+      else idx = c.shuffle ? (int)perm[q] : q;
+      v1[0] = sv[idx];
+      v1[1] = x.coords[3 * idx + 0];
+      v1[2] = x.coords[3 * idx + 1];
+      v1[3] = x.coords[3 * idx + 2];
+      g_forward(s, w, v1, acts, v2);
+      float e = v2[0] - v1[0];
+      loss += e * e;
+      v2[0] = 2.0f * e;
+      g_backward(s, w, acts, v2, c.lr, v3, v4);
+    }
+    c.ctr += 1;
+    return loss / (float)s.P;
+  }
+  if (s.kind == 1 || s.kind == 3) {
+    SV g = x.v(s.o_v1), h = x.v(s.o_v2), gy = x.v(s.o_v2);
+    if (s.kind == 1) g_aggregate(s, smp, g, c.aggregator);
+    else g_fft_reduce(s, smp, g);
+    g_forward(s, w, g, acts, h);
+    float loss = 0.f;
+    for (int k = 0; k < s.A; ++k) {
+      float e = h[k] - g[k];
+      loss += e * e;
+      gy[k] = 2.0f * e / (float)s.A;  // h[k] is dead after this line: gy aliases h
+    }
+    g_backward(s, w, acts, gy, c.lr, v3, v4);
+    c.ctr += 1;
+    return loss / (float)s.A;
+  }
+  // recurrent: one (1, P, 1) sequence, BPTT, one SGD step
+  SV hs = x.v(s.o_hs), h = x.v(s.o_hs + s.P * s.HS), carry = x.v(s.o_hs + s.P * s.HS + s.HS),
+     zeros = x.v(s.o_hs + s.P * s.HS + 2 * s.HS), gw = x.v(s.o_gw);
+  for (int q = 0; q < s.HS; ++q) h[q] = 0.f, carry[q] = 0.f, zeros[q] = 0.f;
+  for (int t = 0; t < s.P; ++t) {
+    g_rnn_step(s, w, smp[t], h, v1, v2);
+    for (int q = 0; q < s.HS; ++q) hs[(int64_t)t * s.HS + q] = h[q];
+  }
+  for (int k = 0; k < s.P; ++k) gw[k] = 0.f;
+  float loss = 0.f;
+  SV dtop = v1, dh = v2, dx = v3, cr = v4;
+  for (int t = s.P - 1; t >= 0; --t) {
+    const SV hst = hs.at((int64_t)t * s.HS), hsp = t > 0 ? hs.at((int64_t)(t - 1) * s.HS) : zeros;
+    float e = hst[s.D * s.W] - smp[t];
+    loss += e * e;
+    dtop[0] = 2.0f * e / (float)s.P;
+    for (int L = s.D; L >= 0; --L) {
+      const int U = s.un[L], I = s.in_[L];
+      for (int j = 0; j < U; ++j) dh[j] = dtop[j] + carry[L * s.W + j];
+      // cell_bwd: kernel / recurrent-kernel grads, input grad (L > 0), carry
+      for (int i = 0; i < I; ++i) {
+        const float xi = L == 0 ? smp[t] : hst[(L - 1) * s.W + i];
+        for (int j = 0; j < U; ++j) gw[s.koff[L] + i * U + j] = fmaf(xi, dh[j], gw[s.koff[L] + i * U + j]);
+      }
+      for (int i = 0; i < U; ++i)
+        for (int j = 0; j < U; ++j) gw[s.roff[L] + i * U + j] = fmaf(hsp[L * s.W + i], dh[j], gw[s.roff[L] + i * U + j]);
+      if (L > 0) {
+        for (int i = 0; i < I; ++i) {
+          float acc = 0.f;
+          for (int j = 0; j < U; ++j) acc = fmaf(w[s.koff[L] + i * U + j], dh[j], acc);
+          dx[i] = acc;
+        }
+      }
+      for (int i = 0; i < U; ++i) {
+        float acc = 0.f;
+        for (int j = 0; j < U; ++j) acc = fmaf(w[s.roff[L] + i * U + j], dh[j], acc);
+        cr[i] = acc;
+      }
+      for (int j = 0; j < U; ++j) carry[L * s.W + j] = cr[j];
+      for (int i = 0; i < I && L > 0; ++i) dtop[i] = dx[i];
+    }
+  }
+  for (int k = 0; k < s.P; ++k) w[k] = fmaf(gw[k], -c.lr, w[k]);
+  c.ctr += 1;
+  return loss / (float)s.P;
+}
+
+// E epochs; SELF: the samples are the weights at each epoch start, else the fixed teacher t
+SRNN_HD float g_train_epochs(const GCtx& x, SV w, const SV& t, int E, bool self, TrainCtx& c) {
+  const GShape& s = *x.s;
+  SV smp = x.v(s.o_t);
+  if (!self && smp.p != t.p) g_copy(s, smp, t);
+  float loss = 0.f;
+  for (int e = 0; e < E; ++e) {
+    if (self) g_copy(s, smp, w);
+    loss = g_train_epoch(x, w, smp, c);
+  }
+  return loss;
+}
+
+// ---------------------------------------------------------------- predicates
+SRNN_HD bool g_diverged(const GShape& s, const SV& w) {
+  bool bad = false;
+  for (int k = 0; k < s.P; ++k) bad |= !finitef(w[k]);
+  return bad;
+}
+SRNN_HD bool g_zero(const GShape& s, const SV& w, float eps) {
+  bool ok = true;
+  for (int k = 0; k < s.P; ++k) ok &= (-eps <= w[k]) && (w[k] <= eps);
+  return ok;
+}
+SRNN_HD bool g_within(const GShape& s, const SV& a, const SV& b, float eps) {
+  bool ok = true;
+  for (int k = 0; k < s.P; ++k) ok &= !(fabsf(a[k] - b[k]) >= eps);
+  return ok;
+}
+// classification of w (reference code/experiment.py:79-91); uses o and f as scratch
+SRNN_HD int8_t g_classify_w(const GCtx& x, const SV& w, float eps, bool with_sec, const ApplyCtx& ac) {
+  const GShape& s = *x.s;
+  if (g_diverged(s, w)) return C_DIVERGENT;
+  SV f1 = x.v(s.o_o);
+  g_apply(x, w, w, f1, ac);
+  g_quant(s, f1);
+  if (!g_diverged(s, f1) && g_within(s, f1, w, eps)) return g_zero(s, w, eps) ? C_FIX_ZERO : C_FIX_OTHER;
+  if (with_sec) {
+    SV f2 = x.v(s.o_f);  // g_apply's shuffle uses o_f as its own scratch: stage f2 in o_t
+    SV f2b = x.v(s.o_t);
+    g_apply(x, w, f1, f2b, ac);
+    (void)f2;
+    g_quant(s, f2b);
+    if (!g_diverged(s, f2b) && g_within(s, f2b, w, eps)) return C_FIX_SEC;
+  }
+  return C_OTHER;
+}
+
+// ==================================================================================
+// Per-item operators (mirror Item<Net, S> of srnn_kernels.h)
+// ==================================================================================
+struct GItem {
+  SRNN_HD static Rng rng(const SrnnArgs& a) { return Rng{(uint32_t)a.seed, (uint32_t)(a.seed >> 32)}; }
+  SRNN_HD static uint64_t uid_of(const SrnnArgs& a, int64_t i) { return a.uid ? (uint64_t)a.uid[i] : (uint64_t)i; }
+  SRNN_HD static char* rowp(const GShape& s, float* b, int64_t i) { return reinterpret_cast<char*>(b) + i * g_rb(s); }
+  SRNN_HD static const char* rowp(const GShape& s, const float* b, int64_t i) {
+    return reinterpret_cast<const char*>(b) + i * g_rb(s);
+  }
+  SRNN_HD static int64_t xb(const GShape& s) { return g_rb(s) + 16; }
+  SRNN_HD static int64_t sr(const GShape& s) { return (48 + xb(s) - 1) / xb(s); }
+  SRNN_HD static ApplyCtx actx(const SrnnArgs& a, const GShape& s, uint64_t uid, uint32_t ctr) {
+    ApplyCtx x;
+    x.rng = rng(a);
+    x.uid = uid;
+    x.ctr = ctr;
+    x.aggregator = s.aggregator;
+    x.shuffler = s.shuffler;
+    x.perm = nullptr;
+    return x;
+  }
+  SRNN_HD static TrainCtx tctx(const SrnnArgs& a, const GShape& s, uint64_t uid, uint32_t ctr) {
+    TrainCtx tc;
+    tc.lr = a.lr;
+    tc.rng = rng(a);
+    tc.uid = uid;
+    tc.ctr = ctr;
+    tc.samp = nullptr;
+    tc.perm = nullptr;
+    tc.shuffle = (a.flags & 1) != 0;
+    tc.stride = 1;
+    tc.aggregator = s.aggregator;
+    return tc;
+  }
+  // generation-start row of global slot g (local table, or the exchange buffers)
+  SRNN_HD static const char* row_of(const GShape& s, const SrnnArgs& a, int64_t g) {
+    if (a.world <= 1 || (g >= a.lo && g < a.lo + a.n)) return rowp(s, a.W2, g - a.lo);
+    if (a.flags & 128) return rowp(s, a.recvbuf, g);
+    return reinterpret_cast<const char*>(a.recvbuf) + (int64_t)a.rmap[g] * xb(s);
+  }
+
+  SRNN_HD static void init(const GCtx& x, const SrnnArgs& a, int64_t i) {
+    SV w = x.v(x.s->o_w);
+    g_init(x, w, rng(a), uid_of(a, i));
+    g_store(*x.s, rowp(*x.s, a.W, i), w);
+  }
+  SRNN_HD static void apply(const GCtx& x, const SrnnArgs& a, int64_t i) {
+    const GShape& s = *x.s;
+    const int64_t fi = a.idx_f ? a.idx_f[i] : i, ti = a.idx_t ? a.idx_t[i] : i, oi = a.idx_o ? a.idx_o[i] : i;
+    SV f = x.v(s.o_w), t = x.v(s.o_t), o = x.v(s.o_o);
+    g_load(s, rowp(s, a.W, fi), f);
+    g_load(s, rowp(s, a.W, ti), t);
+    const uint64_t ouid = a.uid ? (uint64_t)a.uid[ti] : (uint64_t)ti;
+    g_apply(x, f, t, o, actx(a, s, ouid, a.ctr));
+    g_quant(s, o);
+    g_store(s, rowp(s, a.W2, oi), o);
+  }
+  SRNN_HD static void run_fixpoint(const GCtx& x, const SrnnArgs& a, int64_t i) {
+    const GShape& s = *x.s;
+    SV w = x.v(s.o_w), nw = x.v(s.o_t);
+    g_load(s, rowp(s, a.W, i), w);
+    ApplyCtx ac = actx(a, s, uid_of(a, i), a.ctr);
+    if (a.traj) g_store(s, rowp(s, a.traj, i), w);
+    int st = 0;
+    for (; st < a.steps; ++st) {
+      if (a.early_exit) {
+        if (g_diverged(s, w)) break;
+        g_apply(x, w, w, nw, ac);
+        g_quant(s, nw);
+        if (!g_diverged(s, nw) && g_within(s, nw, w, a.eps)) break;
+      } else {
+        g_apply(x, w, w, nw, ac);
+        g_quant(s, nw);
+      }
+      g_copy(s, w, nw);
+      ac.ctr += 1;
+      if (a.traj) g_store(s, rowp(s, a.traj, (int64_t)(st + 1) * a.n + i), w);
+    }
+    g_store(s, rowp(s, a.W, i), w);
+    if (a.nsteps) a.nsteps[i] = st;
+    if (a.cls) a.cls[i] = g_classify_w(x, w, a.eps, (a.flags & 8) != 0, ac);
+  }
+  SRNN_HD static void vary_run(const GCtx& x, const SrnnArgs& a, int64_t i) {
+    const GShape& s = *x.s;
+    SV w = x.v(s.o_w), nw = x.v(s.o_t);
+    g_load(s, rowp(s, a.W, i), w);
+    ApplyCtx ac = actx(a, s, uid_of(a, i), a.ctr);
+    int tts = 0, taf = 0;
+    bool still = true;
+    for (int st = 0; st < a.steps; ++st) {
+      g_apply(x, w, w, nw, ac);
+      g_quant(s, nw);
+      g_copy(s, w, nw);
+      if (g_zero(s, w, a.eps) || g_diverged(s, w)) break;
+      g_apply(x, w, w, nw, ac);
+      g_quant(s, nw);
+      const bool fix = !g_diverged(s, nw) && g_within(s, nw, w, a.eps);
+      if (fix) {
+        if (still) ++taf;
+        else still = true;
+      } else {
+        still = false;
+      }
+      ++tts;
+    }
+    g_store(s, rowp(s, a.W, i), w);
+    a.nsteps[i] = tts;
+    a.loss[i] = (float)taf;
+  }
+  SRNN_HD static void perturb(const GCtx& x, const SrnnArgs& a, int64_t i) {
+    const GShape& s = *x.s;
+    SV w = x.v(s.o_w);
+    g_load(s, rowp(s, a.W, i), w);
+    const Rng r = rng(a);
+    const uint64_t uid = uid_of(a, i);
+    for (int k = 0; k < s.P; ++k) {
+      U4 u = r.draw(uid, a.ctr * 1024u + (uint32_t)k, P_PERTURB);
+      double mag = (double)u01(u.y) * (double)a.eps;
+      w[k] = u01(u.x) < 0.5f ? (float)((double)w[k] + mag) : (float)((double)w[k] - mag);
+    }
+    g_store(s, rowp(s, a.W, i), w);
+  }
+  SRNN_HD static void train(const GCtx& x, const SrnnArgs& a, int64_t i, bool learn) {
+    const GShape& s = *x.s;
+    SV w = x.v(s.o_w), t = x.v(s.o_t);
+    g_load(s, rowp(s, a.W, i), w);
+    if (learn) g_load(s, rowp(s, a.W2, a.idx_t ? a.idx_t[i] : i), t);
+    TrainCtx tc = tctx(a, s, uid_of(a, i), a.ctr);
+    const float loss = g_train_epochs(x, w, t, a.epochs, !learn, tc);
+    g_store(s, rowp(s, a.W, i), w);
+    if (a.loss) a.loss[i] = loss;
+  }
+  SRNN_HD static int8_t classify(const GCtx& x, const SrnnArgs& a, int64_t i) {
+    const GShape& s = *x.s;
+    SV w = x.v(s.o_w);
+    g_load(s, rowp(s, a.W, i), w);
+    const int8_t k = g_classify_w(x, w, a.eps, (a.flags & 8) != 0, actx(a, s, uid_of(a, i), a.ctr));
+    if (a.cls) a.cls[i] = k;
+    return k;
+  }
+
+  // ---------------------------------------------------------------- soup (sharded-safe)
+  SRNN_HD static void soup_pack(const GShape& s, const SrnnArgs& a, int64_t j) {
+    int32_t m = a.need[j];
+    if (!m) return;
+    a.need[j] = 0;
+    const int32_t gen = a.gen_ptr ? a.gen_ptr[0] : a.gen;
+    const char* src = rowp(s, a.W2, j);
+    const int64_t RB = g_rb(s), XB = xb(s);
+    while (m) {
+      const int r = __builtin_ctz((unsigned)m);
+      m &= m - 1;
+      const int32_t pos = atomic_add_i32(a.sendcnt + r, 1);
+      if (pos >= a.cap) {
+        atomic_or_i32(a.ovf, 1);
+        continue;
+      }
+      char* dst = reinterpret_cast<char*>(a.sendbuf) + ((int64_t)r * a.cap + pos) * XB;
+      const uint2* s2 = reinterpret_cast<const uint2*>(src);
+      uint2* d2 = reinterpret_cast<uint2*>(dst);
+      for (int64_t q = 0; q < RB / 8; ++q) d2[q] = s2[q];
+      d2[RB / 8] = make_uint2((uint32_t)(a.lo + j), (uint32_t)gen);
+      d2[RB / 8 + 1] = make_uint2(0u, 0u);
+    }
+  }
+  SRNN_HD static void pack_stats(const GShape& s, const SrnnArgs& a) {
+    for (int r = 0; r < a.world; ++r) {
+      int64_t* d = reinterpret_cast<int64_t*>(reinterpret_cast<char*>(a.sendbuf) + (int64_t)r * a.cap * xb(s));
+      for (int q = 0; q < 6; ++q) d[q] = (int64_t)a.counts[q];
+    }
+  }
+  SRNN_HD static void soup_unpack(const GShape& s, const SrnnArgs& a, int64_t k) {
+    if (k % a.cap < sr(s)) return;
+    const int32_t* tag = reinterpret_cast<const int32_t*>(reinterpret_cast<const char*>(a.recvbuf) + k * xb(s) + g_rb(s));
+    if (tag[1] == (a.gen_ptr ? a.gen_ptr[0] : a.gen)) a.rmap[tag[0]] = (int32_t)k;
+  }
+  SRNN_HD static int64_t stat(const GShape& s, const SrnnArgs& a, int r, int q) {
+    if (a.flags & 256)
+      return reinterpret_cast<const int64_t*>(reinterpret_cast<const char*>(a.recvbuf) + (int64_t)r * a.cap * xb(s))[q];
+    return a.stats[r * 6 + q];
+  }
+
+  // synchronous generation of local row j (Item::soup_evolve)
+  SRNN_HD static void soup_evolve(const GCtx& x, const SrnnArgs& a, int64_t j) {
+    const GShape& s = *x.s;
+    const int64_t g = a.lo + j;
+    SV w = x.v(s.o_w), f = x.v(s.o_t), o = x.v(s.o_o);
+    g_load(s, rowp(s, a.W2, j), w);
+    const uint64_t uid = uid_of(a, j);
+    const int32_t gen = a.gen_ptr ? a.gen_ptr[0] : a.gen;
+    ApplyCtx ac = actx(a, s, uid, (uint32_t)gen * 1024u);
+    const int32_t head = a.i32e[j];
+    a.i32e[j] = -1;
+    int32_t last = -1;
+    while (head >= 0) {
+      int32_t best = INT_MAX;
+      for (int32_t r = head; r >= 0; r = a.i32f[r]) best = (r > last && r < best) ? r : best;
+      if (best == INT_MAX) break;
+      last = best;
+      g_load(s, row_of(s, a, best), f);
+      g_apply(x, f, w, o, ac);
+      g_quant(s, o);
+      ac.ctr += 1;
+      g_copy(s, w, o);
+    }
+    int32_t my_at, te;
+    Item<Weightwise<1, 1>, StF32>::decision(a, g, gen, my_at, te);
+    int8_t act = A_NONE;
+    int64_t cp = -1;
+    if (my_at >= 0) act = A_ATTACKING, cp = my_at;
+    TrainCtx tc = tctx(a, s, uid, (uint32_t)gen * 1024u + 512u);
+    float loss = 0.f;
+    if (te >= 0) {
+      g_load(s, row_of(s, a, te), f);
+      if (a.severity > 0) loss = g_train_epochs(x, w, f, a.severity, false, tc);
+      act = A_LEARN_FROM;
+      cp = te;
+    }
+    if (a.epochs > 0) {
+      loss = g_train_epochs(x, w, f, a.epochs, true, tc);
+      act = A_TRAIN_SELF;
+      cp = -1;
+    }
+    g_quant(s, w);
+    int8_t rs = 0;
+    if ((a.flags & 2) && g_diverged(s, w)) rs = 1;
+    else if ((a.flags & 4) && g_zero(s, w, a.eps)) rs = 2;
+    if (rs && (a.flags & 32)) g_init(x, w, rng(a), respawn_key(gen, g));
+    g_store(s, rowp(s, a.W, j), w);
+    if (a.action) a.action[j] = act;
+    if (a.counterpart) a.counterpart[j] = cp;
+    if (a.loss) a.loss[j] = loss;
+    a.respawn[j] = rs;
+  }
+  SRNN_HD static void respawn(const GCtx& x, const SrnnArgs& a, int64_t j) {
+    if (a.respawn[j] == 0) return;
+    SV w = x.v(x.s->o_w);
+    const int32_t gen = a.gen_ptr ? a.gen_ptr[0] : a.gen;
+    g_init(x, w, rng(a), respawn_key(gen, a.lo + j));
+    g_store(*x.s, rowp(*x.s, a.W, j), w);
+  }
+};
+
+// ==================================================================================
+// Device kernels (grid-stride, lane per row; scratch element-major over all lanes)
+// ==================================================================================
+constexpr int GOP_CLASSIFY_COUNT = 100, GOP_EVOLVE = 101;
+
+template <int OP>
+__global__ __launch_bounds__(GTB) void k_generic(GShape s, SrnnArgs a, int64_t lanes) {
+  extern __shared__ float s_coords[];
+  __shared__ uint32_t s_cnt[6];
+  if (s.kind == 0) make_coords_dev(s, s_coords);
+  if (threadIdx.x < 6) s_cnt[threadIdx.x] = 0;
+  const int64_t lane_id = (int64_t)blockIdx.x * GTB + threadIdx.x;
+  GCtx x{&s, reinterpret_cast<float*>(a.scratch) + lane_id, lanes, s_coords, g_orth(s, a.scratch, lanes, lane_id)};
+  const int64_t stride = (int64_t)gridDim.x * GTB;
+  const int64_t items = a.n;
+  for (int64_t base = (int64_t)blockIdx.x * GTB; base < items; base += stride) {
+    const int64_t i = base + threadIdx.x;
+    const bool on = i < items;
+    if constexpr (OP == OP_INIT) {
+      if (on) GItem::init(x, a, i);
+    } else if constexpr (OP == OP_APPLY) {
+      if (on) GItem::apply(x, a, i);
+    } else if constexpr (OP == OP_RUN_FIXPOINT) {
+      if (on) GItem::run_fixpoint(x, a, i);
+    } else if constexpr (OP == OP_TRAIN || OP == OP_LEARN) {
+      if (on) GItem::train(x, a, i, OP == OP_LEARN);
+    } else if constexpr (OP == OP_PERTURB) {
+      if (on) GItem::perturb(x, a, i);
+    } else if constexpr (OP == OP_VARY_RUN) {
+      if (on) GItem::vary_run(x, a, i);
+    } else if constexpr (OP == OP_RESPAWN) {
+      if (on) GItem::respawn(x, a, i);
+    } else if constexpr (OP == OP_CLASSIFY || OP == GOP_CLASSIFY_COUNT) {
+      int8_t k = on ? GItem::classify(x, a, i) : (int8_t)-1;
+      if constexpr (OP == GOP_CLASSIFY_COUNT) {
+#pragma unroll
+        for (int q = 0; q < 5; ++q) {
+          const unsigned long long m = __ballot(k == q);
+          if (threadIdx.x == 0 && m) s_cnt[q] += (uint32_t)__popcll(m);
+        }
+        if (a.flags & 64) {
+          const unsigned long long m = __ballot(on && a.respawn[i] != 0);
+          if (threadIdx.x == 0) s_cnt[5] += (uint32_t)__popcll(m);
+        }
+      }
+    } else if constexpr (OP == GOP_EVOLVE) {
+      bool rs = false;
+      if (on) {
+        GItem::soup_evolve(x, a, i);
+        rs = a.respawn[i] != 0;
+      }
+      if (a.i32c) {
+        if (a.flags & 16) {
+          if (on) a.i32c[i] = rs ? 1 : 0;
+        } else {
+          const unsigned long long m = __ballot(rs);  // the 64 rows of this block: one ballot word
+          if (threadIdx.x == 0) reinterpret_cast<unsigned long long*>(a.i32c)[base / GTB] = m;
+        }
+      }
+    }
+  }
+  if constexpr (OP == GOP_CLASSIFY_COUNT) {
+    if (threadIdx.x < 6 && s_cnt[threadIdx.x] && (threadIdx.x < 5 || (a.flags & 64)))
+      atomicAdd(a.counts + threadIdx.x, (uint64_t)s_cnt[threadIdx.x]);
+    if ((a.flags & 512) && blockIdx.x == 0 && threadIdx.x == 0) {
+      if (a.gen_out) a.gen_out[0] = a.gen_ptr[0] + 1;
+      else ((int32_t*)a.gen_ptr)[0] = a.gen_ptr[0] + 1;
+    }
+  }
+}
+
+// sharded-soup byte movers with the runtime row size
+__global__ __launch_bounds__(256) void k_g_pack(GShape s, SrnnArgs a) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i == 0) GItem::pack_stats(s, a);
+  if (i < a.n) GItem::soup_pack(s, a, i);
+}
+__global__ __launch_bounds__(256) void k_g_unpack(GShape s, SrnnArgs a) {
+  const int64_t k = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (k == 0)
+    for (int r = 0; r < a.world; ++r) a.sendcnt[r] = (int32_t)GItem::sr(s);
+  if (k < (int64_t)a.world * a.cap) GItem::soup_unpack(s, a, k);
+}
+
+// Single-rank respawn (k_respawn_seq with runtime shapes): one workgroup scans the 64-row
+// respawn ballots in slot order, assigns the uids, re-initialises the rows, advances
+// next_uid and the generation counter.
+constexpr int GTBR = 1024;
+__global__ __launch_bounds__(GTBR) void k_g_respawn_seq(GShape s, SrnnArgs a) {
+  __shared__ int32_t s_wave[GTBR / 64];
+  const unsigned long long* masks = reinterpret_cast<const unsigned long long*>(a.i32c);
+  const int64_t nb = (a.n + GTB - 1) / GTB, ch = (nb + GTBR - 1) / GTBR;
+  const int64_t b0 = (int64_t)threadIdx.x * ch, b1 = b0 + ch < nb ? b0 + ch : nb;
+  int32_t cnt = 0;
+  for (int64_t b = b0; b < b1; ++b) cnt += __popcll(masks[b]);
+  int32_t total;
+  const int32_t incl = block_incl_scan<GTBR>(cnt, s_wave, &total);
+  const int64_t base = *(volatile const int64_t*)a.uid_base;
+  GCtx x{&s, reinterpret_cast<float*>(a.scratch) + threadIdx.x, GTBR, nullptr, g_orth(s, a.scratch, GTBR, threadIdx.x)};
+  const int32_t gen = a.gen_ptr ? a.gen_ptr[0] : a.gen;
+  int64_t k = base + incl - cnt;
+  for (int64_t b = b0; b < b1 && cnt; ++b) {
+    unsigned long long m = masks[b];
+    while (m) {
+      const int bit = __ffsll((long long)m) - 1;
+      m &= m - 1;
+      const int64_t r = b * GTB + bit;
+      a.uid_out[r] = k++;
+      SV w = x.v(s.o_w);
+      g_init(x, w, GItem::rng(a), respawn_key(gen, a.lo + r));
+      g_store(s, GItem::rowp(s, a.W, r), w);
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    ((int64_t*)a.uid_base)[0] = base + total;
+    if (a.gen_out) a.gen_out[0] = gen + 1;
+    else if (a.gen_ptr) ((int32_t*)a.gen_ptr)[0] = gen + 1;
+  }
+  if (a.counts && threadIdx.x < 5) a.counts[threadIdx.x] = 0;
+}
+
+// Sharded soup: uids of the previous generation's newborns (k_uid_assign, runtime rows)
+__global__ __launch_bounds__(GTBR) void k_g_uid_assign(GShape s, SrnnArgs a) {
+  __shared__ int32_t s_wave[GTBR / 64];
+  __shared__ int64_t s_prefix, s_total;
+  if (threadIdx.x == 0) {
+    int64_t pre = 0, tot = 0, cen[5] = {0, 0, 0, 0, 0}, all = 0;
+    for (int r = 0; r < a.world; ++r) {
+      const int64_t k = GItem::stat(s, a, r, 5);
+      if (r < a.rank) pre += k;
+      tot += k;
+      for (int q = 0; q < 5; ++q) cen[q] += GItem::stat(s, a, r, q);
+    }
+    for (int q = 0; q < 5; ++q) all += cen[q];
+    s_prefix = pre;
+    s_total = tot;
+    if (a.census && all > 0)
+      for (int q = 0; q < 5; ++q) a.census[q] = cen[q];
+  }
+  unsigned long long* masks = reinterpret_cast<unsigned long long*>(a.i32c);
+  const int64_t nb = (a.n + GTB - 1) / GTB, ch = (nb + GTBR - 1) / GTBR;
+  const int64_t b0 = (int64_t)threadIdx.x * ch, b1 = b0 + ch < nb ? b0 + ch : nb;
+  int32_t cnt = 0;
+  for (int64_t b = b0; b < b1; ++b) cnt += __popcll(masks[b]);
+  int32_t total_local;
+  const int32_t incl = block_incl_scan<GTBR>(cnt, s_wave, &total_local);
+  const int64_t base = *(volatile const int64_t*)a.uid_base;
+  int64_t k = base + s_prefix + incl - cnt;
+  for (int64_t b = b0; b < b1 && cnt; ++b) {
+    unsigned long long m = masks[b];
+    masks[b] = 0ull;
+    while (m) {
+      const int bit = __ffsll((long long)m) - 1;
+      m &= m - 1;
+      a.uid_out[b * GTB + bit] = k++;
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) ((int64_t*)a.uid_base)[0] = base + s_total;
+  if (a.counts && threadIdx.x < 6) a.counts[threadIdx.x] = 0;
+}
+
+// ==================================================================================
+// Host execution (thread pool; per-thread scratch) and dispatch
+// ==================================================================================
+static void host_generic(int op, const GShape& s, const SrnnArgs& a) {
+  std::vector<float> coords((size_t)(3 * s.P + 3));
+  if (s.kind == 0) make_coords_host(s, coords.data());
+  auto with_ctx = [&](auto&& f) {
+    return [&, f](int64_t i) {
+      thread_local std::vector<float> buf;
+      thread_local std::vector<double> orth;
+      if (buf.size() < (size_t)s.sfloats) buf.resize((size_t)s.sfloats);
+      if (orth.size() < (size_t)s.orthd + 1) orth.resize((size_t)s.orthd + 1);
+      GCtx x{&s, buf.data(), 1, coords.data(), orth.data()};
+      f(x, i);
+    };
+  };
+  switch (op) {
+    case OP_INIT: host_parallel(a.n, with_ctx([&](const GCtx& x, int64_t i) { GItem::init(x, a, i); })); break;
+    case OP_APPLY: host_parallel(a.n, with_ctx([&](const GCtx& x, int64_t i) { GItem::apply(x, a, i); })); break;
+    case OP_RUN_FIXPOINT:
+      host_parallel(a.n, with_ctx([&](const GCtx& x, int64_t i) { GItem::run_fixpoint(x, a, i); }));
+      break;
+    case OP_TRAIN: host_parallel(a.n, with_ctx([&](const GCtx& x, int64_t i) { GItem::train(x, a, i, false); })); break;
+    case OP_LEARN: host_parallel(a.n, with_ctx([&](const GCtx& x, int64_t i) { GItem::train(x, a, i, true); })); break;
+    case OP_PERTURB: host_parallel(a.n, with_ctx([&](const GCtx& x, int64_t i) { GItem::perturb(x, a, i); })); break;
+    case OP_VARY_RUN: host_parallel(a.n, with_ctx([&](const GCtx& x, int64_t i) { GItem::vary_run(x, a, i); })); break;
+    case OP_RESPAWN: host_parallel(a.n, with_ctx([&](const GCtx& x, int64_t i) { GItem::respawn(x, a, i); })); break;
+    case OP_SOUP_EVOLVE:
+      host_parallel(a.n, with_ctx([&](const GCtx& x, int64_t i) { GItem::soup_evolve(x, a, i); }));
+      if (a.i32c)
+        for (int64_t i = 0; i < a.n; ++i) a.i32c[i] = a.respawn[i] != 0 ? 1 : 0;
+      break;
+    case OP_CLASSIFY: {
+      std::vector<int8_t> ks((size_t)a.n);
+      host_parallel(a.n, with_ctx([&](const GCtx& x, int64_t i) { ks[(size_t)i] = GItem::classify(x, a, i); }));
+      if (a.counts) {
+        uint64_t local[5] = {0, 0, 0, 0, 0};
+        for (int64_t i = 0; i < a.n; ++i) local[ks[(size_t)i]]++;
+        for (int q = 0; q < 5; ++q) a.counts[q] += local[q];
+        if (a.flags & 64)
+          for (int64_t i = 0; i < a.n; ++i) a.counts[5] += a.respawn[i] != 0;
+        if (a.flags & 512) {
+          if (a.gen_out) a.gen_out[0] = a.gen_ptr[0] + 1;
+          else ((int32_t*)a.gen_ptr)[0] = a.gen_ptr[0] + 1;
+        }
+      }
+      break;
+    }
+    case OP_RESPAWN_SEQ: {
+      std::vector<float> buf((size_t)s.sfloats);
+      std::vector<double> orth((size_t)s.orthd + 1);
+      GCtx x{&s, buf.data(), 1, coords.data(), orth.data()};
+      int64_t k = a.uid_base[0];
+      const int32_t gen = a.gen_ptr ? a.gen_ptr[0] : a.gen;
+      for (int64_t i = 0; i < a.n; ++i) {
+        if (a.respawn[i] == 0) continue;
+        a.uid_out[i] = k++;
+        SV w = x.v(s.o_w);
+        g_init(x, w, GItem::rng(a), respawn_key(gen, a.lo + i));
+        g_store(s, GItem::rowp(s, a.W, i), w);
+      }
+      ((int64_t*)a.uid_base)[0] = k;
+      if (a.gen_out) a.gen_out[0] = gen + 1;
+      else if (a.gen_ptr) ((int32_t*)a.gen_ptr)[0] = gen + 1;
+      if (a.counts)
+        for (int q = 0; q < 5; ++q) a.counts[q] = 0;
+      break;
+    }
+    case OP_SOUP_PACK:
+      GItem::pack_stats(s, a);
+      for (int64_t j = 0; j < a.n; ++j) GItem::soup_pack(s, a, j);
+      break;
+    case OP_SOUP_UNPACK:
+      for (int r = 0; r < a.world; ++r) a.sendcnt[r] = (int32_t)GItem::sr(s);
+      for (int64_t k = 0; k < (int64_t)a.world * a.cap; ++k) GItem::soup_unpack(s, a, k);
+      break;
+    case OP_UID_ASSIGN: {
+      if (a.flags & 16384) {
+        for (int64_t k = 0; k < (int64_t)a.world * a.cap; ++k) GItem::soup_unpack(s, a, k);
+        for (int r = 0; r < a.world; ++r) a.sendcnt[r] = (int32_t)GItem::sr(s);
+      }
+      int64_t pre = 0, tot = 0, cen[5] = {0, 0, 0, 0, 0}, all = 0;
+      for (int r = 0; r < a.world; ++r) {
+        const int64_t k = GItem::stat(s, a, r, 5);
+        if (r < a.rank) pre += k;
+        tot += k;
+        for (int q = 0; q < 5; ++q) cen[q] += GItem::stat(s, a, r, q);
+      }
+      for (int q = 0; q < 5; ++q) all += cen[q];
+      if (a.census && all > 0)
+        for (int q = 0; q < 5; ++q) a.census[q] = cen[q];
+      int64_t k = a.uid_base[0] + pre;
+      for (int64_t i = 0; i < a.n; ++i)
+        if (a.i32c[i]) {
+          a.uid_out[i] = k++;
+          a.i32c[i] = 0;
+        }
+      ((int64_t*)a.uid_base)[0] += tot;
+      if (a.counts)
+        for (int q = 0; q < 6; ++q) a.counts[q] = 0;
+      break;
+    }
+    default: break;
+  }
+}
+
+static bool generic_op_supported(int op) {
+  switch (op) {
+    case OP_INIT: case OP_APPLY: case OP_RUN_FIXPOINT: case OP_TRAIN: case OP_LEARN: case OP_CLASSIFY:
+    case OP_PERTURB: case OP_SOUP_DECIDE: case OP_RESPAWN_SEQ: case OP_SOUP_EVOLVE: case OP_RESPAWN:
+    case OP_VARY_RUN: case OP_SOUP_PACK: case OP_SOUP_UNPACK: case OP_UID_ASSIGN:
+      return true;
+    default: return false;
+  }
+}
+
+// lanes of a device launch and the scratch bytes they need
+static int64_t generic_lanes(const GShape& s, const SrnnArgs& a, int64_t items) {
+  const int64_t per = g_lane_bytes(s);
+  int64_t cap = per > 0 ? a.scratch_bytes / per : 0;
+  cap = (cap / GTB) * GTB;
+  int64_t want = ((items + GTB - 1) / GTB) * GTB;
+  return want < cap ? want : cap;
+}
+
+static int generic_launch(int op, const GShape& s, const SrnnArgs& a) {
+  hipStream_t st = (hipStream_t)a.stream;
+  if (op == OP_SOUP_DECIDE) {
+    // shape-independent: the decisions / attack lists of srnn_kernels.h
+    SrnnCfg dummy{};
+    return launch<Weightwise<1, 1>, OP_SOUP_DECIDE, StF32>(dummy, a);
+  }
+  if (op == OP_SOUP_PACK) {
+    const int64_t items = a.n > 0 ? a.n : 1;
+    hipLaunchKernelGGL(k_g_pack, dim3((unsigned)((items + 255) / 256)), dim3(256), 0, st, s, a);
+  } else if (op == OP_SOUP_UNPACK) {
+    const int64_t items = (int64_t)a.world * a.cap;
+    if (items > 0) hipLaunchKernelGGL(k_g_unpack, dim3((unsigned)((items + 255) / 256)), dim3(256), 0, st, s, a);
+  } else if (op == OP_UID_ASSIGN) {
+    if (a.flags & 16384) {
+      const int64_t items = (int64_t)a.world * a.cap;
+      if (items > 0) hipLaunchKernelGGL(k_g_unpack, dim3((unsigned)((items + 255) / 256)), dim3(256), 0, st, s, a);
+    }
+    hipLaunchKernelGGL(k_g_uid_assign, dim3(1), dim3(GTBR), 0, st, s, a);
+  } else if (op == OP_RESPAWN_SEQ) {
+    if (!a.scratch || a.scratch_bytes < (int64_t)GTBR * g_lane_bytes(s)) {
+      set_error("generic respawn_seq needs scratch >= 1024 lanes (srnn_generic_scratch_bytes)");
+      return -5;
+    }
+    hipLaunchKernelGGL(k_g_respawn_seq, dim3(1), dim3(GTBR), 0, st, s, a);
+  } else {
+    if (a.n <= 0) return 0;
+    const int64_t lanes = generic_lanes(s, a, a.n);
+    if (lanes <= 0) {
+      set_error("generic engine: scratch buffer missing or too small (srnn_generic_scratch_bytes)");
+      return -5;
+    }
+    const size_t lds = s.kind == 0 ? (size_t)s.P * 3 * sizeof(float) : 0;
+    if (lds > 150 * 1024) {
+      set_error("generic engine: weightwise coordinate table exceeds LDS (P > 12800)");
+      return -5;
+    }
+    const dim3 grid((unsigned)(lanes / GTB)), block(GTB);
+    switch (op) {
+#define SRNN_GK(OPC) hipLaunchKernelGGL((k_generic<OPC>), grid, block, lds, st, s, a, lanes); break;
+      case OP_INIT: SRNN_GK(OP_INIT)
+      case OP_APPLY: SRNN_GK(OP_APPLY)
+      case OP_RUN_FIXPOINT: SRNN_GK(OP_RUN_FIXPOINT)
+      case OP_TRAIN: SRNN_GK(OP_TRAIN)
+      case OP_LEARN: SRNN_GK(OP_LEARN)
+      case OP_PERTURB: SRNN_GK(OP_PERTURB)
+      case OP_VARY_RUN: SRNN_GK(OP_VARY_RUN)
+      case OP_RESPAWN: SRNN_GK(OP_RESPAWN)
+      case OP_SOUP_EVOLVE: SRNN_GK(GOP_EVOLVE)
+      case OP_CLASSIFY:
+        if (a.counts) {
+          SRNN_GK(GOP_CLASSIFY_COUNT)
+        } else {
+          SRNN_GK(OP_CLASSIFY)
+        }
+#undef SRNN_GK
+      default: set_error("op not supported by the generic engine"); return -1;
+    }
+  }
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) {
+    set_error(hipGetErrorString(e));
+    return -3;
+  }
+  return 0;
+}
+
+}  // namespace srnn
+
+// 0 ok / negative error; 1 = not a valid shape for the generic engine, 2 = op not supported
+extern "C" int srnn_dispatch_generic(int op, const SrnnCfg* c, const SrnnArgs* a) {
+  srnn::GShape s;
+  const char* why = "";
+  if (!srnn::make_gshape(*c, s, &why)) {
+    srnn::set_error(why);
+    return 1;
+  }
+  if (op < 0) return 0;
+  if (!srnn::generic_op_supported(op)) return 2;
+  if (!a->dev) {
+    if (op == OP_SOUP_DECIDE) {
+      SrnnCfg dummy{};
+      return srnn::host_run<srnn::Weightwise<1, 1>, OP_SOUP_DECIDE, srnn::StF32>(dummy, *a);
+    }
+    srnn::host_generic(op, s, *a);
+    return 0;
+  }
+  return srnn::generic_launch(op, s, *a);
+}
+
+// Scratch bytes a device launch of the generic engine wants for n rows (lanes = n rounded
+// up to a wave, at most `max_lanes`; the respawn workgroup needs 1024 lanes); 0 = no scratch
+extern "C" int64_t srnn_generic_scratch_bytes(const SrnnCfg* c, int64_t n, int64_t max_lanes) {
+  srnn::GShape s;
+  const char* why = "";
+  if (!srnn::make_gshape(*c, s, &why)) return -1;
+  int64_t lanes = ((n + srnn::GTB - 1) / srnn::GTB) * srnn::GTB;
+  if (max_lanes > 0 && lanes > max_lanes) lanes = (max_lanes / srnn::GTB) * srnn::GTB;
+  if (lanes < srnn::GTBR) lanes = srnn::GTBR;
+  return lanes * srnn::g_lane_bytes(s);
+}

@@ -43,8 +43,18 @@ static SrnnCfg agg422() {
   return c;
 }
 
+static SrnnCfg cfg(int kind, int w, int d, int a, int p, int shuffler = 0, int dtype = 0) {
+  SrnnCfg c{};
+  c.kind = kind, c.width = w, c.depth = d, c.aggregates = a, c.aggregator = 0, c.shuffler = shuffler;
+  c.p = p, c.pp = (p + 3) & ~3, c.dtype = dtype;
+  return c;
+}
+
+extern "C" int srnn_comm_available(const char* hint);
+
 static void ops_smoke(const SrnnCfg& c, int64_t n) {
   const int PP = c.pp;
+  // fp32 tables, or 16-bit ones (dtype 1/2) in the same buffers (half the bytes used)
   std::vector<float> W((size_t)(n * PP), 0.f), O((size_t)(n * PP), 0.f);
   std::vector<int64_t> uid((size_t)n), idx((size_t)n);
   for (int64_t i = 0; i < n; ++i) uid[(size_t)i] = i + 7, idx[(size_t)i] = (i + 1) % n;
@@ -55,10 +65,16 @@ static void ops_smoke(const SrnnCfg& c, int64_t n) {
   SrnnArgs a{};
   a.n = n, a.seed = 11, a.W = W.data(), a.uid = uid.data(), a.dev = 0, a.lr = 0.01f, a.eps = 1e-4f;
   run(OP_INIT, c, a);
-  bool finite = true;
-  for (int64_t i = 0; i < n; ++i)
-    for (int k = 0; k < c.p; ++k) finite &= std::isfinite(W[(size_t)(i * PP + k)]);
-  CHECK(finite);
+  bool finite = true, nonzero = false;
+  if (c.dtype == 0)
+    for (int64_t i = 0; i < n; ++i)
+      for (int k = 0; k < c.p; ++k) {
+        finite &= std::isfinite(W[(size_t)(i * PP + k)]);
+        nonzero |= W[(size_t)(i * PP + k)] != 0.f;
+      }
+  else
+    nonzero = true;
+  CHECK(finite && nonzero);
   SrnnArgs b = a;
   b.W2 = O.data(), b.idx_f = idx.data();
   run(OP_APPLY, c, b);
@@ -78,6 +94,9 @@ static void ops_smoke(const SrnnCfg& c, int64_t n) {
   SrnnArgs p = a;
   p.eps = 1e-3f;
   run(OP_PERTURB, c, p);
+  SrnnArgs v = a;
+  v.steps = 10, v.nsteps = nsteps.data(), v.loss = loss.data();
+  run(OP_VARY_RUN, c, v);
 }
 
 // ---- one soup over R ranks (R = 1: the single-rank pipeline) --------------------------
@@ -193,9 +212,21 @@ static std::vector<float> soup(int R, int64_t N, int gens, std::vector<int64_t>*
 }
 
 int main() {
-  CHECK(srnn_abi_version() == 11);
+  CHECK(srnn_abi_version() == 12);
   ops_smoke(ww22(), 1000);
   ops_smoke(agg422(), 777);
+  ops_smoke(cfg(2, 2, 2, 0, 17), 300);              // Recurrent(2,2): templated BPTT
+  ops_smoke(cfg(3, 2, 2, 4, 20), 300);              // FFT(4,2,2)
+  ops_smoke(cfg(0, 2, 2, 0, 14, 0, 1), 300);        // bf16 table (srnn_lowp.hip)
+  ops_smoke(cfg(1, 2, 2, 4, 20, 1, 2), 300);        // fp16 + shuffle_random
+  // runtime-shape engine (srnn_generic.hip): shapes with no template, and the GPU-only
+  // wave-per-particle shapes on the host
+  ops_smoke(cfg(0, 3, 3, 0, 33), 200);              // Weightwise(3,3)
+  ops_smoke(cfg(2, 3, 2, 0, 34), 100);              // Recurrent(3,2)
+  ops_smoke(cfg(1, 10, 3, 4, 280), 64);             // Aggregating(4,10,3): the north-star net
+  ops_smoke(cfg(1, 3, 2, 4, 33, 1, 1), 64);         // Aggregating(4,3,2), shuffle_random, bf16
+  ops_smoke(cfg(0, 16, 2, 0, 336), 32);             // Weightwise(16,2) (MFMA path on the GPU)
+  CHECK(srnn_comm_available("/nonexistent/librccl.so") == 0 || srnn_comm_available("/nonexistent/librccl.so") == 1);
   std::vector<int64_t> u1, u2, u3;
   int64_t n1 = 0, n2 = 0, n3 = 0;
   const int64_t N = 301;

@@ -74,13 +74,12 @@ class RunConfig:
     device: str = "cuda"                   # cuda | cpu
     backend: Optional[str] = None          # torch.distributed backend (nccl = RCCL; gloo on CPU)
     graph: bool = True                     # capture generations in hipGraphs
-    census_every: int = 1                  # per-generation census (0: only at the end)
+    census_every: int = 1                  # 1: census every generation, 0: only at the end
     metrics_path: Optional[str] = None     # JSONL stream of per-generation metrics
     metrics_every: int = 1
     checkpoint_dir: Optional[str] = None   # periodic native checkpoints (exact resume)
     checkpoint_every: int = 0
     collective_timeout_s: float = 600.0    # process-group timeout (failure detection)
-    reference_compat: bool = True          # reproduce reference quirks
     recorder: RecorderConfig = RecorderConfig()
 
     def validate(self):
@@ -92,6 +91,9 @@ class RunConfig:
             raise ValueError("exchange must be alltoall or allgather")
         if self.device not in ("cuda", "cpu"):
             raise ValueError("device must be cuda or cpu")
+        if self.census_every not in (0, 1):
+            # the census is fused into the generation kernel: on (every generation) or off
+            raise ValueError("census_every must be 0 (final census only) or 1 (every generation)")
         self.recorder.validate()
         return self
 
@@ -122,6 +124,7 @@ class ExperimentConfig:
     @staticmethod
     def from_dict(d: Dict[str, Any]) -> "ExperimentConfig":
         run = dict(d.get("run", {}))
+        run.pop("reference_compat", None)  # accepted from round-1 config files; quirks live in the compat API
         rec = RecorderConfig(**run.pop("recorder", {}))
         return ExperimentConfig(arch=ArchSpec.from_json(json.dumps(d["arch"])) if "arch" in d else ArchSpec.weightwise(2, 2),
                                 soup=SoupConfig(**d.get("soup", {})), run=RunConfig(recorder=rec, **run)).validate()

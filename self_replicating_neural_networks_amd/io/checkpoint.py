@@ -77,11 +77,9 @@ def load_engine(path: str, device="cpu", dist: Optional[Dist] = None):
     spec = ArchSpec(**m["spec"])
     d = dist or Dist()
     lo, hi = d.shard(m["n_total"])
-    W, uid = _read_rows(path, lo, hi, spec.P)
-    full = np.zeros((m["n_total"], spec.P), dtype=np.float32)
-    full[lo:hi] = W
+    W, uid = _read_rows(path, lo, hi, spec.P)  # this rank's rows only: host memory O(shard)
     eng = SoupEngine(spec, m["n_total"], m["params"], device=device, seed=m["seed"], lr=m["lr"],
-                     shuffle=m["shuffle"], dist=d, weights=full, dtype=_DTYPES[m.get("dtype", "float32")],
+                     shuffle=m["shuffle"], dist=d, local_weights=W, dtype=_DTYPES[m.get("dtype", "float32")],
                      exchange=m.get("exchange", "alltoall"))
     eng.uid.copy_(torch.from_numpy(uid))
     eng.next_uid.fill_(m["next_uid"])

@@ -20,7 +20,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 # SRNN_LIB: load another build of the library (A/B of compiler flags on the GPU box)
 LIB_PATH = os.environ.get("SRNN_LIB") or os.path.join(_HERE, "libsrnn.so")
 CSRC = os.path.normpath(os.path.join(_HERE, "..", "..", "csrc"))
-ABI_VERSION = 11
+ABI_VERSION = 12
 
 OP_INIT = 0
 OP_APPLY = 1
@@ -85,6 +85,7 @@ class SrnnArgs(ctypes.Structure):
         ("action", _P), ("counterpart", _P), ("respawn", _P),
         ("temp", _P), ("temp_bytes", ctypes.c_int64),
         ("dev", ctypes.c_int32), ("pad1", ctypes.c_int32), ("stream", _P), ("gen_out", _P),
+        ("scratch", _P), ("scratch_bytes", ctypes.c_int64),
     ]
 
 
@@ -127,6 +128,12 @@ def lib():
         L.srnn_last_error.restype = ctypes.c_char_p
         L.srnn_scan_temp_bytes.argtypes = [ctypes.c_int64]
         L.srnn_scan_temp_bytes.restype = ctypes.c_int64
+        L.srnn_is_generic.argtypes = [ctypes.POINTER(SrnnCfg), ctypes.c_int]
+        L.srnn_is_generic.restype = ctypes.c_int
+        L.srnn_generic_scratch_bytes.argtypes = [ctypes.POINTER(SrnnCfg), ctypes.c_int64, ctypes.c_int64]
+        L.srnn_generic_scratch_bytes.restype = ctypes.c_int64
+        L.srnn_set_force_generic.argtypes = [ctypes.c_int]
+        L.srnn_set_force_generic.restype = None
         vp, i64, cp = ctypes.c_void_p, ctypes.c_int64, ctypes.c_char_p
         for name, args in (("srnn_comm_available", [cp]), ("srnn_comm_unique_id", [cp, vp, ctypes.c_int]),
                            ("srnn_comm_init", [cp, vp, ctypes.c_int, ctypes.c_int, ctypes.c_int,
@@ -157,6 +164,22 @@ def make_cfg(spec, dtype: int = DTYPE_FP32) -> SrnnCfg:
 
 def has_config(spec, dtype: int = DTYPE_FP32) -> bool:
     return bool(lib().srnn_has_config(ctypes.byref(make_cfg(spec, dtype))))
+
+
+def is_generic(spec, op: int, dtype: int = DTYPE_FP32) -> bool:
+    """True when ``op`` of this architecture runs on the runtime-shape engine
+    (csrc/srnn_generic.hip) on the GPU instead of a shape-specialised kernel."""
+    return bool(lib().srnn_is_generic(ctypes.byref(make_cfg(spec, dtype)), int(op)))
+
+
+def set_force_generic(on: bool) -> None:
+    """Route every op to the runtime-shape engine (A/B tests against the templated kernels)."""
+    lib().srnn_set_force_generic(1 if on else 0)
+
+
+def generic_scratch_bytes(spec, n: int, dtype: int = DTYPE_FP32, max_lanes: int = 65536) -> int:
+    """Device scratch the runtime-shape engine needs for ``n`` rows (per-lane vectors)."""
+    return int(lib().srnn_generic_scratch_bytes(ctypes.byref(make_cfg(spec, dtype)), int(n), int(max_lanes)))
 
 
 def run(op: int, spec, args: SrnnArgs, cfg: SrnnCfg = None, dtype: int = DTYPE_FP32) -> None:

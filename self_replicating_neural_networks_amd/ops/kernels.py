@@ -64,21 +64,27 @@ def _check_idx(idx: Optional[torch.Tensor], n_items: int, n_rows: int, dev, name
 def is_wave_per_particle(spec) -> bool:
     """Nets too large for the register kernels run wave-per-particle: aggregating nets
     (csrc/srnn_bignet.hip, chunk-state multi-step) and width >= 16 weightwise nets
-    (csrc/srnn_wide.hip, MFMA)."""
-    return (spec.kind == "aggregating" and spec.P > 64) or (spec.kind == "weightwise" and spec.width >= 16)
+    (csrc/srnn_wide.hip, MFMA) -- for the shapes those files instantiate; every other
+    shape runs on the runtime-shape engine (csrc/srnn_generic.hip)."""
+    return (((spec.kind == "aggregating" and spec.P > 64) or (spec.kind == "weightwise" and spec.width >= 16))
+            and not _lib.is_generic(spec, _lib.OP_RUN_FIXPOINT))
 
 
 def needs_chunk_state_temp(spec) -> bool:
-    return spec.kind == "aggregating" and spec.P > 64
+    return spec.kind == "aggregating" and spec.P > 64 and not _lib.is_generic(spec, _lib.OP_RUN_FIXPOINT)
 
 
-def _base_args(W: torch.Tensor, seed: int = 0, ctr: int = 0) -> SrnnArgs:
+def _base_args(W: torch.Tensor, seed: int = 0, ctr: int = 0, scratch: Optional[torch.Tensor] = None) -> SrnnArgs:
+    """``scratch``: device bytes for the runtime-shape engine (csrc/srnn_generic.hip); when
+    omitted the library uses its own cached buffer (not allowed inside a graph capture)."""
     a = SrnnArgs()
     a.seed = int(seed) & 0xFFFFFFFFFFFFFFFF
     a.ctr = int(ctr) & 0xFFFFFFFF
     if W.device.type == "cuda":
         a.dev = 1
         a.stream = ctypes.c_void_p(torch.cuda.current_stream(W.device).cuda_stream)
+        if scratch is not None:
+            a.scratch, a.scratch_bytes = _p(scratch), scratch.numel() * scratch.element_size()
     else:
         a.dev = 0
     return a
@@ -208,7 +214,7 @@ def learn_from(spec, W: torch.Tensor, teachers: torch.Tensor, idx_t=None, epochs
 
 
 def classify(spec, W: torch.Tensor, eps: float, with_sec: bool = True, uid=None, seed=0, ctr=0,
-             counts: Optional[torch.Tensor] = None):
+             counts: Optional[torch.Tensor] = None, scratch: Optional[torch.Tensor] = None):
     """Per-row class (0 divergent, 1 fix_zero, 2 fix_other, 3 fix_sec, 4 other) and the
     5-bin histogram (reference code/experiment.py:79-91, code/soup.py:89-103)."""
     dt = _check_table(spec, W)
@@ -216,7 +222,7 @@ def classify(spec, W: torch.Tensor, eps: float, with_sec: bool = True, uid=None,
     cls = torch.empty(n, dtype=torch.int8, device=W.device)
     if counts is None:
         counts = torch.zeros(5, dtype=torch.int64, device=W.device)
-    a = _base_args(W, seed, ctr)
+    a = _base_args(W, seed, ctr, scratch)
     a.n, a.eps = n, float(eps)
     a.flags = _lib.FLAG_FIX_SEC if with_sec else 0
     a.W, a.cls, a.counts = _p(W), _p(cls), _p(counts)

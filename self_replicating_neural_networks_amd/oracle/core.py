@@ -127,14 +127,15 @@ def _orthogonal(w, off, N, seed, uids):
         r2 = np.sqrt(np.float32(-2.0) * np.log(u01_open0(u[2])))
         t2 = np.float32(6.283185307179586) * u01(u[3])
         vals += [r1 * np.cos(t1), r1 * np.sin(t1), r2 * np.cos(t2), r2 * np.sin(t2)]
-    a = np.stack(vals[:N * N], axis=1).astype(np.float32).reshape(n, N, N)
+    # modified Gram-Schmidt in float64 (Keras' orthogonal initializer is a float64 QR)
+    a = np.stack(vals[:N * N], axis=1).astype(np.float32).astype(np.float64).reshape(n, N, N)
     for j in range(N):
         for p in range(j):
-            d = np.sum(a[:, :, p] * a[:, :, j], axis=1, dtype=np.float32)
+            d = np.sum(a[:, :, p] * a[:, :, j], axis=1)
             a[:, :, j] -= d[:, None] * a[:, :, p]
-        s = np.sum(a[:, :, j] * a[:, :, j], axis=1, dtype=np.float32)
-        a[:, :, j] *= (np.float32(1.0) / np.sqrt(s))[:, None]
-    w[:, off:off + N * N] = a.reshape(n, N * N)
+        s = np.sum(a[:, :, j] * a[:, :, j], axis=1)
+        a[:, :, j] *= (1.0 / np.sqrt(s))[:, None]
+    w[:, off:off + N * N] = a.astype(np.float32).reshape(n, N * N)
 
 
 def init(spec: ArchSpec, uids, seed) -> np.ndarray:

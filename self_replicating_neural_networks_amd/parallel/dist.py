@@ -145,6 +145,10 @@ class Dist:
         hi = ((self.rank + 1) * n_total) // self.world
         return lo, hi
 
+    def shard_of_rank(self, rank: int, n_total: int):
+        """[lo, hi) rows of ``rank``."""
+        return (rank * n_total) // self.world, ((rank + 1) * n_total) // self.world
+
     def shard_sizes(self, n_total: int):
         return [((r + 1) * n_total) // self.world - (r * n_total) // self.world for r in range(self.world)]
 

@@ -83,21 +83,30 @@ class Population:
         repeated victims are applied in order (sequential per victim)."""
         attackers = attackers.to(self.device, torch.int64).contiguous()
         victims = victims.to(self.device, torch.int64).contiguous()
-        src = self.W.clone()
-        if victims.numel() and torch.unique(victims).numel() != victims.numel():
-            # several attacks on one victim: apply them in order
-            for a, v in zip(attackers.tolist(), victims.tolist()):
-                out = self.W.clone()
-                K.apply(self.spec, torch.cat([src[a:a + 1], self.W[v:v + 1]]), out[:2],
-                        idx_f=torch.tensor([0], device=self.device), idx_t=torch.tensor([1], device=self.device),
-                        idx_o=torch.tensor([0], device=self.device), n=1, uid=self.uid[[v, v]].contiguous(),
-                        seed=self.seed, ctr=self._next_ctr())
-                self.W[v] = out[0]
+        m = victims.numel()
+        if m == 0:
             return self
-        tmp = torch.cat([src, self.W])  # rows [0,N): attacker snapshot, [N,2N): current
-        out = self.W
-        K.apply(self.spec, tmp, out, idx_f=attackers, idx_t=(victims + self.n).contiguous(), idx_o=victims,
-                n=victims.numel(), uid=torch.cat([self.uid, self.uid]).contiguous(), seed=self.seed, ctr=self._next_ctr())
+        tmp = torch.cat([self.W, self.W])  # rows [0,N): attacker snapshot, [N,2N): evolving victims
+        uid2 = torch.cat([self.uid, self.uid]).contiguous()
+        if torch.unique(victims).numel() == m:
+            K.apply(self.spec, tmp, self.W, idx_f=attackers, idx_t=(victims + self.n).contiguous(), idx_o=victims,
+                    n=m, uid=uid2, seed=self.seed, ctr=self._next_ctr())
+            return self
+        # several attacks on one victim, applied in call order: round k applies the k-th
+        # attack of every victim (distinct victims per round, one batched launch each, in
+        # place on the victim half of tmp) -- rounds = the largest multiplicity, not m
+        order = torch.argsort(victims, stable=True)
+        vs, at = victims[order], attackers[order]
+        pos = torch.arange(m, device=self.device)
+        new = torch.ones(m, dtype=torch.bool, device=self.device)
+        new[1:] = vs[1:] != vs[:-1]
+        rank = pos - torch.cummax(torch.where(new, pos, torch.zeros_like(pos)), 0).values
+        for k in range(int(rank.max()) + 1):
+            sel = rank == k
+            v = (vs[sel] + self.n).contiguous()
+            K.apply(self.spec, tmp, tmp, idx_f=at[sel].contiguous(), idx_t=v, idx_o=v, n=v.numel(), uid=uid2,
+                    seed=self.seed, ctr=self._next_ctr())
+        self.W.copy_(tmp[self.n:])
         return self
 
     def train(self, epochs: int = 1, shuffle: bool = True) -> torch.Tensor:

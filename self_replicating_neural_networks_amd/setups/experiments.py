@@ -334,11 +334,13 @@ def network_demo(trials=100, step_limit=100, train_runs=1000, device=None, seed=
             exp.log(exp.counters)
         out[spec.kind] = dict(exp.counters)
     with FixpointExperiment(root=root) as exp:
+        # reference :670-680: ONE net trains one epoch per run_id; every 100 epochs run_net
+        # self-attacks that same net in place (until fixpoint / divergence, epsilon 1e-4)
+        # and training then continues from the self-attacked weights
         pop = Population(WW, 1, device=device, seed=_seed(seed) + 7)
         for run_id in range(0, train_runs + 1, 100):
             pop.train(100 if run_id else 1)
-            probe = Population(WW, 1, device=device, weights=pop.weights().cpu())
-            exp.run_population(probe, step_limit, early_exit=True)
+            exp.run_population(pop, step_limit, early_exit=True, eps=1e-4)
         exp.log(exp.counters)
     out["self_train"] = dict(exp.counters)
     return out

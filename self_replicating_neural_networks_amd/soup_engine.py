@@ -86,7 +86,10 @@ class SoupEngine:
 
     def __init__(self, spec: ArchSpec, n_total: int, params: Dict, device="cpu", seed: int = 0,
                  lr: float = 0.01, shuffle: bool = True, dist: Optional[Dist] = None, weights=None,
-                 dtype: torch.dtype = torch.float32, exchange: str = "alltoall"):
+                 dtype: torch.dtype = torch.float32, exchange: str = "alltoall", local_weights=None):
+        """``weights``: the whole population's initial rows [n_total, >= P] (every rank
+        takes its slice); ``local_weights``: only this rank's rows [hi - lo, >= P] (what a
+        re-sharding checkpoint load passes, so host memory stays O(shard))."""
         self.spec = spec
         self.n_total = int(n_total)
         self.params = dict(attacking_rate=0.1, learn_from_rate=0.1, train=0, learn_from_severity=1)
@@ -125,10 +128,11 @@ class SoupEngine:
             # exchange of the generation-start rows that other ranks need (attackers of
             # their victims, teachers of their learners): fixed-capacity all-to-all
             R = self.dist.world
-            ar = max(float(self.params.get("attacking_rate", 0.1)), 0.0)
-            lr_ = max(float(self.params.get("learn_from_rate", 0.1)), 0.0)
+            if R > 31:
+                # need masks are one int32 bit per destination rank (srnn_kernels.h link_decision)
+                raise ValueError("exchange='alltoall' supports at most 31 ranks; use exchange='allgather'")
             n_max = -(-self.n_total // R)  # identical on every rank (buffers must match)
-            mean = n_max * min(ar + lr_, 2.0) / R
+            mean = self._expected_peer_rows()
             xw = PP * self._bufs[0].element_size() // 4 + 4  # row bytes + 16 tag bytes, in fp32 units
             # the first `stat_rows` rows of each destination block carry the sender's
             # int64[6] stats (previous census + respawns): one collective per generation
@@ -157,7 +161,14 @@ class SoupEngine:
         self._lists_ready = False   # heads[_p] already holds this generation's attacks
         # one launch (+ a one-workgroup finish) per generation: OP_SOUP_GEN; sharded engines
         # with the all-to-all exchange fuse the evolve, census and next decisions too
-        self.fused = not self.dist.enabled or exchange == "alltoall"
+        # shapes without a templated kernel run on the runtime-shape engine: unfused
+        # generation pipeline (decide -> evolve -> respawn -> census), per-lane scratch
+        self.generic = _lib.is_generic(spec, _lib.OP_SOUP_GEN, self.dtype_code)
+        self.fused = (not self.dist.enabled or exchange == "alltoall") and not self.generic
+        self._scratch = None
+        if self.device.type == "cuda" and _lib.is_generic(spec, _lib.OP_SOUP_EVOLVE, self.dtype_code):
+            self._scratch = torch.empty(_lib.generic_scratch_bytes(spec, self.n, self.dtype_code),
+                                        dtype=torch.uint8, device=dev)
         self._mask_src = "i32c"   # where the pending respawn ballots live ("bs": block stats)
         self._packed = False      # sharded: the coming generation's send buffer is packed
         self._fused_census = False
@@ -186,12 +197,50 @@ class SoupEngine:
         self._arg_cache = {}
         # initial particles: uids 0..n_total-1, keyed init (identical for any rank count)
         local = self.local_rows()
-        if weights is not None:
-            w = torch.as_tensor(weights, dtype=torch.float32)
+        if weights is not None or local_weights is not None:
+            if local_weights is not None:
+                w = torch.as_tensor(local_weights, dtype=torch.float32)
+                if w.shape[0] != self.n:
+                    raise ValueError(f"local_weights has {w.shape[0]} rows, this rank owns {self.n}")
+            else:
+                w = torch.as_tensor(weights, dtype=torch.float32)[self.lo:self.hi]
             local.zero_()
-            local[:, : w.shape[1]] = w[self.lo:self.hi].to(dev, dtype)
+            local[:, : w.shape[1]] = w.to(dev, dtype)
         else:
             K.init_rows(spec, local, self.uid, self.seed)
+
+    def _expected_peer_rows(self) -> float:
+        """Largest expected number of rows one rank ships to one peer per generation.
+
+        Row i of rank r goes to rank q when i attacks a victim owned by q, or when a
+        learner owned by q picks i as teacher.  Partners are uniform over the slot's
+        sub-soup (``segment``) or the whole population, so the load of a (r, q) pair is
+        sum over r's slots of ar * |S_i n shard_q| / |S_i| plus sum over q's slots of
+        lr * |S_j n shard_r| / |S_j|.  Segments spanning several shards concentrate the
+        traffic on neighbouring ranks, which a uniform estimate would underestimate."""
+        R = self.dist.world
+        ar = max(float(self.params.get("attacking_rate", 0.1)), 0.0)
+        lr_ = max(float(self.params.get("learn_from_rate", 0.1)), 0.0)
+        seg = int(self.params.get("segment", 0) or 0) or self.n_total
+        bounds = [self.dist.shard_of_rank(r, self.n_total) for r in range(R)]
+        # overlap[r][q] = sum over slots i of shard r of |S_i n shard_q| / |S_i|; a segment
+        # inside one shard only adds to the diagonal, so only the (at most R - 1) segments
+        # holding a shard boundary are visited
+        overlap = [[0.0] * R for _ in range(R)]
+        starts = sorted({(lo // seg) * seg for lo, _ in bounds[1:]})
+        for s0 in starts:
+            s1 = min(s0 + seg, self.n_total)
+            inter = [max(0, min(hi, s1) - max(lo, s0)) for lo, hi in bounds]
+            for r in range(R):
+                if inter[r]:
+                    for q in range(R):
+                        overlap[r][q] += inter[r] * inter[q] / (s1 - s0)
+        worst = 0.0
+        for r in range(R):
+            for q in range(R):
+                if q != r:
+                    worst = max(worst, ar * overlap[r][q] + lr_ * overlap[q][r])
+        return worst
 
     # ------------------------------------------------------------------ views
     @property
@@ -214,7 +263,8 @@ class SoupEngine:
 
     @property
     def eps(self) -> float:
-        return float(self.params.get("epsilon", 1e-4) or 1e-14)
+        # reference default epsilon 1e-14 (code/network.py:78); 0 / None fall back to it
+        return float(self.params.get("epsilon") or 1e-14)
 
     def _flags(self) -> int:
         f = _lib.FLAG_SHUFFLE if self.shuffle else 0
@@ -240,6 +290,8 @@ class SoupEngine:
         if self.device.type == "cuda":
             a.dev = 1
             a.stream = ctypes.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
+            if self._scratch is not None:
+                a.scratch, a.scratch_bytes = _p(self._scratch), self._scratch.numel()
         return a
 
     # ------------------------------------------------------------------ one generation
@@ -432,6 +484,7 @@ class SoupEngine:
         if zero:
             self.counts.zero_()
         cls, _ = K.classify(self.spec, self.local_rows(), self.eps, with_sec, uid=self.uid, seed=self.seed,
+                            scratch=self._scratch,
                             ctr=0x7FFFFFF0, counts=self.counts)
         return cls
 

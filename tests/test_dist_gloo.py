@@ -29,13 +29,14 @@ def _free_port():
 DTYPES = {"float32": torch.float32, "bfloat16": torch.bfloat16, "float16": torch.float16}
 
 
-def _worker(rank, world, port, spec_json, out_dir, dtype="float32", exchange="alltoall", chunks=(GENS,)):
+def _worker(rank, world, port, spec_json, out_dir, dtype="float32", exchange="alltoall", chunks=(GENS,), params=None):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         d = Dist(rank, world, 0, None, force=world == 1)
         spec = ArchSpec.from_json(spec_json)
-        e = SoupEngine(spec, N_TOTAL, PARAMS, device="cpu", seed=21, dist=d, dtype=DTYPES[dtype], exchange=exchange)
+        e = SoupEngine(spec, N_TOTAL, params or PARAMS, device="cpu", seed=21, dist=d, dtype=DTYPES[dtype],
+                       exchange=exchange)
         e.stats = True
         for k in chunks:  # uids of the newborns are settled between evolve calls
             e.evolve(k)
@@ -67,6 +68,37 @@ def test_sharded_soup_equals_single_rank(tmp_path, world, dtype, exchange, chunk
     for p in parts:
         assert int(p["next_uid"][0]) == int(ref.next_uid[0])
         assert list(p["counts"]) == [ref_counts[k] for k in sorted(ref_counts)]
+
+
+@pytest.mark.parametrize("spec,world,exchange", [
+    (ArchSpec.recurrent(3, 2), 2, "alltoall"), (ArchSpec.aggregating(4, 3, 2), 3, "allgather"),
+    (ArchSpec.weightwise(3, 3), 3, "alltoall")], ids=["rnn-3-2", "agg-4-3-2", "ww-3-3"])
+def test_sharded_generic_shapes(tmp_path, spec, world, exchange):
+    """shapes on the runtime-shape engine (unfused generation) shard bitwise too"""
+    ref = SoupEngine(spec, N_TOTAL, PARAMS, device="cpu", seed=21)
+    assert ref.generic
+    ref.evolve(GENS)
+    mp.start_processes(_worker, args=(world, _free_port(), spec.to_json(), str(tmp_path), "float32", exchange, (GENS,)),
+                       nprocs=world, start_method="spawn", join=True)
+    W = np.concatenate([np.load(os.path.join(tmp_path, f"r{r}.npz"))["W"] for r in range(world)])
+    uid = np.concatenate([np.load(os.path.join(tmp_path, f"r{r}.npz"))["uid"] for r in range(world)])
+    assert np.array_equal(W, ref.local_rows().float().numpy(), equal_nan=True)
+    assert np.array_equal(uid, ref.uid.numpy())
+
+
+def test_sharded_segments_spanning_shards(tmp_path):
+    """sub-soups larger than a shard concentrate the row traffic on neighbouring ranks: the
+    exchange capacity is sized from the segment span, so nothing overflows"""
+    p = dict(PARAMS, attacking_rate=0.5, learn_from_rate=0.5)
+    for seg in (29, 203):
+        p["segment"] = seg
+        ref = SoupEngine(ArchSpec.weightwise(2, 2), N_TOTAL, p, device="cpu", seed=21)
+        ref.evolve(GENS)
+        mp.start_processes(_worker, args=(4, _free_port(), ArchSpec.weightwise(2, 2).to_json(), str(tmp_path),
+                                          "float32", "alltoall", (GENS,), dict(p)),
+                           nprocs=4, start_method="spawn", join=True)
+        W = np.concatenate([np.load(os.path.join(tmp_path, f"r{r}.npz"))["W"] for r in range(4)])
+        assert np.array_equal(W, ref.local_rows().float().numpy(), equal_nan=True)
 
 
 def _worker_hi(rank, world, port, out_dir):

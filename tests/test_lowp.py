@@ -97,10 +97,28 @@ def test_lowp_soup_resume_bitwise(tmp_path, dtype):
     assert _eq(a.local_rows(), b.local_rows()) and torch.equal(a.uid, b.uid)
 
 
-def test_lowp_rejects_unsupported_shapes():
+def test_lowp_any_shape_via_generic_engine():
+    """16-bit tables of shapes without a templated 16-bit kernel run on the runtime-shape
+    engine; for an instantiated shape the generic engine equals the templated kernel
+    bitwise (same per-particle arithmetic, same rounding points)."""
     spec = ArchSpec.recurrent(2, 2)
-    assert not _lib.has_config(spec, _lib.DTYPE_BF16)
-    with pytest.raises(_lib.NativeLibraryError):
-        K.init_rows(spec, torch.zeros(4, spec.PP, dtype=torch.bfloat16), torch.arange(4), 0)
+    assert _lib.has_config(spec, _lib.DTYPE_BF16)
+    W = torch.zeros(4, spec.PP, dtype=torch.bfloat16)
+    K.init_rows(spec, W, torch.arange(4), 0)
+    assert torch.isfinite(W.float()).all()
     with pytest.raises(TypeError):
         K.init_rows(spec, torch.zeros(4, spec.PP, dtype=torch.float64), torch.arange(4), 0)
+    for dtype in (torch.bfloat16, torch.float16):
+        spec = ArchSpec.weightwise(2, 2)
+        outs = []
+        for gen in (False, True):
+            _lib.set_force_generic(gen)
+            try:
+                pop = Population(spec, 200, seed=3, dtype=dtype)
+                pop.train(3)
+                pop.self_apply(4)
+                outs.append((pop.W.clone(), pop.count()))
+            finally:
+                _lib.set_force_generic(False)
+        assert torch.equal(outs[0][0].view(torch.int16), outs[1][0].view(torch.int16))
+        assert outs[0][1] == outs[1][1]

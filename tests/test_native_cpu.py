@@ -13,7 +13,12 @@ SPECS = [ArchSpec.weightwise(2, 2), ArchSpec.weightwise(1, 1), ArchSpec.weightwi
          ArchSpec.aggregating(4, 2, 2), ArchSpec.aggregating(4, 2, 2, aggregator="max"),
          ArchSpec.aggregating(4, 2, 2, aggregator="max_ref"), ArchSpec.aggregating(4, 2, 2, shuffler="random"),
          ArchSpec.aggregating(2, 2, 2), ArchSpec.recurrent(2, 2), ArchSpec.recurrent(1, 1), ArchSpec.recurrent(2, 3),
-         ArchSpec.fft(4, 2, 2), ArchSpec.fft(2, 2, 2)]
+         ArchSpec.fft(4, 2, 2), ArchSpec.fft(2, 2, 2),
+         # shapes without a templated kernel: the runtime-shape engine (csrc/srnn_generic.hip);
+         # the reference constructors take any width / depth / aggregates (code/network.py:222-535)
+         ArchSpec.weightwise(3, 3), ArchSpec.weightwise(10, 3), ArchSpec.aggregating(4, 3, 2),
+         ArchSpec.aggregating(4, 10, 2), ArchSpec.aggregating(4, 10, 3), ArchSpec.aggregating(5, 3, 2, shuffler="random"),
+         ArchSpec.recurrent(3, 2), ArchSpec.recurrent(5, 1), ArchSpec.fft(3, 2, 2)]
 IDS = [f"{s.kind}-{s.aggregates}-{s.width}-{s.depth}-{s.aggregator}-{s.shuffler}" for s in SPECS]
 
 
@@ -73,7 +78,9 @@ def test_apply_matches_oracle(spec):
     K.apply(spec, W, out, idx_f=idx_f, uid=uid, seed=5, ctr=11)
     ow = W[:, :spec.P].numpy()
     oo = O.apply(spec, ow[idx_f.numpy()], ow, seed=5, uids=uid.numpy(), ctr=11)
-    assert rowrel(out[:, :spec.P].numpy(), oo) < 1e-5
+    # fma chains vs numpy float32 matmuls: the rounding difference grows with width x depth
+    tol = 1e-5 if spec.width * spec.depth <= 4 else 1e-4
+    assert rowrel(out[:, :spec.P].numpy(), oo) < tol
 
 
 def test_train_epoch_matches_oracle(spec):
@@ -147,7 +154,13 @@ def test_shape_checks_raise_before_launch():
         K.apply(spec, torch.zeros(4, 16), torch.zeros(4, 16), idx_f=torch.tensor([0, 1, 2, 9]))
 
 
-def test_uninstantiated_shape_fails_loudly():
+def test_any_shape_runs_and_bad_layouts_fail_loudly():
+    """Shapes without a templated kernel run on the runtime-shape engine; a table whose
+    layout does not match the architecture is still rejected before any launch."""
     spec = ArchSpec.weightwise(5, 5)
-    with pytest.raises(_lib.NativeLibraryError):
-        K.init_rows(spec, torch.zeros(2, spec.PP), torch.arange(2), 0)
+    W = torch.zeros(2, spec.PP)
+    K.init_rows(spec, W, torch.arange(2), 0)
+    assert torch.isfinite(W).all() and W[:, : spec.P].abs().sum() > 0
+    assert _lib.is_generic(spec, _lib.OP_INIT)
+    with pytest.raises(ValueError):
+        K.init_rows(spec, torch.zeros(2, spec.PP + 4), torch.arange(2), 0)
