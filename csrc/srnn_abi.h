@@ -27,7 +27,8 @@ struct SrnnArgs {
   int32_t early_exit;   // fixpoint run: stop at fixpoint / divergence
   int32_t flags;        // bit0 shuffle, bit1 remove_divergent, bit2 remove_zero, bit3 fix_sec, bit4 per-row respawn flags, bit5 respawn inline, bit6 count respawns in counts[5], bit7 recvbuf is the all-gathered table,
                         // bit8 uid_assign reads the per-rank stats from the exchange's stats rows, bit9 classify advances *gen_ptr,
-                        // bit10 fused generation computes the census
+                        // bit10 fused generation computes the census, bit16 asynchronous finish (OP_SOUP_GEN
+                        // advances the generation counter itself and leaves the finish to OP_GEN_FINISH)
   int32_t gen;          // soup generation (time)
   float eps;
   float lr;
@@ -101,6 +102,8 @@ enum SrnnOp {
   OP_SOUP_UNPACK = 14,  // sharded soup: index the received rows (rmap), reset sendcnt
   OP_SOUP_GEN = 16,     // fused generation: evolve + next decisions + census (+ finish; flag 32768: the
                         // finish launch also packs the next all-to-all = OP_SOUP_PACK)
+  OP_GEN_FINISH = 17,   // single rank, flag 65536: census + newborn uids of the generation whose block
+                        // stats are in temp (the finish half of OP_SOUP_GEN, on a side stream)
   OP_UID_ASSIGN = 15,   // sharded soup: uids of the previous generation's newborns from the per-rank stats
                         // (flag 16384: the same launch also indexes the received rows = OP_SOUP_UNPACK)
 };

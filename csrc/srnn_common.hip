@@ -60,7 +60,7 @@ const char* op_name(int op) {
                                 "srnn:learn",      "srnn:classify",     "srnn:perturb",      "srnn:soup_decide",
                                 "srnn:respawn_seq", "srnn:soup_evolve", "srnn:scan",         "srnn:respawn",
                                 "srnn:vary_run",   "srnn:soup_pack",    "srnn:soup_unpack",  "srnn:uid_assign",
-                                "srnn:soup_gen"};
+                                "srnn:soup_gen",   "srnn:gen_finish"};
   return (op >= 0 && op < (int)(sizeof(names) / sizeof(names[0]))) ? names[op] : "srnn:op";
 }
 }  // namespace

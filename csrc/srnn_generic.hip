@@ -582,7 +582,7 @@ SRNN_HD int8_t g_classify_w(const GCtx& x, const SV& w, float eps, bool with_sec
 // ==================================================================================
 struct GItem {
   SRNN_HD static Rng rng(const SrnnArgs& a) { return Rng{(uint32_t)a.seed, (uint32_t)(a.seed >> 32)}; }
-  SRNN_HD static uint64_t uid_of(const SrnnArgs& a, int64_t i) { return a.uid ? (uint64_t)a.uid[i] : (uint64_t)i; }
+  SRNN_HD static uint64_t uid_of(const SrnnArgs& a, int64_t i) { return a.uid ? (uint64_t)a.uid[i] : (uint64_t)(a.lo + i); }
   SRNN_HD static char* rowp(const GShape& s, float* b, int64_t i) { return reinterpret_cast<char*>(b) + i * g_rb(s); }
   SRNN_HD static const char* rowp(const GShape& s, const float* b, int64_t i) {
     return reinterpret_cast<const char*>(b) + i * g_rb(s);
@@ -766,7 +766,7 @@ struct GItem {
     const int64_t g = a.lo + j;
     SV w = x.v(s.o_w), f = x.v(s.o_t), o = x.v(s.o_o);
     g_load(s, rowp(s, a.W2, j), w);
-    const uint64_t uid = uid_of(a, j);
+    const uint64_t uid = (uint64_t)g;  // stream key of this slot (Item::soup_evolve)
     const int32_t gen = a.gen_ptr ? a.gen_ptr[0] : a.gen;
     ApplyCtx ac = actx(a, s, uid, (uint32_t)gen * 1024u);
     const int32_t head = a.i32e[j];

@@ -235,7 +235,8 @@ struct Item {
     for (int k = 0; k < P; ++k) d[k] = s[k];
   }
   SRNN_HD static Rng rng(const SrnnArgs& a) { return Rng{(uint32_t)a.seed, (uint32_t)(a.seed >> 32)}; }
-  SRNN_HD static uint64_t uid_of(const SrnnArgs& a, int64_t i) { return a.uid ? (uint64_t)a.uid[i] : (uint64_t)i; }
+  // stream key of row i: its uid, or without a uid column its global slot lo + i
+  SRNN_HD static uint64_t uid_of(const SrnnArgs& a, int64_t i) { return a.uid ? (uint64_t)a.uid[i] : (uint64_t)(a.lo + i); }
   SRNN_HD static ApplyCtx actx(const SrnnArgs& a, const SrnnCfg& c, uint64_t uid, uint32_t ctr, uint8_t* perm) {
     ApplyCtx x;
     x.rng = rng(a);
@@ -477,12 +478,15 @@ struct Item {
   }
 
   // Synchronous (Jacobi) generation for local row j: every read is from the
-  // generation-start table W2 (global rows), the result goes to W (local rows).
+  // generation-start table W2 (global rows), the result goes to W (local rows).  The
+  // particle's random streams (SGD shuffles, shuffle_random) are keyed by its global SLOT
+  // and the generation -- not by its uid -- so a generation never waits for the uids of
+  // the previous generation's newborns (their uid assignment overlaps the next generation).
   SRNN_HD static void soup_evolve(const SrnnCfg& c, const SrnnArgs& a, int64_t j, float4* samp, uint8_t* perm) {
     const int64_t g = a.lo + j;
     float w[P], f[P], o[P];
     load(rowp(a.W2, j), w);
-    const uint64_t uid = uid_of(a, j);
+    const uint64_t uid = (uint64_t)g;  // stream key of this slot
     const int32_t gen = gen_of(a);
     ApplyCtx x = actx(a, c, uid, (uint32_t)gen * 1024u, perm);
     // 1. attacks received, in ascending attacker slot order (the list is in arrival order)
@@ -690,8 +694,14 @@ __global__ __launch_bounds__(TB) void k_soup_gen(SrnnCfg c, SrnnArgs a) {
     if (census) {
       float w[P];
       I::load(I::rowp(a.W, i), w);
-      k = I::classify_w(w, a.eps, (a.flags & 8) != 0, I::actx(a, c, I::uid_of(a, i), 0x7FFFFFF0u, perm));
+      k = I::classify_w(w, a.eps, (a.flags & 8) != 0, I::actx(a, c, (uint64_t)(a.lo + i), 0x7FFFFFF0u, perm));
     }
+  }
+  if ((a.flags & 65536) && blockIdx.x == 0 && threadIdx.x == 0) {
+    // asynchronous finish: this launch advances the generation counter (the other ring
+    // slot: no block of this launch reads it) so the next generation needs nothing from
+    // the finish kernel, which runs beside it on a side stream
+    I::set_gen(a, gen + 1);
   }
   const unsigned long long m = __ballot(rs);
   uint32_t cnt[5];
@@ -836,7 +846,8 @@ __global__ __launch_bounds__(NT) void k_gen_finish(SrnnArgs a, int32_t nb) {
   // the uid base and the generation counter are only written by thread 0 after the last
   // barrier: load them up front so their latency overlaps the per-block stats loads
   const int64_t base = *(volatile const int64_t*)a.uid_base;
-  const int32_t gen = I::gen_of(a);
+  const bool async = (a.flags & 65536) != 0;  // the generation kernel advanced the counter
+  const int32_t gen = async ? 0 : I::gen_of(a);
   const int32_t ch = (nb + NT - 1) / NT;
   const int32_t b0 = t * ch, b1 = b0 + ch < nb ? b0 + ch : nb;
   int32_t born = 0;
@@ -872,13 +883,31 @@ __global__ __launch_bounds__(NT) void k_gen_finish(SrnnArgs a, int32_t nb) {
   if (t == 0) {
     const int32_t total = total_born;
     if (!sharded) ((int64_t*)a.uid_base)[0] = base + total;
-    I::set_gen(a, gen + 1);
+    if (!async) I::set_gen(a, gen + 1);
     if (a.counts) {
       for (int q = 0; q < 5; ++q) a.counts[q] = (a.flags & 1024) ? s_cs[q] : 0ull;
       a.counts[5] = (uint64_t)total;
     }
     if (a.flags & 32768) I::pack_stats(a);  // this generation's stats ride on the next exchange
   }
+}
+
+// Asynchronous finish of a single-rank fused generation (OP_GEN_FINISH, flag 65536): the
+// census reduction + uids of the generation whose block stats are in a.temp, launched on a
+// side stream after that generation and beside the next one (host: no-op, soup_gen did it).
+template <class Net, class S>
+int gen_finish(const SrnnCfg&, const SrnnArgs& a) {
+  if (!a.dev) return 0;
+  const int64_t blocks = (a.n + TB - 1) / TB;
+  if (blocks <= 0) return 0;
+  constexpr int FNT = SRNN_FINISH_NT;
+  hipLaunchKernelGGL((k_gen_finish<Net, S, FNT>), dim3(1), dim3(FNT), 0, (hipStream_t)a.stream, a, (int32_t)blocks);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) {
+    set_error(hipGetErrorString(e));
+    return -3;
+  }
+  return 0;
 }
 
 template <class Net, class S>
@@ -915,7 +944,7 @@ int soup_gen(const SrnnCfg& c, const SrnnArgs& a) {
         float w[Net::P];
         uint8_t perm[Net::P + 4];
         I::load(I::rowp(a.W, i), w);
-        ks[(size_t)i] = I::classify_w(w, a.eps, (a.flags & 8) != 0, I::actx(a, c, I::uid_of(a, i), 0x7FFFFFF0u, perm));
+        ks[(size_t)i] = I::classify_w(w, a.eps, (a.flags & 8) != 0, I::actx(a, c, (uint64_t)(a.lo + i), 0x7FFFFFF0u, perm));
       });
       for (int64_t i = 0; i < a.n; ++i) cs[ks[(size_t)i]]++;
     }
@@ -959,7 +988,7 @@ int soup_gen(const SrnnCfg& c, const SrnnArgs& a) {
     return -2;
   }
   hipLaunchKernelGGL((k_soup_gen<Net, S>), dim3((unsigned)blocks), dim3(TB), 0, (hipStream_t)a.stream, c, a);
-  if (a.flags & 2048) {
+  if ((a.flags & 2048) && !(a.flags & 65536)) {
     constexpr int FNT = SRNN_FINISH_NT;
     const int64_t pack_blocks = (a.flags & 32768) ? (a.n + FNT - 1) / FNT : 0;
     hipLaunchKernelGGL((k_gen_finish<Net, S, FNT>), dim3((unsigned)(1 + pack_blocks)), dim3(FNT), 0,
@@ -1396,6 +1425,7 @@ int run_net_op(int op, const SrnnCfg& c, const SrnnArgs& a) {
     case OP_RESPAWN: return run_one<Net, OP_RESPAWN, S>(c, a);
     case OP_VARY_RUN: return run_one<Net, OP_VARY_RUN, S>(c, a);
     case OP_SOUP_GEN: return soup_gen<Net, S>(c, a);
+    case OP_GEN_FINISH: return gen_finish<Net, S>(c, a);
     default: set_error("unknown op"); return -1;
   }
 }

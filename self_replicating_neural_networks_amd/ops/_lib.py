@@ -39,6 +39,7 @@ OP_SOUP_PACK = 13
 OP_SOUP_UNPACK = 14
 OP_UID_ASSIGN = 15
 OP_SOUP_GEN = 16
+OP_GEN_FINISH = 17
 
 FLAG_SHUFFLE = 1
 FLAG_REMOVE_DIVERGENT = 2
@@ -56,6 +57,7 @@ FLAG_SHARDED_DECIDE = 4096
 FLAG_MASKS_BS = 8192
 FLAG_POST_UNPACK = 16384
 FLAG_FINISH_PACK = 32768
+FLAG_ASYNC_FINISH = 65536
 
 
 class SrnnCfg(ctypes.Structure):

@@ -214,7 +214,7 @@ def learn_from(spec, W: torch.Tensor, teachers: torch.Tensor, idx_t=None, epochs
 
 
 def classify(spec, W: torch.Tensor, eps: float, with_sec: bool = True, uid=None, seed=0, ctr=0,
-             counts: Optional[torch.Tensor] = None, scratch: Optional[torch.Tensor] = None):
+             counts: Optional[torch.Tensor] = None, scratch: Optional[torch.Tensor] = None, key_offset: int = 0):
     """Per-row class (0 divergent, 1 fix_zero, 2 fix_other, 3 fix_sec, 4 other) and the
     5-bin histogram (reference code/experiment.py:79-91, code/soup.py:89-103)."""
     dt = _check_table(spec, W)
@@ -224,6 +224,7 @@ def classify(spec, W: torch.Tensor, eps: float, with_sec: bool = True, uid=None,
         counts = torch.zeros(5, dtype=torch.int64, device=W.device)
     a = _base_args(W, seed, ctr, scratch)
     a.n, a.eps = n, float(eps)
+    a.lo = int(key_offset)  # without uids, row i's random streams are keyed by key_offset + i
     a.flags = _lib.FLAG_FIX_SEC if with_sec else 0
     a.W, a.cls, a.counts = _p(W), _p(cls), _p(counts)
     a.uid = _p(_uid(uid, n, W.device))

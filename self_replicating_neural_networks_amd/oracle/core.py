@@ -447,7 +447,9 @@ def soup_decisions(seed, gen, n_total, attacking_rate, learn_from_rate, segment=
 
 def soup_generation_sync(spec, W0, uids, gen, seed, params, lr=0.01, shuffle=True):
     """Synchronous (Jacobi) soup generation — the semantics of the fused kernel
-    (csrc Item::soup_evolve).  Returns (W1, action, counterpart, loss, respawn)."""
+    (csrc Item::soup_evolve).  ``uids`` are the random-stream keys of the slots: the engine
+    keys soup streams by global slot (``np.arange(n)``).  Returns (W1, action, counterpart,
+    loss, respawn)."""
     n = W0.shape[0]
     att, te = soup_decisions(seed, gen, n, params["attacking_rate"], params["learn_from_rate"],
                              int(params.get("segment", 0)))

@@ -175,6 +175,14 @@ class SoupEngine:
         self.two_phase = os.environ.get("SRNN_GEN_TWO_PHASE", "1") == "1"  # + a 1-workgroup finish kernel
         nb = -(-self.n // 64)
         self._blockstat = torch.zeros(max(nb, 1) * 8, **i32)
+        # single rank on a GPU: the finish kernel of generation g (census reduction + uids
+        # of its newborns) runs on a side stream beside generation g + 1; the block stats
+        # it reads are double-buffered by ping-pong parity (SRNN_ASYNC_FINISH=0: serial)
+        self.async_finish = (self.device.type == "cuda" and not self.dist.enabled and self.fused
+                             and os.environ.get("SRNN_ASYNC_FINISH", "1") == "1")
+        self._blockstats = [self._blockstat, torch.zeros_like(self._blockstat)] if self.async_finish else None
+        self._side = torch.cuda.Stream(self.device) if self.async_finish else None
+        self._fin_ev = [None, None]  # finish events of the generations that wrote each block-stats buffer
         self._done = torch.zeros(1, **i32)
         # per-row respawn flags (host) or 64-bit respawn ballots per 64-row wave (device)
         self.flags32 = torch.zeros(max(self.n, 2 * (-(-self.n // 64))), **i32)
@@ -300,7 +308,7 @@ class SoupEngine:
         params: building ctypes structs every generation costs host time)."""
         stream = torch.cuda.current_stream(self.device).cuda_stream if self.device.type == "cuda" else 0
         key = (self._p, stream, tuple(sorted((k, str(v)) for k, v in self.params.items())), self.stats_with_sec,
-               self.lr, self.shuffle, self.stats, self.two_phase)
+               self.lr, self.shuffle, self.stats, self.two_phase, self.async_finish)
         hit = self._arg_cache.get(key)
         if hit is not None:
             return hit
@@ -329,7 +337,7 @@ class SoupEngine:
             ca.n, ca.eps = self.n, self.eps
             ca.flags = ((_lib.FLAG_FIX_SEC if self.stats_with_sec else 0) | _lib.FLAG_COUNT_RESPAWNS
                         | _lib.FLAG_GEN_ADVANCE)
-            ca.W, ca.counts, ca.respawn, ca.uid = _p(self.rows_out), _p(self.counts), _p(self.respawn), _p(self.uid)
+            ca.W, ca.counts, ca.respawn, ca.uid = _p(self.rows_out), _p(self.counts), _p(self.respawn), None
             ca.ctr = 0x7FFFFFF0
         if not self.dist.enabled or self.exchange == "alltoall":
             # fused generation: next generation's lists, block stats, done counter, census
@@ -340,6 +348,10 @@ class SoupEngine:
             fa.temp, fa.temp_bytes = _p(self._blockstat), self._blockstat.numel() * 4
             fa.i32d = _p(self._done)
             fa.flags = a.flags | _lib.FLAG_RESPAWN_INLINE | (_lib.FLAG_TWO_PHASE if self.two_phase else 0)
+            if self.async_finish:
+                bs = self._blockstats[self._p]
+                fa.temp, fa.temp_bytes = _p(bs), bs.numel() * 4
+                fa.flags |= _lib.FLAG_TWO_PHASE | _lib.FLAG_ASYNC_FINISH
             census = self.stats and self.spec.shuffler == "none"
             if self.dist.enabled:
                 # sharded: every global slot's next decisions; counts feed the next pack
@@ -350,6 +362,11 @@ class SoupEngine:
             if self.dist.enabled:
                 self._fused_census = census
                 ca = (ca, fa)
+            elif self.async_finish:
+                fin = self._args()
+                ctypes.pointer(fin)[0] = fa
+                fin.stream = ctypes.c_void_p(self._side.cuda_stream)
+                ca = (fa, fin)
             else:
                 ca = fa
         self._arg_cache[key] = (a, ca, a.flags)
@@ -370,6 +387,23 @@ class SoupEngine:
                 # ONE launch: evolve + next generation's attack lists + census + uids
                 if not self._lists_ready:
                     _lib.run(_lib.OP_SOUP_DECIDE, spec, a, cfg)
+                if self.async_finish:
+                    # generation on the main stream; its finish on the side stream, beside
+                    # the next generation (which only needs the counter it advances itself)
+                    fa, fin = ca
+                    main = torch.cuda.current_stream(self.device)
+                    ev = self._fin_ev[self._p]
+                    if ev is not None:  # this parity's block stats are free again
+                        main.wait_event(ev)
+                    _lib.run(_lib.OP_SOUP_GEN, spec, fa, cfg)
+                    self._side.wait_stream(main)
+                    _lib.run(_lib.OP_GEN_FINISH, spec, fin, cfg)
+                    ev = torch.cuda.Event()
+                    ev.record(self._side)
+                    self._fin_ev[self._p] = ev
+                    self._lists_ready = True
+                    self._p = 1 - self._p
+                    return
                 _lib.run(_lib.OP_SOUP_GEN, spec, ca, cfg)
                 self._lists_ready = True
                 self._p = 1 - self._p
@@ -461,6 +495,13 @@ class SoupEngine:
         else:
             self._pending = True
 
+    def _join_side(self):
+        """Make the current stream wait for the side-stream finish kernels (uids, census,
+        next_uid are final after this)."""
+        if self._side is not None and any(e is not None for e in self._fin_ev):
+            torch.cuda.current_stream(self.device).wait_stream(self._side)
+            self._fin_ev = [None, None]
+
     def _flush(self):
         """Sharded: assign the uids of the last generation's newborns now (all-gather of
         the per-rank stats) instead of with the next generation's row exchange."""
@@ -483,9 +524,9 @@ class SoupEngine:
     def classify_local(self, with_sec: bool = True, zero: bool = True):
         if zero:
             self.counts.zero_()
-        cls, _ = K.classify(self.spec, self.local_rows(), self.eps, with_sec, uid=self.uid, seed=self.seed,
-                            scratch=self._scratch,
-                            ctr=0x7FFFFFF0, counts=self.counts)
+        # census streams (shuffle_random nets) keyed by global slot, like the fused census
+        cls, _ = K.classify(self.spec, self.local_rows(), self.eps, with_sec, uid=None, seed=self.seed,
+                            scratch=self._scratch, ctr=0x7FFFFFF0, counts=self.counts, key_offset=self.lo)
         return cls
 
     def count(self, with_sec: bool = True) -> Dict[str, int]:
@@ -509,6 +550,7 @@ class SoupEngine:
             if (ch is not None and not (record and self.recorder is not None) and left >= ch[2]
                     and self._p == ch[1] and self.trajectory is None and self.metrics is None):
                 # G generations in one graph launch (no inter-graph gaps)
+                self._join_side()
                 ch[0].replay()
                 self.time += ch[2]
                 left -= ch[2]
@@ -517,17 +559,20 @@ class SoupEngine:
             left -= 1
             self.time += 1
             if record and self.recorder is not None:
+                self._join_side()
                 slot_uid = self.global_uids()  # uid of every slot at generation start
                 self._generation(record=True)
                 self._flush()
                 self.recorder.on_generation_end(self, self.time, slot_uid)
             elif self._graphs is not None:
+                self._join_side()
                 self._graphs[self._p].replay()
                 self._p = 1 - self._p
                 self._pending = self.dist.enabled
             else:
                 self._generation()
             self._hooks()
+        self._join_side()
         self._flush()  # uids / census consistent between evolve calls
         if self.dist.native is not None:
             self.dist.native.check()  # RCCL asynchronous errors (peer failure) surface here
@@ -536,6 +581,8 @@ class SoupEngine:
     def _hooks(self):
         """Per-generation observers (host work only when one is due)."""
         t = self.time
+        if (self.trajectory is not None and self.trajectory.due(t)) or (self.metrics is not None and self.metrics.due(t)):
+            self._join_side()
         if self.trajectory is not None and self.trajectory.due(t):
             self._flush()
             self.trajectory.snapshot(self, t)
@@ -572,7 +619,7 @@ class SoupEngine:
         """Every device tensor a generation reads or writes (graph validation)."""
         names = ["_bufs", "uid", "next_uid", "_gen_ring", "heads", "nexts", "flags32", "action", "counterpart",
                  "loss", "respawn", "counts", "census", "need", "sendcnt", "rmap", "ovf", "sendbuf", "recvbuf",
-                 "full", "stats_all", "_blockstat", "_done"]
+                 "full", "stats_all", "_blockstats" if self._blockstats else "_blockstat", "_done"]
         out = []
         for k in names:
             v = getattr(self, k, None)
@@ -610,6 +657,7 @@ class SoupEngine:
             for _ in range(max(warmup, 1 if (self.dist.enabled or self.fused) else 0)):
                 self.time += 1
                 self._generation()
+            self._join_side()
         torch.cuda.current_stream(self.device).wait_stream(s)
         graphs = []
         p0 = self._p
@@ -621,6 +669,7 @@ class SoupEngine:
                 # thread_local: the process group's watchdog thread keeps querying events
                 with torch.cuda.graph(g, stream=s, capture_error_mode="thread_local"):
                     self._generation()  # flips self._p during capture (nothing ran)
+                    self._join_side()   # the side-stream finish joins inside the graph
                 graphs.append(g)
         except Exception as e:  # noqa: BLE001 -- any capture failure -> eager generations
             import sys
@@ -657,6 +706,7 @@ class SoupEngine:
             with torch.cuda.graph(gc, stream=s, capture_error_mode="thread_local"):
                 for _ in range(G):
                     self._generation()
+                self._join_side()
         except Exception as e:  # noqa: BLE001
             import sys
             print(f"multi-generation graph capture failed ({type(e).__name__}: {e})", file=sys.stderr)
@@ -698,6 +748,7 @@ class SoupEngine:
         flags0 = (self._lists_ready, self._mask_src, self._packed)
         for _ in range(gens):
             self._generation()
+        self._join_side()
         torch.cuda.synchronize(self.device)
         flags1 = (self._lists_ready, self._mask_src, self._packed)
         eager = [t.clone() for t in state]

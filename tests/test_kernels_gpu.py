@@ -97,7 +97,7 @@ def test_soup_engine_gpu_vs_oracle(cuda):
                   epsilon=1e-4)
     e = SoupEngine(spec, 3000, params, device=cuda, seed=7)
     W0 = e.local_rows()[:, :spec.P].cpu().numpy().copy()
-    uids = e.uid.cpu().numpy().astype(np.uint64)
+    uids = np.arange(3000, dtype=np.uint64)  # soup streams are keyed by slot, not uid
     e.evolve(1)
     W1, act, cp, loss, resp = O.soup_generation_sync(spec, W0, uids, 1, 7, params)
     keep = resp == 0

@@ -24,7 +24,7 @@ def test_engine_generation_matches_oracle(spec):
     e = SoupEngine(spec, 400, PARAMS, seed=11)
     for g in range(3):
         W0 = e.local_rows()[:, :spec.P].numpy().copy()
-        uids = e.uid.numpy().astype(np.uint64).copy()
+        uids = np.arange(400, dtype=np.uint64)  # soup streams are keyed by slot, not uid
         e.evolve(1)
         W1, act, cp, loss, resp = O.soup_generation_sync(spec, W0, uids, g + 1, 11, PARAMS)
         keep = resp == 0
