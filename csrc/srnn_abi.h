@@ -28,7 +28,8 @@ struct SrnnArgs {
   int32_t flags;        // bit0 shuffle, bit1 remove_divergent, bit2 remove_zero, bit3 fix_sec, bit4 per-row respawn flags, bit5 respawn inline, bit6 count respawns in counts[5], bit7 recvbuf is the all-gathered table,
                         // bit8 uid_assign reads the per-rank stats from the exchange's stats rows, bit9 classify advances *gen_ptr,
                         // bit10 fused generation computes the census, bit16 asynchronous finish (OP_SOUP_GEN
-                        // advances the generation counter itself and leaves the finish to OP_GEN_FINISH)
+                        // advances the generation counter itself and leaves the finish to OP_GEN_FINISH),
+                        // bit17 precomputed SGD permutations (perm_cur / perm_next, helper waves)
   int32_t gen;          // soup generation (time)
   float eps;
   float lr;
@@ -82,6 +83,15 @@ struct SrnnArgs {
                         // so a kernel can advance the counter while its other blocks still read it.
   void* scratch;        // generic (runtime-shape) engine: per-lane vectors, element-major; null ->
   int64_t scratch_bytes;  // the library's own cached device buffer (not inside a graph capture)
+  // fused single-rank generation with precomputed shuffles (flag 131072): the SGD
+  // permutations of generation gen are in perm_cur[k][n] (k < perm_e: learn epochs then
+  // train epochs), helper waves fill perm_next for gen + 1; helper_ctl = work-queue head +
+  // per-SIMD main-wave counts of this parity (re-armed by the finish kernel)
+  uint64_t* perm_cur;
+  uint64_t* perm_next;
+  int32_t* helper_ctl;
+  int32_t perm_e;
+  int32_t helpers;      // helper workgroups appended to the generation grid
 };
 
 enum SrnnOp {
@@ -102,13 +112,14 @@ enum SrnnOp {
   OP_SOUP_UNPACK = 14,  // sharded soup: index the received rows (rmap), reset sendcnt
   OP_SOUP_GEN = 16,     // fused generation: evolve + next decisions + census (+ finish; flag 32768: the
                         // finish launch also packs the next all-to-all = OP_SOUP_PACK)
+  OP_SOUP_PERMS = 18,   // fill perm_next with the SGD permutations of generation *gen_ptr (first generation)
   OP_GEN_FINISH = 17,   // single rank, flag 65536: census + newborn uids of the generation whose block
                         // stats are in temp (the finish half of OP_SOUP_GEN, on a side stream)
   OP_UID_ASSIGN = 15,   // sharded soup: uids of the previous generation's newborns from the per-rank stats
                         // (flag 16384: the same launch also indexes the received rows = OP_SOUP_UNPACK)
 };
 
-int srnn_abi_version();  // 12
+int srnn_abi_version();  // 13
 int srnn_has_config(const SrnnCfg* cfg);
 int srnn_run(int op, const SrnnCfg* cfg, const SrnnArgs* args);
 const char* srnn_last_error();

@@ -60,7 +60,7 @@ const char* op_name(int op) {
                                 "srnn:learn",      "srnn:classify",     "srnn:perturb",      "srnn:soup_decide",
                                 "srnn:respawn_seq", "srnn:soup_evolve", "srnn:scan",         "srnn:respawn",
                                 "srnn:vary_run",   "srnn:soup_pack",    "srnn:soup_unpack",  "srnn:uid_assign",
-                                "srnn:soup_gen",   "srnn:gen_finish"};
+                                "srnn:soup_gen",   "srnn:gen_finish",   "srnn:soup_perms"};
   return (op >= 0 && op < (int)(sizeof(names) / sizeof(names[0]))) ? names[op] : "srnn:op";
 }
 }  // namespace
@@ -177,7 +177,7 @@ static int with_scratch(int op, const SrnnCfg* c, const SrnnArgs* a) {
 
 extern "C" {
 
-int srnn_abi_version() { return 12; }
+int srnn_abi_version() { return 13; }
 
 const char* srnn_last_error() { return srnn::g_err.c_str(); }
 

@@ -388,6 +388,13 @@ struct TrainCtx {
   bool shuffle;
   int stride;        // device: threads per block (slot-major, lane fastest: conflict-free b128)
   int aggregator;    // aggregating nets: samples come from the configured aggregator
+  // precomputed nibble permutations (P <= 16 nets in a fused soup generation): the
+  // permutation of epoch counter ctr is pre[(ctr - pre_ctr0) * pre_stride], k < pre_n;
+  // null -> computed here (Philox + Fisher-Yates).  Same values either way.
+  const unsigned long long* pre = nullptr;
+  int64_t pre_stride = 0;
+  uint32_t pre_ctr0 = 0;
+  int32_t pre_n = 0;
 };
 
 struct ApplyCtx {
@@ -498,11 +505,45 @@ struct Weightwise {
       uint64_t ident = 0;
 #pragma unroll
       for (int k = 0; k < P; ++k) ident |= (uint64_t)k << (4 * k);
+      float loss = 0.f;
+      if (c.shuffle && c.pre) {
+        // permutations precomputed by the soup generation's helper waves: one 8-byte load
+        // per epoch, issued an epoch ahead (no Philox / Fisher-Yates on this lane)
+        auto pre_at = [&](uint32_t ctr) {
+          int32_t k = (int32_t)(ctr - c.pre_ctr0);
+          k = k < c.pre_n - 1 ? k : c.pre_n - 1;
+          return (uint64_t)c.pre[(int64_t)k * c.pre_stride];
+        };
+        uint64_t pn = pre_at(c.ctr);
+        for (int e = 0; e < E; ++e) {
+          if (SELF && e > 0)
+#pragma unroll
+            for (int k = 0; k < P; ++k) reinterpret_cast<float*>(&c.samp[k * c.stride])[0] = w[k];
+          const uint64_t pn_next = pre_at(c.ctr + 1u);
+          float4 smp[P];
+#pragma unroll
+          for (int q = 0; q < P; ++q) smp[q] = c.samp[(int)((pn >> (4 * q)) & 15u) * c.stride];
+          float acc = 0.f;
+#pragma unroll
+          for (int q = 0; q < P; ++q) {
+            float x[4] = {smp[q].x, smp[q].y, smp[q].z, smp[q].w};
+            float acts[Net::NACT], y[1];
+            Net::forward(w, x, acts, y);
+            float err = y[0] - smp[q].x;
+            acc += err * err;
+            float gy[1] = {2.0f * err};
+            Net::backward_update(w, acts, gy, c.lr);
+          }
+          loss = acc / (float)P;
+          c.ctr += 1;
+          pn = pn_next;
+        }
+        return loss;
+      }
       // one Philox draw per pair of epochs (c.ctr is the same for every lane: uniform branch)
       U4 rr = perm_draw(c.rng, c.uid, c.ctr, P_SHUFFLE);
       uint32_t pair = c.ctr >> 1;
       uint64_t pn = c.shuffle ? perm_from_bits<P>(perm_bits(rr, c.ctr)) : ident;
-      float loss = 0.f;
       for (int e = 0; e < E; ++e) {
         if (SELF && e > 0)
 #pragma unroll

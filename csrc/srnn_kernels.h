@@ -522,6 +522,12 @@ struct Item {
     tc.shuffle = (a.flags & 1) != 0;
     tc.stride = SAMP_STRIDE;
     tc.aggregator = c.aggregator;
+    if ((a.flags & 131072) && a.perm_cur) {  // SGD permutations precomputed by helper waves
+      tc.pre = reinterpret_cast<const unsigned long long*>(a.perm_cur) + j;
+      tc.pre_stride = a.n;
+      tc.pre_ctr0 = (uint32_t)gen * 1024u + 512u;
+      tc.pre_n = a.perm_e;
+    }
     float loss = 0.f;
     // 2. learn_from a teacher (its generation-start weights)
     if (te >= 0) {
@@ -574,7 +580,54 @@ struct Item {
     Net::init(w, rng(a), respawn_key(gen_of(a), a.lo + j));
     store(rowp(a.W, j), w);
   }
+
+  // SGD permutations of local row j for generation `gen` (epoch counters gen*1024+512+k,
+  // k < perm_e, keyed by the slot): exactly what train_epochs would draw, into
+  // out[k * n + j] (k-major: the lanes of a wave write consecutive words)
+  SRNN_HD static void perm_fill(const SrnnArgs& a, int64_t j, int32_t gen, uint64_t* out) {
+    if constexpr (Net::KIND == 0 && P <= 16) {
+      const uint64_t key = (uint64_t)(a.lo + j);
+      const uint32_t c0 = (uint32_t)gen * 1024u + 512u;  // even: epochs (k, k+1) share a draw
+      const Rng r = rng(a);
+      for (int32_t k = 0; k < a.perm_e; k += 2) {
+        const U4 d = perm_draw(r, key, c0 + (uint32_t)k, P_SHUFFLE);
+        out[(int64_t)k * a.n + j] = perm_from_bits<P>(perm_bits(d, c0 + (uint32_t)k));
+        if (k + 1 < a.perm_e) out[(int64_t)(k + 1) * a.n + j] = perm_from_bits<P>(perm_bits(d, c0 + (uint32_t)k + 1u));
+      }
+    }
+  }
 };
+
+// ----------------------------------------------------------------------------------
+// Helper waves of the fused generation (flag 131072).  At ~1.5 waves per SIMD the SIMDs
+// carrying two generation waves are issue-saturated while the others run one wave at half
+// issue rate.  The next generation's SGD permutations (the Philox + Fisher-Yates integer
+// work, ~30 % of an epoch's instructions) are computed by extra workgroups that keep
+// going only on SIMDs holding fewer than two generation waves, pulling 64-slot chunks from
+// a work queue; generation waves drain whatever is left when they finish, so the queue
+// always empties inside the launch.  Placement only affects speed, never the result.
+// ----------------------------------------------------------------------------------
+__device__ __forceinline__ int simd_slot() {
+  const uint32_t hw = __builtin_amdgcn_s_getreg((31 << 11) | 4);  // HW_REG_HW_ID
+  const uint32_t xcc = __builtin_amdgcn_s_getreg((3 << 11) | 20);  // HW_REG_XCC_ID[3:0]
+  const uint32_t simd = (hw >> 4) & 3u, cu = (hw >> 8) & 15u, sh = (hw >> 12) & 1u, se = (hw >> 13) & 7u;
+  return (int)((((((xcc & 7u) * 8u + se) * 2u + sh) * 16u + cu) * 4u) + simd);  // < 8192
+}
+constexpr int HELPER_CTL = 1 + 8192;  // queue head + per-SIMD generation-wave counts
+
+template <class Net, class S>
+__device__ void perm_drain(const SrnnArgs& a, int32_t gen_next) {
+  using I = Item<Net, S>;
+  const int64_t nch = (a.n + TB - 1) / TB;
+  for (;;) {
+    int32_t ch = 0;
+    if (threadIdx.x == 0) ch = atomicAdd(a.helper_ctl, 1);
+    ch = __shfl(ch, 0);
+    if ((int64_t)ch >= nch) break;
+    const int64_t j = (int64_t)ch * TB + threadIdx.x;
+    if (j < a.n) I::perm_fill(a, j, gen_next, a.perm_next);
+  }
+}
 
 // ==================================================================================
 // Device kernels
@@ -673,6 +726,19 @@ __global__ __launch_bounds__(TB) void k_soup_gen(SrnnCfg c, SrnnArgs a) {
   uint8_t* perm = s_perm + lane * PERM;
   const int32_t gen = I::gen_of(a);
   const bool census = (a.flags & 1024) != 0;
+  const bool pre = (a.flags & 131072) != 0;
+  if (pre) {
+    const int64_t nb_main = (a.n + TB - 1) / TB;
+    if ((int64_t)blockIdx.x >= nb_main) {
+      // helper workgroup: work only where fewer than two generation waves share the SIMD
+      int32_t cnt = 0;
+      if (lane == 0) cnt = __hip_atomic_load(a.helper_ctl + 1 + simd_slot(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      cnt = __shfl(cnt, 0);
+      if (cnt < 2) perm_drain<Net, S>(a, gen + 1);
+      return;
+    }
+    if (lane == 0) atomicAdd(a.helper_ctl + 1 + simd_slot(), 1);
+  }
   bool rs = false;
   int8_t k = -1;
   if (i < a.n) {
@@ -721,6 +787,7 @@ __global__ __launch_bounds__(TB) void k_soup_gen(SrnnCfg c, SrnnArgs a) {
       mine[2] = (unsigned long long)cnt[2] | ((unsigned long long)cnt[3] << 32);
       mine[3] = (unsigned long long)cnt[4];
     }
+    if (pre) perm_drain<Net, S>(a, gen + 1);  // whatever the helpers left
     return;
   }
   int32_t prev = 0;
@@ -842,6 +909,8 @@ __global__ __launch_bounds__(NT) void k_gen_finish(SrnnArgs a, int32_t nb) {
   __shared__ unsigned long long s_cs[5];
   const int t = threadIdx.x;
   if (t < 5) s_cs[t] = 0;
+  if ((a.flags & 131072) && a.helper_ctl)  // re-arm this parity's helper queue / SIMD counts
+    for (int q = t; q < HELPER_CTL; q += NT) a.helper_ctl[q] = 0;
   const unsigned long long* bs = reinterpret_cast<const unsigned long long*>(a.temp);
   // the uid base and the generation counter are only written by thread 0 after the last
   // barrier: load them up front so their latency overlaps the per-block stats loads
@@ -890,6 +959,36 @@ __global__ __launch_bounds__(NT) void k_gen_finish(SrnnArgs a, int32_t nb) {
     }
     if (a.flags & 32768) I::pack_stats(a);  // this generation's stats ride on the next exchange
   }
+}
+
+// SGD permutations of generation *gen_ptr for every local row into perm_next (OP_SOUP_PERMS:
+// the first precomputed generation; later ones come from the helper waves)
+template <class Net, class S>
+__global__ __launch_bounds__(256) void k_soup_perms(SrnnArgs a) {
+  using I = Item<Net, S>;
+  const int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (j < a.n) I::perm_fill(a, j, I::gen_of(a), a.perm_next);
+}
+template <class Net, class S>
+int soup_perms(const SrnnCfg&, const SrnnArgs& a) {
+  using I = Item<Net, S>;
+  if (!(Net::KIND == 0 && Net::P <= 16)) return 0;  // no per-epoch permutations to precompute
+  if (!a.perm_next || a.perm_e < 1) {
+    set_error("soup_perms needs perm_next and perm_e >= 1");
+    return -5;
+  }
+  if (!a.dev) {
+    for (int64_t j = 0; j < a.n; ++j) I::perm_fill(a, j, I::gen_of(a), a.perm_next);
+    return 0;
+  }
+  if (a.n <= 0) return 0;
+  hipLaunchKernelGGL((k_soup_perms<Net, S>), dim3((unsigned)((a.n + 255) / 256)), dim3(256), 0, (hipStream_t)a.stream, a);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) {
+    set_error(hipGetErrorString(e));
+    return -3;
+  }
+  return 0;
 }
 
 // Asynchronous finish of a single-rank fused generation (OP_GEN_FINISH, flag 65536): the
@@ -987,7 +1086,12 @@ int soup_gen(const SrnnCfg& c, const SrnnArgs& a) {
     set_error("grid too large");
     return -2;
   }
-  hipLaunchKernelGGL((k_soup_gen<Net, S>), dim3((unsigned)blocks), dim3(TB), 0, (hipStream_t)a.stream, c, a);
+  const int64_t helpers = (a.flags & 131072) ? (a.helpers > 0 ? a.helpers : 0) : 0;
+  if ((a.flags & 131072) && (!a.perm_cur || !a.perm_next || !a.helper_ctl || !(a.flags & 2048) || a.perm_e < 1)) {
+    set_error("precomputed permutations need perm_cur / perm_next / helper_ctl, perm_e >= 1 and a two-phase generation");
+    return -5;
+  }
+  hipLaunchKernelGGL((k_soup_gen<Net, S>), dim3((unsigned)(blocks + helpers)), dim3(TB), 0, (hipStream_t)a.stream, c, a);
   if ((a.flags & 2048) && !(a.flags & 65536)) {
     constexpr int FNT = SRNN_FINISH_NT;
     const int64_t pack_blocks = (a.flags & 32768) ? (a.n + FNT - 1) / FNT : 0;
@@ -1426,6 +1530,7 @@ int run_net_op(int op, const SrnnCfg& c, const SrnnArgs& a) {
     case OP_VARY_RUN: return run_one<Net, OP_VARY_RUN, S>(c, a);
     case OP_SOUP_GEN: return soup_gen<Net, S>(c, a);
     case OP_GEN_FINISH: return gen_finish<Net, S>(c, a);
+    case OP_SOUP_PERMS: return soup_perms<Net, S>(c, a);
     default: set_error("unknown op"); return -1;
   }
 }

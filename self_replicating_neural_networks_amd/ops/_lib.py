@@ -20,7 +20,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 # SRNN_LIB: load another build of the library (A/B of compiler flags on the GPU box)
 LIB_PATH = os.environ.get("SRNN_LIB") or os.path.join(_HERE, "libsrnn.so")
 CSRC = os.path.normpath(os.path.join(_HERE, "..", "..", "csrc"))
-ABI_VERSION = 12
+ABI_VERSION = 13
 
 OP_INIT = 0
 OP_APPLY = 1
@@ -40,6 +40,7 @@ OP_SOUP_UNPACK = 14
 OP_UID_ASSIGN = 15
 OP_SOUP_GEN = 16
 OP_GEN_FINISH = 17
+OP_SOUP_PERMS = 18
 
 FLAG_SHUFFLE = 1
 FLAG_REMOVE_DIVERGENT = 2
@@ -58,6 +59,8 @@ FLAG_MASKS_BS = 8192
 FLAG_POST_UNPACK = 16384
 FLAG_FINISH_PACK = 32768
 FLAG_ASYNC_FINISH = 65536
+FLAG_PRE_PERMS = 131072
+HELPER_CTL = 1 + 8192  # helper work-queue head + per-SIMD generation-wave counts (csrc/srnn_kernels.h)
 
 
 class SrnnCfg(ctypes.Structure):
@@ -88,6 +91,8 @@ class SrnnArgs(ctypes.Structure):
         ("temp", _P), ("temp_bytes", ctypes.c_int64),
         ("dev", ctypes.c_int32), ("pad1", ctypes.c_int32), ("stream", _P), ("gen_out", _P),
         ("scratch", _P), ("scratch_bytes", ctypes.c_int64),
+        ("perm_cur", _P), ("perm_next", _P), ("helper_ctl", _P), ("perm_e", ctypes.c_int32),
+        ("helpers", ctypes.c_int32),
     ]
 
 

@@ -183,6 +183,20 @@ class SoupEngine:
         self._blockstats = [self._blockstat, torch.zeros_like(self._blockstat)] if self.async_finish else None
         self._side = torch.cuda.Stream(self.device) if self.async_finish else None
         self._fin_ev = [None, None]  # finish events of the generations that wrote each block-stats buffer
+        # SGD permutations precomputed by helper waves of the previous generation
+        # (Weightwise nets with <= 16 weights, shuffled): [parity][epoch][row] nibble words
+        E = int(self.params.get("train", 0)) + (max(int(self.params.get("learn_from_severity", 1)), 0)
+                                                 if float(self.params.get("learn_from_rate", 0.1)) > 0 else 0)
+        self._perm_e = E
+        self._perms = None
+        self._perms_ready = False
+        if (self.async_finish and self.shuffle and spec.kind == "weightwise" and spec.P <= 16 and 0 < E <= 256
+                and 2 * E * 8 * self.n <= 8 * 2 ** 30 and os.environ.get("SRNN_PRE_PERMS", "1") == "1"):
+            self._perms = [torch.zeros((E, self.n), dtype=torch.int64, device=dev) for _ in range(2)]
+            self._helper_ctl = [torch.zeros(_lib.HELPER_CTL, dtype=torch.int32, device=dev) for _ in range(2)]
+            nb = -(-self.n // 64)
+            # helper workgroups: enough to give every SIMD with one generation wave a partner
+            self._helpers = int(os.environ.get("SRNN_PERM_HELPERS", max(0, 2 * 1024 - nb)))
         self._done = torch.zeros(1, **i32)
         # per-row respawn flags (host) or 64-bit respawn ballots per 64-row wave (device)
         self.flags32 = torch.zeros(max(self.n, 2 * (-(-self.n // 64))), **i32)
@@ -352,6 +366,10 @@ class SoupEngine:
                 bs = self._blockstats[self._p]
                 fa.temp, fa.temp_bytes = _p(bs), bs.numel() * 4
                 fa.flags |= _lib.FLAG_TWO_PHASE | _lib.FLAG_ASYNC_FINISH
+                if self._perms is not None:
+                    fa.flags |= _lib.FLAG_PRE_PERMS
+                    fa.perm_cur, fa.perm_next = _p(self._perms[self._p]), _p(self._perms[1 - self._p])
+                    fa.helper_ctl, fa.perm_e, fa.helpers = _p(self._helper_ctl[self._p]), self._perm_e, self._helpers
             census = self.stats and self.spec.shuffler == "none"
             if self.dist.enabled:
                 # sharded: every global slot's next decisions; counts feed the next pack
@@ -392,6 +410,12 @@ class SoupEngine:
                     # the next generation (which only needs the counter it advances itself)
                     fa, fin = ca
                     main = torch.cuda.current_stream(self.device)
+                    if self._perms is not None and not self._perms_ready:
+                        # first precomputed generation: its permutations by a plain launch
+                        pa = self._args()
+                        pa.perm_next, pa.perm_e = _p(self._perms[self._p]), self._perm_e
+                        _lib.run(_lib.OP_SOUP_PERMS, spec, pa, cfg)
+                        self._perms_ready = True
                     ev = self._fin_ev[self._p]
                     if ev is not None:  # this parity's block stats are free again
                         main.wait_event(ev)
@@ -414,6 +438,7 @@ class SoupEngine:
                 _lib.run(_lib.OP_SOUP_DECIDE, spec, a, cfg)
             _lib.run(_lib.OP_SOUP_EVOLVE, spec, a, cfg)
             self._lists_ready = False
+            self._perms_ready = False  # the next generation's permutations were not precomputed
             if record and self.recorder is not None:
                 self.recorder.on_evolved(self)
             # uids from next_uid (advanced in place), generation counter, census histogram zeroed
@@ -619,7 +644,8 @@ class SoupEngine:
         """Every device tensor a generation reads or writes (graph validation)."""
         names = ["_bufs", "uid", "next_uid", "_gen_ring", "heads", "nexts", "flags32", "action", "counterpart",
                  "loss", "respawn", "counts", "census", "need", "sendcnt", "rmap", "ovf", "sendbuf", "recvbuf",
-                 "full", "stats_all", "_blockstats" if self._blockstats else "_blockstat", "_done"]
+                 "full", "stats_all", "_blockstats" if self._blockstats else "_blockstat", "_done", "_perms",
+                 "_helper_ctl"]
         out = []
         for k in names:
             v = getattr(self, k, None)
@@ -701,7 +727,7 @@ class SoupEngine:
             return
         ok = True
         gc = torch.cuda.CUDAGraph()
-        flags0 = (self._lists_ready, self._mask_src, self._packed)
+        flags0 = (self._lists_ready, self._mask_src, self._packed, self._perms_ready)
         try:
             with torch.cuda.graph(gc, stream=s, capture_error_mode="thread_local"):
                 for _ in range(G):
@@ -712,7 +738,7 @@ class SoupEngine:
             print(f"multi-generation graph capture failed ({type(e).__name__}: {e})", file=sys.stderr)
             ok = False
         self._p, self._pending = p0, pend0
-        self._lists_ready, self._mask_src, self._packed = flags0
+        self._lists_ready, self._mask_src, self._packed, self._perms_ready = flags0
         if ok:
             ok = self._validate_replay(lambda: gc.replay(), G, parity_after=p0)
         if self.dist.enabled:
@@ -745,21 +771,21 @@ class SoupEngine:
         state = self._state()
         saved = [t.clone() for t in state]
         p0, pend0, t0 = self._p, self._pending, self.time
-        flags0 = (self._lists_ready, self._mask_src, self._packed)
+        flags0 = (self._lists_ready, self._mask_src, self._packed, self._perms_ready)
         for _ in range(gens):
             self._generation()
         self._join_side()
         torch.cuda.synchronize(self.device)
-        flags1 = (self._lists_ready, self._mask_src, self._packed)
+        flags1 = (self._lists_ready, self._mask_src, self._packed, self._perms_ready)
         eager = [t.clone() for t in state]
         for t, v in zip(state, saved):
             t.copy_(v)
         self._p, self._pending = p0, pend0
-        self._lists_ready, self._mask_src, self._packed = flags0
+        self._lists_ready, self._mask_src, self._packed, self._perms_ready = flags0
         replay()
         if parity_after is not None:
             self._p = parity_after
-        self._lists_ready, self._mask_src, self._packed = flags1
+        self._lists_ready, self._mask_src, self._packed, self._perms_ready = flags1
         torch.cuda.synchronize(self.device)
         # compare the semantic state only: exchange-buffer row order and the attack
         # lists' link order follow atomics and legitimately differ between runs
@@ -771,6 +797,6 @@ class SoupEngine:
         for t, v in zip(state, saved):
             t.copy_(v)
         self._p, self._pending, self.time = p0, pend0, t0
-        self._lists_ready, self._mask_src, self._packed = flags0
+        self._lists_ready, self._mask_src, self._packed, self._perms_ready = flags0
         torch.cuda.synchronize(self.device)
         return same
