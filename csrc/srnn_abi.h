@@ -29,7 +29,9 @@ struct SrnnArgs {
                         // bit8 uid_assign reads the per-rank stats from the exchange's stats rows, bit9 classify advances *gen_ptr,
                         // bit10 fused generation computes the census, bit16 asynchronous finish (OP_SOUP_GEN
                         // advances the generation counter itself and leaves the finish to OP_GEN_FINISH),
-                        // bit17 precomputed SGD permutations (perm_cur / perm_next, helper waves)
+                        // bit17 precomputed SGD permutations (perm_cur / perm_next, helper waves),
+                        // bit18 OP_GEN_FINISH is a batch of `steps` generations (block stats ring in temp,
+                        // temp_bytes per generation; census = optional [steps][6] history)
   int32_t gen;          // soup generation (time)
   float eps;
   float lr;

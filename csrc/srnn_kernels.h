@@ -961,6 +961,73 @@ __global__ __launch_bounds__(NT) void k_gen_finish(SrnnArgs a, int32_t nb) {
   }
 }
 
+// Batched finish of m single-rank fused generations (OP_GEN_FINISH with steps = m > 1):
+// generation k left its block stats (respawn ballot + class counts per 64-row block) in
+// temp + k * temp_bytes; one workgroup walks the generations in order -- census of each
+// (counts[] keeps the last; a.census, when given, receives [m][6] history rows), newborn
+// uids in slot order from the running next_uid -- then stores next_uid once.  One launch
+// per graph chunk of generations instead of one per generation on the critical path.
+template <class Net, class S, int NT>
+__global__ __launch_bounds__(NT) void k_gen_finish_batch(SrnnArgs a, int32_t nb, int32_t m) {
+  __shared__ int32_t s_wave[NT / 64];
+  __shared__ unsigned long long s_cs[5];
+  __shared__ int64_t s_base;
+  const int t = threadIdx.x;
+  if (t == 0) s_base = *(volatile const int64_t*)a.uid_base;
+  const int32_t ch = (nb + NT - 1) / NT;
+  const int32_t b0 = t * ch, b1 = b0 + ch < nb ? b0 + ch : nb;
+  for (int32_t g = 0; g < m; ++g) {
+    if (t < 5) s_cs[t] = 0;
+    const unsigned long long* bs =
+        reinterpret_cast<const unsigned long long*>(reinterpret_cast<const char*>(a.temp) + (int64_t)g * a.temp_bytes);
+    int32_t born = 0;
+    unsigned long long cs[5] = {0, 0, 0, 0, 0};
+    for (int32_t b = b0; b < b1; ++b) {
+      const unsigned long long* st = bs + (int64_t)b * 4;
+      born += __popcll(st[0]);
+      cs[0] += (uint32_t)st[1];
+      cs[1] += (uint32_t)(st[1] >> 32);
+      cs[2] += (uint32_t)st[2];
+      cs[3] += (uint32_t)(st[2] >> 32);
+      cs[4] += (uint32_t)st[3];
+    }
+    int32_t total_born;
+    const int32_t incl = block_incl_scan<NT>(born, s_wave, &total_born);  // barrier inside (s_base, s_cs visible)
+#pragma unroll
+    for (int q = 0; q < 5; ++q) {
+      unsigned long long v = cs[q];
+      for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+      if ((t & 63) == 0 && v) atomicAdd(&s_cs[q], v);
+    }
+    const int64_t base = s_base;
+    int64_t u = base + incl - born;
+    for (int32_t b = b0; b < b1 && born; ++b) {
+      unsigned long long mm = bs[(int64_t)b * 4];
+      while (mm) {
+        const int bit = __ffsll((long long)mm) - 1;
+        mm &= mm - 1;
+        a.uid_out[(int64_t)b * TB + bit] = u++;
+      }
+    }
+    __syncthreads();
+    if (t == 0) {
+      s_base = base + total_born;
+      const bool census = (a.flags & 1024) != 0;
+      if (a.counts && g == m - 1) {
+        for (int q = 0; q < 5; ++q) a.counts[q] = census ? s_cs[q] : 0ull;
+        a.counts[5] = (uint64_t)total_born;
+      }
+      if (a.census) {
+        for (int q = 0; q < 5; ++q) a.census[(int64_t)g * 6 + q] = census ? (int64_t)s_cs[q] : 0;
+        a.census[(int64_t)g * 6 + 5] = total_born;
+      }
+    }
+    // the next generation's scan reuses s_wave / s_cs: every thread past this iteration's reads
+    __syncthreads();
+  }
+  if (t == 0) ((int64_t*)a.uid_base)[0] = s_base;
+}
+
 // SGD permutations of generation *gen_ptr for every local row into perm_next (OP_SOUP_PERMS:
 // the first precomputed generation; later ones come from the helper waves)
 template <class Net, class S>
@@ -1000,7 +1067,16 @@ int gen_finish(const SrnnCfg&, const SrnnArgs& a) {
   const int64_t blocks = (a.n + TB - 1) / TB;
   if (blocks <= 0) return 0;
   constexpr int FNT = SRNN_FINISH_NT;
-  hipLaunchKernelGGL((k_gen_finish<Net, S, FNT>), dim3(1), dim3(FNT), 0, (hipStream_t)a.stream, a, (int32_t)blocks);
+  if (a.steps > 1 || (a.flags & 262144)) {  // batch of a.steps generations (ring in temp)
+    if (a.steps < 1 || a.temp_bytes < blocks * 32) {
+      set_error("batched finish needs steps >= 1 generations and temp_bytes >= 32 per block");
+      return -5;
+    }
+    hipLaunchKernelGGL((k_gen_finish_batch<Net, S, FNT>), dim3(1), dim3(FNT), 0, (hipStream_t)a.stream, a,
+                       (int32_t)blocks, a.steps);
+  } else {
+    hipLaunchKernelGGL((k_gen_finish<Net, S, FNT>), dim3(1), dim3(FNT), 0, (hipStream_t)a.stream, a, (int32_t)blocks);
+  }
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) {
     set_error(hipGetErrorString(e));

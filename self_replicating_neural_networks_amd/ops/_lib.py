@@ -60,6 +60,7 @@ FLAG_POST_UNPACK = 16384
 FLAG_FINISH_PACK = 32768
 FLAG_ASYNC_FINISH = 65536
 FLAG_PRE_PERMS = 131072
+FLAG_FINISH_BATCH = 262144
 HELPER_CTL = 1 + 8192  # helper work-queue head + per-SIMD generation-wave counts (csrc/srnn_kernels.h)
 
 

@@ -178,8 +178,20 @@ class SoupEngine:
         # single rank on a GPU: the finish kernel of generation g (census reduction + uids
         # of its newborns) runs on a side stream beside generation g + 1; the block stats
         # it reads are double-buffered by ping-pong parity (SRNN_ASYNC_FINISH=0: serial)
-        self.async_finish = (self.device.type == "cuda" and not self.dist.enabled and self.fused
-                             and os.environ.get("SRNN_ASYNC_FINISH", "1") == "1")
+        # where the finish of a single-rank fused generation on a GPU runs (census reduction
+        # + newborn uids, one workgroup): "batch" -- the generation kernel advances the
+        # counter itself, the block stats of up to G generations go to a ring and ONE
+        # launch finishes them all (per graph chunk / evolve call); "async" -- per
+        # generation on a side stream beside the next one (cross-queue sync per generation:
+        # measured slower, profiles/r2b_finish_modes.md); "serial" -- after every generation
+        fm = os.environ.get("SRNN_FINISH_MODE", "batch")
+        if self.device.type != "cuda" or self.dist.enabled or not self.fused:
+            fm = "serial"
+        self.finish_mode = fm
+        self.async_finish = fm == "async"
+        self._batch = max(1, int(os.environ.get("SRNN_GRAPH_CHUNK", "8")))
+        self._bs_ring = torch.zeros((self._batch, max(nb, 1) * 8), **i32) if fm == "batch" else None
+        self._pending_fin = 0  # batch mode: generations whose finish is still due
         self._blockstats = [self._blockstat, torch.zeros_like(self._blockstat)] if self.async_finish else None
         self._side = torch.cuda.Stream(self.device) if self.async_finish else None
         self._fin_ev = [None, None]  # finish events of the generations that wrote each block-stats buffer
@@ -191,7 +203,7 @@ class SoupEngine:
         self._perms = None
         self._perms_ready = False
         if (self.async_finish and self.shuffle and spec.kind == "weightwise" and spec.P <= 16 and 0 < E <= 256
-                and 2 * E * 8 * self.n <= 8 * 2 ** 30 and os.environ.get("SRNN_PRE_PERMS", "1") == "1"):
+                and 2 * E * 8 * self.n <= 8 * 2 ** 30 and os.environ.get("SRNN_PRE_PERMS", "0") == "1"):
             self._perms = [torch.zeros((E, self.n), dtype=torch.int64, device=dev) for _ in range(2)]
             self._helper_ctl = [torch.zeros(_lib.HELPER_CTL, dtype=torch.int32, device=dev) for _ in range(2)]
             nb = -(-self.n // 64)
@@ -322,7 +334,7 @@ class SoupEngine:
         params: building ctypes structs every generation costs host time)."""
         stream = torch.cuda.current_stream(self.device).cuda_stream if self.device.type == "cuda" else 0
         key = (self._p, stream, tuple(sorted((k, str(v)) for k, v in self.params.items())), self.stats_with_sec,
-               self.lr, self.shuffle, self.stats, self.two_phase, self.async_finish)
+               self.lr, self.shuffle, self.stats, self.two_phase, self.finish_mode, self._pending_fin)
         hit = self._arg_cache.get(key)
         if hit is not None:
             return hit
@@ -362,6 +374,10 @@ class SoupEngine:
             fa.temp, fa.temp_bytes = _p(self._blockstat), self._blockstat.numel() * 4
             fa.i32d = _p(self._done)
             fa.flags = a.flags | _lib.FLAG_RESPAWN_INLINE | (_lib.FLAG_TWO_PHASE if self.two_phase else 0)
+            if self.finish_mode == "batch":
+                bs = self._bs_ring[self._pending_fin]
+                fa.temp, fa.temp_bytes = _p(bs), bs.numel() * 4
+                fa.flags |= _lib.FLAG_TWO_PHASE | _lib.FLAG_ASYNC_FINISH
             if self.async_finish:
                 bs = self._blockstats[self._p]
                 fa.temp, fa.temp_bytes = _p(bs), bs.numel() * 4
@@ -405,6 +421,15 @@ class SoupEngine:
                 # ONE launch: evolve + next generation's attack lists + census + uids
                 if not self._lists_ready:
                     _lib.run(_lib.OP_SOUP_DECIDE, spec, a, cfg)
+                if self.finish_mode == "batch":
+                    _lib.run(_lib.OP_SOUP_GEN, spec, ca, cfg)  # advances the counter, no finish
+                    self._fin_flags = ca.flags
+                    self._pending_fin += 1
+                    self._lists_ready = True
+                    self._p = 1 - self._p
+                    if self._pending_fin == self._batch:
+                        self._finish_pending()
+                    return
                 if self.async_finish:
                     # generation on the main stream; its finish on the side stream, beside
                     # the next generation (which only needs the counter it advances itself)
@@ -520,12 +545,29 @@ class SoupEngine:
         else:
             self._pending = True
 
+    def _finish_pending(self):
+        """Batch mode: ONE finish launch for the generations whose block stats wait in the
+        ring (in generation order: census of each, newborn uids, next_uid)."""
+        m = self._pending_fin
+        if m == 0:
+            return
+        a = self._args()
+        a.n = self.n
+        a.steps = m
+        a.flags = (self._fin_flags & _lib.FLAG_FUSED_CENSUS) | _lib.FLAG_FINISH_BATCH
+        a.temp, a.temp_bytes = _p(self._bs_ring), self._bs_ring.stride(0) * 4
+        a.uid_out, a.uid_base, a.counts = _p(self.uid), _p(self.next_uid), _p(self.counts)
+        _lib.run(_lib.OP_GEN_FINISH, self.spec, a, self.cfg)
+        self._pending_fin = 0
+
     def _join_side(self):
         """Make the current stream wait for the side-stream finish kernels (uids, census,
-        next_uid are final after this)."""
+        next_uid are final after this) and run any batched finish still due."""
         if self._side is not None and any(e is not None for e in self._fin_ev):
             torch.cuda.current_stream(self.device).wait_stream(self._side)
             self._fin_ev = [None, None]
+        if self._pending_fin:
+            self._finish_pending()
 
     def _flush(self):
         """Sharded: assign the uids of the last generation's newborns now (all-gather of
@@ -645,7 +687,7 @@ class SoupEngine:
         names = ["_bufs", "uid", "next_uid", "_gen_ring", "heads", "nexts", "flags32", "action", "counterpart",
                  "loss", "respawn", "counts", "census", "need", "sendcnt", "rmap", "ovf", "sendbuf", "recvbuf",
                  "full", "stats_all", "_blockstats" if self._blockstats else "_blockstat", "_done", "_perms",
-                 "_helper_ctl"]
+                 "_helper_ctl", "_bs_ring"]
         out = []
         for k in names:
             v = getattr(self, k, None)
@@ -727,7 +769,7 @@ class SoupEngine:
             return
         ok = True
         gc = torch.cuda.CUDAGraph()
-        flags0 = (self._lists_ready, self._mask_src, self._packed, self._perms_ready)
+        flags0 = (self._lists_ready, self._mask_src, self._packed, self._perms_ready, self._pending_fin)
         try:
             with torch.cuda.graph(gc, stream=s, capture_error_mode="thread_local"):
                 for _ in range(G):
@@ -738,7 +780,7 @@ class SoupEngine:
             print(f"multi-generation graph capture failed ({type(e).__name__}: {e})", file=sys.stderr)
             ok = False
         self._p, self._pending = p0, pend0
-        self._lists_ready, self._mask_src, self._packed, self._perms_ready = flags0
+        self._lists_ready, self._mask_src, self._packed, self._perms_ready, self._pending_fin = flags0
         if ok:
             ok = self._validate_replay(lambda: gc.replay(), G, parity_after=p0)
         if self.dist.enabled:
@@ -771,21 +813,21 @@ class SoupEngine:
         state = self._state()
         saved = [t.clone() for t in state]
         p0, pend0, t0 = self._p, self._pending, self.time
-        flags0 = (self._lists_ready, self._mask_src, self._packed, self._perms_ready)
+        flags0 = (self._lists_ready, self._mask_src, self._packed, self._perms_ready, self._pending_fin)
         for _ in range(gens):
             self._generation()
         self._join_side()
         torch.cuda.synchronize(self.device)
-        flags1 = (self._lists_ready, self._mask_src, self._packed, self._perms_ready)
+        flags1 = (self._lists_ready, self._mask_src, self._packed, self._perms_ready, self._pending_fin)
         eager = [t.clone() for t in state]
         for t, v in zip(state, saved):
             t.copy_(v)
         self._p, self._pending = p0, pend0
-        self._lists_ready, self._mask_src, self._packed, self._perms_ready = flags0
+        self._lists_ready, self._mask_src, self._packed, self._perms_ready, self._pending_fin = flags0
         replay()
         if parity_after is not None:
             self._p = parity_after
-        self._lists_ready, self._mask_src, self._packed, self._perms_ready = flags1
+        self._lists_ready, self._mask_src, self._packed, self._perms_ready, self._pending_fin = flags1
         torch.cuda.synchronize(self.device)
         # compare the semantic state only: exchange-buffer row order and the attack
         # lists' link order follow atomics and legitimately differ between runs
@@ -797,6 +839,6 @@ class SoupEngine:
         for t, v in zip(state, saved):
             t.copy_(v)
         self._p, self._pending, self.time = p0, pend0, t0
-        self._lists_ready, self._mask_src, self._packed, self._perms_ready = flags0
+        self._lists_ready, self._mask_src, self._packed, self._perms_ready, self._pending_fin = flags0
         torch.cuda.synchronize(self.device)
         return same
