@@ -110,6 +110,37 @@ def config4(args):
     return res
 
 
+def config4s(args):
+    """The north-star net living in a soup: Aggregating(4,10,3) particles attack, learn
+    from and self-train each other (reference code/soup.py:132-134 with the P = 280 net),
+    fp32 and bf16 tables, shuffle_not and shuffle_random."""
+    n, gens = args.n4s, args.gens4s
+    dev = torch.device("cuda", 0)
+    params = dict(attacking_rate=0.1, learn_from_rate=0.1, learn_from_severity=1, train=args.train4s,
+                  remove_divergent=True, remove_zero=True, epsilon=1e-4)
+    res = dict(config="4s", name=f"{n} Aggregating(4,10,3) soup", n=n, params=params, gens=gens)
+    for label, shuffler, dtype in (("fp32", "none", torch.float32), ("bf16", "none", torch.bfloat16),
+                                   ("fp32_shuffle_random", "random", torch.float32)):
+        spec = ArchSpec.aggregating(4, 10, 3, shuffler=shuffler)
+        eng = SoupEngine(spec, n, params, device=dev, seed=0, dtype=dtype)
+        eng.stats = True
+        graphed = eng.capture(warmup=1)
+        eng.evolve(2)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        eng.evolve(gens)
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+        res[f"{label}_ms_per_generation"] = dt / gens * 1e3
+        res[f"{label}_particle_generations_per_s"] = n * gens / dt
+        res[f"{label}_graph"] = graphed
+        res[f"{label}_generic_engine"] = bool(eng.generic)
+        res[f"{label}_census"] = eng.count()
+        del eng
+        torch.cuda.empty_cache()
+    return res
+
+
 def config5(args):
     spec = ArchSpec.weightwise(2, 2)
     dev = torch.device("cuda", 0)
@@ -146,9 +177,12 @@ def main():
     ap.add_argument("--n4", type=int, default=1_000_000)
     ap.add_argument("--n5", type=int, default=10_000_000)
     ap.add_argument("--gens5", type=int, default=10)
+    ap.add_argument("--n4s", type=int, default=1_000_000)
+    ap.add_argument("--gens4s", type=int, default=5)
+    ap.add_argument("--train4s", type=int, default=20)
     args = ap.parse_args()
     for c in args.only.split(","):
-        fn = {"1": config1, "2": config2, "4": config4, "5": config5}[c.strip()]
+        fn = {"1": config1, "2": config2, "4": config4, "4s": config4s, "5": config5}[c.strip()]
         if c.strip() != "1" and not torch.cuda.is_available():
             print(json.dumps(dict(config=int(c), skipped="no GPU")), flush=True)
             continue
