@@ -875,23 +875,585 @@ __global__ __launch_bounds__(TBROW) void k_big_row(SrnnCfg c, SrnnArgs a) {
   }
 }
 
+// ==================================================================================
+// Storage formats, shuffle_random and soups of the big nets (lane per particle).
+//
+// Rows are fp32, bf16 or fp16 (S = StF32 / StBF16 / StF16 of srnn_kernels.h): decoded to
+// fp32 registers on load, rounded on every store and after every application, exactly
+// where the runtime-shape engine rounds (g_quant / g_store of srnn_generic.hip), so a big
+// net gives the same bits here as on the runtime-shape engine on the same device.
+//
+// shuffle_random (reference code/network.py:319-322, applied to the output of
+// apply_to_weights): the output of an aggregating net is chunk-constant, out = expand(h),
+// so the shuffled output out[k] = expand(h)[perm[k]] = h[chunk(perm[k])].  Fisher-Yates is
+// therefore run directly on the CHUNK IDS (4 bits per weight, 35 words per lane in LDS)
+// with the draws of fisher_yates(P_AGGSHUF): swapping entries of perm swaps the entries of
+// chunk o perm, so no 280-entry index permutation is ever materialised.
+// ==================================================================================
+template <class T, class S>
+struct BRow {
+  static constexpr int RB = T::PP * S::BYTES;  // bytes per table row
+  static constexpr int XB = RB + 16;           // exchange row: weights + (slot, gen) tags
+  __device__ static const char* at(const float* base, int64_t i) {
+    return reinterpret_cast<const char*>(base) + i * RB;
+  }
+  __device__ static char* at(float* base, int64_t i) { return reinterpret_cast<char*>(base) + i * RB; }
+  __device__ static void load(const char* row, float (&w)[T::P]) {
+    if constexpr (S::ID == 0) {
+      // integer-typed loads (as for the 16-bit formats): with float loads the compiler
+      // reorders/duplicates row loads across the soup kernel's control flow and spills
+      const uint4* r4 = reinterpret_cast<const uint4*>(row);
+#pragma unroll
+      for (int q = 0; q < T::PP / 4; ++q) {
+        const uint4 v = r4[q];
+        const uint32_t u[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          if (4 * q + e < T::P) w[4 * q + e] = __uint_as_float(u[e]);
+      }
+    } else {
+      const uint2* r2 = reinterpret_cast<const uint2*>(row);
+#pragma unroll
+      for (int q = 0; q < T::PP / 4; ++q) {
+        const uint2 v = r2[q];
+        const uint16_t h[4] = {(uint16_t)(v.x & 0xffffu), (uint16_t)(v.x >> 16), (uint16_t)(v.y & 0xffffu),
+                               (uint16_t)(v.y >> 16)};
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          if (4 * q + e < T::P) w[4 * q + e] = S::dec(h[e]);
+      }
+    }
+  }
+  __device__ static void store(char* row, const float (&w)[T::P]) {
+    if constexpr (S::ID == 0) {
+      uint4* r4 = reinterpret_cast<uint4*>(row);
+#pragma unroll
+      for (int q = 0; q < T::PP / 4; ++q) {
+        uint32_t u[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) u[e] = (4 * q + e < T::P) ? __float_as_uint(w[4 * q + e]) : 0u;
+        r4[q] = make_uint4(u[0], u[1], u[2], u[3]);
+      }
+    } else {
+      uint2* r2 = reinterpret_cast<uint2*>(row);
+#pragma unroll
+      for (int q = 0; q < T::PP / 4; ++q) {
+        uint32_t h[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) h[e] = (4 * q + e < T::P) ? (uint32_t)S::enc(w[4 * q + e]) : 0u;
+        r2[q] = make_uint2(h[0] | (h[1] << 16), h[2] | (h[3] << 16));
+      }
+    }
+  }
+  __device__ static void quant(float (&w)[T::P]) {
+    if constexpr (S::ID != 0) {
+#pragma unroll
+      for (int k = 0; k < T::P; ++k) w[k] = S::q(w[k]);
+    }
+  }
+  __device__ static void quant_a(float* h) {
+    if constexpr (S::ID != 0) {
+#pragma unroll
+      for (int k = 0; k < T::A; ++k) h[k] = S::q(h[k]);
+    }
+  }
+  // chunk aggregation of a streamed row (teacher / attack target): the row is never held
+  __device__ static void stream_aggregate(const char* row, float* g, int aggregator) {
+    {
+      double acc[T::A];
+      float m[T::A];
+#pragma unroll
+      for (int c = 0; c < T::A; ++c) acc[c] = 0.0, m[c] = 0.f;
+#pragma unroll
+      for (int q = 0; q < T::PP / 4; ++q) {
+        float v[4];
+        if constexpr (S::ID == 0) {
+          const uint4 u = reinterpret_cast<const uint4*>(row)[q];
+          v[0] = __uint_as_float(u.x), v[1] = __uint_as_float(u.y), v[2] = __uint_as_float(u.z),
+          v[3] = __uint_as_float(u.w);
+        } else {
+          const uint2 u = reinterpret_cast<const uint2*>(row)[q];
+          v[0] = S::dec((uint16_t)(u.x & 0xffffu)), v[1] = S::dec((uint16_t)(u.x >> 16)),
+          v[2] = S::dec((uint16_t)(u.y & 0xffffu)), v[3] = S::dec((uint16_t)(u.y >> 16));
+        }
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int k = 4 * q + e;
+          if (k >= T::P) continue;
+          const int c = T::chunk_c(k);
+          if (aggregator == 0) acc[c] += (double)v[e];
+          else if (k == c * T::CS) m[c] = v[e];
+          else m[c] = (aggregator == 1) ? (v[e] > m[c] ? v[e] : m[c]) : ((v[e] > m[c] && v[e] != 0.0f) ? v[e] : m[c]);
+        }
+      }
+#pragma unroll
+      for (int c = 0; c < T::A; ++c) {
+        const int b = c * T::CS, e = (c == T::A - 1) ? T::P : b + T::CS;
+        g[c] = aggregator == 0 ? (float)(acc[c] / (double)(e - b)) : m[c];
+      }
+    }
+  }
+  // generation-start row of global slot g: this rank's table (W2) or the exchange buffers
+  // (flag 128: all-gathered [n_total] table; else the all-to-all rows indexed by rmap)
+  __device__ static const char* row_of(const SrnnArgs& a, int64_t g) {
+    if (a.world <= 1 || (g >= a.lo && g < a.lo + a.n)) return at(a.W2, g - a.lo);
+    if (a.flags & 128) return at(a.recvbuf, g);
+    return reinterpret_cast<const char*>(a.recvbuf) + (int64_t)a.rmap[g] * XB;
+  }
+  // glorot init of a particle straight into its (global) row: the draws and values of
+  // glorot_fill / g_glorot, encoded to the storage format
+  __device__ static void init_row(char* row, const Rng& rng, uint64_t uid) {
+    for (int l = 0; l <= T::D; ++l) {
+      const int r = T::rows(l), cc = T::cols(l), off = T::off(l), n = r * cc;
+      const float lim = sqrtf(6.0f / (float)(r + cc));
+      for (int b = 0; b < (n + 3) / 4; ++b) {
+        const U4 u = rng.draw(uid, (uint32_t)off * 1024u + (uint32_t)b, P_INIT);
+        const uint32_t xs[4] = {u.x, u.y, u.z, u.w};
+        for (int q = 0; q < 4; ++q) {
+          const int k = b * 4 + q;
+          if (k < n) put(row, off + k, -lim + 2.0f * lim * u01(xs[q]));
+        }
+      }
+    }
+    for (int k = T::P; k < T::PP; ++k) put(row, k, 0.f);
+  }
+  __device__ static void put(char* row, int k, float v) {
+    if constexpr (S::ID == 0) reinterpret_cast<float*>(row)[k] = v;
+    else reinterpret_cast<uint16_t*>(row)[k] = S::enc(v);
+  }
+};
+
+// chunk ids of the shuffled output (4 bits per weight) in LDS, word w of lane L at
+// cw[w * TBROW + L] (consecutive lanes -> consecutive banks)
+template <class T>
+struct ChunkPerm {
+  static constexpr int NW = (T::P + 7) / 8;
+  static_assert(T::A <= 16, "chunk ids are 4-bit");
+  uint32_t* cw;
+  __device__ uint32_t word(int w) const { return cw[w * TBROW]; }
+  __device__ int cid(int k) const { return (int)((cw[(k >> 3) * TBROW] >> (4 * (k & 7))) & 15u); }
+  // fisher_yates(perm, P, rng, id, step, P_AGGSHUF) applied to chunk(perm[k])
+  __device__ void draw(const Rng& rng, uint64_t id, uint32_t step) const {
+#pragma unroll
+    for (int w = 0; w < NW; ++w) {
+      uint32_t x = 0;
+#pragma unroll
+      for (int e = 0; e < 8; ++e)
+        if (8 * w + e < T::P) x |= (uint32_t)T::chunk_c(8 * w + e) << (4 * e);
+      cw[w * TBROW] = x;
+    }
+    U4 r{0, 0, 0, 0};
+    int used = 4;
+    uint32_t blk = 0;
+    for (int i = T::P - 1; i > 0; --i) {
+      if (used == 4) {
+        r = rng.draw(id, step * 64u + blk, P_AGGSHUF);
+        ++blk;
+        used = 0;
+      }
+      const uint32_t x = used == 0 ? r.x : used == 1 ? r.y : used == 2 ? r.z : r.w;
+      ++used;
+      int j = (int)(u01(x) * (float)(i + 1));
+      if (j > i) j = i;
+      const int wi = i >> 3, wj = j >> 3, si = 4 * (i & 7), sj = 4 * (j & 7);
+      const uint32_t xi = cw[wi * TBROW], xj = cw[wj * TBROW];
+      const uint32_t d = ((xi >> si) ^ (xj >> sj)) & 15u;
+      if (wi == wj) {
+        cw[wi * TBROW] = xi ^ (d << si) ^ (d << sj);
+      } else {
+        cw[wi * TBROW] = xi ^ (d << si);
+        cw[wj * TBROW] = xj ^ (d << sj);
+      }
+    }
+  }
+};
+
+// h[c] for a runtime chunk id c (A-way select, no dynamic register indexing)
+template <class T>
+__device__ __forceinline__ float pick(const float* h, int c) {
+  float v = h[0];
+#pragma unroll
+  for (int q = 1; q < T::A; ++q) v = (c == q) ? h[q] : v;
+  return v;
+}
+// w = expand(h) (chunk-constant) or its shuffled form h[chunk(perm[k])]
+template <class T, bool SHUF>
+__device__ __forceinline__ void expand_out(float (&w)[T::P], const float* h, const ChunkPerm<T>& cp) {
+  if constexpr (SHUF) {
+#pragma unroll
+    for (int wd = 0; wd < ChunkPerm<T>::NW; ++wd) {
+      const uint32_t x = cp.word(wd);
+#pragma unroll
+      for (int e = 0; e < 8; ++e)
+        if (8 * wd + e < T::P) w[8 * wd + e] = pick<T>(h, (int)((x >> (4 * e)) & 15u));
+    }
+  } else {
+#pragma unroll
+    for (int k = 0; k < T::P; ++k) w[k] = h[T::chunk_c(k)];
+  }
+}
+// every |expand'(h)[k] - w[k]| < eps (expand' = shuffled or plain)
+template <class T, bool SHUF>
+__device__ __forceinline__ bool close_out(const float (&w)[T::P], const float* h, float eps, const ChunkPerm<T>& cp) {
+  bool ok = true;
+  if constexpr (SHUF) {
+#pragma unroll
+    for (int wd = 0; wd < ChunkPerm<T>::NW; ++wd) {
+      const uint32_t x = cp.word(wd);
+#pragma unroll
+      for (int e = 0; e < 8; ++e)
+        if (8 * wd + e < T::P) ok &= !(fabsf(pick<T>(h, (int)((x >> (4 * e)) & 15u)) - w[8 * wd + e]) >= eps);
+    }
+  } else {
+    ok = lrow_close_state<T>(w, h, eps);
+  }
+  return ok;
+}
+// chunk aggregation of expand'(h) (mean: double sums in index order, like g_aggregate of the
+// materialised vector; without the shuffle the result is h itself, exactly)
+template <class T, bool SHUF>
+__device__ __forceinline__ void aggregate_out(const float* h, float* g, int aggregator, const ChunkPerm<T>& cp) {
+  if constexpr (!SHUF) {
+#pragma unroll
+    for (int c = 0; c < T::A; ++c) g[c] = h[c];
+  } else {
+#pragma unroll
+    for (int c = 0; c < T::A; ++c) {
+      const int b = c * T::CS, e = (c == T::A - 1) ? T::P : b + T::CS;
+      double acc = 0.0;
+      float m = pick<T>(h, cp.cid(b));
+      for (int k = b; k < e; ++k) {
+        const float v = pick<T>(h, cp.cid(k));
+        acc += (double)v;
+        m = (aggregator == 1) ? (v > m ? v : m) : ((v > m && v != 0.0f) ? v : m);
+      }
+      g[c] = aggregator == 0 ? (float)(acc / (double)(e - b)) : m;
+    }
+  }
+}
+// census class of a register row (g_classify_w): f1 = apply(w, w), f2 = apply(w, f1), both
+// with the same shuffle permutation (one ApplyCtx), rounded to the storage format
+template <class T, class S, bool SHUF>
+__device__ int8_t bclassify(const float (&w)[T::P], float eps, bool with_sec, int aggregator, const ChunkPerm<T>& cp) {
+  bool fin = true;
+#pragma unroll
+  for (int k = 0; k < T::P; ++k) fin &= finitef(w[k]);
+  if (!fin) return C_DIVERGENT;
+  float g[T::A], h1[T::A], h2[T::A];
+  lrow_aggregate<T>(w, g, aggregator);
+  lmlp<T>(w, g, h1);
+  BRow<T, S>::quant_a(h1);
+  if (finite_all<T>(h1) && close_out<T, SHUF>(w, h1, eps, cp)) {
+    bool zero = true;
+#pragma unroll
+    for (int k = 0; k < T::P; ++k) zero &= (-eps <= w[k]) && (w[k] <= eps);
+    return zero ? C_FIX_ZERO : C_FIX_OTHER;
+  }
+  if (with_sec) {
+    aggregate_out<T, SHUF>(h1, g, aggregator, cp);
+    lmlp<T>(w, g, h2);
+    BRow<T, S>::quant_a(h2);
+    if (finite_all<T>(h2) && close_out<T, SHUF>(w, h2, eps, cp)) return C_FIX_SEC;
+  }
+  return C_OTHER;
+}
+
+// classify (+ histogram, + respawn count flag 64, + generation advance flag 512), attack,
+// train and learn_from with any storage format and shuffler
+template <class T, class S, bool SHUF, int OP>
+__global__ __launch_bounds__(TBROW) void k_big_rows(SrnnCfg c, SrnnArgs a) {
+  using R = BRow<T, S>;
+  __shared__ uint32_t s_cw[SHUF ? ChunkPerm<T>::NW * TBROW : 1];
+  const ChunkPerm<T> cp{s_cw + threadIdx.x};
+  const int64_t p = (int64_t)blockIdx.x * TBROW + threadIdx.x;
+  const Rng rng{(uint32_t)a.seed, (uint32_t)(a.seed >> 32)};
+  float w[T::P];
+  if constexpr (OP == OP_CLASSIFY) {
+    __shared__ uint32_t s_cnt[6];
+    if (threadIdx.x < 6) s_cnt[threadIdx.x] = 0;
+    __syncthreads();
+    int8_t k = -1;
+    if (p < a.n) {
+      R::load(R::at(a.W, p), w);
+      if constexpr (SHUF) cp.draw(rng, a.uid ? (uint64_t)a.uid[p] : (uint64_t)(a.lo + p), a.ctr);
+      k = bclassify<T, S, SHUF>(w, a.eps, (a.flags & 8) != 0, c.aggregator, cp);
+      if (a.cls) a.cls[p] = k;
+    }
+    if (a.counts) {  // wave ballots -> LDS -> one atomic per (block, class)
+#pragma unroll
+      for (int q = 0; q < 5; ++q) {
+        const unsigned long long m = __ballot(k == q);
+        if ((threadIdx.x & 63) == 0 && m) atomicAdd(&s_cnt[q], (uint32_t)__popcll(m));
+      }
+      if (a.flags & 64) {
+        const unsigned long long m = __ballot(p < a.n && a.respawn[p] != 0);
+        if ((threadIdx.x & 63) == 0 && m) atomicAdd(&s_cnt[5], (uint32_t)__popcll(m));
+      }
+      __syncthreads();
+      if (threadIdx.x < 6 && s_cnt[threadIdx.x] && (threadIdx.x < 5 || (a.flags & 64)))
+        atomicAdd(a.counts + threadIdx.x, (uint64_t)s_cnt[threadIdx.x]);
+    }
+    if ((a.flags & 512) && blockIdx.x == 0 && threadIdx.x == 0) {
+      if (a.gen_out) a.gen_out[0] = a.gen_ptr[0] + 1;
+      else ((int32_t*)a.gen_ptr)[0] = a.gen_ptr[0] + 1;
+    }
+    return;
+  }
+  if (p >= a.n) return;
+  if constexpr (OP == OP_APPLY) {
+    const int64_t fi = a.idx_f ? a.idx_f[p] : p, ti = a.idx_t ? a.idx_t[p] : p, oi = a.idx_o ? a.idx_o[p] : p;
+    float g[T::A], h[T::A];
+    R::stream_aggregate(R::at(a.W, ti), g, c.aggregator);
+    R::load(R::at(a.W, fi), w);
+    lmlp<T>(w, g, h);
+    R::quant_a(h);
+    if constexpr (SHUF) cp.draw(rng, a.uid ? (uint64_t)a.uid[ti] : (uint64_t)ti, a.ctr);
+    expand_out<T, SHUF>(w, h, cp);
+    R::store(R::at(a.W2, oi), w);
+  } else {  // OP_TRAIN / OP_LEARN (no randomness in an aggregating net's SGD step)
+    float g[T::A];
+    if constexpr (OP == OP_LEARN) R::stream_aggregate(R::at(a.W2, a.idx_t ? a.idx_t[p] : p), g, c.aggregator);
+    R::load(R::at(a.W, p), w);
+    float loss = 0.f;
+    for (int e = 0; e < a.epochs; ++e) {
+      if constexpr (OP == OP_TRAIN) lrow_aggregate<T>(w, g, c.aggregator);
+      loss = ltrain_step<T>(w, g, a.lr);
+    }
+    R::store(R::at(a.W, p), w);
+    if (a.loss) a.loss[p] = loss;
+  }
+}
+
+// init / perturb / respawn of big rows in any storage format (lane per particle)
+template <class T, class S, int OP>
+__global__ __launch_bounds__(256) void k_big_lane_s(SrnnCfg c, SrnnArgs a) {
+  using R = BRow<T, S>;
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= a.n) return;
+  const Rng rng{(uint32_t)a.seed, (uint32_t)(a.seed >> 32)};
+  char* row = R::at(a.W, i);
+  if constexpr (OP == OP_INIT) {
+    R::init_row(row, rng, a.uid ? (uint64_t)a.uid[i] : (uint64_t)i);
+  } else if constexpr (OP == OP_RESPAWN) {
+    if (a.respawn[i] != 0) R::init_row(row, rng, respawn_key(a.gen_ptr ? a.gen_ptr[0] : a.gen, a.lo + i));
+  } else {  // OP_PERTURB
+    const uint64_t uid = a.uid ? (uint64_t)a.uid[i] : (uint64_t)i;
+    float w[T::P];
+    R::load(row, w);
+    for (int k = 0; k < T::P; ++k) {
+      const U4 u = rng.draw(uid, a.ctr * 1024u + (uint32_t)k, P_PERTURB);
+      const double mag = (double)u01(u.y) * (double)a.eps;
+      R::put(row, k, u01(u.x) < 0.5f ? (float)((double)w[k] + mag) : (float)((double)w[k] - mag));
+    }
+  }
+}
+
+// Synchronous soup generation of local row j (Item::soup_evolve / GItem::soup_evolve with
+// the row in VGPRs): attacks received in ascending attacker-slot order (generation-start
+// attacker rows), learn_from `severity` epochs on the teacher's aggregated generation-start
+// row, `epochs` self-train steps, respawn flags (+ inline re-init, flag 32), the 64-row
+// respawn ballot (or per-row flags, flag 16).  Only one 280-float row is live at a time:
+// the victim's aggregate is taken before the attacker's row is loaded into the same
+// registers (an attack rewrites every weight of the victim).
+template <class T, class S, bool SHUF>
+__global__ __launch_bounds__(TBROW) void k_big_soup_evolve(SrnnCfg c, SrnnArgs a) {
+  using R = BRow<T, S>;
+  __shared__ uint32_t s_cw[SHUF ? ChunkPerm<T>::NW * TBROW : 1];
+  const ChunkPerm<T> cp{s_cw + threadIdx.x};
+  const int64_t j = (int64_t)blockIdx.x * TBROW + threadIdx.x;
+  const Rng rng{(uint32_t)a.seed, (uint32_t)(a.seed >> 32)};
+  bool rs_any = false;
+  if (j < a.n) {
+    const int64_t g = a.lo + j;
+    const int32_t gen = a.gen_ptr ? a.gen_ptr[0] : a.gen;
+    float w[T::P];
+    R::load(R::at(a.W2, j), w);
+    uint32_t ctr = (uint32_t)gen * 1024u;
+    const int32_t head = a.i32e[j];
+    a.i32e[j] = -1;  // list consumed: reset for the next generation's decide
+    int32_t last = -1;
+    while (head >= 0) {
+      int32_t best = INT_MAX;
+      for (int32_t r = head; r >= 0; r = a.i32f[r]) best = (r > last && r < best) ? r : best;
+      if (best == INT_MAX) break;
+      last = best;
+      float gv[T::A], h[T::A];
+      lrow_aggregate<T>(w, gv, c.aggregator);
+      R::load(R::row_of(a, best), w);
+      lmlp<T>(w, gv, h);
+      R::quant_a(h);
+      if constexpr (SHUF) cp.draw(rng, (uint64_t)g, ctr);
+      expand_out<T, SHUF>(w, h, cp);
+      ctr += 1;
+    }
+    int32_t my_at, te;
+    Item<Weightwise<1, 1>, StF32>::decision(a, g, gen, my_at, te);
+    int8_t act = A_NONE;
+    int64_t cpart = -1;
+    if (my_at >= 0) act = A_ATTACKING, cpart = my_at;
+    // learn_from (`severity` steps on the teacher's aggregate) then self-train (`epochs`
+    // steps on the own aggregate) as ONE step loop: a single inlined SGD step keeps the
+    // register allocation of the 280-float row to one copy
+    float gt[T::A];
+    int nlearn = 0;
+    if (te >= 0) {
+      R::stream_aggregate(R::row_of(a, te), gt, c.aggregator);
+      nlearn = a.severity > 0 ? a.severity : 0;
+      act = A_LEARN_FROM;
+      cpart = te;
+    }
+    if (a.epochs > 0) act = A_TRAIN_SELF, cpart = -1;
+    const int nsteps = nlearn + (a.epochs > 0 ? a.epochs : 0);
+    float loss = 0.f;
+    for (int s = 0; s < nsteps; ++s) {
+      float gs[T::A];
+      if (s < nlearn) {
+#pragma unroll
+        for (int q = 0; q < T::A; ++q) gs[q] = gt[q];
+      } else {
+        lrow_aggregate<T>(w, gs, c.aggregator);
+      }
+      loss = ltrain_step<T>(w, gs, a.lr);
+    }
+    R::quant(w);  // the stored state decides respawn
+    bool bad = false, zero = true;
+#pragma unroll
+    for (int k = 0; k < T::P; ++k) {
+      bad |= !finitef(w[k]);
+      zero &= (-a.eps <= w[k]) && (w[k] <= a.eps);
+    }
+    int8_t rsp = 0;
+    if ((a.flags & 2) && bad) rsp = 1;
+    else if ((a.flags & 4) && zero) rsp = 2;
+    if (rsp && (a.flags & 32)) R::init_row(R::at(a.W, j), rng, respawn_key(gen, g));  // newborn
+    else R::store(R::at(a.W, j), w);
+    if (a.action) a.action[j] = act;
+    if (a.counterpart) a.counterpart[j] = cpart;
+    if (a.loss) a.loss[j] = loss;
+    a.respawn[j] = rsp;
+    rs_any = rsp != 0;
+  }
+  if (a.i32c) {
+    if (a.flags & 16) {
+      if (j < a.n) a.i32c[j] = rs_any ? 1 : 0;
+    } else {
+      const unsigned long long m = __ballot(rs_any);
+      if ((threadIdx.x & 63) == 0) reinterpret_cast<unsigned long long*>(a.i32c)[j >> 6] = m;
+    }
+  }
+}
+
+// Single-rank respawn of big nets (k_respawn_seq): one workgroup scans the 64-row ballots
+// in slot order, assigns the newborns' uids, re-initialises their rows, advances next_uid
+// and the generation counter, zeroes the census histogram.
+template <class T, class S>
+__global__ __launch_bounds__(TBR) void k_big_respawn_seq(SrnnCfg c, SrnnArgs a) {
+  using R = BRow<T, S>;
+  __shared__ int32_t s_wave[TBR / 64];
+  const unsigned long long* masks = reinterpret_cast<const unsigned long long*>(a.i32c);
+  const int64_t nb = (a.n + 63) / 64;
+  const int64_t ch = (nb + TBR - 1) / TBR;
+  const int64_t b0 = (int64_t)threadIdx.x * ch;
+  const int64_t b1 = b0 + ch < nb ? b0 + ch : nb;
+  int32_t cnt = 0;
+  for (int64_t b = b0; b < b1; ++b) cnt += __popcll(masks[b]);
+  int32_t total;
+  const int32_t incl = block_incl_scan<TBR>(cnt, s_wave, &total);
+  const int64_t base = *(volatile const int64_t*)a.uid_base;
+  const int32_t gen = a.gen_ptr ? a.gen_ptr[0] : a.gen;
+  const Rng rng{(uint32_t)a.seed, (uint32_t)(a.seed >> 32)};
+  int64_t k = base + incl - cnt;
+  for (int64_t b = b0; b < b1 && cnt; ++b) {
+    unsigned long long m = masks[b];
+    while (m) {
+      const int bit = __ffsll((long long)m) - 1;
+      m &= m - 1;
+      const int64_t r = b * 64 + bit;
+      a.uid_out[r] = k++;
+      if (!(a.flags & 32)) R::init_row(R::at(a.W, r), rng, respawn_key(gen, a.lo + r));  // else done inline
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    ((int64_t*)a.uid_base)[0] = base + total;
+    if (a.gen_out) a.gen_out[0] = gen + 1;
+    else if (a.gen_ptr) ((int32_t*)a.gen_ptr)[0] = gen + 1;
+  }
+  if (a.counts && threadIdx.x < 5) a.counts[threadIdx.x] = 0;
+}
+
+// ops of the big nets that take any storage format / shuffler (everything a soup needs)
+template <class T, class S, bool SHUF>
+int big_run_s(int op, const SrnnCfg& c, const SrnnArgs& a) {
+  hipStream_t st = (hipStream_t)a.stream;
+  const unsigned gl = (unsigned)((a.n + 255) / 256), g64 = (unsigned)((a.n + TBROW - 1) / TBROW);
+  switch (op) {
+    case OP_INIT: hipLaunchKernelGGL((k_big_lane_s<T, S, OP_INIT>), dim3(gl), dim3(256), 0, st, c, a); break;
+    case OP_PERTURB: hipLaunchKernelGGL((k_big_lane_s<T, S, OP_PERTURB>), dim3(gl), dim3(256), 0, st, c, a); break;
+    case OP_RESPAWN: hipLaunchKernelGGL((k_big_lane_s<T, S, OP_RESPAWN>), dim3(gl), dim3(256), 0, st, c, a); break;
+    case OP_APPLY: hipLaunchKernelGGL((k_big_rows<T, S, SHUF, OP_APPLY>), dim3(g64), dim3(TBROW), 0, st, c, a); break;
+    case OP_CLASSIFY:
+      hipLaunchKernelGGL((k_big_rows<T, S, SHUF, OP_CLASSIFY>), dim3(g64), dim3(TBROW), 0, st, c, a);
+      break;
+    case OP_TRAIN: hipLaunchKernelGGL((k_big_rows<T, S, SHUF, OP_TRAIN>), dim3(g64), dim3(TBROW), 0, st, c, a); break;
+    case OP_LEARN: hipLaunchKernelGGL((k_big_rows<T, S, SHUF, OP_LEARN>), dim3(g64), dim3(TBROW), 0, st, c, a); break;
+    case OP_SOUP_EVOLVE:
+      hipLaunchKernelGGL((k_big_soup_evolve<T, S, SHUF>), dim3(g64), dim3(TBROW), 0, st, c, a);
+      break;
+    case OP_RESPAWN_SEQ: hipLaunchKernelGGL((k_big_respawn_seq<T, S>), dim3(1), dim3(TBR), 0, st, c, a); break;
+    case OP_SOUP_DECIDE: {
+      // decisions are shape independent: every global slot
+      if (a.n_total <= 0) return 0;
+      hipLaunchKernelGGL((k_op<Weightwise<1, 1>, OP_SOUP_DECIDE, StF32>), dim3((unsigned)((a.n_total + TB - 1) / TB)),
+                         dim3(TB), 0, st, SrnnCfg{}, a);
+      break;
+    }
+    default: set_error("op not supported for big aggregating nets"); return -5;
+  }
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) {
+    set_error(hipGetErrorString(e));
+    return -3;
+  }
+  return 0;
+}
+
+// true when big_run serves (op, storage, shuffler); the rest goes to the runtime-shape engine
+constexpr bool big_serves(int op, int dtype, int shuffler) {
+  if (op == OP_INIT || op == OP_PERTURB || op == OP_RESPAWN || op == OP_APPLY || op == OP_CLASSIFY ||
+      op == OP_TRAIN || op == OP_LEARN || op == OP_SOUP_EVOLVE || op == OP_RESPAWN_SEQ || op == OP_SOUP_DECIDE)
+    return true;
+  return op == OP_RUN_FIXPOINT && dtype == 0 && shuffler == 0;
+}
+
 template <class T>
 int big_run(int op, const SrnnCfg& c, const SrnnArgs& a) {
   if (!a.dev) {
     set_error("wave-per-particle nets run on the GPU only (use a smaller shape on the host)");
     return -5;
   }
-  if (c.shuffler != 0 && op != OP_INIT && op != OP_PERTURB && op != OP_TRAIN && op != OP_LEARN) {
-    set_error("wave-per-particle aggregating nets: shuffle_random is not supported");
+  if (!big_serves(op, c.dtype, c.shuffler)) {
+    set_error("op not served by the big-net kernels (runtime-shape engine)");
     return -5;
+  }
+  // lane-per-particle row kernels (default) or the wave-per-particle ones (SRNN_BIG_WAVE=1,
+  // fp32 tables without shuffle only)
+  const char* wave_env = std::getenv("SRNN_BIG_WAVE");
+  const bool row_kernels = !(wave_env && wave_env[0] == '1');
+  const bool wave_op = !row_kernels && (op == OP_APPLY || op == OP_CLASSIFY || op == OP_TRAIN || op == OP_LEARN);
+  if (op != OP_RUN_FIXPOINT && !(wave_op && c.dtype == 0 && c.shuffler == 0)) {
+    if (a.n <= 0 && op != OP_SOUP_DECIDE) return 0;
+    const bool sh = c.shuffler != 0;
+#ifndef SRNN_BIG_FAST  // (register-allocation experiments: fp32 instantiations only)
+    if (c.dtype == 1) return sh ? big_run_s<T, StBF16, true>(op, c, a) : big_run_s<T, StBF16, false>(op, c, a);
+    if (c.dtype == 2) return sh ? big_run_s<T, StF16, true>(op, c, a) : big_run_s<T, StF16, false>(op, c, a);
+#endif
+    return sh ? big_run_s<T, StF32, true>(op, c, a) : big_run_s<T, StF32, false>(op, c, a);
   }
   hipStream_t st = (hipStream_t)a.stream;
   if (a.n <= 0) return 0;
   const unsigned gw = (unsigned)((a.n + BW - 1) / BW), gl = (unsigned)((a.n + 255) / 256);
   const unsigned g64 = (unsigned)((a.n + TBROW - 1) / TBROW);
-  // lane-per-particle row kernels (default) or the wave-per-particle ones (SRNN_BIG_WAVE=1)
-  const char* wave_env = std::getenv("SRNN_BIG_WAVE");
-  const bool row_kernels = !(wave_env && wave_env[0] == '1');
   switch (op) {
     case OP_INIT: hipLaunchKernelGGL((k_big_lane<T, OP_INIT>), dim3(gl), dim3(256), 0, st, c, a); break;
     case OP_PERTURB: hipLaunchKernelGGL((k_big_lane<T, OP_PERTURB>), dim3(gl), dim3(256), 0, st, c, a); break;
@@ -947,9 +1509,13 @@ using AGGB_4_16_2 = srnn::AggBig<4, 16, 2>;
     return srnn::big_run<T>(op, *c, *a);                                         \
   }
 
+extern "C" int srnn_aggbig_serves(int op, int dtype, int shuffler) { return srnn::big_serves(op, dtype, shuffler) ? 1 : 0; }
+
 extern "C" int srnn_dispatch_aggbig(int op, const SrnnCfg* c, const SrnnArgs* a) {
   SRNN_TRY_BIG(AGGB_4_10_3, 10, 3, 4)
+#ifndef SRNN_BIG_FAST
   SRNN_TRY_BIG(AGGB_4_8_2, 8, 2, 4)
   SRNN_TRY_BIG(AGGB_4_16_2, 16, 2, 4)
+#endif
   return 1;
 }

@@ -16,6 +16,7 @@ extern "C" int srnn_dispatch_agg(int op, const SrnnCfg* c, const SrnnArgs* a);
 extern "C" int srnn_dispatch_rnn(int op, const SrnnCfg* c, const SrnnArgs* a);
 extern "C" int srnn_dispatch_fft(int op, const SrnnCfg* c, const SrnnArgs* a);
 extern "C" int srnn_dispatch_aggbig(int op, const SrnnCfg* c, const SrnnArgs* a);
+extern "C" int srnn_aggbig_serves(int op, int dtype, int shuffler);
 extern "C" int srnn_dispatch_lowp(int op, const SrnnCfg* c, const SrnnArgs* a);
 
 extern "C" int srnn_dispatch_generic(int op, const SrnnCfg* c, const SrnnArgs* a);
@@ -73,7 +74,9 @@ static int dispatch_special(int op, const SrnnCfg* c, const SrnnArgs* a) {
       srnn::set_error("unknown weight-table dtype");
       return -1;
     }
-    return srnn_dispatch_lowp(op, c, a);
+    const int r = srnn_dispatch_lowp(op, c, a);
+    // big aggregating nets take every storage format in their own row kernels
+    return (r == 1 && c->kind == 1) ? srnn_dispatch_aggbig(op, c, a) : r;
   }
   switch (c->kind) {
     case 0: return srnn_dispatch_ww(op, c, a);
@@ -110,10 +113,7 @@ static int route(int op, const SrnnCfg* c, const SrnnArgs* a) {
       if (k == 0) return 0;  // lane-per-particle templates: every op, host and device
       const bool host = a && !a->dev;
       if (host) return 1;  // wave-per-particle paths are GPU only
-      if (k == 1 && (op == OP_INIT || op == OP_APPLY || op == OP_RUN_FIXPOINT || op == OP_CLASSIFY ||
-                     op == OP_TRAIN || op == OP_LEARN || op == OP_PERTURB) &&
-          (c->shuffler == 0 || op == OP_INIT || op == OP_PERTURB || op == OP_TRAIN || op == OP_LEARN))
-        return 0;
+      if (k == 1 && srnn_aggbig_serves(op, c->dtype, c->shuffler)) return 0;
       if (k == 2 && (op == OP_INIT || op == OP_APPLY || op == OP_RUN_FIXPOINT || op == OP_CLASSIFY)) return 0;
       return 1;
     }

@@ -929,6 +929,7 @@ __global__ __launch_bounds__(GTBR) void k_g_respawn_seq(GShape s, SrnnArgs a) {
       m &= m - 1;
       const int64_t r = b * GTB + bit;
       a.uid_out[r] = k++;
+      if (a.flags & 32) continue;  // re-initialised inline by the evolve kernel
       SV w = x.v(s.o_w);
       g_init(x, w, GItem::rng(a), respawn_key(gen, a.lo + r));
       g_store(s, GItem::rowp(s, a.W, r), w);
@@ -1041,6 +1042,7 @@ static void host_generic(int op, const GShape& s, const SrnnArgs& a) {
       for (int64_t i = 0; i < a.n; ++i) {
         if (a.respawn[i] == 0) continue;
         a.uid_out[i] = k++;
+        if (a.flags & 32) continue;  // re-initialised inline by the evolve
         SV w = x.v(s.o_w);
         g_init(x, w, GItem::rng(a), respawn_key(gen, a.lo + i));
         g_store(s, GItem::rowp(s, a.W, i), w);

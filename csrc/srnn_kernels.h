@@ -107,7 +107,11 @@ struct StBF16 {  // round-to-nearest-even, NaN kept quiet
   SRNN_HD static uint16_t enc(float x) {
 #ifdef __HIP_DEVICE_COMPILE__
     // gfx950 v_cvt_pk_bf16_f32: the same RNE rounding and NaN quieting as the host form
-    // (tests/test_kernels_gpu.py::test_bf16_encode_matches_host_rounding)
+    // (tests/test_kernels_gpu.py::test_bf16_encode_matches_host_rounding).  The barrier keeps
+    // the fp32 rounding of the producing fma: without it the backend may fold
+    // fptrunc(fma) into one bf16-rounded fma (as for fp16 below), so a kernel that rounds a
+    // freshly trained weight would differ from one that rounds it after a store
+    asm volatile("" : "+v"(x));
     return __builtin_bit_cast(uint16_t, (__bf16)x);
 #else
     uint32_t u = f_bits(x);
@@ -1422,9 +1426,11 @@ __global__ __launch_bounds__(TBR) void k_respawn_seq(SrnnCfg c, SrnnArgs a) {
         m &= m - 1;
         const int64_t r = b * TB + bit;
         a.uid_out[r] = k;
-        float w[Net::P];
-        Net::init(w, I::rng(a), respawn_key(I::gen_of(a), a.lo + r));
-        I::store(I::rowp(a.W, r), w);
+        if (!(a.flags & 32)) {  // flag 32: re-initialised inline by the evolve kernel
+          float w[Net::P];
+          Net::init(w, I::rng(a), respawn_key(I::gen_of(a), a.lo + r));
+          I::store(I::rowp(a.W, r), w);
+        }
         ++k;
       }
     }
@@ -1453,9 +1459,11 @@ int respawn_seq(const SrnnCfg& c, const SrnnArgs& a) {
   for (int64_t i = 0; i < a.n; ++i) {
     if (a.respawn[i] == 0) continue;
     a.uid_out[i] = k;
-    float w[Net::P];
-    Net::init(w, I::rng(a), respawn_key(I::gen_of(a), a.lo + i));
-    I::store(I::rowp(a.W, i), w);
+    if (!(a.flags & 32)) {
+      float w[Net::P];
+      Net::init(w, I::rng(a), respawn_key(I::gen_of(a), a.lo + i));
+      I::store(I::rowp(a.W, i), w);
+    }
     ++k;
   }
   ((int64_t*)a.uid_base)[0] = k;

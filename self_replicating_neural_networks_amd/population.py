@@ -29,7 +29,8 @@ class Population:
     """N particles of one architecture on one device."""
 
     def __init__(self, spec: ArchSpec, n: int, device="cpu", seed: int = 0, uid_start: int = 0,
-                 weights: Optional[torch.Tensor] = None, lr: float = 0.01, dtype: torch.dtype = torch.float32):
+                 weights: Optional[torch.Tensor] = None, lr: float = 0.01, dtype: torch.dtype = torch.float32,
+                 init: bool = True):
         self.spec = spec
         self.device = torch.device(device)
         self.seed = int(seed)
@@ -38,10 +39,10 @@ class Population:
         self.uid = torch.arange(uid_start, uid_start + n, dtype=torch.int64, device=self.device)
         K.dtype_code(dtype)
         self.W = torch.zeros((n, spec.PP), dtype=dtype, device=self.device)
-        if weights is None:
-            K.init_rows(spec, self.W, self.uid, self.seed)
-        else:
+        if weights is not None:
             self.set_weights(weights)
+        elif init:
+            K.init_rows(spec, self.W, self.uid, self.seed)
 
     # -------------------------------------------------------------- helpers
     def __len__(self):

@@ -86,10 +86,12 @@ class SoupEngine:
 
     def __init__(self, spec: ArchSpec, n_total: int, params: Dict, device="cpu", seed: int = 0,
                  lr: float = 0.01, shuffle: bool = True, dist: Optional[Dist] = None, weights=None,
-                 dtype: torch.dtype = torch.float32, exchange: str = "alltoall", local_weights=None):
+                 dtype: torch.dtype = torch.float32, exchange: str = "alltoall", local_weights=None,
+                 init: bool = True):
         """``weights``: the whole population's initial rows [n_total, >= P] (every rank
-        takes its slice); ``local_weights``: only this rank's rows [hi - lo, >= P] (what a
-        re-sharding checkpoint load passes, so host memory stays O(shard))."""
+        takes its slice); ``local_weights``: only this rank's rows [hi - lo, >= P];
+        ``init=False``: leave the rows for the caller to fill (the streaming checkpoint
+        loader writes them straight into the device table)."""
         self.spec = spec
         self.n_total = int(n_total)
         self.params = dict(attacking_rate=0.1, learn_from_rate=0.1, train=0, learn_from_severity=1)
@@ -189,7 +191,9 @@ class SoupEngine:
             fm = "serial"
         self.finish_mode = fm
         self.async_finish = fm == "async"
-        self._batch = max(1, int(os.environ.get("SRNN_GRAPH_CHUNK", "8")))
+        # the ring holds 32 B per 64-row block per pending generation: at HBM-filling sizes
+        # (2e9 rows = 1 GB per generation) fewer generations share one finish launch
+        self._batch = max(1, min(int(os.environ.get("SRNN_GRAPH_CHUNK", "8")), (512 << 20) // (max(nb, 1) * 32)))
         self._bs_ring = torch.zeros((self._batch, max(nb, 1) * 8), **i32) if fm == "batch" else None
         self._pending_fin = 0  # batch mode: generations whose finish is still due
         self._blockstats = [self._blockstat, torch.zeros_like(self._blockstat)] if self.async_finish else None
@@ -240,7 +244,7 @@ class SoupEngine:
                 w = torch.as_tensor(weights, dtype=torch.float32)[self.lo:self.hi]
             local.zero_()
             local[:, : w.shape[1]] = w.to(dev, dtype)
-        else:
+        elif init:
             K.init_rows(spec, local, self.uid, self.seed)
 
     def _expected_peer_rows(self) -> float:
@@ -461,6 +465,11 @@ class SoupEngine:
                 return
             if not self._lists_ready:
                 _lib.run(_lib.OP_SOUP_DECIDE, spec, a, cfg)
+            # newborn rows are re-initialised by the (parallel) evolve kernel unless the
+            # recorder needs the dead particles' final rows first; the one-workgroup
+            # respawn scan then only assigns the uids
+            inline = not (record and self.recorder is not None)
+            a.flags = flags | (_lib.FLAG_RESPAWN_INLINE if inline else 0)
             _lib.run(_lib.OP_SOUP_EVOLVE, spec, a, cfg)
             self._lists_ready = False
             self._perms_ready = False  # the next generation's permutations were not precomputed
@@ -468,6 +477,7 @@ class SoupEngine:
                 self.recorder.on_evolved(self)
             # uids from next_uid (advanced in place), generation counter, census histogram zeroed
             _lib.run(_lib.OP_RESPAWN_SEQ, spec, a, cfg)
+            a.flags = flags
             self._p = 1 - self._p
             if self.stats:
                 # per-generation fixpoint-fraction statistics (reference Soup.count, code/soup.py:89-103)

@@ -1,0 +1,98 @@
+"""Big aggregating nets (P > 64, the north-star Aggregating(4, 10, 3)) on their lane-per-
+particle row kernels (csrc/srnn_bignet.hip) for every storage format and shuffler: each
+operator and whole soup generations bitwise against the runtime-shape engine on the same
+device (csrc/srnn_generic.hip, itself checked against the numpy oracle in
+tests/test_generic_gpu.py)."""
+import pytest
+import torch
+
+from self_replicating_neural_networks_amd.arch import ArchSpec
+from self_replicating_neural_networks_amd.ops import _lib
+from self_replicating_neural_networks_amd.ops import kernels as K
+from self_replicating_neural_networks_amd.soup_engine import SoupEngine
+
+pytestmark = pytest.mark.gpu
+
+SOUP = dict(attacking_rate=0.3, learn_from_rate=0.3, train=3, learn_from_severity=2, remove_divergent=True,
+            remove_zero=True, epsilon=1e-4)
+DTYPES = [torch.float32, torch.bfloat16, torch.float16]
+dt_id = lambda d: str(d).replace("torch.", "")
+
+
+def _bits(t):
+    return t.contiguous().view(torch.uint8)
+
+
+def _both(fn):
+    outs = []
+    for gen in (False, True):
+        _lib.set_force_generic(gen)
+        try:
+            outs.append(fn())
+        finally:
+            _lib.set_force_generic(False)
+    return outs
+
+
+@pytest.mark.parametrize("shuffler", ["none", "random"])
+@pytest.mark.parametrize("dtype", DTYPES, ids=dt_id)
+def test_big_ops_equal_generic(cuda, dtype, shuffler):
+    spec = ArchSpec.aggregating(4, 10, 3, shuffler=shuffler)
+    code = K.dtype_code(dtype)
+    for op in (_lib.OP_INIT, _lib.OP_APPLY, _lib.OP_CLASSIFY, _lib.OP_TRAIN, _lib.OP_LEARN, _lib.OP_SOUP_EVOLVE):
+        assert not _lib.is_generic(spec, op, code), op
+    n = 1500
+
+    def ops():
+        uid = torch.arange(n, dtype=torch.int64, device=cuda) + 3
+        W = torch.zeros(n, spec.PP, dtype=dtype, device=cuda)
+        K.init_rows(spec, W, uid, 5)
+        idx = torch.roll(torch.arange(n, device=cuda), 7).contiguous()
+        A = torch.zeros_like(W)
+        K.apply(spec, W, A, idx_f=idx, uid=uid, seed=5, ctr=9)
+        T = W.clone()
+        tl = K.train(spec, T, epochs=4, uid=uid, seed=5, ctr=2)
+        L = W.clone()
+        K.learn_from(spec, L, W, idx_t=idx, epochs=2, uid=uid, seed=5, ctr=4)
+        c1, n1 = K.classify(spec, W, 1e-4, uid=uid, seed=5)
+        c2, n2 = K.classify(spec, A, 1e-2, uid=uid, seed=5)  # chunk-constant rows: fixpoint candidates
+        torch.cuda.synchronize()
+        return dict(init=W, apply=A, train=T, loss=tl, learn=L, cls1=c1, cnt1=n1, cls2=c2, cnt2=n2)
+
+    a, b = _both(ops)
+    bad = [k for k in a if not torch.equal(_bits(a[k]) if a[k].is_floating_point() else a[k],
+                                           _bits(b[k]) if b[k].is_floating_point() else b[k])]
+    assert not bad, bad
+
+
+@pytest.mark.parametrize("shuffler", ["none", "random"])
+@pytest.mark.parametrize("dtype", DTYPES, ids=dt_id)
+def test_big_soup_equals_generic(cuda, dtype, shuffler):
+    """decide -> evolve (attacks, learn_from, self-train, respawn) -> uids -> census of the
+    north-star net: specialised row kernels == runtime-shape engine, bitwise, and the
+    hipGraph replay == eager"""
+    spec = ArchSpec.aggregating(4, 10, 3, shuffler=shuffler)
+
+    def soup():
+        e = SoupEngine(spec, 900, SOUP, device=cuda, seed=21, dtype=dtype)
+        e.stats = True
+        e.evolve(4)
+        torch.cuda.synchronize()
+        return (e.local_rows().clone(), e.uid.clone(), e.loss.clone(), e.action.clone(), e.counterpart.clone(),
+                e.respawn.clone(), e.count())
+
+    a, b = _both(soup)
+    for x, y in zip(a[:-1], b[:-1]):
+        assert torch.equal(_bits(x) if x.is_floating_point() else x, _bits(y) if y.is_floating_point() else y)
+    assert a[-1] == b[-1]
+    assert int((a[3] == 3).sum()) > 0  # self-training happened
+    g = SoupEngine(spec, 900, SOUP, device=cuda, seed=21, dtype=dtype)
+    g.stats = True
+    assert g.capture(warmup=1)
+    e = SoupEngine(spec, 900, SOUP, device=cuda, seed=21, dtype=dtype)
+    e.stats = True
+    e.evolve(1)
+    g.evolve(3)
+    e.evolve(3)
+    torch.cuda.synchronize()
+    assert torch.equal(_bits(g.local_rows()), _bits(e.local_rows())) and torch.equal(g.uid, e.uid)

@@ -69,3 +69,35 @@ def test_checkpoint_reshards_1_to_2(tmp_path):
     mp.start_processes(_resume_worker, args=(2, _port(), ck, str(tmp_path)), nprocs=2, start_method="spawn", join=True)
     W = np.concatenate([np.load(os.path.join(tmp_path, f"r{r}.npy")) for r in range(2)])
     assert np.array_equal(W, a.local_rows().numpy(), equal_nan=True)
+
+
+def test_streaming_checkpoint_16bit_chunks_and_v1_compat(tmp_path):
+    """v2 shards keep the storage format (bf16 as raw bits), stream in chunks smaller than a
+    shard, resume bit-exactly; a v1 (torch .pt, fp32) directory still loads."""
+    spec = ArchSpec.weightwise(2, 2)
+    for dt in (torch.bfloat16, torch.float16):
+        a = SoupEngine(spec, 257, PARAMS, seed=5, dtype=dt)
+        a.evolve(4)
+        b = SoupEngine(spec, 257, PARAMS, seed=5, dtype=dt)
+        b.evolve(2)
+        ck = str(tmp_path / f"ck{dt}")
+        C.save_engine(b, ck, chunk_bytes=1000)  # ~35 rows per chunk
+        r = np.load(os.path.join(ck, f"rows-{0:012d}-{257:012d}.npy"), mmap_mode="r")
+        assert r.dtype == (np.uint16 if dt == torch.bfloat16 else np.float16) and r.shape == (257, spec.P)
+        c = C.load_engine(ck, chunk_bytes=700)
+        c.evolve(2)
+        assert c.dtype == dt and torch.equal(a.local_rows().view(torch.int16), c.local_rows().view(torch.int16))
+        assert torch.equal(a.uid, c.uid)
+    # v1 layout written by the round-1 writer
+    e = SoupEngine(spec, 40, PARAMS, seed=1)
+    e.evolve(2)
+    v1 = tmp_path / "v1"
+    v1.mkdir()
+    torch.save({"W": e.local_rows()[:, :spec.P].clone(), "uid": e.uid.clone()}, str(v1 / f"shard-{0:012d}-{40:012d}.pt"))
+    import json
+    m = dict(format="srnn-checkpoint-v1", kind="soup", spec=json.loads(spec.to_json()), n_total=40, params=PARAMS,
+             seed=1, lr=0.01, shuffle=True, time=2, gen=int(e.gen_dev.item()), next_uid=int(e.next_uid.item()),
+             world=1, dtype="float32", exchange="alltoall")
+    (v1 / "manifest.json").write_text(json.dumps(m))
+    f = C.load_engine(str(v1))
+    assert torch.equal(f.local_rows(), e.local_rows()) and torch.equal(f.uid, e.uid)

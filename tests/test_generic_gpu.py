@@ -64,7 +64,8 @@ def test_generic_equals_templated_on_device(cuda, spec):
                                   ArchSpec.aggregating(4, 10, 3, shuffler="random"), ArchSpec.recurrent(3, 2),
                                   ArchSpec.fft(3, 2, 2)], ids=ids)
 def test_reference_shapes_on_device_vs_oracle(cuda, spec):
-    assert _lib.is_generic(spec, _lib.OP_APPLY)
+    # big aggregating nets (P > 64) have their own row kernels for every dtype / shuffler
+    assert _lib.is_generic(spec, _lib.OP_APPLY) == (not (spec.kind == "aggregating" and spec.P > 64))
     n = 1024
     out = _ops(spec, cuda, n)
     uid = np.arange(n) + 5
