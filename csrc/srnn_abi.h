@@ -94,6 +94,11 @@ struct SrnnArgs {
   int32_t* helper_ctl;
   int32_t perm_e;
   int32_t helpers;      // helper workgroups appended to the generation grid
+  // sharded fused generation with the post-exchange work folded in (flag 524288): the
+  // respawn ballots of the PREVIOUS generation (block stats, u64[4] per 64 rows; temp holds
+  // this generation's) and the counter the unpack workgroups bump for the generation waves
+  void* temp2;
+  int32_t* xdone;
 };
 
 enum SrnnOp {
@@ -121,7 +126,7 @@ enum SrnnOp {
                         // (flag 16384: the same launch also indexes the received rows = OP_SOUP_UNPACK)
 };
 
-int srnn_abi_version();  // 13
+int srnn_abi_version();  // 14
 int srnn_has_config(const SrnnCfg* cfg);
 int srnn_run(int op, const SrnnCfg* cfg, const SrnnArgs* args);
 const char* srnn_last_error();

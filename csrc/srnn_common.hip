@@ -177,7 +177,7 @@ static int with_scratch(int op, const SrnnCfg* c, const SrnnArgs* a) {
 
 extern "C" {
 
-int srnn_abi_version() { return 13; }
+int srnn_abi_version() { return 14; }
 
 const char* srnn_last_error() { return srnn::g_err.c_str(); }
 

@@ -178,6 +178,11 @@ struct Item {
   SRNN_HD static const char* row_of(const SrnnArgs& a, int64_t g) {
     if (a.world <= 1 || (g >= a.lo && g < a.lo + a.n)) return rowp(a.W2, g - a.lo);
     if (a.flags & 128) return rowp(a.recvbuf, g);
+#if defined(__HIP_DEVICE_COMPILE__)
+    if (a.flags & 524288)  // indexed by unpack workgroups of this same launch: memory-side read
+      return reinterpret_cast<const char*>(a.recvbuf) +
+             (int64_t)__hip_atomic_load(a.rmap + g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) * XB;
+#endif
     return reinterpret_cast<const char*>(a.recvbuf) + (int64_t)a.rmap[g] * XB;
   }
 
@@ -705,6 +710,89 @@ __global__ __launch_bounds__(TB) void k_soup_evolve(SrnnCfg c, SrnnArgs a) {
 }
 
 // ----------------------------------------------------------------------------------
+// Post-exchange work of a sharded generation folded into its generation launch (flag
+// 524288) instead of a separate launch between the all-to-all and the generation:
+//   workgroup 0        -- uids of the previous generation's newborns (stats rows of the
+//                         exchange: lower ranks' respawn counts; the previous generation's
+//                         ballots in temp2) + the global census + send-counter reset;
+//   workgroups 1..U    -- index the received rows (rmap[slot] = row, memory-side atomic
+//                         stores), then bump xdone;
+//   the rest           -- generation waves: the next generation's decisions first (they do
+//                         not need the received rows), then wait for xdone == U (bounded
+//                         spin, overflow flag 2 on timeout: never a hang), then evolve.
+// The unpack workgroups have the lowest block ids, so they are dispatched before any
+// generation wave can occupy the machine: the wait always ends.
+// ----------------------------------------------------------------------------------
+template <class Net, class S>
+__device__ void post_uids(const SrnnArgs& a) {
+  using I = Item<Net, S>;
+  const int lane = threadIdx.x;
+  if (lane < a.world) a.sendcnt[lane] = I::SR;  // the finish launch packs the next exchange
+  int64_t pre = 0, tot = 0;
+  if (lane == 0) {
+    int64_t cen[5] = {0, 0, 0, 0, 0}, all = 0;
+    for (int r = 0; r < a.world; ++r) {
+      const int64_t k = I::stat(a, r, 5);
+      if (r < a.rank) pre += k;
+      tot += k;
+      for (int q = 0; q < 5; ++q) cen[q] += I::stat(a, r, q);
+    }
+    for (int q = 0; q < 5; ++q) all += cen[q];
+    if (a.census && all > 0)
+      for (int q = 0; q < 5; ++q) a.census[q] = cen[q];
+  }
+  pre = __shfl(pre, 0);
+  tot = __shfl(tot, 0);
+  unsigned long long* masks = reinterpret_cast<unsigned long long*>(a.temp2);
+  const int64_t nb = (a.n + TB - 1) / TB, ch = (nb + TB - 1) / TB;
+  const int64_t b0 = (int64_t)lane * ch, b1 = b0 + ch < nb ? b0 + ch : nb;
+  int32_t cnt = 0;
+  for (int64_t b = b0; b < b1; ++b) cnt += __popcll(masks[b * 4]);
+  int32_t incl = cnt;
+#pragma unroll
+  for (int off = 1; off < TB; off <<= 1) {
+    const int32_t v = __shfl_up(incl, off);
+    if (lane >= off) incl += v;
+  }
+  const int64_t base = *(volatile const int64_t*)a.uid_base;
+  int64_t u = base + pre + incl - cnt;
+  for (int64_t b = b0; b < b1 && cnt; ++b) {
+    unsigned long long m = masks[b * 4];
+    masks[b * 4] = 0ull;
+    while (m) {
+      const int bit = __ffsll((long long)m) - 1;
+      m &= m - 1;
+      a.uid_out[b * TB + bit] = u++;
+    }
+  }
+  if (lane == 0) ((int64_t*)a.uid_base)[0] = base + tot;
+}
+template <class Net, class S>
+__device__ void post_unpack(const SrnnArgs& a, int64_t k) {
+  using I = Item<Net, S>;
+  if (k < (int64_t)a.world * a.cap && k % a.cap >= I::SR) {
+    const int32_t* tag = reinterpret_cast<const int32_t*>(reinterpret_cast<const char*>(a.recvbuf) + k * I::XB + I::RB);
+    if (tag[1] == I::gen_of(a)) __hip_atomic_store(a.rmap + tag[0], (int32_t)k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's index stores are at memory
+  if (threadIdx.x == 0) __hip_atomic_fetch_add(a.xdone, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void post_wait(const SrnnArgs& a, int32_t want) {
+  int32_t ok = 1;
+  if (threadIdx.x == 0) {
+    uint32_t it = 0;
+    while (__hip_atomic_load(a.xdone, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < want) {
+      __builtin_amdgcn_s_sleep(2);
+      if (++it > (1u << 24)) {  // ~1 s: report instead of hanging the GPU
+        ok = 0;
+        break;
+      }
+    }
+    if (!ok) atomic_or_i32(a.ovf, 2);
+  }
+}
+
+// ----------------------------------------------------------------------------------
 // Fused single-rank soup generation (OP_SOUP_GEN): ONE launch per generation instead of
 // decide -> evolve -> respawn -> classify.  Per lane: the generation (attacks received,
 // learn_from, self-train, respawn + inline re-init), then the NEXT generation's decision
@@ -725,7 +813,23 @@ __global__ __launch_bounds__(TB) void k_soup_gen(SrnnCfg c, SrnnArgs a) {
   constexpr int PERM = (P + 4) & ~3;
   __shared__ float4 s_samp[TB * SAMP];
   __shared__ uint8_t s_perm[TB * PERM];
-  const int64_t i = (int64_t)blockIdx.x * TB + threadIdx.x;
+  const bool post = (a.flags & 524288) != 0;
+  int64_t xoff = 0;
+  int32_t nunpack = 0;
+  if (post) {
+    nunpack = (int32_t)(((int64_t)a.world * a.cap + TB - 1) / TB);
+    if (blockIdx.x == 0) {
+      post_uids<Net, S>(a);
+      return;
+    }
+    if ((int64_t)blockIdx.x <= nunpack) {
+      post_unpack<Net, S>(a, (int64_t)(blockIdx.x - 1) * TB + threadIdx.x);
+      return;
+    }
+    xoff = 1 + nunpack;
+  }
+  const int64_t gb = (int64_t)blockIdx.x - xoff;  // generation block: rows gb*64 ..
+  const int64_t i = gb * TB + threadIdx.x;
   const int lane = threadIdx.x;
   uint8_t* perm = s_perm + lane * PERM;
   const int32_t gen = I::gen_of(a);
@@ -733,7 +837,7 @@ __global__ __launch_bounds__(TB) void k_soup_gen(SrnnCfg c, SrnnArgs a) {
   const bool pre = (a.flags & 131072) != 0;
   if (pre) {
     const int64_t nb_main = (a.n + TB - 1) / TB;
-    if ((int64_t)blockIdx.x >= nb_main) {
+    if (gb >= nb_main) {
       // helper workgroup: work only where fewer than two generation waves share the SIMD
       int32_t cnt = 0;
       if (lane == 0) cnt = __hip_atomic_load(a.helper_ctl + 1 + simd_slot(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -745,18 +849,21 @@ __global__ __launch_bounds__(TB) void k_soup_gen(SrnnCfg c, SrnnArgs a) {
   }
   bool rs = false;
   int8_t k = -1;
+  if (i < a.n && (a.flags & 4096)) {
+    // sharded: the next generation's decisions of EVERY global slot (this lane takes
+    // slots i, i + n, ...): attack lists of local victims + need masks for the pack.
+    // First: they need nothing from the exchange, so they overlap the unpack workgroups
+    for (int64_t g = i; g < a.n_total; g += a.n) {
+      int32_t at, te;
+      I::decision(a, g, gen + 1, at, te);
+      I::link_decision(a, g, at, te, a.i32a, a.i32b);
+    }
+  }
+  if (post) post_wait(a, nunpack);
   if (i < a.n) {
     I::soup_evolve(c, a, i, s_samp + lane, perm);
     rs = a.respawn[i] != 0;
-    if (a.flags & 4096) {
-      // sharded: the next generation's decisions of EVERY global slot (this lane takes
-      // slots i, i + n, ...): attack lists of local victims + need masks for the pack
-      for (int64_t g = i; g < a.n_total; g += a.n) {
-        int32_t at, te;
-        I::decision(a, g, gen + 1, at, te);
-        I::link_decision(a, g, at, te, a.i32a, a.i32b);
-      }
-    } else {
+    if (!(a.flags & 4096)) {
       int32_t at, te;
       I::decision(a, i, gen + 1, at, te);
       if (at >= 0) a.i32b[i] = atomicExch(a.i32a + at, (int32_t)i);
@@ -767,7 +874,7 @@ __global__ __launch_bounds__(TB) void k_soup_gen(SrnnCfg c, SrnnArgs a) {
       k = I::classify_w(w, a.eps, (a.flags & 8) != 0, I::actx(a, c, (uint64_t)(a.lo + i), 0x7FFFFFF0u, perm));
     }
   }
-  if ((a.flags & 65536) && blockIdx.x == 0 && threadIdx.x == 0) {
+  if ((a.flags & 65536) && gb == 0 && threadIdx.x == 0) {
     // asynchronous finish: this launch advances the generation counter (the other ring
     // slot: no block of this launch reads it) so the next generation needs nothing from
     // the finish kernel, which runs beside it on a side stream
@@ -785,7 +892,7 @@ __global__ __launch_bounds__(TB) void k_soup_gen(SrnnCfg c, SrnnArgs a) {
   unsigned long long* bs = reinterpret_cast<unsigned long long*>(a.temp);
   if (a.flags & 2048) {  // two-phase: plain stores, k_gen_finish reads them after the kernel boundary
     if (lane == 0) {
-      unsigned long long* mine = bs + (int64_t)blockIdx.x * 4;
+      unsigned long long* mine = bs + gb * 4;
       mine[0] = m;
       mine[1] = (unsigned long long)cnt[0] | ((unsigned long long)cnt[1] << 32);
       mine[2] = (unsigned long long)cnt[2] | ((unsigned long long)cnt[3] << 32);
@@ -796,7 +903,7 @@ __global__ __launch_bounds__(TB) void k_soup_gen(SrnnCfg c, SrnnArgs a) {
   }
   int32_t prev = 0;
   if (lane == 0) {
-    unsigned long long* mine = bs + (int64_t)blockIdx.x * 4;
+    unsigned long long* mine = bs + gb * 4;
     __hip_atomic_store(mine + 0, m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __hip_atomic_store(mine + 1, (unsigned long long)cnt[0] | ((unsigned long long)cnt[1] << 32), __ATOMIC_RELAXED,
                        __HIP_MEMORY_SCOPE_AGENT);
@@ -807,7 +914,7 @@ __global__ __launch_bounds__(TB) void k_soup_gen(SrnnCfg c, SrnnArgs a) {
     prev = __hip_atomic_fetch_add(a.i32d, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   prev = __shfl(prev, 0);
-  const int32_t nb = (int32_t)gridDim.x;
+  const int32_t nb = (int32_t)(gridDim.x - xoff);
   if (prev != nb - 1) return;
   // ---- last wave: census + sequential uids of the newborns (blocks in slot order)
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
@@ -913,6 +1020,7 @@ __global__ __launch_bounds__(NT) void k_gen_finish(SrnnArgs a, int32_t nb) {
   __shared__ unsigned long long s_cs[5];
   const int t = threadIdx.x;
   if (t < 5) s_cs[t] = 0;
+  if (t == 0 && a.xdone) *a.xdone = 0;  // re-armed for the next generation's unpack workgroups
   if ((a.flags & 131072) && a.helper_ctl)  // re-arm this parity's helper queue / SIMD counts
     for (int q = t; q < HELPER_CTL; q += NT) a.helper_ctl[q] = 0;
   const unsigned long long* bs = reinterpret_cast<const unsigned long long*>(a.temp);
@@ -1090,10 +1198,22 @@ int gen_finish(const SrnnCfg&, const SrnnArgs& a) {
 }
 
 template <class Net, class S>
+int uid_assign(const SrnnCfg& c, const SrnnArgs& a);
+
+template <class Net, class S>
 int soup_gen(const SrnnCfg& c, const SrnnArgs& a) {
   using I = Item<Net, S>;
   if (!a.dev) {
     // host: the same steps in order (evolve all rows, link next decisions, census, uids)
+    if (a.flags & 524288) {
+      // post-exchange work first: previous generation's uids (ballots in temp2), received-row
+      // index, send-counter reset -- the device's workgroup 0 and unpack workgroups
+      SrnnArgs ua = a;
+      ua.flags = (a.flags & ~524288) | 16384 | 8192;
+      ua.temp = a.temp2;
+      ua.counts = nullptr;
+      uid_assign<Net, S>(c, ua);
+    }
     const int32_t gen = I::gen_of(a);
     host_parallel(a.n, [&](int64_t i) {
       float4 samp[Net::P + 1];
@@ -1167,11 +1287,20 @@ int soup_gen(const SrnnCfg& c, const SrnnArgs& a) {
     return -2;
   }
   const int64_t helpers = (a.flags & 131072) ? (a.helpers > 0 ? a.helpers : 0) : 0;
+  int64_t xblocks = 0;
+  if (a.flags & 524288) {
+    if (!(a.flags & 4096) || !(a.flags & 2048) || !a.temp2 || !a.xdone || !a.rmap || !a.recvbuf || a.world > 64) {
+      set_error("post-exchange generation needs a sharded two-phase generation, temp2, xdone, rmap, recvbuf");
+      return -5;
+    }
+    xblocks = 1 + ((int64_t)a.world * a.cap + TB - 1) / TB;
+  }
   if ((a.flags & 131072) && (!a.perm_cur || !a.perm_next || !a.helper_ctl || !(a.flags & 2048) || a.perm_e < 1)) {
     set_error("precomputed permutations need perm_cur / perm_next / helper_ctl, perm_e >= 1 and a two-phase generation");
     return -5;
   }
-  hipLaunchKernelGGL((k_soup_gen<Net, S>), dim3((unsigned)(blocks + helpers)), dim3(TB), 0, (hipStream_t)a.stream, c, a);
+  hipLaunchKernelGGL((k_soup_gen<Net, S>), dim3((unsigned)(xblocks + blocks + helpers)), dim3(TB), 0,
+                     (hipStream_t)a.stream, c, a);
   if ((a.flags & 2048) && !(a.flags & 65536)) {
     constexpr int FNT = SRNN_FINISH_NT;
     const int64_t pack_blocks = (a.flags & 32768) ? (a.n + FNT - 1) / FNT : 0;

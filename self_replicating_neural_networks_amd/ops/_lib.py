@@ -20,7 +20,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 # SRNN_LIB: load another build of the library (A/B of compiler flags on the GPU box)
 LIB_PATH = os.environ.get("SRNN_LIB") or os.path.join(_HERE, "libsrnn.so")
 CSRC = os.path.normpath(os.path.join(_HERE, "..", "..", "csrc"))
-ABI_VERSION = 13
+ABI_VERSION = 14
 
 OP_INIT = 0
 OP_APPLY = 1
@@ -61,6 +61,7 @@ FLAG_FINISH_PACK = 32768
 FLAG_ASYNC_FINISH = 65536
 FLAG_PRE_PERMS = 131072
 FLAG_FINISH_BATCH = 262144
+FLAG_GEN_POST = 524288   # sharded: uids + received-row index folded into the generation launch
 HELPER_CTL = 1 + 8192  # helper work-queue head + per-SIMD generation-wave counts (csrc/srnn_kernels.h)
 
 
@@ -93,7 +94,7 @@ class SrnnArgs(ctypes.Structure):
         ("dev", ctypes.c_int32), ("pad1", ctypes.c_int32), ("stream", _P), ("gen_out", _P),
         ("scratch", _P), ("scratch_bytes", ctypes.c_int64),
         ("perm_cur", _P), ("perm_next", _P), ("helper_ctl", _P), ("perm_e", ctypes.c_int32),
-        ("helpers", ctypes.c_int32),
+        ("helpers", ctypes.c_int32), ("temp2", _P), ("xdone", _P),
     ]
 
 

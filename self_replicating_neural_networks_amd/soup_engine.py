@@ -197,6 +197,15 @@ class SoupEngine:
         self._bs_ring = torch.zeros((self._batch, max(nb, 1) * 8), **i32) if fm == "batch" else None
         self._pending_fin = 0  # batch mode: generations whose finish is still due
         self._blockstats = [self._blockstat, torch.zeros_like(self._blockstat)] if self.async_finish else None
+        # sharded fused generations fold the post-exchange launch (previous generation's
+        # uids + received-row index) into the generation launch: block stats by parity (the
+        # launch reads the previous generation's ballots while writing its own) and the
+        # unpack-done counter its generation waves wait on (SRNN_POST_IN_GEN=0: separate
+        # post-exchange launch, round-1 pipeline)
+        self.post_in_gen = (self.dist.enabled and exchange == "alltoall" and self.fused
+                            and os.environ.get("SRNN_POST_IN_GEN", "1") == "1")
+        self._bs2 = [self._blockstat, torch.zeros_like(self._blockstat)] if self.post_in_gen else None
+        self._xdone = torch.zeros(1, **i32) if self.post_in_gen else None
         self._side = torch.cuda.Stream(self.device) if self.async_finish else None
         self._fin_ev = [None, None]  # finish events of the generations that wrote each block-stats buffer
         # SGD permutations precomputed by helper waves of the previous generation
@@ -395,6 +404,11 @@ class SoupEngine:
                 # sharded: every global slot's next decisions; counts feed the next pack
                 fa.flags |= _lib.FLAG_TWO_PHASE | _lib.FLAG_SHARDED_DECIDE | _lib.FLAG_FINISH_PACK
                 census = self.spec.shuffler == "none"
+                if self.post_in_gen:
+                    bs, prev = self._bs2[self._p], self._bs2[1 - self._p]
+                    fa.temp, fa.temp_bytes = _p(bs), bs.numel() * 4
+                    fa.temp2, fa.xdone = _p(prev), _p(self._xdone)
+                    fa.flags |= _lib.FLAG_GEN_POST | _lib.FLAG_STATS_X
             if census:
                 fa.flags |= _lib.FLAG_FUSED_CENSUS | (_lib.FLAG_FIX_SEC if self.stats_with_sec else 0)
             if self.dist.enabled:
@@ -409,6 +423,13 @@ class SoupEngine:
                 ca = fa
         self._arg_cache[key] = (a, ca, a.flags)
         return self._arg_cache[key]
+
+    def _ballots(self) -> torch.Tensor:
+        """Block stats holding the pending respawn ballots: the last generation's parity
+        buffer when it was a post-in-gen fused generation, else the single buffer."""
+        if self.post_in_gen and self._mask_src == "bs":
+            return self._bs2[1 - self._p]
+        return self._blockstat
 
     def _uid_flags(self, flags: int) -> int:
         """uid assignment reads the respawn ballots where the producing generation left
@@ -500,12 +521,13 @@ class SoupEngine:
             if not self._packed:
                 _lib.run(_lib.OP_SOUP_PACK, spec, a, cfg)
             d.all_to_all(self.recvbuf, self.sendbuf)
-            # post-exchange launch: block 0 assigns the uids of the previous generation's
-            # newborns (stats rows of the exchange), the other blocks index the received rows
-            a.flags = self._uid_flags(flags | _lib.FLAG_STATS_X | _lib.FLAG_POST_UNPACK)
-            a.temp, a.temp_bytes = _p(self._blockstat), self._blockstat.numel() * 4
-            _lib.run(_lib.OP_UID_ASSIGN, spec, a, cfg)
-            a.flags = flags
+            if not self.post_in_gen:
+                # post-exchange launch: block 0 assigns the uids of the previous generation's
+                # newborns (stats rows of the exchange), the other blocks index the received rows
+                a.flags = self._uid_flags(flags | _lib.FLAG_STATS_X | _lib.FLAG_POST_UNPACK)
+                a.temp, a.temp_bytes = _p(self._blockstat), self._blockstat.numel() * 4
+                _lib.run(_lib.OP_UID_ASSIGN, spec, a, cfg)
+                a.flags = flags
             # generation (evolve + census + next decisions of every slot); finish launch:
             # block 0 closes the generation, the other blocks pack the next exchange
             _lib.run(_lib.OP_SOUP_GEN, spec, fa, cfg)
@@ -535,7 +557,8 @@ class SoupEngine:
             d.all_to_all(self.recvbuf, self.sendbuf)
             _lib.run(_lib.OP_SOUP_UNPACK, spec, a, cfg)
             a.flags = self._uid_flags(flags | _lib.FLAG_STATS_X)
-            a.temp, a.temp_bytes = _p(self._blockstat), self._blockstat.numel() * 4
+            bs = self._ballots()
+            a.temp, a.temp_bytes = _p(bs), bs.numel() * 4
             _lib.run(_lib.OP_UID_ASSIGN, spec, a, cfg)
         self._lists_ready = False
         self._mask_src = "i32c"
@@ -586,7 +609,8 @@ class SoupEngine:
             return
         a, _, flags = self._gen_args()
         a.flags = self._uid_flags(flags)
-        a.temp, a.temp_bytes = _p(self._blockstat), self._blockstat.numel() * 4
+        bs = self._ballots()
+        a.temp, a.temp_bytes = _p(bs), bs.numel() * 4
         self.dist.all_gather_into(self.stats_all, self.counts)
         _lib.run(_lib.OP_UID_ASSIGN, self.spec, a, self.cfg)
         a.flags = flags
@@ -696,8 +720,8 @@ class SoupEngine:
         """Every device tensor a generation reads or writes (graph validation)."""
         names = ["_bufs", "uid", "next_uid", "_gen_ring", "heads", "nexts", "flags32", "action", "counterpart",
                  "loss", "respawn", "counts", "census", "need", "sendcnt", "rmap", "ovf", "sendbuf", "recvbuf",
-                 "full", "stats_all", "_blockstats" if self._blockstats else "_blockstat", "_done", "_perms",
-                 "_helper_ctl", "_bs_ring"]
+                 "full", "stats_all", "_blockstats" if self._blockstats else ("_bs2" if self._bs2 else "_blockstat"),
+                 "_done", "_perms", "_helper_ctl", "_bs_ring", "_xdone"]
         out = []
         for k in names:
             v = getattr(self, k, None)
@@ -723,11 +747,11 @@ class SoupEngine:
             # torch's process-group collectives are not captured: their watchdog thread
             # queries events recorded by the capturing stream
             return False
-        if self.dist.world > 1 and os.environ.get("SRNN_SHARDED_GRAPH", "0") != "1":
-            # multi-GPU generations run eagerly by default: a generation is ~0.1 ms of GPU
-            # work against ~0.04 ms of host enqueue, so the host stays ahead; capturing RCCL
-            # peer-to-peer collectives is validated with one rank only (opt in with
-            # SRNN_SHARDED_GRAPH=1)
+        if self.dist.world > 1 and os.environ.get("SRNN_SHARDED_GRAPH", "1") != "1":
+            # SRNN_SHARDED_GRAPH=0: multi-GPU generations run eagerly (RCCL all-to-all
+            # enqueued per generation from the host).  By default the all-to-all is captured
+            # with the kernels; the replay is validated bitwise against eager generations on
+            # every rank and all ranks fall back to eager unless every rank agrees
             return False
         s = torch.cuda.Stream(self.device)
         s.wait_stream(torch.cuda.current_stream(self.device))
