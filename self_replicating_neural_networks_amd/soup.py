@@ -9,7 +9,8 @@
   generation is one fused kernel pipeline (``SoupEngine``), optionally sharded over the
   ranks of a process group.  Within a generation all reads come from the
   generation-start weights (synchronous update); population-level statistics match the
-  sequential mode (tests/test_soup.py::test_device_vs_sequential_statistics_training_soup).
+  sequential mode and the published curves (tests/test_soup_statistics.py: learn_from
+  severities, Mann-Whitney U device vs sequential; trajectory-soup census 13/7).
 
 ``mode="auto"`` picks sequential for ``size <= 100`` and device otherwise.
 """
