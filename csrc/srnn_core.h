@@ -330,6 +330,80 @@ SRNN_HD void glorot_fill(float* w, int off, int r, int c, const Rng& rng, uint64
   }
 }
 
+// Keras 2.2.4's Orthogonal initializer is the left singular matrix U of a gaussian matrix,
+// taken from numpy.linalg.svd -- LAPACK dgesdd, whose sign conventions make U far from Haar:
+// for 2x2 it is ALWAYS a reflection (det -1) with a biased angle, for 1x1 it is sign(a).
+// That changes the dynamics of linear SimpleRNN stacks: RecurrentNeuralNetwork(2, 2)
+// self-training diverges for 76 % of the nets with LAPACK's U (the published 38/50) and for
+// ~48 % with a Haar-distributed orthogonal kernel (bench/rnn_divergence_bisect.py).
+// lapack_u2 reproduces dgesdd's U for a 2x2 matrix step by step (dgebrd: one Householder
+// reflector dlarfg on the first column; dbdsqr on the 2x2 upper bidiagonal: dlasv2's left
+// rotation; singular values made positive by flipping rows of V^T, already sorted), which
+// tests/test_native_cpu.py checks against numpy.linalg.svd to ~1e-14.
+SRNN_HD inline double f_sign(double a, double b) { return b >= 0.0 ? fabs(a) : -fabs(a); }  // Fortran SIGN
+SRNN_HD inline void dlasv2_left(double f, double g, double h, double* csl, double* snl) {
+  double ft = f, fa = fabs(f), ht = h, ha = fabs(h);
+  int pmax = 1;
+  const bool swap = ha > fa;
+  if (swap) {
+    pmax = 3;
+    double t = ft; ft = ht; ht = t;
+    t = fa; fa = ha; ha = t;
+  }
+  const double gt = g, ga = fabs(g);
+  double clt, crt, slt, srt;
+  if (ga == 0.0) {
+    clt = 1.0, crt = 1.0, slt = 0.0, srt = 0.0;
+  } else {
+    bool gasmal = true;
+    if (ga > fa) {
+      pmax = 2;
+      if (fa / ga < 2.220446049250313e-16) {
+        gasmal = false;
+        clt = 1.0, slt = ht / gt, srt = 1.0, crt = ft / gt;
+      }
+    }
+    if (gasmal) {
+      const double d = fa - ha;
+      double l = (d == fa) ? 1.0 : d / fa;
+      const double m = gt / ft;
+      double t = 2.0 - l;
+      const double mm = m * m, tt = t * t;
+      const double s = sqrt(tt + mm);
+      const double r = (l == 0.0) ? fabs(m) : sqrt(l * l + mm);
+      const double a = 0.5 * (s + r);
+      if (mm == 0.0) t = (l == 0.0) ? f_sign(2.0, ft) * f_sign(1.0, gt) : gt / f_sign(d, ft) + m / t;
+      else t = (m / (s + t) + m / (r + l)) * (1.0 + a);
+      l = sqrt(t * t + 4.0);
+      crt = 2.0 / l, srt = t / l;
+      clt = (crt + srt * m) / a;
+      slt = (ht / ft) * srt / a;
+    }
+  }
+  (void)pmax;
+  if (swap) *csl = srt, *snl = crt;
+  else *csl = clt, *snl = slt;
+}
+// U of numpy.linalg.svd(a) for a 2x2 a (row-major), in place
+SRNN_HD inline void lapack_u2(double (&a)[2][2]) {
+  const double a11 = a[0][0], a12 = a[0][1], a21 = a[1][0], a22 = a[1][1];
+  double tau = 0.0, v = 0.0, beta = a11;
+  if (a21 != 0.0) {  // dlarfg(2, a11, a21)
+    beta = -f_sign(hypot(a11, a21), a11);
+    tau = (beta - a11) / beta;
+    v = a21 / (a11 - beta);
+  }
+  const double w = a12 + v * a22;
+  double csl, snl;
+  dlasv2_left(beta, a12 - tau * w, a22 - tau * v * w, &csl, &snl);
+  // U = (I - tau [1 v]^T [1 v]) * [[csl, -snl], [snl, csl]]
+  const double q00 = 1.0 - tau, q01 = -tau * v, q11 = 1.0 - tau * v * v;
+  a[0][0] = q00 * csl + q01 * snl;
+  a[0][1] = -q00 * snl + q01 * csl;
+  a[1][0] = q01 * csl + q11 * snl;
+  a[1][1] = -q01 * snl + q11 * csl;
+}
+
 // orthogonal (n, n) kernel by modified Gram-Schmidt of a gaussian matrix with
 // sign(diag R) correction == QR with positive diagonal (Haar distributed).  The
 // orthogonalisation runs in double (Keras' initializer is a float64 numpy QR): in float32
@@ -358,7 +432,14 @@ SRNN_HD void orthogonal_fill(float* w, int off, const Rng& rng, uint64_t uid) {
       a[i][j] = (double)nrm[cnt & 3];
       ++cnt;
     }
-  // Gram-Schmidt on columns
+  if constexpr (N == 2) {  // Keras / LAPACK convention (see lapack_u2)
+    lapack_u2(a);
+    for (int i = 0; i < N; ++i)
+      for (int j = 0; j < N; ++j) w[off + i * N + j] = (float)a[i][j];
+    return;
+  }
+  // Gram-Schmidt on columns (N = 1: sign(a), LAPACK's U too; N >= 3: Haar, an approximation
+  // of LAPACK's sign conventions -- parity is pinned for the reference's width-2 nets)
   for (int j = 0; j < N; ++j) {
     for (int p = 0; p < j; ++p) {
       double d = 0.0;

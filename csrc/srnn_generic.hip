@@ -313,6 +313,13 @@ SRNN_HD void g_orthogonal(SV w, int off, int N, double* a, const Rng& rng, uint6
       a[i * N + j] = (double)nrm[cnt & 3];
       ++cnt;
     }
+  if (N == 2) {  // Keras / LAPACK convention (lapack_u2 of srnn_core.h)
+    double m[2][2] = {{a[0], a[1]}, {a[2], a[3]}};
+    lapack_u2(m);
+    for (int i = 0; i < 2; ++i)
+      for (int j = 0; j < 2; ++j) w[off + i * 2 + j] = (float)m[i][j];
+    return;
+  }
   for (int j = 0; j < N; ++j) {
     for (int p = 0; p < j; ++p) {
       double d = 0.0;

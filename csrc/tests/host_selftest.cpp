@@ -212,7 +212,7 @@ static std::vector<float> soup(int R, int64_t N, int gens, std::vector<int64_t>*
 }
 
 int main() {
-  CHECK(srnn_abi_version() == 13);
+  CHECK(srnn_abi_version() == 14);
   ops_smoke(ww22(), 1000);
   ops_smoke(agg422(), 777);
   ops_smoke(cfg(2, 2, 2, 0, 17), 300);              // Recurrent(2,2): templated BPTT

@@ -127,8 +127,13 @@ def _orthogonal(w, off, N, seed, uids):
         r2 = np.sqrt(np.float32(-2.0) * np.log(u01_open0(u[2])))
         t2 = np.float32(6.283185307179586) * u01(u[3])
         vals += [r1 * np.cos(t1), r1 * np.sin(t1), r2 * np.cos(t2), r2 * np.sin(t2)]
-    # modified Gram-Schmidt in float64 (Keras' orthogonal initializer is a float64 QR)
     a = np.stack(vals[:N * N], axis=1).astype(np.float32).astype(np.float64).reshape(n, N, N)
+    if N == 2:
+        # Keras 2.2.4 Orthogonal = U of numpy.linalg.svd (LAPACK dgesdd): for 2x2 always a
+        # reflection with a biased angle -- not Haar (csrc/srnn_core.h lapack_u2)
+        w[:, off:off + 4] = np.linalg.svd(a)[0].astype(np.float32).reshape(n, 4)
+        return
+    # modified Gram-Schmidt in float64 (N = 1: sign(a) = LAPACK's U; N >= 3: Haar)
     for j in range(N):
         for p in range(j):
             d = np.sum(a[:, :, p] * a[:, :, j], axis=1)

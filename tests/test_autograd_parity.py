@@ -135,9 +135,10 @@ def test_weightwise_train_matches_autograd_gpu():
 
 
 def test_recurrent_divergence_rate_matches_autograd_model():
-    """The 1000-epoch Recurrent divergence fraction (the open parity item, docs/semantics.md §7)
+    """The 1000-epoch Recurrent divergence fraction (published 38/50 = 76 %, docs/semantics.md §7)
     is decided within the first few SGD steps; our kernel and the autograd model of the Keras
-    math agree on which nets diverge in the first 10 steps."""
+    math agree on which nets diverge in the first 10 steps, at the published rate (Keras'
+    LAPACK-convention orthogonal init, csrc/srnn_core.h lapack_u2)."""
     spec = ArchSpec.recurrent(2, 2)
     pop = _pop(spec, 400, "cpu", 11)
     w0 = pop.weights().detach().cpu().double()
@@ -146,7 +147,7 @@ def test_recurrent_divergence_rate_matches_autograd_model():
     ref = _rnn_autograd_train(spec, w0, 10)
     refd = ~torch.isfinite(ref).all(1) | (ref.abs() > 3e38).any(1)
     frac = got.float().mean().item()
-    assert 0.35 < frac < 0.6, frac
+    assert 0.66 < frac < 0.86, frac
     assert (got != refd).float().mean().item() < 0.02
 
 

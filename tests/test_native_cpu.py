@@ -164,3 +164,21 @@ def test_any_shape_runs_and_bad_layouts_fail_loudly():
     assert _lib.is_generic(spec, _lib.OP_INIT)
     with pytest.raises(ValueError):
         K.init_rows(spec, torch.zeros(2, spec.PP + 4), torch.arange(2), 0)
+
+
+def test_orthogonal_init_follows_lapack_svd_conventions():
+    """Keras' Orthogonal = U of numpy.linalg.svd: 2x2 recurrent kernels are reflections
+    (det -1) and equal numpy's U of the same gaussian matrix (oracle) to float32 rounding."""
+    import numpy as np
+    from self_replicating_neural_networks_amd.oracle import core as O
+    spec = ArchSpec.recurrent(2, 2)
+    uid = torch.arange(3000, dtype=torch.int64)
+    W = torch.zeros(3000, spec.PP)
+    K.init_rows(spec, W, uid, 13)
+    w = W[:, :spec.P].numpy()
+    o = O.init(spec, np.arange(3000), 13)
+    assert np.max(np.abs(w - o)) < 1e-5  # float32 Box-Muller: host libm vs numpy ulps
+    off = spec.offsets[1]  # first recurrent kernel (2x2)
+    R = w[:, off:off + 4].reshape(-1, 2, 2).astype(np.float64)
+    assert np.allclose(np.linalg.det(R), -1.0, atol=1e-5)
+    assert np.allclose(R @ R.transpose(0, 2, 1), np.eye(2), atol=1e-6)

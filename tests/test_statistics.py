@@ -89,3 +89,17 @@ def test_network_trajectorys_records(tmp_path):
     assert len(t.historical_particles) == 20
     states = next(iter(t.historical_particles.values()))
     assert states[0]["action"] == "init" and [s["time"] for s in states] == list(range(len(states)))
+
+
+def test_training_fixpoints_recurrent_divergence():
+    """1000-epoch Recurrent self-training: published 38/50 divergent, 12/50 other
+    (code/results/exp-training_fixpoint-*/log.txt:9-10).  Pinned by Keras' Orthogonal
+    initializer being LAPACK's SVD U (a reflection for 2x2 kernels), csrc/srnn_core.h
+    lapack_u2; with a Haar orthogonal init ~48 % diverge."""
+    import tempfile
+    with tempfile.TemporaryDirectory() as d:
+        r = E.training_fixpoints(trials=400, device="cpu", seed=8, root=d, specs=(E.RNN,))
+    c = r["counters"][0]
+    assert c["divergent"] + c["other"] + c["fix_other"] + c["fix_zero"] + c["fix_sec"] == 400
+    assert within(c["divergent"] / 400, 400, 38 / 50, 50)
+    assert c["divergent"] / 400 > 0.62
