@@ -193,7 +193,7 @@ class SoupEngine:
         self.async_finish = fm == "async"
         # the ring holds 32 B per 64-row block per pending generation: at HBM-filling sizes
         # (2e9 rows = 1 GB per generation) fewer generations share one finish launch
-        self._batch = max(1, min(int(os.environ.get("SRNN_GRAPH_CHUNK", "8")), (512 << 20) // (max(nb, 1) * 32)))
+        self._batch = max(1, min(max(self._chunk_sizes() or [1]), (512 << 20) // (max(nb, 1) * 32)))
         self._bs_ring = torch.zeros((self._batch, max(nb, 1) * 8), **i32) if fm == "batch" else None
         self._pending_fin = 0  # batch mode: generations whose finish is still due
         self._blockstats = [self._blockstat, torch.zeros_like(self._blockstat)] if self.async_finish else None
@@ -240,7 +240,8 @@ class SoupEngine:
         self.stats = False          # classify + all-reduce every generation
         self.stats_with_sec = True
         self._graphs = None
-        self._chunk = None          # (graph of G generations, start parity, G)
+        self._chunk = None          # (graph of G generations, start parity, G): the largest
+        self._chunks = []           # every captured multi-generation graph, largest first
         self._arg_cache = {}
         # initial particles: uids 0..n_total-1, keyed init (identical for any rank count)
         local = self.local_rows()
@@ -647,8 +648,9 @@ class SoupEngine:
     def evolve(self, iterations: int = 1, record: bool = False):
         left = int(iterations)
         while left > 0:
-            ch = self._chunk
-            if (ch is not None and not (record and self.recorder is not None) and left >= ch[2]
+            # the largest captured multi-generation graph that fits what is left
+            ch = next((c for c in self._chunks if c[2] <= left), None)
+            if (ch is not None and not (record and self.recorder is not None)
                     and self._p == ch[1] and self.trajectory is None and self.metrics is None):
                 # G generations in one graph launch (no inter-graph gaps)
                 self._join_side()
@@ -793,14 +795,27 @@ class SoupEngine:
         self._capture_chunk(s, p0, pend0)
         return True
 
+    @staticmethod
+    def _chunk_sizes():
+        """Generations per multi-generation graph (SRNN_GRAPH_CHUNKS, even sizes): an evolve
+        of K generations replays the largest that fit, so a short timed region pays few
+        launches and few finish launches (16 + 4 for K = 20 instead of 8 + 8 + 4 singles)."""
+        v = os.environ.get("SRNN_GRAPH_CHUNKS") or os.environ.get("SRNN_GRAPH_CHUNK") or "16,8,4,2"
+        return sorted({int(x) for x in v.split(",") if int(x) >= 2 and int(x) % 2 == 0}, reverse=True)
+
     def _capture_chunk(self, s, p0, pend0):
+        self._chunks = []
+        for G in self._chunk_sizes():
+            ch = self._capture_chunk_g(s, p0, pend0, G)
+            if ch is None:
+                break
+            self._chunks.append(ch)
+        self._chunk = self._chunks[0] if self._chunks else None
+
+    def _capture_chunk_g(self, s, p0, pend0, G):
         """A graph of G consecutive generations (G even: it starts and ends at parity
         p0) replayed as one launch, removing the per-generation graph-launch gap;
         validated bitwise against G eager generations (all ranks agree or none use it)."""
-        self._chunk = None
-        G = int(os.environ.get("SRNN_GRAPH_CHUNK", "8"))
-        if G < 2 or G % 2:
-            return
         ok = True
         gc = torch.cuda.CUDAGraph()
         flags0 = (self._lists_ready, self._mask_src, self._packed, self._perms_ready, self._pending_fin)
@@ -821,18 +836,18 @@ class SoupEngine:
             flag = torch.tensor([1 if ok else 0], dtype=torch.int32, device=self.device)
             torch.distributed.all_reduce(flag, op=torch.distributed.ReduceOp.MIN)
             ok = bool(flag.item())
-        if ok:
-            self._chunk = (gc, p0, G)
+        return (gc, p0, G) if ok else None
 
     def release_graphs(self):
         """Drop the captured graphs (before tearing down the process group: an RCCL
         communicator must not be destroyed while graph executables still reference it)."""
-        if self._graphs is not None or self._chunk is not None:
+        if self._graphs is not None or self._chunks:
             torch.cuda.synchronize(self.device)
-            for g in (self._graphs or []) + ([self._chunk[0]] if self._chunk else []):
+            for g in (self._graphs or []) + [c[0] for c in self._chunks]:
                 g.reset()
             self._graphs = None
             self._chunk = None
+            self._chunks = []
 
     def _validate_graphs(self, graphs) -> bool:
         def replay():

@@ -287,8 +287,8 @@ def test_fused_generation_equals_unfused(cuda, spec):
 
 
 def test_multi_generation_graph_equals_eager(cuda):
-    """capture() also records a graph of 8 consecutive generations (one launch): 21
-    generations through it (+ single-generation graphs for the remainder) == eager."""
+    """capture() also records graphs of 16, 8, 4 and 2 consecutive generations (one launch
+    each): 21 generations through them (16 + 4 + a single-generation graph) == eager."""
     spec = ArchSpec.weightwise(2, 2)
     params = dict(attacking_rate=0.1, learn_from_rate=0.1, train=4, remove_divergent=True, remove_zero=True,
                   epsilon=1e-4)
@@ -296,7 +296,7 @@ def test_multi_generation_graph_equals_eager(cuda):
     b = SoupEngine(spec, 30000, params, device=cuda, seed=21)
     a.stats = b.stats = True
     assert a.capture(warmup=1)
-    assert a._chunk is not None and a._chunk[2] == 8
+    assert a._chunk is not None and [c[2] for c in a._chunks] == [16, 8, 4, 2]
     b.evolve(1)
     a.evolve(21)
     b.evolve(21)
