@@ -340,8 +340,8 @@ SRNN_HD void glorot_fill(float* w, int off, int r, int c, const Rng& rng, uint64
 // reflector dlarfg on the first column; dbdsqr on the 2x2 upper bidiagonal: dlasv2's left
 // rotation; singular values made positive by flipping rows of V^T, already sorted), which
 // tests/test_native_cpu.py checks against numpy.linalg.svd to ~1e-14.
-SRNN_HD inline double f_sign(double a, double b) { return b >= 0.0 ? fabs(a) : -fabs(a); }  // Fortran SIGN
-SRNN_HD inline void dlasv2_left(double f, double g, double h, double* csl, double* snl) {
+SRNN_HD double f_sign(double a, double b) { return b >= 0.0 ? fabs(a) : -fabs(a); }  // Fortran SIGN
+SRNN_HD void dlasv2_left(double f, double g, double h, double* csl, double* snl) {
   double ft = f, fa = fabs(f), ht = h, ha = fabs(h);
   int pmax = 1;
   const bool swap = ha > fa;
@@ -385,7 +385,7 @@ SRNN_HD inline void dlasv2_left(double f, double g, double h, double* csl, doubl
   else *csl = clt, *snl = slt;
 }
 // U of numpy.linalg.svd(a) for a 2x2 a (row-major), in place
-SRNN_HD inline void lapack_u2(double (&a)[2][2]) {
+SRNN_HD void lapack_u2(double (&a)[2][2]) {
   const double a11 = a[0][0], a12 = a[0][1], a21 = a[1][0], a22 = a[1][1];
   double tau = 0.0, v = 0.0, beta = a11;
   if (a21 != 0.0) {  // dlarfg(2, a11, a21)

@@ -18,6 +18,7 @@
 // 64 lanes of a wave touch 64 consecutive floats (coalesced) on every access.
 #include "srnn_kernels.h"
 
+#include <cstdlib>
 #include <cstring>
 #include <vector>
 
@@ -1099,6 +1100,308 @@ static void host_generic(int op, const GShape& s, const SrnnArgs& a) {
   }
 }
 
+// ==================================================================================
+// Long recurrent nets, wave per particle (the analogue of long context is the
+// sequence length P of a Recurrent net -- its own weight vector).  The lane-per-particle
+// path above streams every weight and state of a wide net through its element-major
+// scratch on every multiply (RecurrentNeuralNetwork(16, 2), P = 801: 30M BPTT timesteps/s).
+// Here one 64-lane wave owns a particle: the weights, the gradient accumulators and the
+// input sequence live in LDS (3P floats), lane j computes unit j of a layer, the hidden
+// state is double-buffered in LDS (one wave barrier per layer and timestep), and the
+// per-timestep states needed by BPTT go to a per-wave region of device scratch (written
+// forward, read backward, coalesced).  Every dot product keeps the lane path's order (x[0]*k
+// then fma over the inputs; BPTT sums over j from 0), so results equal the lane path's.
+// ==================================================================================
+constexpr int RW_MIN_WIDTH = 8;  // narrower nets stay lane per particle (64 particles per wave)
+
+struct RWave {
+  float* w;      // [P] the net's weights
+  float* aux;    // [P] gradient accumulators / application output
+  float* seq;    // [P] input sequence (samples / target weights)
+  float* h0;     // [HS] hidden state, double-buffered
+  float* h1;
+  float* carry;  // [HS]
+  float* dtop;   // [64]
+  float* dh;     // [64]
+  float* hst;    // [HS] staged states of timestep t and t - 1 (BPTT)
+  float* hsp;
+};
+__device__ __forceinline__ RWave rw_layout(const GShape& s, float* sm) {
+  RWave r;
+  r.w = sm;
+  r.aux = r.w + s.P;
+  r.seq = r.aux + s.P;
+  r.h0 = r.seq + s.P;
+  r.h1 = r.h0 + s.HS;
+  r.carry = r.h1 + s.HS;
+  r.hst = r.carry + s.HS;
+  r.hsp = r.hst + s.HS;
+  r.dtop = r.hsp + s.HS;
+  r.dh = r.dtop + 64;
+  return r;
+}
+static inline size_t rw_lds_bytes(const GShape& s) { return ((size_t)3 * s.P + 6 * s.HS + 128) * sizeof(float); }
+__device__ __forceinline__ void rw_sync() { __syncthreads(); }  // one-wave workgroup: orders LDS
+
+// acc = x[0]*k[0] then fma over i (mul_first), or fma over i from acc; k strided by ks.  The
+// LDS loads of 8 terms are issued together before their (ordered) fma chain: the same
+// rounding as the plain loop, without one LDS round trip per multiply-add
+__device__ __forceinline__ float rw_dot(const float* x, const float* k, int ks, int n, bool mul_first, float acc) {
+  int i = 0;
+  if (mul_first && n > 0) {
+    acc = x[0] * k[0];
+    i = 1;
+  }
+  for (; i < n; i += 8) {
+    float xv[8], kv[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u)
+      if (i + u < n) xv[u] = x[i + u], kv[u] = k[(i + u) * ks];
+#pragma unroll
+    for (int u = 0; u < 8; ++u)
+      if (i + u < n) acc = fmaf(xv[u], kv[u], acc);
+  }
+  return acc;
+}
+
+// forward over the sequence: y_t = h_D[t][0]; states to hs (global, [P][HS]) and/or the
+// outputs to out (LDS, [P]) when given
+__device__ void rw_forward(const GShape& s, const RWave& r, const float* wts, const float* seq, float* hs,
+                           float* out) {
+  const int lane = threadIdx.x;
+  float* hc = r.h0;  // time t
+  float* hp = r.h1;  // time t - 1
+  for (int q = lane; q < s.HS; q += 64) hc[q] = 0.f, hp[q] = 0.f;
+  rw_sync();
+  for (int t = 0; t < s.P; ++t) {
+    const float x0 = seq[t];
+    for (int L = 0; L < s.NL; ++L) {
+      const int I = s.in_[L], U = s.un[L];
+      float hn = 0.f;
+      if (lane < U) {
+        const float* K = wts + s.koff[L];
+        const float* R = wts + s.roff[L];
+        // layer L-1 at time t (this timestep), or the scalar input
+        const float xk = L == 0 ? x0 * K[lane] : rw_dot(hc + (L - 1) * s.W, K + lane, U, I, true, 0.f);
+        const float hr = rw_dot(hp + L * s.W, R + lane, U, U, true, 0.f);
+        hn = xk + hr;
+      }
+      if (lane < U) hc[L * s.W + lane] = hn;
+      rw_sync();
+    }
+    if (hs)
+      for (int q = lane; q < s.HS; q += 64) hs[(int64_t)t * s.HS + q] = hc[q];
+    if (out && lane == 0) out[t] = hc[s.D * s.W];
+    float* tmp = hc;  // h(t) becomes h(t - 1); the old buffer is overwritten layer by layer
+    hc = hp;
+    hp = tmp;
+    rw_sync();
+  }
+}
+
+// one self-train / learn epoch (g_train_epoch, recurrent branch): forward with states, BPTT,
+// one SGD step; returns the loss (mean over timesteps)
+__device__ float rw_train_epoch(const GShape& s, const RWave& r, float* hs, float lr) {
+  const int lane = threadIdx.x;
+  rw_forward(s, r, r.w, r.seq, hs, nullptr);
+  // the states are read back by other lanes of this wave: the stores are at L2 after the
+  // wait, and the reads below are memory-side (L2) loads -- never a stale L1 line left by the
+  // previous particle's pass over the same region
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  float* gw = r.aux;
+  for (int k = lane; k < s.P; k += 64) gw[k] = 0.f;
+  for (int q = lane; q < s.HS; q += 64) r.carry[q] = 0.f;
+  rw_sync();
+  float loss = 0.f;
+  for (int t = s.P - 1; t >= 0; --t) {
+    for (int q = lane; q < s.HS; q += 64) {
+      r.hst[q] = __hip_atomic_load(hs + (int64_t)t * s.HS + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      r.hsp[q] = t > 0 ? __hip_atomic_load(hs + (int64_t)(t - 1) * s.HS + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                       : 0.f;
+    }
+    rw_sync();
+    const float e = r.hst[s.D * s.W] - r.seq[t];
+    loss += e * e;
+    if (lane == 0) r.dtop[0] = 2.0f * e / (float)s.P;
+    rw_sync();
+    for (int L = s.D; L >= 0; --L) {
+      const int U = s.un[L], I = s.in_[L];
+      float dhj = 0.f;
+      if (lane < U) dhj = r.dtop[lane] + r.carry[L * s.W + lane];
+      if (lane < U) r.dh[lane] = dhj;
+      rw_sync();
+      if (lane < U) {  // kernel / recurrent-kernel gradients of column j = lane
+        for (int i = 0; i < I; ++i) {
+          const float xi = L == 0 ? r.seq[t] : r.hst[(L - 1) * s.W + i];
+          float* gk = gw + s.koff[L] + i * U + lane;
+          *gk = fmaf(xi, dhj, *gk);
+        }
+        for (int i = 0; i < U; ++i) {
+          float* gr = gw + s.roff[L] + i * U + lane;
+          *gr = fmaf(r.hsp[L * s.W + i], dhj, *gr);
+        }
+      }
+      float dxi = 0.f, cri = 0.f;
+      if (L > 0 && lane < I) dxi = rw_dot(r.dh, r.w + s.koff[L] + lane * U, 1, U, false, 0.f);
+      if (lane < U) cri = rw_dot(r.dh, r.w + s.roff[L] + lane * U, 1, U, false, 0.f);
+      rw_sync();
+      if (lane < U) r.carry[L * s.W + lane] = cri;
+      if (L > 0 && lane < I) r.dtop[lane] = dxi;
+      rw_sync();
+    }
+  }
+  for (int k = lane; k < s.P; k += 64) r.w[k] = fmaf(gw[k], -lr, r.w[k]);
+  rw_sync();
+  return loss / (float)s.P;
+}
+
+__device__ __forceinline__ bool rw_all(bool b) { return __ballot(!b) == 0ull; }
+__device__ bool rw_diverged(const GShape& s, const float* v) {
+  bool bad = false;
+  for (int k = threadIdx.x; k < s.P; k += 64) bad |= !finitef(v[k]);
+  return !rw_all(!bad);
+}
+__device__ bool rw_within(const GShape& s, const float* a, const float* b, float eps) {
+  bool ok = true;
+  for (int k = threadIdx.x; k < s.P; k += 64) ok &= !(fabsf(a[k] - b[k]) >= eps);
+  return rw_all(ok);
+}
+__device__ bool rw_zero(const GShape& s, const float* v, float eps) {
+  bool ok = true;
+  for (int k = threadIdx.x; k < s.P; k += 64) ok &= (-eps <= v[k]) && (v[k] <= eps);
+  return rw_all(ok);
+}
+__device__ void rw_load(const GShape& s, const char* row, float* dst) {
+  for (int k = threadIdx.x; k < s.P; k += 64) dst[k] = g_dec(row, k, s.dtype);
+}
+__device__ void rw_store(const GShape& s, char* row, const float* src) {
+  for (int k = threadIdx.x; k < s.PP; k += 64) {
+    const float v = k < s.P ? src[k] : 0.f;
+    if (s.dtype == 0) reinterpret_cast<float*>(row)[k] = v;
+    else reinterpret_cast<uint16_t*>(row)[k] = s.dtype == 1 ? StBF16::enc(v) : StF16::enc(v);
+  }
+}
+__device__ void rw_quant(const GShape& s, float* v) {
+  if (s.dtype != 0)
+    for (int k = threadIdx.x; k < s.P; k += 64) v[k] = g_q(v[k], s.dtype);
+}
+
+// classification (g_classify_w): f1 = apply(w, w), f2 = apply(w, f1); uses aux and seq
+__device__ int8_t rw_classify(const GShape& s, const RWave& r, float eps, bool with_sec) {
+  if (rw_diverged(s, r.w)) return C_DIVERGENT;
+  float* f1 = r.aux;
+  rw_forward(s, r, r.w, r.w, nullptr, f1);
+  rw_quant(s, f1);
+  rw_sync();
+  if (!rw_diverged(s, f1) && rw_within(s, f1, r.w, eps)) return rw_zero(s, r.w, eps) ? C_FIX_ZERO : C_FIX_OTHER;
+  if (with_sec) {
+    float* f2 = r.seq;
+    rw_forward(s, r, r.w, f1, nullptr, f2);
+    rw_quant(s, f2);
+    rw_sync();
+    if (!rw_diverged(s, f2) && rw_within(s, f2, r.w, eps)) return C_FIX_SEC;
+  }
+  return C_OTHER;
+}
+
+template <int OP>
+__global__ __launch_bounds__(64) void k_rnn_wave(GShape s, SrnnArgs a) {
+  extern __shared__ float sm[];
+  const RWave r = rw_layout(s, sm);
+  const int lane = threadIdx.x;
+  float* hs = reinterpret_cast<float*>(a.scratch) + (int64_t)blockIdx.x * s.P * s.HS;
+  for (int64_t i = blockIdx.x; i < a.n; i += gridDim.x) {
+    if constexpr (OP == OP_APPLY) {
+      const int64_t fi = a.idx_f ? a.idx_f[i] : i, ti = a.idx_t ? a.idx_t[i] : i, oi = a.idx_o ? a.idx_o[i] : i;
+      rw_load(s, GItem::rowp(s, a.W, fi), r.w);
+      rw_load(s, GItem::rowp(s, a.W, ti), r.seq);
+      rw_sync();
+      rw_forward(s, r, r.w, r.seq, nullptr, r.aux);
+      rw_quant(s, r.aux);
+      rw_sync();
+      rw_store(s, GItem::rowp(s, a.W2, oi), r.aux);
+    } else if constexpr (OP == OP_TRAIN || OP == OP_LEARN) {
+      rw_load(s, GItem::rowp(s, a.W, i), r.w);
+      if (OP == OP_LEARN) rw_load(s, GItem::rowp(s, a.W2, a.idx_t ? a.idx_t[i] : i), r.seq);
+      rw_sync();
+      float loss = 0.f;
+      for (int e = 0; e < a.epochs; ++e) {
+        if (OP == OP_TRAIN) {  // samples = the weights at the epoch start
+          for (int k = lane; k < s.P; k += 64) r.seq[k] = r.w[k];
+          rw_sync();
+        }
+        loss = rw_train_epoch(s, r, hs, a.lr);
+      }
+      rw_store(s, GItem::rowp(s, a.W, i), r.w);
+      if (a.loss && lane == 0) a.loss[i] = loss;
+    } else if constexpr (OP == OP_RUN_FIXPOINT) {
+      rw_load(s, GItem::rowp(s, a.W, i), r.w);
+      rw_sync();
+      int st = 0;
+      for (; st < a.steps; ++st) {
+        if (a.early_exit && rw_diverged(s, r.w)) break;
+        rw_forward(s, r, r.w, r.w, nullptr, r.aux);
+        rw_quant(s, r.aux);
+        rw_sync();
+        if (a.early_exit && !rw_diverged(s, r.aux) && rw_within(s, r.aux, r.w, a.eps)) break;
+        for (int k = lane; k < s.P; k += 64) r.w[k] = r.aux[k];
+        rw_sync();
+      }
+      rw_store(s, GItem::rowp(s, a.W, i), r.w);
+      if (a.nsteps && lane == 0) a.nsteps[i] = st;
+      if (a.cls) {
+        const int8_t k = rw_classify(s, r, a.eps, (a.flags & 8) != 0);
+        if (lane == 0) a.cls[i] = k;
+      }
+    }
+    rw_sync();
+  }
+}
+
+// recurrent nets at least RW_MIN_WIDTH wide whose three P-vectors fit a workgroup's LDS run
+// apply / train / learn / run_fixpoint (no trajectory) wave per particle
+static int g_rnn_wave = -1;  // SRNN_RNN_WAVE=0: lane path for every width (A/B tests)
+extern "C" void srnn_set_rnn_wave(int on) { g_rnn_wave = on ? 1 : 0; }
+static bool rw_serves(int op, const GShape& s, const SrnnArgs& a) {
+  if (g_rnn_wave < 0) {
+    const char* e = std::getenv("SRNN_RNN_WAVE");
+    g_rnn_wave = (e && e[0] == '0') ? 0 : 1;
+  }
+  if (!g_rnn_wave) return false;
+  if (s.kind != 2 || s.W < RW_MIN_WIDTH || s.W > 64 || rw_lds_bytes(s) > 60 * 1024 || !a.dev) return false;
+  if (op == OP_RUN_FIXPOINT) return a.traj == nullptr;
+  return op == OP_APPLY || op == OP_TRAIN || op == OP_LEARN;
+}
+static int rw_launch(int op, const GShape& s, const SrnnArgs& a) {
+  if (a.n <= 0) return 0;
+  const int64_t per = (int64_t)s.P * s.HS * (int64_t)sizeof(float);
+  int64_t blocks = a.scratch ? a.scratch_bytes / per : 0;
+  if (op != OP_TRAIN && op != OP_LEARN) blocks = 4096;  // no BPTT states
+  blocks = blocks < a.n ? blocks : a.n;
+  blocks = blocks < 8192 ? blocks : 8192;
+  if (blocks <= 0) {
+    set_error("generic engine: scratch buffer missing or too small for the recurrent wave path");
+    return -5;
+  }
+  const size_t lds = rw_lds_bytes(s);
+  hipStream_t st = (hipStream_t)a.stream;
+  switch (op) {
+    case OP_APPLY: hipLaunchKernelGGL((k_rnn_wave<OP_APPLY>), dim3((unsigned)blocks), dim3(64), lds, st, s, a); break;
+    case OP_TRAIN: hipLaunchKernelGGL((k_rnn_wave<OP_TRAIN>), dim3((unsigned)blocks), dim3(64), lds, st, s, a); break;
+    case OP_LEARN: hipLaunchKernelGGL((k_rnn_wave<OP_LEARN>), dim3((unsigned)blocks), dim3(64), lds, st, s, a); break;
+    case OP_RUN_FIXPOINT:
+      hipLaunchKernelGGL((k_rnn_wave<OP_RUN_FIXPOINT>), dim3((unsigned)blocks), dim3(64), lds, st, s, a);
+      break;
+    default: set_error("recurrent wave path: op"); return -1;
+  }
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) {
+    set_error(hipGetErrorString(e));
+    return -3;
+  }
+  return 0;
+}
+
 static bool generic_op_supported(int op) {
   switch (op) {
     case OP_INIT: case OP_APPLY: case OP_RUN_FIXPOINT: case OP_TRAIN: case OP_LEARN: case OP_CLASSIFY:
@@ -1143,6 +1446,8 @@ static int generic_launch(int op, const GShape& s, const SrnnArgs& a) {
       return -5;
     }
     hipLaunchKernelGGL(k_g_respawn_seq, dim3(1), dim3(GTBR), 0, st, s, a);
+  } else if (rw_serves(op, s, a)) {
+    return rw_launch(op, s, a);
   } else {
     if (a.n <= 0) return 0;
     const int64_t lanes = generic_lanes(s, a, a.n);

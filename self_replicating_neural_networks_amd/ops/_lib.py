@@ -143,6 +143,8 @@ def lib():
         L.srnn_generic_scratch_bytes.restype = ctypes.c_int64
         L.srnn_set_force_generic.argtypes = [ctypes.c_int]
         L.srnn_set_force_generic.restype = None
+        L.srnn_set_rnn_wave.argtypes = [ctypes.c_int]
+        L.srnn_set_rnn_wave.restype = None
         vp, i64, cp = ctypes.c_void_p, ctypes.c_int64, ctypes.c_char_p
         for name, args in (("srnn_comm_available", [cp]), ("srnn_comm_unique_id", [cp, vp, ctypes.c_int]),
                            ("srnn_comm_init", [cp, vp, ctypes.c_int, ctypes.c_int, ctypes.c_int,
@@ -184,6 +186,11 @@ def is_generic(spec, op: int, dtype: int = DTYPE_FP32) -> bool:
 def set_force_generic(on: bool) -> None:
     """Route every op to the runtime-shape engine (A/B tests against the templated kernels)."""
     lib().srnn_set_force_generic(1 if on else 0)
+
+
+def set_rnn_wave(on: bool) -> None:
+    """Wide Recurrent nets wave per particle (default) or lane per particle (A/B tests)."""
+    lib().srnn_set_rnn_wave(1 if on else 0)
 
 
 def generic_scratch_bytes(spec, n: int, dtype: int = DTYPE_FP32, max_lanes: int = 65536) -> int:

@@ -1,0 +1,56 @@
+"""Wide / long Recurrent nets wave per particle (csrc/srnn_generic.hip k_rnn_wave):
+equal to the lane-per-particle path on the same device (same operation order) and close to
+the host path, for self-application, run_fixpoint + census, self-training and learn_from."""
+import numpy as np
+import pytest
+import torch
+
+from self_replicating_neural_networks_amd.arch import ArchSpec
+from self_replicating_neural_networks_amd.ops import _lib
+from self_replicating_neural_networks_amd.ops import kernels as K
+from self_replicating_neural_networks_amd.population import Population
+
+pytestmark = pytest.mark.gpu
+
+
+def _ops(spec, dev, n=300):
+    pop = Population(spec, n, device=dev, seed=4)
+    W0 = pop.W.clone()
+    out = {}
+    pop.self_apply(2)
+    out["apply"] = pop.W.clone()
+    pop.W.copy_(W0)
+    cls, steps, _ = K.run_fixpoint(spec, pop.W, 4, 1e-4, early_exit=True)
+    out["fix"], out["cls"], out["steps"] = pop.W.clone(), cls.clone(), steps.clone()
+    pop.W.copy_(W0)
+    out["loss"] = pop.train(3).clone()
+    out["train"] = pop.W.clone()
+    pop.W.copy_(W0)
+    idx = torch.roll(torch.arange(n, device=dev), 3).contiguous()
+    pop.learn_from(W0.clone(), idx, epochs=2)
+    out["learn"] = pop.W.clone()
+    torch.cuda.synchronize() if dev != "cpu" else None
+    return out
+
+
+@pytest.mark.parametrize("w,d", [(8, 2), (16, 2), (12, 3)])
+def test_rnn_wave_equals_lane_path(cuda, w, d):
+    spec = ArchSpec.recurrent(w, d)
+    outs = []
+    for wave in (True, False):
+        _lib.set_rnn_wave(wave)
+        try:
+            outs.append(_ops(spec, cuda))
+        finally:
+            _lib.set_rnn_wave(True)
+    a, b = outs
+    for k in a:
+        x, y = a[k], b[k]
+        if x.is_floating_point():
+            assert torch.equal(x.view(torch.int32) if x.dtype == torch.float32 else x, y.view(torch.int32)
+                               if y.dtype == torch.float32 else y), k
+        else:
+            assert torch.equal(x, y), k
+    h = _ops(spec, "cpu")
+    ok = torch.isfinite(h["apply"]).all(1) & torch.isfinite(a["apply"].cpu()).all(1)
+    assert torch.allclose(a["apply"].cpu()[ok], h["apply"][ok], rtol=1e-3, atol=1e-5)
