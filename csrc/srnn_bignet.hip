@@ -1203,7 +1203,11 @@ __global__ __launch_bounds__(TBROW) void k_big_rows(SrnnCfg c, SrnnArgs a) {
   if constexpr (OP == OP_APPLY) {
     const int64_t fi = a.idx_f ? a.idx_f[p] : p, ti = a.idx_t ? a.idx_t[p] : p, oi = a.idx_o ? a.idx_o[p] : p;
     float g[T::A], h[T::A];
-    R::stream_aggregate(R::at(a.W, ti), g, c.aggregator);
+    // target row into the registers (all its loads in flight at once), aggregated, then
+    // overwritten by the attacker's row: streaming the target one load at a time halved
+    // the attack rate (1.72 vs 0.82 ms at 1M particles)
+    R::load(R::at(a.W, ti), w);
+    lrow_aggregate<T>(w, g, c.aggregator);
     R::load(R::at(a.W, fi), w);
     lmlp<T>(w, g, h);
     R::quant_a(h);
