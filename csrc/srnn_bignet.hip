@@ -1,1525 +1,27 @@
-// srnn_bignet.hip — wave-per-particle kernels for Aggregating nets too large for the
-// lane-per-particle register kernels (north-star config: Aggregating(4, 10, 3), P = 280,
-// 1M particles; reference code/network.py:292-439).
-//
-// One 64-lane wave owns one particle: the row is streamed HBM -> LDS with float4 loads
-// (coalesced, 1120 B per particle), chunk means are wave reductions (fp64, like the
-// reference's python-float sums), every dense layer is computed by lanes j < out reading
-// column j of the kernel from LDS, and the output row is written back coalesced.
-//
-// Self-application to convergence runs on a 4-number state: after one application an
-// aggregating net's weights are constant over each aggregation chunk (no shuffle), the
-// chunk means of such a vector are exactly those constants (double sums of identical
-// floats), so every further application is a function of the A chunk values only --
-// bit-identical to re-evaluating the expanded weights, with no memory traffic until the
-// final write.  MFMA does not apply: each particle is a GEMV chain with its own weights
-// (M = 1), see docs/kernels.md.
-#include "srnn_kernels.h"
-#include <cstdlib>
+// srnn_bignet.hip — dispatch of the big aggregating nets (kernels: srnn_bignet.h, one
+// shape per srnn_bignet_<a>_<w>_<d>.hip)
+#include "srnn_bignet.h"
 
-namespace srnn {
+extern "C" int srnn_big_4_10_3(int op, const SrnnCfg* c, const SrnnArgs* a);
+extern "C" int srnn_big_4_8_2(int op, const SrnnCfg* c, const SrnnArgs* a);
+extern "C" int srnn_big_4_16_2(int op, const SrnnCfg* c, const SrnnArgs* a);
 
-constexpr int BW = 4;            // waves (particles) per block
-constexpr int TBB = 64 * BW;
-
-template <int A_, int W_, int D_>
-struct AggBig {
-  static constexpr int A = A_, W = W_, D = D_;
-  using Net = MLP<A, W, D, A>;
-  static constexpr int P = Net::P;
-  static constexpr int PP = (P + 3) & ~3;
-  static constexpr int NL = D + 1;
-  static constexpr int CS = P / A;
-  static_assert(P / CS == A, "invalid aggregation (SURVEY S4)");
-  static constexpr int MAXW = (A > W ? A : W);
-  static constexpr int rows(int l) { return l == 0 ? A : W; }
-  static constexpr int cols(int l) { return l == D ? A : W; }
-  static constexpr int off(int l) { return Net::off(l); }
-  __device__ static int chunk(int k) { int c = k / CS; return c < A ? c : A - 1; }
-  static constexpr int chunk_c(int k) { return k / CS < A ? k / CS : A - 1; }
-};
-
-__device__ __forceinline__ double wave_sum(double v) {
-#pragma unroll
-  for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
-  return v;
-}
-__device__ __forceinline__ float wave_max(float v) {
-#pragma unroll
-  for (int o = 32; o >= 1; o >>= 1) {
-    float u = __shfl_xor(v, o, 64);
-    v = u > v ? u : v;
-  }
-  return v;
-}
-__device__ __forceinline__ bool wave_all(bool b) { return __ballot(!b) == 0ull; }
-
-// per-wave LDS scratch: weights [PP] + vectors for backprop
-template <class T>
-struct WaveLds {
-  float w[T::PP];
-  float t[T::PP];             // second row (attack target)
-  float act[T::NL][T::MAXW];  // input of every layer
-  float st[T::MAXW];          // propagated step
-  float st2[T::MAXW];
-};
-
-template <class T>
-__device__ void load_row(float* __restrict__ sw, const float* __restrict__ row, int lane) {
-  const float4* r4 = reinterpret_cast<const float4*>(row);
-  float4* s4 = reinterpret_cast<float4*>(sw);
-  for (int q = lane; q < T::PP / 4; q += 64) s4[q] = r4[q];
-}
-template <class T>
-__device__ void store_state(float* __restrict__ row, const float* s, int lane) {
-  // expand the chunk state into the full row
-  float4* r4 = reinterpret_cast<float4*>(row);
-  for (int q = lane; q < T::PP / 4; q += 64) {
-    float v[4];
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const int k = 4 * q + e;
-      float x = 0.f;
-#pragma unroll
-      for (int c = 0; c < T::A; ++c) x = (k < T::P && T::chunk(k) == c) ? s[c] : x;
-      v[e] = x;
-    }
-    r4[q] = make_float4(v[0], v[1], v[2], v[3]);
-  }
-}
-template <class T>
-__device__ void store_lds(float* __restrict__ row, const float* __restrict__ sw, int lane) {
-  float4* r4 = reinterpret_cast<float4*>(row);
-  const float4* s4 = reinterpret_cast<const float4*>(sw);
-  for (int q = lane; q < T::PP / 4; q += 64) r4[q] = s4[q];
-}
-
-// chunk aggregation of an LDS row (aggregator: 0 mean, 1 max, 2 max with the reference quirk)
-template <class T>
-__device__ void aggregate_lds(const float* __restrict__ sw, float* g, int lane, int aggregator) {
-#pragma unroll
-  for (int c = 0; c < T::A; ++c) {
-    const int b = c * T::CS, e = (c == T::A - 1) ? T::P : b + T::CS;
-    if (aggregator == 0) {
-      double acc = 0.0;
-      for (int k = b + lane; k < e; k += 64) acc += (double)sw[k];
-      g[c] = (float)(wave_sum(acc) / (double)(e - b));
-    } else {
-      // sequential semantics of the reference loop (first element seeds the max)
-      float m = sw[b];
-      if (lane == 0)
-        for (int k = b; k < e; ++k) {
-          const float v = sw[k];
-          m = (aggregator == 1) ? (v > m ? v : m) : ((v > m && v != 0.0f) ? v : m);
-        }
-      g[c] = __shfl(m, 0, 64);
-    }
-  }
-}
-
-// y = x . K for the layer at LDS offset `o` (rows I, cols O); x replicated in all lanes,
-// y returned replicated.  Lane j < O accumulates column j in the kernels' order.
-template <int I, int O>
-__device__ void dense_lds(const float* __restrict__ k, const float* x, float* y, int lane) {
-  float acc = 0.f;
-  if (lane < O) {
-    acc = x[0] * k[lane];
-#pragma unroll
-    for (int i = 1; i < I; ++i) acc = fmaf(x[i], k[i * O + lane], acc);
-  }
-#pragma unroll
-  for (int j = 0; j < O; ++j) y[j] = __shfl(acc, j, 64);
-}
-
-// same with piecewise-constant weights: K[i][j] = s[chunk(o + i*O + j)]
-template <class T, int I, int O>
-__device__ void dense_state(int o, const float* s, const float* x, float* y, int lane) {
-  float acc = 0.f;
-  if (lane < O) {
-    float kv = 0.f;
-    int f = o + lane;
-    int c = T::chunk(f);
-#pragma unroll
-    for (int q = 0; q < T::A; ++q) kv = (c == q) ? s[q] : kv;
-    acc = x[0] * kv;
-#pragma unroll
-    for (int i = 1; i < I; ++i) {
-      f = o + i * O + lane;
-      c = T::chunk(f);
-#pragma unroll
-      for (int q = 0; q < T::A; ++q) kv = (c == q) ? s[q] : kv;
-      acc = fmaf(x[i], kv, acc);
-    }
-  }
-#pragma unroll
-  for (int j = 0; j < O; ++j) y[j] = __shfl(acc, j, 64);
-}
-
-template <class T>
-__device__ void mlp_lds(const float* __restrict__ sw, const float* g, float* h, int lane) {
-  float x[T::MAXW], y[T::MAXW];
-#pragma unroll
-  for (int i = 0; i < T::A; ++i) x[i] = g[i];
-  dense_lds<T::A, T::W>(sw + T::off(0), x, y, lane);
-#pragma unroll
-  for (int l = 1; l < T::D; ++l) {
-#pragma unroll
-    for (int i = 0; i < T::W; ++i) x[i] = y[i];
-    dense_lds<T::W, T::W>(sw + T::off(l), x, y, lane);
-  }
-#pragma unroll
-  for (int i = 0; i < T::W; ++i) x[i] = y[i];
-  dense_lds<T::W, T::A>(sw + T::off(T::D), x, h, lane);
-}
-
-template <class T>
-__device__ void mlp_state(const float* s, const float* g, float* h, int lane) {
-  float x[T::MAXW], y[T::MAXW];
-#pragma unroll
-  for (int i = 0; i < T::A; ++i) x[i] = g[i];
-  dense_state<T, T::A, T::W>(T::off(0), s, x, y, lane);
-#pragma unroll
-  for (int l = 1; l < T::D; ++l) {
-#pragma unroll
-    for (int i = 0; i < T::W; ++i) x[i] = y[i];
-    dense_state<T, T::W, T::W>(T::off(l), s, x, y, lane);
-  }
-#pragma unroll
-  for (int i = 0; i < T::W; ++i) x[i] = y[i];
-  dense_state<T, T::W, T::A>(T::off(T::D), s, x, h, lane);
-}
-
-template <class T>
-__device__ bool finite_all(const float* v) {
-  bool ok = true;
-#pragma unroll
-  for (int i = 0; i < T::A; ++i) ok &= finitef(v[i]);
-  return ok;
-}
-template <class T>
-__device__ bool close_all(const float* a, const float* b, float eps) {
-  bool ok = true;
-#pragma unroll
-  for (int i = 0; i < T::A; ++i) ok &= !(fabsf(a[i] - b[i]) >= eps);
-  return ok;
-}
-template <class T>
-__device__ bool lds_finite(const float* sw, int lane) {
-  bool ok = true;
-  for (int k = lane; k < T::P; k += 64) ok &= finitef(sw[k]);
-  return wave_all(ok);
-}
-// |state-expanded(s) - lds weights| < eps for every weight
-template <class T>
-__device__ bool lds_close_state(const float* sw, const float* s, float eps, int lane) {
-  bool ok = true;
-  for (int k = lane; k < T::P; k += 64) {
-    const int c = T::chunk(k);
-    float v = 0.f;
-#pragma unroll
-    for (int q = 0; q < T::A; ++q) v = (c == q) ? s[q] : v;
-    ok &= !(fabsf(v - sw[k]) >= eps);
-  }
-  return wave_all(ok);
-}
-template <class T>
-__device__ bool lds_zero(const float* sw, float eps, int lane) {
-  bool ok = true;
-  for (int k = lane; k < T::P; k += 64) ok &= (-eps <= sw[k]) && (sw[k] <= eps);
-  return wave_all(ok);
-}
-
-// classification of general (LDS) weights: f = f_W(W) = expand(h1), f2 = expand(h2)
-template <class T>
-__device__ int8_t classify_lds(const float* sw, float eps, bool with_sec, int aggregator, int lane) {
-  if (!lds_finite<T>(sw, lane)) return C_DIVERGENT;
-  float g[T::A], h1[T::A], h2[T::A];
-  aggregate_lds<T>(sw, g, lane, aggregator);
-  mlp_lds<T>(sw, g, h1, lane);
-  if (finite_all<T>(h1) && lds_close_state<T>(sw, h1, eps, lane))
-    return lds_zero<T>(sw, eps, lane) ? C_FIX_ZERO : C_FIX_OTHER;
-  if (with_sec) {
-    mlp_lds<T>(sw, h1, h2, lane);  // aggregate(expand(h1)) == h1 exactly
-    if (finite_all<T>(h2) && lds_close_state<T>(sw, h2, eps, lane)) return C_FIX_SEC;
-  }
-  return C_OTHER;
-}
-// classification of chunk-constant weights expand(s)
-template <class T>
-__device__ int8_t classify_state(const float* s, float eps, bool with_sec, int lane) {
-  if (!finite_all<T>(s)) return C_DIVERGENT;
-  float h1[T::A], h2[T::A];
-  mlp_state<T>(s, s, h1, lane);
-  if (finite_all<T>(h1) && close_all<T>(h1, s, eps)) {
-    bool zero = true;
-#pragma unroll
-    for (int i = 0; i < T::A; ++i) zero &= (-eps <= s[i]) && (s[i] <= eps);
-    return zero ? C_FIX_ZERO : C_FIX_OTHER;
-  }
-  if (with_sec) {
-    mlp_state<T>(s, h1, h2, lane);
-    if (finite_all<T>(h2) && close_all<T>(h2, s, eps)) return C_FIX_SEC;
-  }
-  return C_OTHER;
-}
-
-// one SGD step on x = y = aggregate(own or teacher weights); weights in LDS (updated)
-template <class T>
-__device__ float train_step_lds(float* sw, WaveLds<T>& L, const float* g, float lr, int lane) {
-  // forward keeping every layer input
-  float x[T::MAXW], y[T::MAXW];
-#pragma unroll
-  for (int i = 0; i < T::A; ++i) x[i] = g[i];
-#pragma unroll
-  for (int l = 0; l <= T::D; ++l) {
-    if (lane < T::rows(l)) {
-      float v = x[0];
-#pragma unroll
-      for (int i = 1; i < T::MAXW; ++i) v = (lane == i) ? x[i] : v;
-      L.act[l][lane] = v;
-    }
-    if (l == 0) dense_lds<T::A, T::W>(sw + T::off(0), x, y, lane);
-    else if (l < T::D) dense_lds<T::W, T::W>(sw + T::off(l), x, y, lane);
-    else dense_lds<T::W, T::A>(sw + T::off(T::D), x, y, lane);
-#pragma unroll
-    for (int i = 0; i < T::MAXW; ++i) x[i] = y[i];
-  }
-  // loss mean over A, step = -lr * dL/dh
-  float loss = 0.f;
-  float st = 0.f;
-#pragma unroll
-  for (int k = 0; k < T::A; ++k) {
-    const float e = x[k] - g[k];
-    loss += e * e;
-    if (lane == k) st = -lr * (2.0f * e / (float)T::A);
-  }
-  if (lane < T::A) L.st[lane] = st;
-  __builtin_amdgcn_wave_barrier();
-  // backward: st_in = K . st_out (pre-update K), K += act (x) st_out
-#pragma unroll
-  for (int l = T::D; l >= 0; --l) {
-    const int R = T::rows(l), Cc = T::cols(l);
-    float* k = sw + T::off(l);
-    if (l > 0 && lane < R) {
-      float acc = k[lane * Cc] * L.st[0];
-      for (int j = 1; j < Cc; ++j) acc = fmaf(k[lane * Cc + j], L.st[j], acc);
-      L.st2[lane] = acc;
-    }
-    __builtin_amdgcn_wave_barrier();
-    for (int f = lane; f < R * Cc; f += 64) {
-      const int i = f / Cc, j = f - i * Cc;
-      k[f] = fmaf(L.act[l][i], L.st[j], k[f]);
-    }
-    __builtin_amdgcn_wave_barrier();
-    if (l > 0 && lane < R) L.st[lane] = L.st2[lane];
-    __builtin_amdgcn_wave_barrier();
-  }
-  return loss / (float)T::A;
-}
-
-// ------------------------------------------------------------------------------ kernel
-template <class T, int OP>
-__global__ __launch_bounds__(TBB) void k_big(SrnnCfg c, SrnnArgs a) {
-  __shared__ WaveLds<T> lds[BW];
-  __shared__ uint32_t s_cnt[5];
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const int64_t p = (int64_t)blockIdx.x * BW + wv;  // particle (wave-uniform)
-  WaveLds<T>& L = lds[wv];
-  if (OP == OP_CLASSIFY && threadIdx.x < 5) s_cnt[threadIdx.x] = 0;
-  __syncthreads();
-  int8_t cls = -1;
-  if (p < a.n) {
-    if constexpr (OP == OP_APPLY) {
-      const int64_t fi = a.idx_f ? a.idx_f[p] : p, ti = a.idx_t ? a.idx_t[p] : p, oi = a.idx_o ? a.idx_o[p] : p;
-      // both rows in flight at once, then aggregate the target and run the attacker's net
-      {
-        const float4* f4 = reinterpret_cast<const float4*>(a.W + fi * T::PP);
-        const float4* t4 = reinterpret_cast<const float4*>(a.W + ti * T::PP);
-        float4* sw4 = reinterpret_cast<float4*>(L.w);
-        float4* st4 = reinterpret_cast<float4*>(L.t);
-        for (int q = lane; q < T::PP / 4; q += 64) {
-          const float4 x = f4[q], y = t4[q];
-          sw4[q] = x;
-          st4[q] = y;
-        }
-      }
-      __builtin_amdgcn_wave_barrier();
-      float g[T::A], h[T::A];
-      aggregate_lds<T>(L.t, g, lane, c.aggregator);
-      mlp_lds<T>(L.w, g, h, lane);
-      store_state<T>(a.W2 + oi * T::PP, h, lane);
-    } else if constexpr (OP == OP_RUN_FIXPOINT || OP == OP_CLASSIFY) {
-      load_row<T>(L.w, a.W + p * T::PP, lane);
-      __builtin_amdgcn_wave_barrier();
-      const bool with_sec = (a.flags & 8) != 0;
-      int s = 0;
-      float st[T::A];
-      bool compressed = false;
-      if constexpr (OP == OP_RUN_FIXPOINT) {
-        float g[T::A], h[T::A];
-        for (; s < a.steps; ++s) {
-          if (!compressed) {
-            if (a.early_exit && !lds_finite<T>(L.w, lane)) break;
-            aggregate_lds<T>(L.w, g, lane, c.aggregator);
-            mlp_lds<T>(L.w, g, h, lane);
-            if (a.early_exit && finite_all<T>(h) && lds_close_state<T>(L.w, h, a.eps, lane)) break;
-          } else {
-            if (a.early_exit && !finite_all<T>(st)) break;
-            mlp_state<T>(st, st, h, lane);
-            if (a.early_exit && finite_all<T>(h) && close_all<T>(h, st, a.eps)) break;
-          }
-#pragma unroll
-          for (int i = 0; i < T::A; ++i) st[i] = h[i];
-          compressed = true;
-        }
-        if (compressed) store_state<T>(a.W + p * T::PP, st, lane);
-        if (a.nsteps && lane == 0) a.nsteps[p] = s;
-      }
-      cls = compressed ? classify_state<T>(st, a.eps, with_sec, lane)
-                       : classify_lds<T>(L.w, a.eps, with_sec, c.aggregator, lane);
-      if (a.cls && lane == 0) a.cls[p] = cls;
-    } else if constexpr (OP == OP_TRAIN || OP == OP_LEARN) {
-      load_row<T>(L.w, a.W + p * T::PP, lane);
-      float g[T::A];
-      if constexpr (OP == OP_LEARN) {
-        // teacher samples are fixed: aggregate the teacher row once (through L.act as scratch)
-        const float* tr = a.W2 + (a.idx_t ? a.idx_t[p] : p) * T::PP;
-        if (c.aggregator != 0) {  // max aggregators: stage the teacher row, sequential semantics
-          load_row<T>(L.t, tr, lane);
-          __builtin_amdgcn_wave_barrier();
-          aggregate_lds<T>(L.t, g, lane, c.aggregator);
-        }
-        double acc[T::A];
-#pragma unroll
-        for (int q = 0; q < T::A; ++q) acc[q] = 0.0;
-        for (int k = lane; k < T::P; k += 64) {
-          const int ch = T::chunk(k);
-#pragma unroll
-          for (int q = 0; q < T::A; ++q) acc[q] += (ch == q) ? (double)tr[k] : 0.0;
-        }
-#pragma unroll
-        for (int q = 0; q < T::A; ++q) {
-          const int b = q * T::CS, e = (q == T::A - 1) ? T::P : b + T::CS;
-          const float mean = (float)(wave_sum(acc[q]) / (double)(e - b));
-          if (c.aggregator == 0) g[q] = mean;
-        }
-      }
-      __builtin_amdgcn_wave_barrier();
-      float loss = 0.f;
-      for (int e = 0; e < a.epochs; ++e) {
-        if constexpr (OP == OP_TRAIN) aggregate_lds<T>(L.w, g, lane, c.aggregator);
-        loss = train_step_lds<T>(L.w, L, g, a.lr, lane);
-      }
-      __builtin_amdgcn_wave_barrier();
-      store_lds<T>(a.W + p * T::PP, L.w, lane);
-      if (a.loss && lane == 0) a.loss[p] = loss;
-    }
-  }
-  if constexpr (OP == OP_CLASSIFY) {
-    if (a.counts && lane == 0 && cls >= 0) atomicAdd(&s_cnt[cls], 1u);
-    __syncthreads();
-    if (a.counts && threadIdx.x < 5 && s_cnt[threadIdx.x]) atomicAdd(a.counts + threadIdx.x, (uint64_t)s_cnt[threadIdx.x]);
-  }
-}
-
-// ------------------------------------------------------------------ run_fixpoint, 3 phases
-// phase 1 (wave per particle): step-0 checks and the first application on the full row;
-// phase 2 (lane per particle): every further step on the A-float chunk state, with the
-//   chunk index of every weight a compile-time constant (fully unrolled MLP);
-// phase 3 (wave per particle): expand the final state into the row, coalesced.
-// temp = state float[n][A] followed by flags int8[n] (1 = continues in phase 2).
-
-template <class T, int L>
-__device__ __forceinline__ void dense_state_lane(const float* s, const float* x, float* y) {
-  constexpr int I = T::rows(L), O = T::cols(L), OFF = T::off(L);
-#pragma unroll
-  for (int j = 0; j < O; ++j) {
-    float acc = x[0] * s[T::chunk_c(OFF + j)];
-#pragma unroll
-    for (int i = 1; i < I; ++i) acc = fmaf(x[i], s[T::chunk_c(OFF + i * O + j)], acc);
-    y[j] = acc;
-  }
-}
-template <class T, int L>
-__device__ __forceinline__ void mlp_state_lane_rec(const float* s, float* x) {
-  float y[T::MAXW];
-  dense_state_lane<T, L>(s, x, y);
-#pragma unroll
-  for (int j = 0; j < T::cols(L); ++j) x[j] = y[j];
-  if constexpr (L < T::D) mlp_state_lane_rec<T, L + 1>(s, x);
-}
-template <class T>
-__device__ __forceinline__ void mlp_state_lane(const float* s, const float* g, float* h) {
-  float x[T::MAXW];
-#pragma unroll
-  for (int i = 0; i < T::A; ++i) x[i] = g[i];
-  mlp_state_lane_rec<T, 0>(s, x);
-#pragma unroll
-  for (int i = 0; i < T::A; ++i) h[i] = x[i];
-}
-
-template <class T>
-__global__ __launch_bounds__(TBB) void k_big_fix1(SrnnCfg c, SrnnArgs a) {
-  __shared__ WaveLds<T> lds[BW];
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const int64_t p = (int64_t)blockIdx.x * BW + wv;
-  if (p >= a.n) return;
-  WaveLds<T>& L = lds[wv];
-  float* state = reinterpret_cast<float*>(a.temp);
-  int8_t* flag = reinterpret_cast<int8_t*>(state + a.n * T::A);
-  load_row<T>(L.w, a.W + p * T::PP, lane);
-  __builtin_amdgcn_wave_barrier();
-  const bool with_sec = (a.flags & 8) != 0;
-  bool stop = a.steps <= 0;
-  float g[T::A], h[T::A];
-  if (!stop && a.early_exit && !lds_finite<T>(L.w, lane)) stop = true;
-  if (!stop) {
-    aggregate_lds<T>(L.w, g, lane, c.aggregator);
-    mlp_lds<T>(L.w, g, h, lane);
-    if (a.early_exit && finite_all<T>(h) && lds_close_state<T>(L.w, h, a.eps, lane)) stop = true;
-  }
-  if (stop) {  // no step taken: the row is unchanged, classify the general weights
-    const int8_t k = classify_lds<T>(L.w, a.eps, with_sec, c.aggregator, lane);
-    if (lane == 0) {
-      flag[p] = 0;
-      if (a.nsteps) a.nsteps[p] = 0;
-      if (a.cls) a.cls[p] = k;
-    }
-  } else if (lane < T::A) {
-    float v = h[0];
-#pragma unroll
-    for (int q = 1; q < T::A; ++q) v = (lane == q) ? h[q] : v;
-    state[p * T::A + lane] = v;
-    if (lane == 0) flag[p] = 1;
-  }
-}
-
-template <class T>
-__global__ __launch_bounds__(256) void k_big_fix2(SrnnCfg c, SrnnArgs a) {
-  const int64_t p = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (p >= a.n) return;
-  float* state = reinterpret_cast<float*>(a.temp);
-  const int8_t* flag = reinterpret_cast<const int8_t*>(state + a.n * T::A);
-  if (!flag[p]) return;
-  float st[T::A], h[T::A];
-#pragma unroll
-  for (int i = 0; i < T::A; ++i) st[i] = state[p * T::A + i];
-  int taken = 1;
-  for (int k = 1; k < a.steps; ++k) {
-    if (a.early_exit && !finite_all<T>(st)) break;
-    mlp_state_lane<T>(st, st, h);
-    if (a.early_exit && finite_all<T>(h) && close_all<T>(h, st, a.eps)) break;
-#pragma unroll
-    for (int i = 0; i < T::A; ++i) st[i] = h[i];
-    ++taken;
-  }
-#pragma unroll
-  for (int i = 0; i < T::A; ++i) state[p * T::A + i] = st[i];
-  if (a.nsteps) a.nsteps[p] = taken;
-  if (a.cls) {
-    // classify the chunk-constant weights expand(st)
-    int8_t k;
-    if (!finite_all<T>(st)) k = C_DIVERGENT;
-    else {
-      float h1[T::A], h2[T::A];
-      mlp_state_lane<T>(st, st, h1);
-      if (finite_all<T>(h1) && close_all<T>(h1, st, a.eps)) {
-        bool zero = true;
-#pragma unroll
-        for (int i = 0; i < T::A; ++i) zero &= (-a.eps <= st[i]) && (st[i] <= a.eps);
-        k = zero ? C_FIX_ZERO : C_FIX_OTHER;
-      } else {
-        k = C_OTHER;
-        if (a.flags & 8) {
-          mlp_state_lane<T>(st, h1, h2);
-          if (finite_all<T>(h2) && close_all<T>(h2, st, a.eps)) k = C_FIX_SEC;
-        }
-      }
-    }
-    a.cls[p] = k;
-  }
-}
-
-template <class T>
-__global__ __launch_bounds__(TBB) void k_big_fix3(SrnnCfg c, SrnnArgs a) {
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const int64_t p = (int64_t)blockIdx.x * BW + wv;
-  if (p >= a.n) return;
-  const float* state = reinterpret_cast<const float*>(a.temp);
-  const int8_t* flag = reinterpret_cast<const int8_t*>(state + a.n * T::A);
-  if (!flag[p]) return;
-  float st[T::A];
-#pragma unroll
-  for (int i = 0; i < T::A; ++i) st[i] = state[p * T::A + i];
-  store_state<T>(a.W + p * T::PP, st, lane);
-}
-
-// lane-per-particle ops writing straight to global memory (init, perturb)
-template <class T, int OP>
-__global__ __launch_bounds__(256) void k_big_lane(SrnnCfg c, SrnnArgs a) {
-  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (i >= a.n) return;
-  float* row = a.W + i * T::PP;
-  const Rng rng{(uint32_t)a.seed, (uint32_t)(a.seed >> 32)};
-  const uint64_t uid = a.uid ? (uint64_t)a.uid[i] : (uint64_t)i;
-  if constexpr (OP == OP_INIT) {
-    glorot_fill(row, 0, T::A, T::W, rng, uid);
-    for (int l = 1; l < T::D; ++l) glorot_fill(row, T::off(l), T::W, T::W, rng, uid);
-    glorot_fill(row, T::off(T::D), T::W, T::A, rng, uid);
-    for (int k = T::P; k < T::PP; ++k) row[k] = 0.f;
-  } else {
-    for (int k = 0; k < T::P; ++k) {
-      U4 u = rng.draw(uid, a.ctr * 1024u + (uint32_t)k, P_PERTURB);
-      double mag = (double)u01(u.y) * (double)a.eps;
-      row[k] = u01(u.x) < 0.5f ? (float)((double)row[k] + mag) : (float)((double)row[k] - mag);
-    }
-  }
-}
-
-// ------------------------------------------------------------------ lane per particle
-// classify / attack / train with the particle's whole row in VGPRs (P = 280 floats:
-// ~360 VGPRs, one wave per SIMD): every lane does useful work instead of the 10 of 64
-// lanes of the wave-per-particle layers, and the kernels become HBM-bound (1.1 KB row per
-// particle).  Arithmetic in the same order as the wave kernels (dense: x[0]*k then fma
-// over the inputs; chunk means as double sums, here in index order).
-template <class T>
-__device__ __forceinline__ void lrow_load(const float* __restrict__ row, float (&w)[T::P]) {
-  const float4* r4 = reinterpret_cast<const float4*>(row);
-#pragma unroll
-  for (int q = 0; q < T::PP / 4; ++q) {
-    const float4 v = r4[q];
-    if (4 * q + 0 < T::P) w[4 * q + 0] = v.x;
-    if (4 * q + 1 < T::P) w[4 * q + 1] = v.y;
-    if (4 * q + 2 < T::P) w[4 * q + 2] = v.z;
-    if (4 * q + 3 < T::P) w[4 * q + 3] = v.w;
-  }
-}
-template <class T>
-__device__ __forceinline__ void lrow_store(float* __restrict__ row, const float (&w)[T::P]) {
-  float4* r4 = reinterpret_cast<float4*>(row);
-#pragma unroll
-  for (int q = 0; q < T::PP / 4; ++q) {
-    float v[4];
-#pragma unroll
-    for (int e = 0; e < 4; ++e) v[e] = (4 * q + e < T::P) ? w[4 * q + e] : 0.f;
-    r4[q] = make_float4(v[0], v[1], v[2], v[3]);
-  }
-}
-template <class T>
-__device__ __forceinline__ void lrow_store_state(float* __restrict__ row, const float* h) {
-  float4* r4 = reinterpret_cast<float4*>(row);
-#pragma unroll
-  for (int q = 0; q < T::PP / 4; ++q) {
-    float v[4];
-#pragma unroll
-    for (int e = 0; e < 4; ++e) v[e] = (4 * q + e < T::P) ? h[T::chunk_c(4 * q + e)] : 0.f;
-    r4[q] = make_float4(v[0], v[1], v[2], v[3]);
-  }
-}
-// chunk aggregation of a register row (reference: python-float sums / sequential max)
-template <class T>
-__device__ __forceinline__ void lrow_aggregate(const float (&w)[T::P], float* g, int aggregator) {
-#pragma unroll
-  for (int c = 0; c < T::A; ++c) {
-    constexpr int dummy = 0;
-    (void)dummy;
-    const int b = c * T::CS, e = (c == T::A - 1) ? T::P : b + T::CS;
-    if (aggregator == 0) {
-      double acc = 0.0;
-#pragma unroll
-      for (int k = 0; k < T::P; ++k)
-        if (k >= b && k < e) acc += (double)w[k];
-      g[c] = (float)(acc / (double)(e - b));
-    } else {
-      float m = w[b];
-#pragma unroll
-      for (int k = 0; k < T::P; ++k)
-        if (k >= b && k < e) m = (aggregator == 1) ? (w[k] > m ? w[k] : m) : ((w[k] > m && w[k] != 0.0f) ? w[k] : m);
-      g[c] = m;
-    }
-  }
-}
-// aggregation of a streamed row (attack target / teacher): float4 by float4 into the
-// chunk accumulators (same per-chunk order as lrow_aggregate), the row is never held
-template <class T>
-__device__ __forceinline__ void lstream_aggregate(const float* __restrict__ row, float* g, int aggregator) {
-  const float4* r4 = reinterpret_cast<const float4*>(row);
-  double acc[T::A];
-  float m[T::A];
-#pragma unroll
-  for (int c = 0; c < T::A; ++c) acc[c] = 0.0;
-#pragma unroll
-  for (int q = 0; q < T::PP / 4; ++q) {
-    const float4 v4 = r4[q];
-    const float v[4] = {v4.x, v4.y, v4.z, v4.w};
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const int k = 4 * q + e;
-      if (k >= T::P) continue;
-      const int c = T::chunk_c(k);
-      if (aggregator == 0) {
-        acc[c] += (double)v[e];
-      } else if (k == c * T::CS) {
-        m[c] = v[e];
-      } else {
-        m[c] = (aggregator == 1) ? (v[e] > m[c] ? v[e] : m[c]) : ((v[e] > m[c] && v[e] != 0.0f) ? v[e] : m[c]);
-      }
-    }
-  }
-#pragma unroll
-  for (int c = 0; c < T::A; ++c) {
-    const int b = c * T::CS, e = (c == T::A - 1) ? T::P : b + T::CS;
-    g[c] = aggregator == 0 ? (float)(acc[c] / (double)(e - b)) : m[c];
-  }
-}
-template <class T, int L>
-__device__ __forceinline__ void lmlp_rec(const float (&w)[T::P], float* x) {
-  constexpr int I = T::rows(L), O = T::cols(L), OFF = T::off(L);
-  float y[T::MAXW];
-#pragma unroll
-  for (int j = 0; j < O; ++j) {
-    float acc = x[0] * w[OFF + j];
-#pragma unroll
-    for (int i = 1; i < I; ++i) acc = fmaf(x[i], w[OFF + i * O + j], acc);
-    y[j] = acc;
-  }
-#pragma unroll
-  for (int j = 0; j < O; ++j) x[j] = y[j];
-  if constexpr (L < T::D) lmlp_rec<T, L + 1>(w, x);
-}
-template <class T>
-__device__ __forceinline__ void lmlp(const float (&w)[T::P], const float* g, float* h) {
-  float x[T::MAXW];
-#pragma unroll
-  for (int i = 0; i < T::A; ++i) x[i] = g[i];
-  lmlp_rec<T, 0>(w, x);
-#pragma unroll
-  for (int i = 0; i < T::A; ++i) h[i] = x[i];
-}
-template <class T>
-__device__ __forceinline__ bool lrow_close_state(const float (&w)[T::P], const float* h, float eps) {
-  bool ok = true;
-#pragma unroll
-  for (int k = 0; k < T::P; ++k) ok &= !(fabsf(h[T::chunk_c(k)] - w[k]) >= eps);
-  return ok;
-}
-template <class T>
-__device__ __forceinline__ int8_t lclassify(const float (&w)[T::P], float eps, bool with_sec, int aggregator) {
-  bool fin = true;
-#pragma unroll
-  for (int k = 0; k < T::P; ++k) fin &= finitef(w[k]);
-  if (!fin) return C_DIVERGENT;
-  float g[T::A], h1[T::A], h2[T::A];
-  lrow_aggregate<T>(w, g, aggregator);
-  lmlp<T>(w, g, h1);
-  if (finite_all<T>(h1) && lrow_close_state<T>(w, h1, eps)) {
-    bool zero = true;
-#pragma unroll
-    for (int k = 0; k < T::P; ++k) zero &= (-eps <= w[k]) && (w[k] <= eps);
-    return zero ? C_FIX_ZERO : C_FIX_OTHER;
-  }
-  if (with_sec) {
-    lmlp<T>(w, h1, h2);  // aggregate(expand(h1)) == h1 exactly
-    if (finite_all<T>(h2) && lrow_close_state<T>(w, h2, eps)) return C_FIX_SEC;
-  }
-  return C_OTHER;
-}
-// one SGD step on x = y = g (same order as train_step_lds)
-template <class T>
-__device__ __forceinline__ float ltrain_step(float (&w)[T::P], const float* g, float lr) {
-  float act[T::NL][T::MAXW];
-  float x[T::MAXW];
-#pragma unroll
-  for (int i = 0; i < T::A; ++i) x[i] = g[i];
-#pragma unroll
-  for (int l = 0; l <= T::D; ++l) {
-#pragma unroll
-    for (int i = 0; i < T::MAXW; ++i) act[l][i] = x[i];
-    const int I = T::rows(l), O = T::cols(l), OFF = T::off(l);
-    float y[T::MAXW];
-#pragma unroll
-    for (int j = 0; j < T::MAXW; ++j) {
-      if (j < O) {
-        float acc = x[0] * w[OFF + j];
-#pragma unroll
-        for (int i = 1; i < T::MAXW; ++i)
-          if (i < I) acc = fmaf(x[i], w[OFF + i * O + j], acc);
-        y[j] = acc;
-      } else {
-        y[j] = 0.f;
-      }
-    }
-#pragma unroll
-    for (int j = 0; j < T::MAXW; ++j) x[j] = y[j];
-  }
-  float loss = 0.f, st[T::MAXW], st2[T::MAXW];
-#pragma unroll
-  for (int k = 0; k < T::MAXW; ++k) st[k] = 0.f;
-#pragma unroll
-  for (int k = 0; k < T::A; ++k) {
-    const float e = x[k] - g[k];
-    loss += e * e;
-    st[k] = -lr * (2.0f * e / (float)T::A);
-  }
-#pragma unroll
-  for (int l = T::D; l >= 0; --l) {
-    const int R = T::rows(l), Cc = T::cols(l), OFF = T::off(l);
-    if (l > 0) {
-#pragma unroll
-      for (int i = 0; i < T::MAXW; ++i) {
-        if (i < R) {
-          float acc = w[OFF + i * Cc] * st[0];
-#pragma unroll
-          for (int j = 1; j < T::MAXW; ++j)
-            if (j < Cc) acc = fmaf(w[OFF + i * Cc + j], st[j], acc);
-          st2[i] = acc;
-        }
-      }
-    }
-#pragma unroll
-    for (int i = 0; i < T::MAXW; ++i)
-#pragma unroll
-      for (int j = 0; j < T::MAXW; ++j)
-        if (i < R && j < Cc) w[OFF + i * Cc + j] = fmaf(act[l][i], st[j], w[OFF + i * Cc + j]);
-    if (l > 0) {
-#pragma unroll
-      for (int i = 0; i < T::MAXW; ++i) st[i] = (i < R) ? st2[i] : 0.f;
-    }
-  }
-  return loss / (float)T::A;
-}
-
-constexpr int TBROW = 256;  // 4 waves: one per SIMD at ~360 VGPRs
-
-// run_fixpoint phase 1 with the row in VGPRs (same decisions as k_big_fix1)
-template <class T>
-__global__ __launch_bounds__(TBROW) void k_big_fix1_row(SrnnCfg c, SrnnArgs a) {
-  const int64_t p = (int64_t)blockIdx.x * TBROW + threadIdx.x;
-  if (p >= a.n) return;
-  float* state = reinterpret_cast<float*>(a.temp);
-  int8_t* flag = reinterpret_cast<int8_t*>(state + a.n * T::A);
-  float w[T::P];
-  lrow_load<T>(a.W + p * T::PP, w);
-  bool stop = a.steps <= 0;
-  if (!stop && a.early_exit) {
-    bool fin = true;
-#pragma unroll
-    for (int k = 0; k < T::P; ++k) fin &= finitef(w[k]);
-    stop = !fin;
-  }
-  float g[T::A], h[T::A];
-  if (!stop) {
-    lrow_aggregate<T>(w, g, c.aggregator);
-    lmlp<T>(w, g, h);
-    if (a.early_exit && finite_all<T>(h) && lrow_close_state<T>(w, h, a.eps)) stop = true;
-  }
-  if (stop) {  // no step taken: the row is unchanged, classify the general weights
-    flag[p] = 0;
-    if (a.nsteps) a.nsteps[p] = 0;
-    if (a.cls) a.cls[p] = lclassify<T>(w, a.eps, (a.flags & 8) != 0, c.aggregator);
-  } else {
-#pragma unroll
-    for (int i = 0; i < T::A; ++i) state[p * T::A + i] = h[i];
-    flag[p] = 1;
-  }
-}
-template <class T, int OP>
-__global__ __launch_bounds__(TBROW) void k_big_row(SrnnCfg c, SrnnArgs a) {
-  const int64_t p = (int64_t)blockIdx.x * TBROW + threadIdx.x;
-  float w[T::P];
-  if constexpr (OP == OP_CLASSIFY) {
-    __shared__ uint32_t s_cnt[5];
-    if (threadIdx.x < 5) s_cnt[threadIdx.x] = 0;
-    __syncthreads();
-    int8_t k = -1;
-    if (p < a.n) {
-      lrow_load<T>(a.W + p * T::PP, w);
-      k = lclassify<T>(w, a.eps, (a.flags & 8) != 0, c.aggregator);
-      if (a.cls) a.cls[p] = k;
-    }
-    if (a.counts) {  // histogram: wave ballots -> LDS -> one atomic per (block, class)
-#pragma unroll
-      for (int q = 0; q < 5; ++q) {
-        const unsigned long long m = __ballot(k == q);
-        if ((threadIdx.x & 63) == 0 && m) atomicAdd(&s_cnt[q], (uint32_t)__popcll(m));
-      }
-      __syncthreads();
-      if (threadIdx.x < 5 && s_cnt[threadIdx.x]) atomicAdd(a.counts + threadIdx.x, (uint64_t)s_cnt[threadIdx.x]);
-    }
-    return;
-  }
-  if (p >= a.n) return;
-  if constexpr (OP == OP_APPLY) {
-    const int64_t fi = a.idx_f ? a.idx_f[p] : p, ti = a.idx_t ? a.idx_t[p] : p, oi = a.idx_o ? a.idx_o[p] : p;
-    float g[T::A], h[T::A];
-    {  // target row into registers (all 70 loads in flight), aggregated, then dropped
-      float t[T::P];
-      lrow_load<T>(a.W + ti * T::PP, t);
-      lrow_aggregate<T>(t, g, c.aggregator);
-    }
-    lrow_load<T>(a.W + fi * T::PP, w);
-    lmlp<T>(w, g, h);
-    lrow_store_state<T>(a.W2 + oi * T::PP, h);
-  } else {  // OP_TRAIN / OP_LEARN
-    float g[T::A];
-    // teacher samples first (its row dies after the aggregation: one row live at a time)
-    if constexpr (OP == OP_LEARN) lstream_aggregate<T>(a.W2 + (a.idx_t ? a.idx_t[p] : p) * T::PP, g, c.aggregator);
-    lrow_load<T>(a.W + p * T::PP, w);
-    float loss = 0.f;
-    for (int e = 0; e < a.epochs; ++e) {
-      if constexpr (OP == OP_TRAIN) lrow_aggregate<T>(w, g, c.aggregator);
-      loss = ltrain_step<T>(w, g, a.lr);
-    }
-    lrow_store<T>(a.W + p * T::PP, w);
-    if (a.loss) a.loss[p] = loss;
-  }
-}
-
-// ==================================================================================
-// Storage formats, shuffle_random and soups of the big nets (lane per particle).
-//
-// Rows are fp32, bf16 or fp16 (S = StF32 / StBF16 / StF16 of srnn_kernels.h): decoded to
-// fp32 registers on load, rounded on every store and after every application, exactly
-// where the runtime-shape engine rounds (g_quant / g_store of srnn_generic.hip), so a big
-// net gives the same bits here as on the runtime-shape engine on the same device.
-//
-// shuffle_random (reference code/network.py:319-322, applied to the output of
-// apply_to_weights): the output of an aggregating net is chunk-constant, out = expand(h),
-// so the shuffled output out[k] = expand(h)[perm[k]] = h[chunk(perm[k])].  Fisher-Yates is
-// therefore run directly on the CHUNK IDS (4 bits per weight, 35 words per lane in LDS)
-// with the draws of fisher_yates(P_AGGSHUF): swapping entries of perm swaps the entries of
-// chunk o perm, so no 280-entry index permutation is ever materialised.
-// ==================================================================================
-template <class T, class S>
-struct BRow {
-  static constexpr int RB = T::PP * S::BYTES;  // bytes per table row
-  static constexpr int XB = RB + 16;           // exchange row: weights + (slot, gen) tags
-  __device__ static const char* at(const float* base, int64_t i) {
-    return reinterpret_cast<const char*>(base) + i * RB;
-  }
-  __device__ static char* at(float* base, int64_t i) { return reinterpret_cast<char*>(base) + i * RB; }
-  __device__ static void load(const char* row, float (&w)[T::P]) {
-    if constexpr (S::ID == 0) {
-      // integer-typed loads (as for the 16-bit formats): with float loads the compiler
-      // reorders/duplicates row loads across the soup kernel's control flow and spills
-      const uint4* r4 = reinterpret_cast<const uint4*>(row);
-#pragma unroll
-      for (int q = 0; q < T::PP / 4; ++q) {
-        const uint4 v = r4[q];
-        const uint32_t u[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-        for (int e = 0; e < 4; ++e)
-          if (4 * q + e < T::P) w[4 * q + e] = __uint_as_float(u[e]);
-      }
-    } else {
-      const uint2* r2 = reinterpret_cast<const uint2*>(row);
-#pragma unroll
-      for (int q = 0; q < T::PP / 4; ++q) {
-        const uint2 v = r2[q];
-        const uint16_t h[4] = {(uint16_t)(v.x & 0xffffu), (uint16_t)(v.x >> 16), (uint16_t)(v.y & 0xffffu),
-                               (uint16_t)(v.y >> 16)};
-#pragma unroll
-        for (int e = 0; e < 4; ++e)
-          if (4 * q + e < T::P) w[4 * q + e] = S::dec(h[e]);
-      }
-    }
-  }
-  __device__ static void store(char* row, const float (&w)[T::P]) {
-    if constexpr (S::ID == 0) {
-      uint4* r4 = reinterpret_cast<uint4*>(row);
-#pragma unroll
-      for (int q = 0; q < T::PP / 4; ++q) {
-        uint32_t u[4];
-#pragma unroll
-        for (int e = 0; e < 4; ++e) u[e] = (4 * q + e < T::P) ? __float_as_uint(w[4 * q + e]) : 0u;
-        r4[q] = make_uint4(u[0], u[1], u[2], u[3]);
-      }
-    } else {
-      uint2* r2 = reinterpret_cast<uint2*>(row);
-#pragma unroll
-      for (int q = 0; q < T::PP / 4; ++q) {
-        uint32_t h[4];
-#pragma unroll
-        for (int e = 0; e < 4; ++e) h[e] = (4 * q + e < T::P) ? (uint32_t)S::enc(w[4 * q + e]) : 0u;
-        r2[q] = make_uint2(h[0] | (h[1] << 16), h[2] | (h[3] << 16));
-      }
-    }
-  }
-  __device__ static void quant(float (&w)[T::P]) {
-    if constexpr (S::ID != 0) {
-#pragma unroll
-      for (int k = 0; k < T::P; ++k) w[k] = S::q(w[k]);
-    }
-  }
-  __device__ static void quant_a(float* h) {
-    if constexpr (S::ID != 0) {
-#pragma unroll
-      for (int k = 0; k < T::A; ++k) h[k] = S::q(h[k]);
-    }
-  }
-  // chunk aggregation of a streamed row (teacher / attack target): the row is never held
-  __device__ static void stream_aggregate(const char* row, float* g, int aggregator) {
-    {
-      double acc[T::A];
-      float m[T::A];
-#pragma unroll
-      for (int c = 0; c < T::A; ++c) acc[c] = 0.0, m[c] = 0.f;
-#pragma unroll
-      for (int q = 0; q < T::PP / 4; ++q) {
-        float v[4];
-        if constexpr (S::ID == 0) {
-          const uint4 u = reinterpret_cast<const uint4*>(row)[q];
-          v[0] = __uint_as_float(u.x), v[1] = __uint_as_float(u.y), v[2] = __uint_as_float(u.z),
-          v[3] = __uint_as_float(u.w);
-        } else {
-          const uint2 u = reinterpret_cast<const uint2*>(row)[q];
-          v[0] = S::dec((uint16_t)(u.x & 0xffffu)), v[1] = S::dec((uint16_t)(u.x >> 16)),
-          v[2] = S::dec((uint16_t)(u.y & 0xffffu)), v[3] = S::dec((uint16_t)(u.y >> 16));
-        }
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const int k = 4 * q + e;
-          if (k >= T::P) continue;
-          const int c = T::chunk_c(k);
-          if (aggregator == 0) acc[c] += (double)v[e];
-          else if (k == c * T::CS) m[c] = v[e];
-          else m[c] = (aggregator == 1) ? (v[e] > m[c] ? v[e] : m[c]) : ((v[e] > m[c] && v[e] != 0.0f) ? v[e] : m[c]);
-        }
-      }
-#pragma unroll
-      for (int c = 0; c < T::A; ++c) {
-        const int b = c * T::CS, e = (c == T::A - 1) ? T::P : b + T::CS;
-        g[c] = aggregator == 0 ? (float)(acc[c] / (double)(e - b)) : m[c];
-      }
-    }
-  }
-  // generation-start row of global slot g: this rank's table (W2) or the exchange buffers
-  // (flag 128: all-gathered [n_total] table; else the all-to-all rows indexed by rmap)
-  __device__ static const char* row_of(const SrnnArgs& a, int64_t g) {
-    if (a.world <= 1 || (g >= a.lo && g < a.lo + a.n)) return at(a.W2, g - a.lo);
-    if (a.flags & 128) return at(a.recvbuf, g);
-    return reinterpret_cast<const char*>(a.recvbuf) + (int64_t)a.rmap[g] * XB;
-  }
-  // glorot init of a particle straight into its (global) row: the draws and values of
-  // glorot_fill / g_glorot, encoded to the storage format
-  __device__ static void init_row(char* row, const Rng& rng, uint64_t uid) {
-    for (int l = 0; l <= T::D; ++l) {
-      const int r = T::rows(l), cc = T::cols(l), off = T::off(l), n = r * cc;
-      const float lim = sqrtf(6.0f / (float)(r + cc));
-      for (int b = 0; b < (n + 3) / 4; ++b) {
-        const U4 u = rng.draw(uid, (uint32_t)off * 1024u + (uint32_t)b, P_INIT);
-        const uint32_t xs[4] = {u.x, u.y, u.z, u.w};
-        for (int q = 0; q < 4; ++q) {
-          const int k = b * 4 + q;
-          if (k < n) put(row, off + k, -lim + 2.0f * lim * u01(xs[q]));
-        }
-      }
-    }
-    for (int k = T::P; k < T::PP; ++k) put(row, k, 0.f);
-  }
-  __device__ static void put(char* row, int k, float v) {
-    if constexpr (S::ID == 0) reinterpret_cast<float*>(row)[k] = v;
-    else reinterpret_cast<uint16_t*>(row)[k] = S::enc(v);
-  }
-};
-
-// chunk ids of the shuffled output (4 bits per weight) in LDS, word w of lane L at
-// cw[w * TBROW + L] (consecutive lanes -> consecutive banks)
-template <class T>
-struct ChunkPerm {
-  static constexpr int NW = (T::P + 7) / 8;
-  static_assert(T::A <= 16, "chunk ids are 4-bit");
-  uint32_t* cw;
-  __device__ uint32_t word(int w) const { return cw[w * TBROW]; }
-  __device__ int cid(int k) const { return (int)((cw[(k >> 3) * TBROW] >> (4 * (k & 7))) & 15u); }
-  // fisher_yates(perm, P, rng, id, step, P_AGGSHUF) applied to chunk(perm[k])
-  __device__ void draw(const Rng& rng, uint64_t id, uint32_t step) const {
-#pragma unroll
-    for (int w = 0; w < NW; ++w) {
-      uint32_t x = 0;
-#pragma unroll
-      for (int e = 0; e < 8; ++e)
-        if (8 * w + e < T::P) x |= (uint32_t)T::chunk_c(8 * w + e) << (4 * e);
-      cw[w * TBROW] = x;
-    }
-    U4 r{0, 0, 0, 0};
-    int used = 4;
-    uint32_t blk = 0;
-    for (int i = T::P - 1; i > 0; --i) {
-      if (used == 4) {
-        r = rng.draw(id, step * 64u + blk, P_AGGSHUF);
-        ++blk;
-        used = 0;
-      }
-      const uint32_t x = used == 0 ? r.x : used == 1 ? r.y : used == 2 ? r.z : r.w;
-      ++used;
-      int j = (int)(u01(x) * (float)(i + 1));
-      if (j > i) j = i;
-      const int wi = i >> 3, wj = j >> 3, si = 4 * (i & 7), sj = 4 * (j & 7);
-      const uint32_t xi = cw[wi * TBROW], xj = cw[wj * TBROW];
-      const uint32_t d = ((xi >> si) ^ (xj >> sj)) & 15u;
-      if (wi == wj) {
-        cw[wi * TBROW] = xi ^ (d << si) ^ (d << sj);
-      } else {
-        cw[wi * TBROW] = xi ^ (d << si);
-        cw[wj * TBROW] = xj ^ (d << sj);
-      }
-    }
-  }
-};
-
-// h[c] for a runtime chunk id c (A-way select, no dynamic register indexing)
-template <class T>
-__device__ __forceinline__ float pick(const float* h, int c) {
-  float v = h[0];
-#pragma unroll
-  for (int q = 1; q < T::A; ++q) v = (c == q) ? h[q] : v;
-  return v;
-}
-// w = expand(h) (chunk-constant) or its shuffled form h[chunk(perm[k])]
-template <class T, bool SHUF>
-__device__ __forceinline__ void expand_out(float (&w)[T::P], const float* h, const ChunkPerm<T>& cp) {
-  if constexpr (SHUF) {
-#pragma unroll
-    for (int wd = 0; wd < ChunkPerm<T>::NW; ++wd) {
-      const uint32_t x = cp.word(wd);
-#pragma unroll
-      for (int e = 0; e < 8; ++e)
-        if (8 * wd + e < T::P) w[8 * wd + e] = pick<T>(h, (int)((x >> (4 * e)) & 15u));
-    }
-  } else {
-#pragma unroll
-    for (int k = 0; k < T::P; ++k) w[k] = h[T::chunk_c(k)];
-  }
-}
-// every |expand'(h)[k] - w[k]| < eps (expand' = shuffled or plain)
-template <class T, bool SHUF>
-__device__ __forceinline__ bool close_out(const float (&w)[T::P], const float* h, float eps, const ChunkPerm<T>& cp) {
-  bool ok = true;
-  if constexpr (SHUF) {
-#pragma unroll
-    for (int wd = 0; wd < ChunkPerm<T>::NW; ++wd) {
-      const uint32_t x = cp.word(wd);
-#pragma unroll
-      for (int e = 0; e < 8; ++e)
-        if (8 * wd + e < T::P) ok &= !(fabsf(pick<T>(h, (int)((x >> (4 * e)) & 15u)) - w[8 * wd + e]) >= eps);
-    }
-  } else {
-    ok = lrow_close_state<T>(w, h, eps);
-  }
-  return ok;
-}
-// chunk aggregation of expand'(h) (mean: double sums in index order, like g_aggregate of the
-// materialised vector; without the shuffle the result is h itself, exactly)
-template <class T, bool SHUF>
-__device__ __forceinline__ void aggregate_out(const float* h, float* g, int aggregator, const ChunkPerm<T>& cp) {
-  if constexpr (!SHUF) {
-#pragma unroll
-    for (int c = 0; c < T::A; ++c) g[c] = h[c];
-  } else {
-#pragma unroll
-    for (int c = 0; c < T::A; ++c) {
-      const int b = c * T::CS, e = (c == T::A - 1) ? T::P : b + T::CS;
-      double acc = 0.0;
-      float m = pick<T>(h, cp.cid(b));
-      for (int k = b; k < e; ++k) {
-        const float v = pick<T>(h, cp.cid(k));
-        acc += (double)v;
-        m = (aggregator == 1) ? (v > m ? v : m) : ((v > m && v != 0.0f) ? v : m);
-      }
-      g[c] = aggregator == 0 ? (float)(acc / (double)(e - b)) : m;
-    }
-  }
-}
-// census class of a register row (g_classify_w): f1 = apply(w, w), f2 = apply(w, f1), both
-// with the same shuffle permutation (one ApplyCtx), rounded to the storage format
-template <class T, class S, bool SHUF>
-__device__ int8_t bclassify(const float (&w)[T::P], float eps, bool with_sec, int aggregator, const ChunkPerm<T>& cp) {
-  bool fin = true;
-#pragma unroll
-  for (int k = 0; k < T::P; ++k) fin &= finitef(w[k]);
-  if (!fin) return C_DIVERGENT;
-  float g[T::A], h1[T::A], h2[T::A];
-  lrow_aggregate<T>(w, g, aggregator);
-  lmlp<T>(w, g, h1);
-  BRow<T, S>::quant_a(h1);
-  if (finite_all<T>(h1) && close_out<T, SHUF>(w, h1, eps, cp)) {
-    bool zero = true;
-#pragma unroll
-    for (int k = 0; k < T::P; ++k) zero &= (-eps <= w[k]) && (w[k] <= eps);
-    return zero ? C_FIX_ZERO : C_FIX_OTHER;
-  }
-  if (with_sec) {
-    aggregate_out<T, SHUF>(h1, g, aggregator, cp);
-    lmlp<T>(w, g, h2);
-    BRow<T, S>::quant_a(h2);
-    if (finite_all<T>(h2) && close_out<T, SHUF>(w, h2, eps, cp)) return C_FIX_SEC;
-  }
-  return C_OTHER;
-}
-
-// classify (+ histogram, + respawn count flag 64, + generation advance flag 512), attack,
-// train and learn_from with any storage format and shuffler
-template <class T, class S, bool SHUF, int OP>
-__global__ __launch_bounds__(TBROW) void k_big_rows(SrnnCfg c, SrnnArgs a) {
-  using R = BRow<T, S>;
-  __shared__ uint32_t s_cw[SHUF ? ChunkPerm<T>::NW * TBROW : 1];
-  const ChunkPerm<T> cp{s_cw + threadIdx.x};
-  const int64_t p = (int64_t)blockIdx.x * TBROW + threadIdx.x;
-  const Rng rng{(uint32_t)a.seed, (uint32_t)(a.seed >> 32)};
-  float w[T::P];
-  if constexpr (OP == OP_CLASSIFY) {
-    __shared__ uint32_t s_cnt[6];
-    if (threadIdx.x < 6) s_cnt[threadIdx.x] = 0;
-    __syncthreads();
-    int8_t k = -1;
-    if (p < a.n) {
-      R::load(R::at(a.W, p), w);
-      if constexpr (SHUF) cp.draw(rng, a.uid ? (uint64_t)a.uid[p] : (uint64_t)(a.lo + p), a.ctr);
-      k = bclassify<T, S, SHUF>(w, a.eps, (a.flags & 8) != 0, c.aggregator, cp);
-      if (a.cls) a.cls[p] = k;
-    }
-    if (a.counts) {  // wave ballots -> LDS -> one atomic per (block, class)
-#pragma unroll
-      for (int q = 0; q < 5; ++q) {
-        const unsigned long long m = __ballot(k == q);
-        if ((threadIdx.x & 63) == 0 && m) atomicAdd(&s_cnt[q], (uint32_t)__popcll(m));
-      }
-      if (a.flags & 64) {
-        const unsigned long long m = __ballot(p < a.n && a.respawn[p] != 0);
-        if ((threadIdx.x & 63) == 0 && m) atomicAdd(&s_cnt[5], (uint32_t)__popcll(m));
-      }
-      __syncthreads();
-      if (threadIdx.x < 6 && s_cnt[threadIdx.x] && (threadIdx.x < 5 || (a.flags & 64)))
-        atomicAdd(a.counts + threadIdx.x, (uint64_t)s_cnt[threadIdx.x]);
-    }
-    if ((a.flags & 512) && blockIdx.x == 0 && threadIdx.x == 0) {
-      if (a.gen_out) a.gen_out[0] = a.gen_ptr[0] + 1;
-      else ((int32_t*)a.gen_ptr)[0] = a.gen_ptr[0] + 1;
-    }
-    return;
-  }
-  if (p >= a.n) return;
-  if constexpr (OP == OP_APPLY) {
-    const int64_t fi = a.idx_f ? a.idx_f[p] : p, ti = a.idx_t ? a.idx_t[p] : p, oi = a.idx_o ? a.idx_o[p] : p;
-    float g[T::A], h[T::A];
-    // target row into the registers (all its loads in flight at once), aggregated, then
-    // overwritten by the attacker's row: streaming the target one load at a time halved
-    // the attack rate (1.72 vs 0.82 ms at 1M particles)
-    R::load(R::at(a.W, ti), w);
-    lrow_aggregate<T>(w, g, c.aggregator);
-    R::load(R::at(a.W, fi), w);
-    lmlp<T>(w, g, h);
-    R::quant_a(h);
-    if constexpr (SHUF) cp.draw(rng, a.uid ? (uint64_t)a.uid[ti] : (uint64_t)ti, a.ctr);
-    expand_out<T, SHUF>(w, h, cp);
-    R::store(R::at(a.W2, oi), w);
-  } else {  // OP_TRAIN / OP_LEARN (no randomness in an aggregating net's SGD step)
-    float g[T::A];
-    if constexpr (OP == OP_LEARN) R::stream_aggregate(R::at(a.W2, a.idx_t ? a.idx_t[p] : p), g, c.aggregator);
-    R::load(R::at(a.W, p), w);
-    float loss = 0.f;
-    for (int e = 0; e < a.epochs; ++e) {
-      if constexpr (OP == OP_TRAIN) lrow_aggregate<T>(w, g, c.aggregator);
-      loss = ltrain_step<T>(w, g, a.lr);
-    }
-    R::store(R::at(a.W, p), w);
-    if (a.loss) a.loss[p] = loss;
-  }
-}
-
-// init / perturb / respawn of big rows in any storage format (lane per particle)
-template <class T, class S, int OP>
-__global__ __launch_bounds__(256) void k_big_lane_s(SrnnCfg c, SrnnArgs a) {
-  using R = BRow<T, S>;
-  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (i >= a.n) return;
-  const Rng rng{(uint32_t)a.seed, (uint32_t)(a.seed >> 32)};
-  char* row = R::at(a.W, i);
-  if constexpr (OP == OP_INIT) {
-    R::init_row(row, rng, a.uid ? (uint64_t)a.uid[i] : (uint64_t)i);
-  } else if constexpr (OP == OP_RESPAWN) {
-    if (a.respawn[i] != 0) R::init_row(row, rng, respawn_key(a.gen_ptr ? a.gen_ptr[0] : a.gen, a.lo + i));
-  } else {  // OP_PERTURB
-    const uint64_t uid = a.uid ? (uint64_t)a.uid[i] : (uint64_t)i;
-    float w[T::P];
-    R::load(row, w);
-    for (int k = 0; k < T::P; ++k) {
-      const U4 u = rng.draw(uid, a.ctr * 1024u + (uint32_t)k, P_PERTURB);
-      const double mag = (double)u01(u.y) * (double)a.eps;
-      R::put(row, k, u01(u.x) < 0.5f ? (float)((double)w[k] + mag) : (float)((double)w[k] - mag));
-    }
-  }
-}
-
-// Synchronous soup generation of local row j (Item::soup_evolve / GItem::soup_evolve with
-// the row in VGPRs): attacks received in ascending attacker-slot order (generation-start
-// attacker rows), learn_from `severity` epochs on the teacher's aggregated generation-start
-// row, `epochs` self-train steps, respawn flags (+ inline re-init, flag 32), the 64-row
-// respawn ballot (or per-row flags, flag 16).  Only one 280-float row is live at a time:
-// the victim's aggregate is taken before the attacker's row is loaded into the same
-// registers (an attack rewrites every weight of the victim).
-template <class T, class S, bool SHUF>
-__global__ __launch_bounds__(TBROW) void k_big_soup_evolve(SrnnCfg c, SrnnArgs a) {
-  using R = BRow<T, S>;
-  __shared__ uint32_t s_cw[SHUF ? ChunkPerm<T>::NW * TBROW : 1];
-  const ChunkPerm<T> cp{s_cw + threadIdx.x};
-  const int64_t j = (int64_t)blockIdx.x * TBROW + threadIdx.x;
-  const Rng rng{(uint32_t)a.seed, (uint32_t)(a.seed >> 32)};
-  bool rs_any = false;
-  if (j < a.n) {
-    const int64_t g = a.lo + j;
-    const int32_t gen = a.gen_ptr ? a.gen_ptr[0] : a.gen;
-    float w[T::P];
-    R::load(R::at(a.W2, j), w);
-    uint32_t ctr = (uint32_t)gen * 1024u;
-    const int32_t head = a.i32e[j];
-    a.i32e[j] = -1;  // list consumed: reset for the next generation's decide
-    int32_t last = -1;
-    while (head >= 0) {
-      int32_t best = INT_MAX;
-      for (int32_t r = head; r >= 0; r = a.i32f[r]) best = (r > last && r < best) ? r : best;
-      if (best == INT_MAX) break;
-      last = best;
-      float gv[T::A], h[T::A];
-      lrow_aggregate<T>(w, gv, c.aggregator);
-      R::load(R::row_of(a, best), w);
-      lmlp<T>(w, gv, h);
-      R::quant_a(h);
-      if constexpr (SHUF) cp.draw(rng, (uint64_t)g, ctr);
-      expand_out<T, SHUF>(w, h, cp);
-      ctr += 1;
-    }
-    int32_t my_at, te;
-    Item<Weightwise<1, 1>, StF32>::decision(a, g, gen, my_at, te);
-    int8_t act = A_NONE;
-    int64_t cpart = -1;
-    if (my_at >= 0) act = A_ATTACKING, cpart = my_at;
-    // learn_from (`severity` steps on the teacher's aggregate) then self-train (`epochs`
-    // steps on the own aggregate) as ONE step loop: a single inlined SGD step keeps the
-    // register allocation of the 280-float row to one copy
-    float gt[T::A];
-    int nlearn = 0;
-    if (te >= 0) {
-      R::stream_aggregate(R::row_of(a, te), gt, c.aggregator);
-      nlearn = a.severity > 0 ? a.severity : 0;
-      act = A_LEARN_FROM;
-      cpart = te;
-    }
-    if (a.epochs > 0) act = A_TRAIN_SELF, cpart = -1;
-    const int nsteps = nlearn + (a.epochs > 0 ? a.epochs : 0);
-    float loss = 0.f;
-    for (int s = 0; s < nsteps; ++s) {
-      float gs[T::A];
-      if (s < nlearn) {
-#pragma unroll
-        for (int q = 0; q < T::A; ++q) gs[q] = gt[q];
-      } else {
-        lrow_aggregate<T>(w, gs, c.aggregator);
-      }
-      loss = ltrain_step<T>(w, gs, a.lr);
-    }
-    R::quant(w);  // the stored state decides respawn
-    bool bad = false, zero = true;
-#pragma unroll
-    for (int k = 0; k < T::P; ++k) {
-      bad |= !finitef(w[k]);
-      zero &= (-a.eps <= w[k]) && (w[k] <= a.eps);
-    }
-    int8_t rsp = 0;
-    if ((a.flags & 2) && bad) rsp = 1;
-    else if ((a.flags & 4) && zero) rsp = 2;
-    if (rsp && (a.flags & 32)) R::init_row(R::at(a.W, j), rng, respawn_key(gen, g));  // newborn
-    else R::store(R::at(a.W, j), w);
-    if (a.action) a.action[j] = act;
-    if (a.counterpart) a.counterpart[j] = cpart;
-    if (a.loss) a.loss[j] = loss;
-    a.respawn[j] = rsp;
-    rs_any = rsp != 0;
-  }
-  if (a.i32c) {
-    if (a.flags & 16) {
-      if (j < a.n) a.i32c[j] = rs_any ? 1 : 0;
-    } else {
-      const unsigned long long m = __ballot(rs_any);
-      if ((threadIdx.x & 63) == 0) reinterpret_cast<unsigned long long*>(a.i32c)[j >> 6] = m;
-    }
-  }
-}
-
-// Single-rank respawn of big nets (k_respawn_seq): one workgroup scans the 64-row ballots
-// in slot order, assigns the newborns' uids, re-initialises their rows, advances next_uid
-// and the generation counter, zeroes the census histogram.
-template <class T, class S>
-__global__ __launch_bounds__(TBR) void k_big_respawn_seq(SrnnCfg c, SrnnArgs a) {
-  using R = BRow<T, S>;
-  __shared__ int32_t s_wave[TBR / 64];
-  const unsigned long long* masks = reinterpret_cast<const unsigned long long*>(a.i32c);
-  const int64_t nb = (a.n + 63) / 64;
-  const int64_t ch = (nb + TBR - 1) / TBR;
-  const int64_t b0 = (int64_t)threadIdx.x * ch;
-  const int64_t b1 = b0 + ch < nb ? b0 + ch : nb;
-  int32_t cnt = 0;
-  for (int64_t b = b0; b < b1; ++b) cnt += __popcll(masks[b]);
-  int32_t total;
-  const int32_t incl = block_incl_scan<TBR>(cnt, s_wave, &total);
-  const int64_t base = *(volatile const int64_t*)a.uid_base;
-  const int32_t gen = a.gen_ptr ? a.gen_ptr[0] : a.gen;
-  const Rng rng{(uint32_t)a.seed, (uint32_t)(a.seed >> 32)};
-  int64_t k = base + incl - cnt;
-  for (int64_t b = b0; b < b1 && cnt; ++b) {
-    unsigned long long m = masks[b];
-    while (m) {
-      const int bit = __ffsll((long long)m) - 1;
-      m &= m - 1;
-      const int64_t r = b * 64 + bit;
-      a.uid_out[r] = k++;
-      if (!(a.flags & 32)) R::init_row(R::at(a.W, r), rng, respawn_key(gen, a.lo + r));  // else done inline
-    }
-  }
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    ((int64_t*)a.uid_base)[0] = base + total;
-    if (a.gen_out) a.gen_out[0] = gen + 1;
-    else if (a.gen_ptr) ((int32_t*)a.gen_ptr)[0] = gen + 1;
-  }
-  if (a.counts && threadIdx.x < 5) a.counts[threadIdx.x] = 0;
-}
-
-// ops of the big nets that take any storage format / shuffler (everything a soup needs)
-template <class T, class S, bool SHUF>
-int big_run_s(int op, const SrnnCfg& c, const SrnnArgs& a) {
-  hipStream_t st = (hipStream_t)a.stream;
-  const unsigned gl = (unsigned)((a.n + 255) / 256), g64 = (unsigned)((a.n + TBROW - 1) / TBROW);
-  switch (op) {
-    case OP_INIT: hipLaunchKernelGGL((k_big_lane_s<T, S, OP_INIT>), dim3(gl), dim3(256), 0, st, c, a); break;
-    case OP_PERTURB: hipLaunchKernelGGL((k_big_lane_s<T, S, OP_PERTURB>), dim3(gl), dim3(256), 0, st, c, a); break;
-    case OP_RESPAWN: hipLaunchKernelGGL((k_big_lane_s<T, S, OP_RESPAWN>), dim3(gl), dim3(256), 0, st, c, a); break;
-    case OP_APPLY: hipLaunchKernelGGL((k_big_rows<T, S, SHUF, OP_APPLY>), dim3(g64), dim3(TBROW), 0, st, c, a); break;
-    case OP_CLASSIFY:
-      hipLaunchKernelGGL((k_big_rows<T, S, SHUF, OP_CLASSIFY>), dim3(g64), dim3(TBROW), 0, st, c, a);
-      break;
-    case OP_TRAIN: hipLaunchKernelGGL((k_big_rows<T, S, SHUF, OP_TRAIN>), dim3(g64), dim3(TBROW), 0, st, c, a); break;
-    case OP_LEARN: hipLaunchKernelGGL((k_big_rows<T, S, SHUF, OP_LEARN>), dim3(g64), dim3(TBROW), 0, st, c, a); break;
-    case OP_SOUP_EVOLVE:
-      hipLaunchKernelGGL((k_big_soup_evolve<T, S, SHUF>), dim3(g64), dim3(TBROW), 0, st, c, a);
-      break;
-    case OP_RESPAWN_SEQ: hipLaunchKernelGGL((k_big_respawn_seq<T, S>), dim3(1), dim3(TBR), 0, st, c, a); break;
-    case OP_SOUP_DECIDE: {
-      // decisions are shape independent: every global slot
-      if (a.n_total <= 0) return 0;
-      hipLaunchKernelGGL((k_op<Weightwise<1, 1>, OP_SOUP_DECIDE, StF32>), dim3((unsigned)((a.n_total + TB - 1) / TB)),
-                         dim3(TB), 0, st, SrnnCfg{}, a);
-      break;
-    }
-    default: set_error("op not supported for big aggregating nets"); return -5;
-  }
-  hipError_t e = hipGetLastError();
-  if (e != hipSuccess) {
-    set_error(hipGetErrorString(e));
-    return -3;
-  }
-  return 0;
-}
-
-// true when big_run serves (op, storage, shuffler); the rest goes to the runtime-shape engine
-constexpr bool big_serves(int op, int dtype, int shuffler) {
-  if (op == OP_INIT || op == OP_PERTURB || op == OP_RESPAWN || op == OP_APPLY || op == OP_CLASSIFY ||
-      op == OP_TRAIN || op == OP_LEARN || op == OP_SOUP_EVOLVE || op == OP_RESPAWN_SEQ || op == OP_SOUP_DECIDE)
-    return true;
-  return op == OP_RUN_FIXPOINT && dtype == 0 && shuffler == 0;
-}
-
-template <class T>
-int big_run(int op, const SrnnCfg& c, const SrnnArgs& a) {
-  if (!a.dev) {
-    set_error("wave-per-particle nets run on the GPU only (use a smaller shape on the host)");
-    return -5;
-  }
-  if (!big_serves(op, c.dtype, c.shuffler)) {
-    set_error("op not served by the big-net kernels (runtime-shape engine)");
-    return -5;
-  }
-  // lane-per-particle row kernels (default) or the wave-per-particle ones (SRNN_BIG_WAVE=1,
-  // fp32 tables without shuffle only)
-  const char* wave_env = std::getenv("SRNN_BIG_WAVE");
-  const bool row_kernels = !(wave_env && wave_env[0] == '1');
-  const bool wave_op = !row_kernels && (op == OP_APPLY || op == OP_CLASSIFY || op == OP_TRAIN || op == OP_LEARN);
-  if (op != OP_RUN_FIXPOINT && !(wave_op && c.dtype == 0 && c.shuffler == 0)) {
-    if (a.n <= 0 && op != OP_SOUP_DECIDE) return 0;
-    const bool sh = c.shuffler != 0;
-#ifndef SRNN_BIG_FAST  // (register-allocation experiments: fp32 instantiations only)
-    if (c.dtype == 1) return sh ? big_run_s<T, StBF16, true>(op, c, a) : big_run_s<T, StBF16, false>(op, c, a);
-    if (c.dtype == 2) return sh ? big_run_s<T, StF16, true>(op, c, a) : big_run_s<T, StF16, false>(op, c, a);
-#endif
-    return sh ? big_run_s<T, StF32, true>(op, c, a) : big_run_s<T, StF32, false>(op, c, a);
-  }
-  hipStream_t st = (hipStream_t)a.stream;
-  if (a.n <= 0) return 0;
-  const unsigned gw = (unsigned)((a.n + BW - 1) / BW), gl = (unsigned)((a.n + 255) / 256);
-  const unsigned g64 = (unsigned)((a.n + TBROW - 1) / TBROW);
-  switch (op) {
-    case OP_INIT: hipLaunchKernelGGL((k_big_lane<T, OP_INIT>), dim3(gl), dim3(256), 0, st, c, a); break;
-    case OP_PERTURB: hipLaunchKernelGGL((k_big_lane<T, OP_PERTURB>), dim3(gl), dim3(256), 0, st, c, a); break;
-    case OP_APPLY:
-      if (row_kernels) hipLaunchKernelGGL((k_big_row<T, OP_APPLY>), dim3(g64), dim3(TBROW), 0, st, c, a);
-      else hipLaunchKernelGGL((k_big<T, OP_APPLY>), dim3(gw), dim3(TBB), 0, st, c, a);
-      break;
-    case OP_RUN_FIXPOINT:
-      if (!a.temp || a.temp_bytes < a.n * (T::A * 4 + 1)) {
-        set_error("run_fixpoint on wave-per-particle nets needs temp >= n*(4*aggregates+1) bytes");
-        return -5;
-      }
-      if (row_kernels) hipLaunchKernelGGL((k_big_fix1_row<T>), dim3(g64), dim3(TBROW), 0, st, c, a);
-      else hipLaunchKernelGGL((k_big_fix1<T>), dim3(gw), dim3(TBB), 0, st, c, a);
-      hipLaunchKernelGGL((k_big_fix2<T>), dim3(gl), dim3(256), 0, st, c, a);
-      hipLaunchKernelGGL((k_big_fix3<T>), dim3(gw), dim3(TBB), 0, st, c, a);
-      break;
-    case OP_CLASSIFY:
-      if (row_kernels) hipLaunchKernelGGL((k_big_row<T, OP_CLASSIFY>), dim3(g64), dim3(TBROW), 0, st, c, a);
-      else hipLaunchKernelGGL((k_big<T, OP_CLASSIFY>), dim3(gw), dim3(TBB), 0, st, c, a);
-      break;
-    case OP_TRAIN:
-      if (row_kernels) hipLaunchKernelGGL((k_big_row<T, OP_TRAIN>), dim3(g64), dim3(TBROW), 0, st, c, a);
-      else hipLaunchKernelGGL((k_big<T, OP_TRAIN>), dim3(gw), dim3(TBB), 0, st, c, a);
-      break;
-    case OP_LEARN:
-      if (row_kernels) hipLaunchKernelGGL((k_big_row<T, OP_LEARN>), dim3(g64), dim3(TBROW), 0, st, c, a);
-      else hipLaunchKernelGGL((k_big<T, OP_LEARN>), dim3(gw), dim3(TBB), 0, st, c, a);
-      break;
-    default: set_error("op not supported for wave-per-particle nets"); return -5;
-  }
-  hipError_t e = hipGetLastError();
-  if (e != hipSuccess) {
-    set_error(hipGetErrorString(e));
-    return -3;
-  }
-  return 0;
-}
-
-}  // namespace srnn
-
-using AGGB_4_10_3 = srnn::AggBig<4, 10, 3>;
-using AGGB_4_8_2 = srnn::AggBig<4, 8, 2>;
-using AGGB_4_16_2 = srnn::AggBig<4, 16, 2>;
-
-#define SRNN_TRY_BIG(T, W_, D_, A_)                                              \
-  if (c->width == (W_) && c->depth == (D_) && c->aggregates == (A_)) {           \
-    if (c->p != T::P || c->pp != T::PP) {                                        \
-      srnn::set_error("layout mismatch (p/pp) for instantiated shape");          \
-      return -4;                                                                 \
-    }                                                                            \
-    if (op < 0) return 0;                                                        \
-    return srnn::big_run<T>(op, *c, *a);                                         \
+#define SRNN_TRY_BIG(FN, W_, D_, A_)                                                   \
+  if (c->width == (W_) && c->depth == (D_) && c->aggregates == (A_)) {                 \
+    using T = srnn::AggBig<A_, W_, D_>;                                                \
+    if (c->p != T::P || c->pp != T::PP) {                                              \
+      srnn::set_error("layout mismatch (p/pp) for instantiated shape");                \
+      return -4;                                                                       \
+    }                                                                                  \
+    if (op < 0) return 0;                                                              \
+    return FN(op, c, a);                                                               \
   }
 
 extern "C" int srnn_aggbig_serves(int op, int dtype, int shuffler) { return srnn::big_serves(op, dtype, shuffler) ? 1 : 0; }
 
 extern "C" int srnn_dispatch_aggbig(int op, const SrnnCfg* c, const SrnnArgs* a) {
-  SRNN_TRY_BIG(AGGB_4_10_3, 10, 3, 4)
-#ifndef SRNN_BIG_FAST
-  SRNN_TRY_BIG(AGGB_4_8_2, 8, 2, 4)
-  SRNN_TRY_BIG(AGGB_4_16_2, 16, 2, 4)
-#endif
+  SRNN_TRY_BIG(srnn_big_4_10_3, 10, 3, 4)
+  SRNN_TRY_BIG(srnn_big_4_8_2, 8, 2, 4)
+  SRNN_TRY_BIG(srnn_big_4_16_2, 16, 2, 4)
   return 1;
 }
