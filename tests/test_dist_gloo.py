@@ -51,7 +51,8 @@ def _worker(rank, world, port, spec_json, out_dir, dtype="float32", exchange="al
 @pytest.mark.parametrize("world,dtype,exchange,chunks", [
     (2, "float32", "alltoall", (GENS,)), (3, "float32", "alltoall", (1, 2, 3)), (4, "float32", "alltoall", (GENS,)),
     (2, "float32", "allgather", (2, 4)), (2, "bfloat16", "alltoall", (GENS,)), (3, "float16", "allgather", (GENS,)),
-    (1, "float32", "alltoall", (2, 1, 3))])
+    (1, "float32", "alltoall", (2, 1, 3)),
+    (8, "float32", "alltoall", (4, 2))])  # the node's rank count (bench.py --gpus 8)
 def test_sharded_soup_equals_single_rank(tmp_path, world, dtype, exchange, chunks):
     """world 1 = the forced sharded path (collectives over a one-rank group)."""
     spec = ArchSpec.weightwise(2, 2)
