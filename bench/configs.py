@@ -28,12 +28,18 @@ from self_replicating_neural_networks_amd.ops import kernels as K  # noqa: E402
 from self_replicating_neural_networks_amd.soup_engine import SoupEngine, plan_population  # noqa: E402
 
 
-def timeit(fn, reps=5, warmup=2):
+def timeit(fn, reps=5, warmup=2, pre=None):
+    """Median event time of fn(); ``pre`` (untimed) runs before every call, e.g. to restore
+    the input table of an in-place operator."""
     for _ in range(warmup):
+        if pre is not None:
+            pre()
         fn()
     torch.cuda.synchronize()
     ts = []
     for _ in range(reps):
+        if pre is not None:
+            pre()
         a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         a.record()
         fn()
@@ -70,9 +76,8 @@ def config2(args):
         W = W0.clone()
 
         def run():
-            W.copy_(W0)
             K.run_fixpoint(spec, W, steps, 1e-4, early_exit=False, with_sec=False)
-        t = timeit(run, args.reps)
+        t = timeit(run, args.reps, pre=lambda: W.copy_(W0))
         res[f"{dt_name}_us"] = t * 1e6
         res[f"{dt_name}_self_applications_per_s"] = n * steps / t
     return res
@@ -90,9 +95,8 @@ def config4(args):
     res = dict(config=4, name=f"{n} Aggregating(4,10,3) particles (P={spec.P})")
 
     def selfapp():
-        W.copy_(W0)
         K.run_fixpoint(spec, W, 100, 1e-4, early_exit=False, with_sec=False)
-    t = timeit(selfapp, args.reps)
+    t = timeit(selfapp, args.reps, pre=lambda: W.copy_(W0))
     res["self_apply100_ms"] = t * 1e3
     res["self_applications_per_s"] = n * 100 / t
     t = timeit(lambda: K.apply(spec, W0, out, idx_f=idx), args.reps)
@@ -100,12 +104,13 @@ def config4(args):
     res["attack_GBps"] = 3 * n * spec.PP * 4 / t / 1e9
     t = timeit(lambda: K.classify(spec, W0, 1e-4), args.reps)
     res["classify_ms"] = t * 1e3
+    res["classify_GBps"] = n * spec.PP * 4 / t / 1e9
 
     def train():
-        W.copy_(W0)
         K.train(spec, W, epochs=1, uid=uid, seed=3)
-    t = timeit(train, args.reps)
+    t = timeit(train, args.reps, pre=lambda: W.copy_(W0))
     res["train_epoch_ms"] = t * 1e3
+    res["train_epoch_GBps"] = 2 * n * spec.PP * 4 / t / 1e9
     res["sgd_steps_per_s"] = n / t
     return res
 

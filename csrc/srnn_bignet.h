@@ -18,6 +18,7 @@
 #pragma once
 #include "srnn_kernels.h"
 #include <cstdlib>
+#include <utility>
 
 namespace srnn {
 
@@ -793,15 +794,124 @@ __device__ __forceinline__ float ltrain_step(float (&w)[T::P], const float* g, f
 
 constexpr int TBROW = 256;  // 4 waves: one per SIMD at ~360 VGPRs
 
-// run_fixpoint phase 1 with the row in VGPRs (same decisions as k_big_fix1)
+// ---- coalesced row staging through LDS --------------------------------------------------
+// A lane-per-row load has every wave instruction fetch 16-byte pieces of 64 rows 1120 B
+// apart (64 cache lines per instruction): 3.9 TB/s measured on 1M rows.  Staged, the wave
+// moves its 64 rows in passes of Q 16-byte pieces per row: piece slot k of lane L is piece
+// (64 k + L) % Q of row (64 k + L) / Q, so one wave instruction covers ~64/Q consecutive row
+// segments (5.6-5.8 TB/s, the streaming-read ceiling 5.85; bench/micro/row_load.hip), goes
+// through this wave's LDS area (row pitch Q|1 pieces: an odd multiple of 4 dwords, so the
+// 16 lanes of a ds_read_b128 quarter-wave hit distinct bank groups) and each lane then reads
+// its own row segment.  Rows are addressed by a 32-bit index into one table (idx < 0: no
+// row); every lane of the wave must execute the call (wave-uniform control flow).
+#ifndef SRNN_STAGE_Q
+#define SRNN_STAGE_Q 18
+#endif
+template <int NQ>  // 16-byte pieces per row
+struct Stage {
+  static constexpr int Q = SRNN_STAGE_Q < NQ ? SRNN_STAGE_Q : NQ;
+  static constexpr int PI = Q | 1;
+  static constexpr int NPASS = (NQ + Q - 1) / Q;
+  static constexpr int WAVE_U4 = 64 * PI;  // LDS uint4 per wave
+  static constexpr int len(int s) { return NQ - Q * s < Q ? NQ - Q * s : Q; }
+};
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+// per piece slot k: the row index of its owner lane and the piece within the pass (every
+// loop over slots / pieces is a compile-time fold: a runtime index into these arrays or into
+// the row registers would put them in scratch memory)
+template <int NQ>
+struct StageMap {
+  static constexpr int Q = Stage<NQ>::Q, PI = Stage<NQ>::PI;
+  int32_t rk[Q];
+  int32_t fk[Q];
+  template <int K>
+  __device__ __forceinline__ void set(int32_t idx, int L) {
+    const int t = 64 * K + L, r = t / Q;
+    fk[K] = t - r * Q;
+    rk[K] = __shfl(idx, r);
+  }
+  template <int... K>
+  __device__ __forceinline__ void init(int32_t idx, int L, std::integer_sequence<int, K...>) {
+    (set<K>(idx, L), ...);
+  }
+  __device__ __forceinline__ StageMap(int32_t idx, int L) { init(idx, L, std::make_integer_sequence<int, Q>{}); }
+  // LDS slot (uint4) of piece slot k: row r at r * PI + f
+  __device__ __forceinline__ static int lds_slot(int k, int L) {
+    const int t = 64 * k + L, r = t / Q;
+    return r * PI + (t - r * Q);
+  }
+};
+template <int NQ, int S, int K>
+__device__ __forceinline__ uint4 stage_fetch(const char* __restrict__ base, const StageMap<NQ>& m) {
+  constexpr int Q = Stage<NQ>::Q, LEN = Stage<NQ>::len(S);
+  constexpr int64_t RB = (int64_t)NQ * 16;
+  const bool ok = m.rk[K] >= 0 && m.fk[K] < LEN;  // else a harmless load of piece 0 of row 0
+  const int64_t off = ok ? (int64_t)m.rk[K] * RB + (int64_t)(Q * S + m.fk[K]) * 16 : 0;
+  return *reinterpret_cast<const uint4*>(base + off);
+}
+template <int NQ, int S, int K>
+__device__ __forceinline__ void stage_put(char* __restrict__ base, const StageMap<NQ>& m, const uint4* st, int L) {
+  constexpr int Q = Stage<NQ>::Q, LEN = Stage<NQ>::len(S);
+  constexpr int64_t RB = (int64_t)NQ * 16;
+  const uint4 v = st[StageMap<NQ>::lds_slot(K, L)];
+  if (m.rk[K] >= 0 && m.fk[K] < LEN)
+    *reinterpret_cast<uint4*>(base + (int64_t)m.rk[K] * RB + (int64_t)(Q * S + m.fk[K]) * 16) = v;
+}
+// pass S of a staged load in two halves: fetch (the wave's global loads, into registers)
+// and commit (after every lane's reads of the previous pass: pieces to LDS, wave barrier).
+// The loads of pass S + 1 are issued before pass S is committed, so a wave keeps one pass of
+// loads in flight while it stages and decodes the previous one.
+template <int NQ>
+struct StageBuf {
+  uint4 v[Stage<NQ>::Q];
+};
+template <int NQ, int S, int... K>
+__device__ __forceinline__ StageBuf<NQ> stage_fetch_(const char* __restrict__ base, const StageMap<NQ>& m,
+                                                     std::integer_sequence<int, K...>) {
+  return StageBuf<NQ>{{stage_fetch<NQ, S, K>(base, m)...}};
+}
+template <int NQ, int S>
+__device__ __forceinline__ StageBuf<NQ> stage_fetch_pass(const char* __restrict__ base, const StageMap<NQ>& m) {
+  return stage_fetch_<NQ, S>(base, m, std::make_integer_sequence<int, Stage<NQ>::Q>{});
+}
+template <int NQ, int... K>
+__device__ __forceinline__ void stage_commit_(const StageBuf<NQ>& b, uint4* st, int L, std::integer_sequence<int, K...>) {
+  wave_lds_sync();  // every lane is done reading the previous pass's segment
+  ((st[StageMap<NQ>::lds_slot(K, L)] = b.v[K]), ...);
+  wave_lds_sync();
+}
+template <int NQ>
+__device__ __forceinline__ void stage_commit(const StageBuf<NQ>& b, uint4* st, int L) {
+  stage_commit_<NQ>(b, st, L, std::make_integer_sequence<int, Stage<NQ>::Q>{});
+}
+template <int NQ, int S, int... K>
+__device__ __forceinline__ void stage_pass_out_(char* __restrict__ base, const StageMap<NQ>& m, const uint4* st, int L,
+                                                std::integer_sequence<int, K...>) {
+  wave_lds_sync();
+  (stage_put<NQ, S, K>(base, m, st, L), ...);
+  wave_lds_sync();
+}
+template <int NQ, int S>
+__device__ __forceinline__ void stage_pass_out(char* __restrict__ base, const StageMap<NQ>& m, const uint4* st, int L) {
+  stage_pass_out_<NQ, S>(base, m, st, L, std::make_integer_sequence<int, Stage<NQ>::Q>{});
+}
+
+template <class T, class S> struct BRow;
 template <class T>
 __global__ __launch_bounds__(TBROW) void k_big_fix1_row(SrnnCfg c, SrnnArgs a) {
+  using R = BRow<T, StF32>;
+  __shared__ uint4 s_stg[(TBROW / 64) * R::G::WAVE_U4];
   const int64_t p = (int64_t)blockIdx.x * TBROW + threadIdx.x;
-  if (p >= a.n) return;
+  if (blockIdx.x * (int64_t)TBROW + (threadIdx.x & ~63) >= a.n) return;  // whole wave past n
   float* state = reinterpret_cast<float*>(a.temp);
   int8_t* flag = reinterpret_cast<int8_t*>(state + a.n * T::A);
   float w[T::P];
-  lrow_load<T>(a.W + p * T::PP, w);
+  R::load_staged(a.W, p < a.n ? (int32_t)p : -1, w, s_stg + (threadIdx.x >> 6) * R::G::WAVE_U4);
+  if (p >= a.n) return;
   bool stop = a.steps <= 0;
   if (!stop && a.early_exit) {
     bool fin = true;
@@ -1023,6 +1133,113 @@ struct BRow {
     if constexpr (S::ID == 0) reinterpret_cast<float*>(row)[k] = v;
     else reinterpret_cast<uint16_t*>(row)[k] = S::enc(v);
   }
+  // ---- staged (coalesced) row transfers: row idx of the table at base <-> w (see Stage)
+  static constexpr int NQ = RB / 16;
+  static_assert(RB % 16 == 0, "staged rows move 16-byte pieces");
+  using G = Stage<NQ>;
+  __device__ __forceinline__ static void dec_piece(int j, const uint4& u, float (&w)[T::P]) {
+    if constexpr (S::ID == 0) {
+      const uint32_t x[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        if (4 * j + e < T::P) w[4 * j + e] = __uint_as_float(x[e]);
+    } else {
+      const uint32_t x[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+      for (int e = 0; e < 8; ++e)
+        if (8 * j + e < T::P) w[8 * j + e] = S::dec((uint16_t)((x[e >> 1] >> (16 * (e & 1))) & 0xffffu));
+    }
+  }
+  __device__ __forceinline__ static uint4 enc_piece(int j, const float (&w)[T::P]) {
+    uint32_t x[4];
+    if constexpr (S::ID == 0) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) x[e] = (4 * j + e < T::P) ? __float_as_uint(w[4 * j + e]) : 0u;
+    } else {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const uint32_t lo = (8 * j + 2 * e < T::P) ? (uint32_t)S::enc(w[8 * j + 2 * e]) : 0u;
+        const uint32_t hi = (8 * j + 2 * e + 1 < T::P) ? (uint32_t)S::enc(w[8 * j + 2 * e + 1]) : 0u;
+        x[e] = lo | (hi << 16);
+      }
+    }
+    return make_uint4(x[0], x[1], x[2], x[3]);
+  }
+  template <int PS, int... Qi>
+  __device__ __forceinline__ static void dec_pass(const uint4* st, int L, float (&w)[T::P], std::integer_sequence<int, Qi...>) {
+    (dec_piece(G::Q * PS + Qi, st[L * G::PI + Qi], w), ...);
+  }
+  template <int PS>
+  __device__ __forceinline__ static void load_passes(const char* base, const StageMap<NQ>& m, const StageBuf<NQ>& cur,
+                                                     float (&w)[T::P], uint4* st, int L) {
+    if constexpr (PS < G::NPASS) {
+      if constexpr (PS + 1 < G::NPASS) {
+        const StageBuf<NQ> nxt = stage_fetch_pass<NQ, PS + 1>(base, m);  // in flight during this pass
+        stage_commit<NQ>(cur, st, L);
+        dec_pass<PS>(st, L, w, std::make_integer_sequence<int, G::len(PS)>{});
+        load_passes<PS + 1>(base, m, nxt, w, st, L);
+      } else {
+        stage_commit<NQ>(cur, st, L);
+        dec_pass<PS>(st, L, w, std::make_integer_sequence<int, G::len(PS)>{});
+      }
+    }
+  }
+  // sources of a staged store: a register row, or the chunk state of a chunk-constant row
+  struct RowSrc {
+    const float (&w)[T::P];
+    template <int J>
+    __device__ __forceinline__ uint4 piece() const { return enc_piece(J, w); }
+  };
+  struct StateSrc {
+    const float* s;  // T::A chunk values
+    template <int J>
+    __device__ __forceinline__ uint4 piece() const {
+      constexpr int j = J;
+      float v[T::P > 0 ? 8 : 1];
+      constexpr int E = S::ID == 0 ? 4 : 8;
+#pragma unroll
+      for (int e = 0; e < E; ++e) v[e] = (E * j + e < T::P) ? s[T::chunk_c(E * j + e)] : 0.f;
+      uint32_t x[4];
+      if constexpr (S::ID == 0) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) x[e] = __float_as_uint(v[e]);
+      } else {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) x[e] = (uint32_t)S::enc(v[2 * e]) | ((uint32_t)S::enc(v[2 * e + 1]) << 16);
+      }
+      return make_uint4(x[0], x[1], x[2], x[3]);
+    }
+  };
+  template <int PS, class Src, int... Qi>
+  __device__ __forceinline__ static void enc_pass(uint4* st, int L, const Src& src, std::integer_sequence<int, Qi...>) {
+    ((st[L * G::PI + Qi] = src.template piece<G::Q * PS + Qi>()), ...);
+  }
+  template <int PS, class Src>
+  __device__ __forceinline__ static void store_passes(char* base, const StageMap<NQ>& m, const Src& src, uint4* st, int L) {
+    if constexpr (PS < G::NPASS) {
+      enc_pass<PS>(st, L, src, std::make_integer_sequence<int, G::len(PS)>{});
+      stage_pass_out<NQ, PS>(base, m, st, L);
+      store_passes<PS + 1>(base, m, src, st, L);
+    }
+  }
+  // w <- row idx of the table (idx < 0: w unchanged); st: this wave's G::WAVE_U4 LDS area
+  __device__ __forceinline__ static void load_staged(const float* table, int32_t idx, float (&w)[T::P], uint4* st) {
+    const int L = threadIdx.x & 63;
+    const StageMap<NQ> m(idx, L);
+    const char* base = reinterpret_cast<const char*>(table);
+    load_passes<0>(base, m, stage_fetch_pass<NQ, 0>(base, m), w, st, L);
+  }
+  __device__ __forceinline__ static void store_staged(float* table, int32_t idx, const float (&w)[T::P], uint4* st) {
+    const int L = threadIdx.x & 63;
+    const StageMap<NQ> m(idx, L);
+    store_passes<0>(reinterpret_cast<char*>(table), m, RowSrc{w}, st, L);
+  }
+  // row idx <- expand(s) (chunk state, T::A values)
+  __device__ __forceinline__ static void store_state_staged(float* table, int32_t idx, const float* s, uint4* st) {
+    const int L = threadIdx.x & 63;
+    const StageMap<NQ> m(idx, L);
+    store_passes<0>(reinterpret_cast<char*>(table), m, StateSrc{s}, st, L);
+  }
 };
 
 // chunk ids of the shuffled output (4 bits per weight) in LDS, word w of lane L at
@@ -1166,17 +1383,22 @@ template <class T, class S, bool SHUF, int OP>
 __global__ __launch_bounds__(TBROW) void k_big_rows(SrnnCfg c, SrnnArgs a) {
   using R = BRow<T, S>;
   __shared__ uint32_t s_cw[SHUF ? ChunkPerm<T>::NW * TBROW : 1];
+  __shared__ uint4 s_stg[(TBROW / 64) * R::G::WAVE_U4];
+  uint4* st = s_stg + (threadIdx.x >> 6) * R::G::WAVE_U4;  // this wave's staging area
   const ChunkPerm<T> cp{s_cw + threadIdx.x};
   const int64_t p = (int64_t)blockIdx.x * TBROW + threadIdx.x;
+  const bool valid = p < a.n;
   const Rng rng{(uint32_t)a.seed, (uint32_t)(a.seed >> 32)};
   float w[T::P];
+  // rows move through the wave's LDS staging area (coalesced, see Stage): every lane takes
+  // part in the transfers, lanes past n with row index -1
   if constexpr (OP == OP_CLASSIFY) {
     __shared__ uint32_t s_cnt[6];
     if (threadIdx.x < 6) s_cnt[threadIdx.x] = 0;
     __syncthreads();
     int8_t k = -1;
-    if (p < a.n) {
-      R::load(R::at(a.W, p), w);
+    R::load_staged(a.W, valid ? (int32_t)p : -1, w, st);
+    if (valid) {
       if constexpr (SHUF) cp.draw(rng, a.uid ? (uint64_t)a.uid[p] : (uint64_t)(a.lo + p), a.ctr);
       k = bclassify<T, S, SHUF>(w, a.eps, (a.flags & 8) != 0, c.aggregator, cp);
       if (a.cls) a.cls[p] = k;
@@ -1188,7 +1410,7 @@ __global__ __launch_bounds__(TBROW) void k_big_rows(SrnnCfg c, SrnnArgs a) {
         if ((threadIdx.x & 63) == 0 && m) atomicAdd(&s_cnt[q], (uint32_t)__popcll(m));
       }
       if (a.flags & 64) {
-        const unsigned long long m = __ballot(p < a.n && a.respawn[p] != 0);
+        const unsigned long long m = __ballot(valid && a.respawn[p] != 0);
         if ((threadIdx.x & 63) == 0 && m) atomicAdd(&s_cnt[5], (uint32_t)__popcll(m));
       }
       __syncthreads();
@@ -1201,33 +1423,57 @@ __global__ __launch_bounds__(TBROW) void k_big_rows(SrnnCfg c, SrnnArgs a) {
     }
     return;
   }
-  if (p >= a.n) return;
+  if (blockIdx.x * (int64_t)TBROW + (threadIdx.x & ~63) >= a.n) return;  // whole wave past n
   if constexpr (OP == OP_APPLY) {
-    const int64_t fi = a.idx_f ? a.idx_f[p] : p, ti = a.idx_t ? a.idx_t[p] : p, oi = a.idx_o ? a.idx_o[p] : p;
+    int32_t fi = -1, ti = -1, oi = -1;
+    if (valid) {
+      fi = (int32_t)(a.idx_f ? a.idx_f[p] : p);
+      ti = (int32_t)(a.idx_t ? a.idx_t[p] : p);
+      oi = (int32_t)(a.idx_o ? a.idx_o[p] : p);
+    }
     float g[T::A], h[T::A];
-    // target row into the registers (all its loads in flight at once), aggregated, then
-    // overwritten by the attacker's row: streaming the target one load at a time halved
-    // the attack rate (1.72 vs 0.82 ms at 1M particles)
-    R::load(R::at(a.W, ti), w);
+    // target row (aggregated), then the attacker's row into the same registers
+    R::load_staged(a.W, ti, w, st);
     lrow_aggregate<T>(w, g, c.aggregator);
-    R::load(R::at(a.W, fi), w);
+    R::load_staged(a.W, fi, w, st);
     lmlp<T>(w, g, h);
     R::quant_a(h);
-    if constexpr (SHUF) cp.draw(rng, a.uid ? (uint64_t)a.uid[ti] : (uint64_t)ti, a.ctr);
+    if constexpr (SHUF) cp.draw(rng, a.uid ? (uint64_t)a.uid[ti < 0 ? 0 : ti] : (uint64_t)ti, a.ctr);
     expand_out<T, SHUF>(w, h, cp);
-    R::store(R::at(a.W2, oi), w);
+    R::store_staged(a.W2, oi, w, st);
   } else {  // OP_TRAIN / OP_LEARN (no randomness in an aggregating net's SGD step)
     float g[T::A];
-    if constexpr (OP == OP_LEARN) R::stream_aggregate(R::at(a.W2, a.idx_t ? a.idx_t[p] : p), g, c.aggregator);
-    R::load(R::at(a.W, p), w);
+    if constexpr (OP == OP_LEARN) {  // teacher row first, aggregated (same sums as stream_aggregate)
+      R::load_staged(a.W2, valid ? (int32_t)(a.idx_t ? a.idx_t[p] : p) : -1, w, st);
+      lrow_aggregate<T>(w, g, c.aggregator);
+    }
+    R::load_staged(a.W, valid ? (int32_t)p : -1, w, st);
     float loss = 0.f;
     for (int e = 0; e < a.epochs; ++e) {
       if constexpr (OP == OP_TRAIN) lrow_aggregate<T>(w, g, c.aggregator);
       loss = ltrain_step<T>(w, g, a.lr);
     }
-    R::store(R::at(a.W, p), w);
-    if (a.loss) a.loss[p] = loss;
+    R::store_staged(a.W, valid ? (int32_t)p : -1, w, st);
+    if (valid && a.loss) a.loss[p] = loss;
   }
+}
+
+// run_fixpoint phase 3, lane per row: rows that took steps <- expand(chunk state), written
+// through the staging area (the wave-per-row k_big_fix3 issued one 1.1 KB row per wave:
+// launch-bound, 3.6 TB/s)
+template <class T>
+__global__ __launch_bounds__(TBROW) void k_big_fix3_row(SrnnCfg c, SrnnArgs a) {
+  using R = BRow<T, StF32>;
+  __shared__ uint4 s_stg[(TBROW / 64) * R::G::WAVE_U4];
+  const int64_t p = (int64_t)blockIdx.x * TBROW + threadIdx.x;
+  if (blockIdx.x * (int64_t)TBROW + (threadIdx.x & ~63) >= a.n) return;  // whole wave past n
+  const float* state = reinterpret_cast<const float*>(a.temp);
+  const int8_t* flag = reinterpret_cast<const int8_t*>(state + a.n * T::A);
+  const bool on = p < a.n && flag[p] != 0;
+  float st[T::A];
+#pragma unroll
+  for (int i = 0; i < T::A; ++i) st[i] = on ? state[p * T::A + i] : 0.f;
+  R::store_state_staged(a.W, on ? (int32_t)p : -1, st, s_stg + (threadIdx.x >> 6) * R::G::WAVE_U4);
 }
 
 // init / perturb / respawn of big rows in any storage format (lane per particle)
@@ -1269,6 +1515,8 @@ __global__ __launch_bounds__(TBROW) void k_big_soup_evolve(SrnnCfg c, SrnnArgs a
   const int64_t j = (int64_t)blockIdx.x * TBROW + threadIdx.x;
   const Rng rng{(uint32_t)a.seed, (uint32_t)(a.seed >> 32)};
   bool rs_any = false;
+  // the own row stays a per-lane load (the generation is SGD-bound: staging it through LDS
+  // measured slower, profiles/r2j_staged_rows_finish_par.md)
   if (j < a.n) {
     const int64_t g = a.lo + j;
     const int32_t gen = a.gen_ptr ? a.gen_ptr[0] : a.gen;
@@ -1475,7 +1723,8 @@ int big_run(int op, const SrnnCfg& c, const SrnnArgs& a) {
       if (row_kernels) hipLaunchKernelGGL((k_big_fix1_row<T>), dim3(g64), dim3(TBROW), 0, st, c, a);
       else hipLaunchKernelGGL((k_big_fix1<T>), dim3(gw), dim3(TBB), 0, st, c, a);
       hipLaunchKernelGGL((k_big_fix2<T>), dim3(gl), dim3(256), 0, st, c, a);
-      hipLaunchKernelGGL((k_big_fix3<T>), dim3(gw), dim3(TBB), 0, st, c, a);
+      if (row_kernels) hipLaunchKernelGGL((k_big_fix3_row<T>), dim3(g64), dim3(TBROW), 0, st, c, a);
+      else hipLaunchKernelGGL((k_big_fix3<T>), dim3(gw), dim3(TBB), 0, st, c, a);
       break;
     case OP_CLASSIFY:
       if (row_kernels) hipLaunchKernelGGL((k_big_row<T, OP_CLASSIFY>), dim3(g64), dim3(TBROW), 0, st, c, a);

@@ -591,6 +591,8 @@ class SoupEngine:
         a.flags = (self._fin_flags & _lib.FLAG_FUSED_CENSUS) | _lib.FLAG_FINISH_BATCH
         a.temp, a.temp_bytes = _p(self._bs_ring), self._bs_ring.stride(0) * 4
         a.uid_out, a.uid_base, a.counts = _p(self.uid), _p(self.next_uid), _p(self.counts)
+        if os.environ.get("SRNN_FINISH_PAR", "1") == "1":
+            a.i32d = _p(self._done)  # done counter: one finish workgroup per generation
         _lib.run(_lib.OP_GEN_FINISH, self.spec, a, self.cfg)
         self._pending_fin = 0
 

@@ -56,8 +56,14 @@ def test_big_ops_equal_generic(cuda, dtype, shuffler):
         K.learn_from(spec, L, W, idx_t=idx, epochs=2, uid=uid, seed=5, ctr=4)
         c1, n1 = K.classify(spec, W, 1e-4, uid=uid, seed=5)
         c2, n2 = K.classify(spec, A, 1e-2, uid=uid, seed=5)  # chunk-constant rows: fixpoint candidates
+        out = dict(init=W, apply=A, train=T, loss=tl, learn=L, cls1=c1, cnt1=n1, cls2=c2, cnt2=n2)
+        if dtype == torch.float32 and shuffler == "none":
+            # run_fixpoint: row phase (staged loads), chunk-state steps, staged write-back
+            F = W.clone()
+            fc, fs, _ = K.run_fixpoint(spec, F, 6, 1e-4, early_exit=True)
+            out.update(fix=F, fix_cls=fc, fix_steps=fs)
         torch.cuda.synchronize()
-        return dict(init=W, apply=A, train=T, loss=tl, learn=L, cls1=c1, cnt1=n1, cls2=c2, cnt2=n2)
+        return out
 
     a, b = _both(ops)
     bad = [k for k in a if not torch.equal(_bits(a[k]) if a[k].is_floating_point() else a[k],
