@@ -706,6 +706,70 @@ __device__ __forceinline__ bool lrow_close_state(const float (&w)[T::P], const f
   for (int k = 0; k < T::P; ++k) ok &= !(fabsf(h[T::chunk_c(k)] - w[k]) >= eps);
   return ok;
 }
+// One pass over a register row for the census: chunk sums (double, index order = the mean
+// aggregator's sums), per-chunk min / max.  Every census predicate is a function of these:
+//   all weights finite   <=> every chunk sum finite (a NaN or an infinity in a chunk makes its
+//                            double sum non-finite; finite floats cannot overflow a double sum)
+//   all |w| <= eps       <=> min >= -eps and max <= eps
+//   all |h[c(k)] - w[k]| < eps  <=>  h[c] - min_c < eps and max_c - h[c] < eps for every chunk:
+//     fl(h - w) is monotone in w and fl(w - h) = -fl(h - w), so the largest rounded distance of
+//     a chunk is attained at its min or max -- the same decisions as the per-weight test with
+//     ~16 instead of ~1100 instructions (the per-weight compares made the census issue-bound)
+template <class T>
+struct RowSummary {
+  double sum[T::A];
+  float mn[T::A], mx[T::A];
+  __device__ __forceinline__ explicit RowSummary(const float (&w)[T::P]) {
+#pragma unroll
+    for (int c = 0; c < T::A; ++c) {
+      const int b = c * T::CS, e = (c == T::A - 1) ? T::P : b + T::CS;
+      double acc = 0.0;  // index order (the reference's sums)
+      float lo[4] = {w[b], w[b], w[b], w[b]}, hi[4] = {w[b], w[b], w[b], w[b]};  // order-free: 4 chains
+#pragma unroll
+      for (int k = 0; k < T::P; ++k)
+        if (k >= b && k < e) {
+          acc += (double)w[k];
+          lo[k & 3] = fminf(lo[k & 3], w[k]);
+          hi[k & 3] = fmaxf(hi[k & 3], w[k]);
+        }
+      sum[c] = acc;
+      mn[c] = fminf(fminf(lo[0], lo[1]), fminf(lo[2], lo[3]));
+      mx[c] = fmaxf(fmaxf(hi[0], hi[1]), fmaxf(hi[2], hi[3]));
+    }
+  }
+  __device__ __forceinline__ bool finite() const {
+    bool ok = true;
+#pragma unroll
+    for (int c = 0; c < T::A; ++c) ok &= __builtin_isfinite(sum[c]) != 0;
+    return ok;
+  }
+  __device__ __forceinline__ bool zero(float eps) const {
+    bool ok = true;
+#pragma unroll
+    for (int c = 0; c < T::A; ++c) ok &= (-eps <= mn[c]) && (mx[c] <= eps);
+    return ok;
+  }
+  // every |expand(h)[k] - w[k]| < eps (h finite, w finite)
+  __device__ __forceinline__ bool close(const float* h, float eps) const {
+    bool ok = true;
+#pragma unroll
+    for (int c = 0; c < T::A; ++c) ok &= !(h[c] - mn[c] >= eps) && !(mx[c] - h[c] >= eps);
+    return ok;
+  }
+  // chunk means (aggregator 0) exactly as lrow_aggregate; the max aggregators walk the row
+  __device__ __forceinline__ void aggregate(const float (&w)[T::P], float* g, int aggregator) const {
+    if (aggregator == 0) {
+#pragma unroll
+      for (int c = 0; c < T::A; ++c) {
+        const int b = c * T::CS, e = (c == T::A - 1) ? T::P : b + T::CS;
+        g[c] = (float)(sum[c] / (double)(e - b));
+      }
+    } else {
+      lrow_aggregate<T>(w, g, aggregator);
+    }
+  }
+};
+
 template <class T>
 __device__ __forceinline__ int8_t lclassify(const float (&w)[T::P], float eps, bool with_sec, int aggregator) {
   bool fin = true;
@@ -901,6 +965,24 @@ __device__ __forceinline__ void stage_pass_out(char* __restrict__ base, const St
 }
 
 template <class T, class S> struct BRow;
+// census class of a register row from its summary (no shuffler): f1 = apply(w, w), f2 =
+// apply(w, f1) with aggregate(expand(f1)) == f1, both rounded to the storage format
+template <class T, class S>
+__device__ __forceinline__ int8_t sclassify(const float (&w)[T::P], const RowSummary<T>& sm, float eps, bool with_sec,
+                                            int aggregator) {
+  if (!sm.finite()) return C_DIVERGENT;
+  float g[T::A], h1[T::A], h2[T::A];
+  sm.aggregate(w, g, aggregator);
+  lmlp<T>(w, g, h1);
+  BRow<T, S>::quant_a(h1);
+  if (finite_all<T>(h1) && sm.close(h1, eps)) return sm.zero(eps) ? C_FIX_ZERO : C_FIX_OTHER;
+  if (with_sec) {
+    lmlp<T>(w, h1, h2);
+    BRow<T, S>::quant_a(h2);
+    if (finite_all<T>(h2) && sm.close(h2, eps)) return C_FIX_SEC;
+  }
+  return C_OTHER;
+}
 template <class T>
 __global__ __launch_bounds__(TBROW) void k_big_fix1_row(SrnnCfg c, SrnnArgs a) {
   using R = BRow<T, StF32>;
@@ -912,23 +994,20 @@ __global__ __launch_bounds__(TBROW) void k_big_fix1_row(SrnnCfg c, SrnnArgs a) {
   float w[T::P];
   R::load_staged(a.W, p < a.n ? (int32_t)p : -1, w, s_stg + (threadIdx.x >> 6) * R::G::WAVE_U4);
   if (p >= a.n) return;
+  const RowSummary<T> sm(w);
   bool stop = a.steps <= 0;
-  if (!stop && a.early_exit) {
-    bool fin = true;
-#pragma unroll
-    for (int k = 0; k < T::P; ++k) fin &= finitef(w[k]);
-    stop = !fin;
-  }
+  if (!stop && a.early_exit) stop = !sm.finite();
   float g[T::A], h[T::A];
   if (!stop) {
-    lrow_aggregate<T>(w, g, c.aggregator);
+    sm.aggregate(w, g, c.aggregator);
     lmlp<T>(w, g, h);
-    if (a.early_exit && finite_all<T>(h) && lrow_close_state<T>(w, h, a.eps)) stop = true;
+    // (a non-finite row never gets here with early_exit; without it the close test is off)
+    if (a.early_exit && finite_all<T>(h) && sm.close(h, a.eps)) stop = true;
   }
   if (stop) {  // no step taken: the row is unchanged, classify the general weights
     flag[p] = 0;
     if (a.nsteps) a.nsteps[p] = 0;
-    if (a.cls) a.cls[p] = lclassify<T>(w, a.eps, (a.flags & 8) != 0, c.aggregator);
+    if (a.cls) a.cls[p] = sclassify<T, StF32>(w, sm, a.eps, (a.flags & 8) != 0, c.aggregator);
   } else {
 #pragma unroll
     for (int i = 0; i < T::A; ++i) state[p * T::A + i] = h[i];
@@ -1400,7 +1479,8 @@ __global__ __launch_bounds__(TBROW) void k_big_rows(SrnnCfg c, SrnnArgs a) {
     R::load_staged(a.W, valid ? (int32_t)p : -1, w, st);
     if (valid) {
       if constexpr (SHUF) cp.draw(rng, a.uid ? (uint64_t)a.uid[p] : (uint64_t)(a.lo + p), a.ctr);
-      k = bclassify<T, S, SHUF>(w, a.eps, (a.flags & 8) != 0, c.aggregator, cp);
+      if constexpr (SHUF) k = bclassify<T, S, SHUF>(w, a.eps, (a.flags & 8) != 0, c.aggregator, cp);
+      else k = sclassify<T, S>(w, RowSummary<T>(w), a.eps, (a.flags & 8) != 0, c.aggregator);
       if (a.cls) a.cls[p] = k;
     }
     if (a.counts) {  // wave ballots -> LDS -> one atomic per (block, class)
@@ -1570,12 +1650,22 @@ __global__ __launch_bounds__(TBROW) void k_big_soup_evolve(SrnnCfg c, SrnnArgs a
       loss = ltrain_step<T>(w, gs, a.lr);
     }
     R::quant(w);  // the stored state decides respawn
-    bool bad = false, zero = true;
+    // any non-finite weight <=> NaN in sum(w * 0); all |w| <= eps <=> min / max within
+    // (fminf / fmaxf skip NaNs: a NaN row is never a zero row, as in the per-weight test)
+    // (8 independent partial chains: min / max / NaN propagation are order-free)
+    float nz[8], lo[8], hi[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) nz[q] = 0.f, lo[q] = w[0], hi[q] = w[0];
 #pragma unroll
     for (int k = 0; k < T::P; ++k) {
-      bad |= !finitef(w[k]);
-      zero &= (-a.eps <= w[k]) && (w[k] <= a.eps);
+      nz[k & 7] = fmaf(w[k], 0.f, nz[k & 7]);
+      lo[k & 7] = fminf(lo[k & 7], w[k]);
+      hi[k & 7] = fmaxf(hi[k & 7], w[k]);
     }
+#pragma unroll
+    for (int q = 1; q < 8; ++q) nz[0] += nz[q], lo[0] = fminf(lo[0], lo[q]), hi[0] = fmaxf(hi[0], hi[q]);
+    const bool bad = !finitef(nz[0]);
+    const bool zero = !bad && (-a.eps <= lo[0]) && (hi[0] <= a.eps);
     int8_t rsp = 0;
     if ((a.flags & 2) && bad) rsp = 1;
     else if ((a.flags & 4) && zero) rsp = 2;

@@ -897,6 +897,8 @@ __global__ __launch_bounds__(TB) void k_soup_gen(SrnnCfg c, SrnnArgs a) {
       mine[1] = (unsigned long long)cnt[0] | ((unsigned long long)cnt[1] << 32);
       mine[2] = (unsigned long long)cnt[2] | ((unsigned long long)cnt[3] << 32);
       mine[3] = (unsigned long long)cnt[4];
+      // flag 1048576: the generation's newborn count after the block stats (batched finish)
+      if ((a.flags & 1048576) && m) atomicAdd(bs + ((a.n + TB - 1) / TB) * 4, (unsigned long long)__popcll(m));
     }
     if (pre) perm_drain<Net, S>(a, gen + 1);  // whatever the helpers left
     return;
@@ -1161,14 +1163,25 @@ __global__ __launch_bounds__(NT) void k_gen_finish_par(SrnnArgs a, int32_t nb, i
   auto ring = [&](int32_t k) {
     return reinterpret_cast<const unsigned long long*>(reinterpret_cast<const char*>(a.temp) + (int64_t)k * a.temp_bytes);
   };
+  const bool totals = (a.flags & 1048576) != 0 && m <= NT;  // newborn count of generation k at ring(k)[4 nb]
   int32_t before = 0, all = 0;
+  if (totals) {
+    // thread k < m loads generation k's count: m loads in flight at once (a loop over k in
+    // one thread paid one memory latency per generation, ~0.9 us each)
+    if (t < m) {
+      const int32_t c = (int32_t)ring(t)[(int64_t)nb * 4];
+      all = c;
+      before = t < g ? c : 0;
+    }
+  } else {
 #pragma unroll 8  // independent loads in flight (the walk over generations is latency bound)
-  for (int32_t k = 0; k < m; ++k) {
-    const unsigned long long* bk = ring(k);
-    int32_t c = 0;
-    for (int32_t b = b0; b < b1; ++b) c += __popcll(bk[(int64_t)b * 4]);
-    all += c;
-    before += k < g ? c : 0;
+    for (int32_t k = 0; k < m; ++k) {
+      const unsigned long long* bk = ring(k);
+      int32_t c = 0;
+      for (int32_t b = b0; b < b1; ++b) c += __popcll(bk[(int64_t)b * 4]);
+      all += c;
+      before += k < g ? c : 0;
+    }
   }
   const unsigned long long* bs = ring(g);
   int32_t born = 0;
@@ -1221,6 +1234,8 @@ __global__ __launch_bounds__(NT) void k_gen_finish_par(SrnnArgs a, int32_t nb, i
     const int32_t prev = atomicAdd(a.i32d, 1);
     if (prev == m - 1) {
       ((int64_t*)a.uid_base)[0] = base + total_all;
+      if (totals)  // every workgroup has read the counts: re-armed for the next batch
+        for (int32_t k = 0; k < m; ++k) const_cast<unsigned long long*>(ring(k))[(int64_t)nb * 4] = 0ull;
       __hip_atomic_store(a.i32d, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }

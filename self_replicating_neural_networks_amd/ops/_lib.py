@@ -62,6 +62,7 @@ FLAG_ASYNC_FINISH = 65536
 FLAG_PRE_PERMS = 131072
 FLAG_FINISH_BATCH = 262144
 FLAG_GEN_POST = 524288   # sharded: uids + received-row index folded into the generation launch
+FLAG_BORN_TOTAL = 1048576  # batched finish: each generation keeps its newborn count after its block stats
 HELPER_CTL = 1 + 8192  # helper work-queue head + per-SIMD generation-wave counts (csrc/srnn_kernels.h)
 
 

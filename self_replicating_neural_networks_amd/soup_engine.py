@@ -194,7 +194,8 @@ class SoupEngine:
         # the ring holds 32 B per 64-row block per pending generation: at HBM-filling sizes
         # (2e9 rows = 1 GB per generation) fewer generations share one finish launch
         self._batch = max(1, min(max(self._chunk_sizes() or [1]), (512 << 20) // (max(nb, 1) * 32)))
-        self._bs_ring = torch.zeros((self._batch, max(nb, 1) * 8), **i32) if fm == "batch" else None
+        # (+ 8 bytes per generation: its newborn count, accumulated by the generation waves)
+        self._bs_ring = torch.zeros((self._batch, max(nb, 1) * 8 + 2), **i32) if fm == "batch" else None
         self._pending_fin = 0  # batch mode: generations whose finish is still due
         self._blockstats = [self._blockstat, torch.zeros_like(self._blockstat)] if self.async_finish else None
         # sharded fused generations fold the post-exchange launch (previous generation's
@@ -391,7 +392,7 @@ class SoupEngine:
             if self.finish_mode == "batch":
                 bs = self._bs_ring[self._pending_fin]
                 fa.temp, fa.temp_bytes = _p(bs), bs.numel() * 4
-                fa.flags |= _lib.FLAG_TWO_PHASE | _lib.FLAG_ASYNC_FINISH
+                fa.flags |= _lib.FLAG_TWO_PHASE | _lib.FLAG_ASYNC_FINISH | _lib.FLAG_BORN_TOTAL
             if self.async_finish:
                 bs = self._blockstats[self._p]
                 fa.temp, fa.temp_bytes = _p(bs), bs.numel() * 4
@@ -588,7 +589,7 @@ class SoupEngine:
         a = self._args()
         a.n = self.n
         a.steps = m
-        a.flags = (self._fin_flags & _lib.FLAG_FUSED_CENSUS) | _lib.FLAG_FINISH_BATCH
+        a.flags = (self._fin_flags & (_lib.FLAG_FUSED_CENSUS | _lib.FLAG_BORN_TOTAL)) | _lib.FLAG_FINISH_BATCH
         a.temp, a.temp_bytes = _p(self._bs_ring), self._bs_ring.stride(0) * 4
         a.uid_out, a.uid_base, a.counts = _p(self.uid), _p(self.next_uid), _p(self.counts)
         if os.environ.get("SRNN_FINISH_PAR", "1") == "1":
