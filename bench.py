@@ -92,7 +92,8 @@ def main():
     dt = float(t.item())
     if eng.exchange_overflowed():
         # rows that did not fit the all-to-all capacity were dropped: the generation is invalid
-        raise SystemExit("soup row exchange overflowed its capacity: the measured generations are invalid")
+        raise SystemExit(f"soup row exchange overflowed its capacity (ovf flags {int(eng.ovf.item())}: 1 rows dropped, "
+                         "2 a wait timed out): the measured generations are invalid")
     census = eng.count()
     value = n_total * args.steps / dt
     if d.rank == 0:
