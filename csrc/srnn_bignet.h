@@ -1274,7 +1274,7 @@ struct BRow {
     template <int J>
     __device__ __forceinline__ uint4 piece() const {
       constexpr int j = J;
-      float v[T::P > 0 ? 8 : 1];
+      float v[8];
       constexpr int E = S::ID == 0 ? 4 : 8;
 #pragma unroll
       for (int e = 0; e < E; ++e) v[e] = (E * j + e < T::P) ? s[T::chunk_c(E * j + e)] : 0.f;
