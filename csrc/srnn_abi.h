@@ -120,6 +120,7 @@ enum SrnnOp {
   OP_SOUP_GEN = 16,     // fused generation: evolve + next decisions + census (+ finish; flag 32768: the
                         // finish launch also packs the next all-to-all = OP_SOUP_PACK)
   OP_SOUP_PERMS = 18,   // fill perm_next with the SGD permutations of generation *gen_ptr (first generation)
+  OP_SOUP_SEQ = 19,     // host: `steps` sequential (Gauss-Seidel, in-place, index-order) soup generations
   OP_GEN_FINISH = 17,   // single rank, flag 65536: census + newborn uids of the generation whose block
                         // stats are in temp (the finish half of OP_SOUP_GEN, on a side stream)
   OP_UID_ASSIGN = 15,   // sharded soup: uids of the previous generation's newborns from the per-rank stats

@@ -583,6 +583,76 @@ struct Item {
     }
   }
 
+  // Sequential (Gauss-Seidel) generation step of particle j (reference Soup.evolve,
+  // code/soup.py:51-87, semantics S11): the table W is updated IN PLACE in index order, so
+  // particle j sees every earlier particle's changes of this generation.  Decisions as the
+  // synchronous engine's (slot, generation) Philox stream; j attacks `at` (W[at] <- f_j(W[at]),
+  // shuffle_random keyed by the attacker), learns from `te`'s CURRENT weights (severity
+  // epochs), self-trains `epochs` epochs (SGD shuffles keyed by (slot, generation)), and is
+  // re-initialised when divergent / zero (init key respawn_key(gen, j); the caller numbers
+  // the newborns in index order).
+  SRNN_HD static void soup_seq_one(const SrnnCfg& c, const SrnnArgs& a, int64_t j, int32_t gen, float4* samp,
+                                   uint8_t* perm) {
+    float w[P], f[P], o[P];
+    int32_t at, te;
+    decision(a, j, gen, at, te);
+    int8_t act = A_NONE;
+    int64_t cp = -1;
+    if (at >= 0) {  // 1. attack: the victim's weights become f_j(victim)
+      load(rowp(a.W, j), w);
+      load(rowp(a.W, at), f);
+      Net::apply(w, f, o, actx(a, c, (uint64_t)j, (uint32_t)gen * 1024u + 1u, perm));
+      q(o);
+      store(rowp(a.W, at), o);
+      act = A_ATTACKING;
+      cp = at;
+    }
+    load(rowp(a.W, j), w);  // (j may have attacked itself)
+    TrainCtx tc;
+    tc.lr = a.lr;
+    tc.rng = rng(a);
+    tc.uid = (uint64_t)j;
+    tc.ctr = (uint32_t)gen * 1024u + 512u;
+    tc.samp = samp;
+    tc.perm = perm;
+    tc.shuffle = (a.flags & 1) != 0;
+    tc.stride = SAMP_STRIDE;
+    tc.aggregator = c.aggregator;
+    float loss = 0.f;
+    if (te >= 0) {  // 2. learn_from the teacher's current weights
+      load(rowp(a.W, te), f);
+      if constexpr (Net::KIND == 0) {
+        if (a.severity > 0) loss = Net::template train_epochs<false>(w, f, a.severity, tc);
+      } else {
+        for (int e = 0; e < a.severity; ++e) loss = Net::train_epoch(w, f, tc);
+      }
+      act = A_LEARN_FROM;
+      cp = te;
+    }
+    if (a.epochs > 0) {  // 3. self-train
+      if constexpr (Net::KIND == 0) {
+        loss = Net::template train_epochs<true>(w, f, a.epochs, tc);
+      } else {
+        for (int e = 0; e < a.epochs; ++e) {
+          copy(f, w);
+          loss = Net::train_epoch(w, f, tc);
+        }
+      }
+      act = A_TRAIN_SELF;
+      cp = -1;
+    }
+    q(w);  // 4. respawn (the zero test on the old particle: at most one of the two)
+    int8_t rs = 0;
+    if ((a.flags & 2) && is_diverged<P>(w)) rs = 1;
+    else if ((a.flags & 4) && is_zero<P>(w, a.eps)) rs = 2;
+    if (rs) Net::init(w, rng(a), respawn_key(gen, j));
+    store(rowp(a.W, j), w);
+    if (a.action) a.action[j] = act;
+    if (a.counterpart) a.counterpart[j] = cp;
+    if (a.loss) a.loss[j] = loss;
+    if (a.respawn) a.respawn[j] = rs;
+  }
+
   SRNN_HD static void respawn(const SrnnArgs& a, int64_t j) {
     if (a.respawn[j] == 0) return;
     float w[P];
@@ -1305,6 +1375,37 @@ int gen_finish(const SrnnCfg&, const SrnnArgs& a) {
 template <class Net, class S>
 int uid_assign(const SrnnCfg& c, const SrnnArgs& a);
 
+// OP_SOUP_SEQ: `steps` sequential soup generations starting at generation *gen_ptr (or
+// a.gen) on a host table, one particle after another (the reference order is serial by
+// definition: a single CPU core runs it ~100x faster than per-particle device launches and
+// faster than one GPU lane).  Newborns get uids from *uid_base in index order; uid_out
+// receives them; the generation counter advances by `steps`.
+template <class Net, class S>
+int soup_seq(const SrnnCfg& c, const SrnnArgs& a) {
+  using I = Item<Net, S>;
+  if (a.dev) {
+    set_error("sequential soups run on the host (their update order is serial)");
+    return -5;
+  }
+  if (a.world > 1 || a.lo != 0 || (a.n_total && a.n_total != a.n) || !a.uid_base || !a.uid_out) {
+    set_error("sequential soup: one unsharded table, uid_base and uid_out needed");
+    return -5;
+  }
+  float4 samp[Net::P + 1];
+  uint8_t perm[Net::P + 4];
+  const int32_t gen0 = I::gen_of(a);
+  int64_t next = a.uid_base[0];
+  for (int32_t s = 0; s < a.steps; ++s) {
+    for (int64_t j = 0; j < a.n; ++j) {
+      I::soup_seq_one(c, a, j, gen0 + s, samp, perm);
+      if (a.respawn && a.respawn[j]) a.uid_out[j] = next++;
+    }
+  }
+  ((int64_t*)a.uid_base)[0] = next;
+  I::set_gen(a, gen0 + a.steps);
+  return 0;
+}
+
 template <class Net, class S>
 int soup_gen(const SrnnCfg& c, const SrnnArgs& a) {
   using I = Item<Net, S>;
@@ -1849,6 +1950,7 @@ int run_net_op(int op, const SrnnCfg& c, const SrnnArgs& a) {
     case OP_SOUP_GEN: return soup_gen<Net, S>(c, a);
     case OP_GEN_FINISH: return gen_finish<Net, S>(c, a);
     case OP_SOUP_PERMS: return soup_perms<Net, S>(c, a);
+    case OP_SOUP_SEQ: return soup_seq<Net, S>(c, a);
     default: set_error("unknown op"); return -1;
   }
 }

@@ -41,6 +41,7 @@ OP_UID_ASSIGN = 15
 OP_SOUP_GEN = 16
 OP_GEN_FINISH = 17
 OP_SOUP_PERMS = 18
+OP_SOUP_SEQ = 19  # host: sequential (Gauss-Seidel) soup generations
 
 FLAG_SHUFFLE = 1
 FLAG_REMOVE_DIVERGENT = 2

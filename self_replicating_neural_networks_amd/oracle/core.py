@@ -494,3 +494,57 @@ def soup_generation_sync(spec, W0, uids, gen, seed, params, lr=0.01, shuffle=Tru
         if params.get("remove_zero"):
             respawn[(respawn == 0) & is_zero(W, eps)] = 2
     return W, action, cp, loss, respawn
+
+
+def respawn_key(gen, slot):
+    """csrc respawn_key: init key of the particle born in `slot` at generation `gen`."""
+    return (1 << 62) | ((int(gen) & M32) << 32) | int(slot)
+
+
+def soup_generation_seq(spec, W0, gen, seed, params, lr=0.01, shuffle=True):
+    """Sequential (Gauss-Seidel) soup generation -- the reference order (code/soup.py:51-87,
+    S11) with the native engine's keys (csrc Item::soup_seq_one): particles in index order,
+    the table updated in place; j attacks att[j] (shuffle_random keyed by the attacker),
+    learns from te[j]'s current weights, self-trains, and is re-initialised with
+    respawn_key(gen, j) when divergent / zero.  Returns (W1, action, counterpart, loss,
+    respawn)."""
+    n = W0.shape[0]
+    att, te = soup_decisions(seed, gen, n, params["attacking_rate"], params["learn_from_rate"],
+                             int(params.get("segment", 0)))
+    W = np.array(W0, dtype=np.float32, copy=True)
+    keys = np.arange(n, dtype=np.uint64)
+    action = np.zeros(n, dtype=np.int8)
+    cp = np.full(n, -1, dtype=np.int64)
+    loss = np.zeros(n, dtype=np.float32)
+    respawn = np.zeros(n, dtype=np.int8)
+    eps = params.get("epsilon", 1e-14)
+    sev = int(params.get("learn_from_severity", 1))
+    with np.errstate(over="ignore", invalid="ignore"):
+        for j in range(n):
+            v = att[j]
+            if v >= 0:
+                W[v:v + 1] = apply(spec, W[j:j + 1].copy(), W[v:v + 1].copy(), seed=seed, uids=keys[j:j + 1],
+                                   ctr=(gen * 1024 + 1) & M32)
+                action[j], cp[j] = 1, v
+            c = (gen * 1024 + 512) & M32
+            if te[j] >= 0:
+                for _ in range(sev):
+                    W[j:j + 1], l = train_epoch(spec, W[j:j + 1], W[te[j]:te[j] + 1].copy(), lr, shuffle, seed,
+                                                keys[j:j + 1], c)
+                    loss[j] = l[0]
+                    c += 1
+                action[j], cp[j] = 2, te[j]
+            for _ in range(int(params.get("train", 0))):
+                W[j:j + 1], l = train_epoch(spec, W[j:j + 1], W[j:j + 1].copy(), lr, shuffle, seed, keys[j:j + 1], c)
+                loss[j] = l[0]
+                c += 1
+                action[j], cp[j] = 3, -1
+            rs = 0
+            if params.get("remove_divergent") and is_diverged(W[j:j + 1])[0]:
+                rs = 1
+            elif params.get("remove_zero") and is_zero(W[j:j + 1], eps)[0]:
+                rs = 2
+            if rs:
+                W[j] = init(spec, np.array([respawn_key(gen, j)], dtype=np.uint64), seed)[0]
+            respawn[j] = rs
+    return W, action, cp, loss, respawn

@@ -5,6 +5,9 @@
   index order and in place within a generation, each particle a network
   facade on the host; decisions from a seeded ``random.Random`` stream (``prng``).
   Meant for the reference's small soups (10-100 particles).
+* ``mode="native"`` — the sequential algorithm on a weight table in one native call per
+  ``evolve`` (``seq_soup.SequentialSoupEngine``, any size; slot-keyed Philox streams instead
+  of the process-wide ``prng``; no per-step state recording).
 * ``mode="device"`` — the population lives in a device weight table and every
   generation is one fused kernel pipeline (``SoupEngine``), optionally sharded over the
   ranks of a process group.  Within a generation all reads come from the
@@ -47,8 +50,10 @@ class Soup(object):
         self.time = 0
         if mode == "auto":
             mode = "sequential" if size <= 100 and dist is None else "device"
-        if mode not in ("sequential", "device"):
-            raise ValueError("mode must be 'sequential', 'device' or 'auto'")
+        if mode not in ("sequential", "native", "device"):
+            raise ValueError("mode must be 'sequential', 'native', 'device' or 'auto'")
+        if mode == "native" and dist is not None:
+            raise ValueError("native sequential soups are single-process (their order is serial)")
         self.mode = mode
         self.device = device
         self.seed_value = seed
@@ -108,14 +113,21 @@ class Soup(object):
         else:
             if self.engine is None:
                 self._seed_device()
-            for _ in range(iterations):
-                self.time += 1
-                self.engine.evolve(1, record=self.record)
+            if self.mode == "native":
+                self.engine.evolve(iterations)
+                self.time += iterations
+                ParticleDecorator.next_uid = max(ParticleDecorator.next_uid, int(self.engine.next_uid[0]))
+            else:
+                for _ in range(iterations):
+                    self.time += 1
+                    self.engine.evolve(1, record=self.record)
             self._refresh_views()
         return self
 
     def count(self):
-        if self.mode == "device":
+        if self.mode in ("device", "native"):
+            if self.engine is None:
+                self._seed_device()
             return self.engine.count()
         counters = dict(divergent=0, fix_zero=0, fix_other=0, fix_sec=0, other=0)
         for p in self.particles:
@@ -188,6 +200,17 @@ class Soup(object):
         params = dict(self.params)
         params.setdefault("epsilon", inner.get_params().get("epsilon", 1e-14))
         lr = probe._lr() if hasattr(probe, "_lr") else 0.01
+        if self.mode == "native":
+            from .seq_soup import SequentialSoupEngine
+            seed = self.seed_value if self.seed_value is not None else _rng.get_seed() ^ ParticleDecorator.next_uid
+            self.engine = SequentialSoupEngine(spec, self.size, params, seed=seed, lr=lr)
+            base = ParticleDecorator.next_uid
+            self.engine.uid.add_(base)
+            self.engine.next_uid.add_(base)
+            ParticleDecorator.next_uid += self.size
+            self._uid_offset = base
+            self._refresh_views()
+            return
         device = self.device
         if device is None:
             device = "cuda" if torch.cuda.is_available() else "cpu"

@@ -1,0 +1,94 @@
+"""Native sequential (Gauss-Seidel) soups, any size (OP_SOUP_SEQ, seq_soup.py): bitwise
+against the numpy oracle of the same algorithm and keys, and statistically against the
+synchronous device engine and the published curves (reference code/soup.py:51-87, S11)."""
+import numpy as np
+import pytest
+import torch
+from scipy.stats import mannwhitneyu
+
+from self_replicating_neural_networks_amd.oracle import core as O
+from self_replicating_neural_networks_amd.arch import ArchSpec
+from self_replicating_neural_networks_amd.population import Population
+from self_replicating_neural_networks_amd.seq_soup import SequentialSoupEngine
+from self_replicating_neural_networks_amd.soup_engine import SoupEngine
+
+P = dict(attacking_rate=0.3, learn_from_rate=0.3, train=2, learn_from_severity=2, remove_divergent=True,
+         remove_zero=True, epsilon=1e-4)
+
+
+@pytest.mark.parametrize("spec", [ArchSpec.weightwise(2, 2), ArchSpec.aggregating(4, 2, 2), ArchSpec.recurrent(2, 2)],
+                         ids=["ww", "agg", "rnn"])
+def test_sequential_soup_matches_oracle(spec):
+    """native generation == the numpy oracle of the same algorithm and keys (fp32 to within
+    fma-contraction rounding -- numpy rounds every product, the C++ contracts a*b+c --
+    re-synchronised each generation as in tests/test_soup.py);
+    decisions, actions, respawns and uids exactly"""
+    n, seed = 60, 11
+    e = SequentialSoupEngine(spec, n, P, seed=seed)
+    acted = 0
+    for g in range(1, 4):
+        W0 = e.W[:, :spec.P].numpy().copy()
+        uid0, nxt = e.uid.numpy().copy(), int(e.next_uid[0])
+        e.evolve(1)
+        W1, act, cp, loss, rs = O.soup_generation_seq(spec, W0, g, seed, P)
+        assert np.array_equal(e.action.numpy(), act) and np.array_equal(e.counterpart.numpy(), cp)
+        assert np.array_equal(e.respawn.numpy(), rs)
+        uid1 = uid0.copy()
+        for j in np.nonzero(rs)[0]:  # newborns numbered in index order
+            uid1[j] = nxt
+            nxt += 1
+        assert np.array_equal(e.uid.numpy(), uid1) and int(e.next_uid[0]) == nxt
+        got = e.W[:, :spec.P].numpy()
+        ok = np.all(np.isfinite(W1), 1)
+        scale = np.max(np.abs(W1[ok]), 1, keepdims=True) + 1e-6
+        # in-place updates chain the rounding differences of earlier particles: 5e-3 (rnn 2e-2)
+        assert np.max(np.abs(got[ok] - W1[ok]) / scale) < (2e-2 if spec.kind == "recurrent" else 5e-3)
+        assert np.array_equal(np.isfinite(got), np.isfinite(W1))
+        acted += int((act > 0).sum())
+    assert acted > 0
+
+
+def test_sequential_order_matters():
+    """in place: a particle attacked earlier in the generation trains from its new weights,
+    so sequential and synchronous generations differ (same decisions and keys)"""
+    spec = ArchSpec.weightwise(2, 2)
+    p = dict(P, remove_divergent=False, remove_zero=False)
+    s = SequentialSoupEngine(spec, 40, p, seed=5)
+    W0 = s.W[:, :spec.P].numpy().copy()
+    s.evolve(1)
+    sync = O.soup_generation_sync(spec, W0, np.arange(40, dtype=np.uint64), 1, 5, p)[0]
+    assert not np.array_equal(s.W[:, :spec.P].numpy(), sync)
+
+
+def _fix_other(W, eps):
+    pop = Population(ArchSpec.weightwise(2, 2), W.shape[0], weights=W)
+    cls, _ = pop.classify(eps)
+    return cls.numpy()
+
+
+@pytest.mark.parametrize("severity,published", [(10, 1.2), (30, 7.4)])
+def test_learn_from_soups_sequential_vs_synchronous(severity, published):
+    """200 independent 10-particle sequential soups in ONE native call (segment = 10) vs 200
+    synchronous ones; the published curve (code/results/exp-learn-from-soup-*/log.txt)"""
+    spec = ArchSpec.weightwise(2, 2)
+    p = dict(attacking_rate=-1, learn_from_rate=0.1, train=0, learn_from_severity=severity, epsilon=1e-4, segment=10)
+    seq = SequentialSoupEngine(spec, 2000, p, seed=7).evolve(100)
+    dev = SoupEngine(spec, 2000, p, seed=3)
+    dev.evolve(100)
+    fs = (_fix_other(seq.W[:, :spec.P].clone(), 1e-4).reshape(200, 10) == 2).sum(1)
+    fd = (_fix_other(dev.local_rows()[:, :spec.P].clone(), 1e-4).reshape(200, 10) == 2).sum(1)
+    assert mannwhitneyu(fs, fd).pvalue > 1e-3, (fs.mean(), fd.mean())
+    assert abs(fs.mean() - published) < 4 * fs.std() / np.sqrt(10) + 0.1, (fs.mean(), published)
+
+
+def test_trajectory_soups_sequential():
+    """40 sequential trajectory soups (20 WW, train 30, attacks 0.1, respawn; published run:
+    fix_other 13 / other 7, code/results/Soup/log.txt) in one native call"""
+    spec = ArchSpec.weightwise(2, 2)
+    p = dict(attacking_rate=0.1, learn_from_rate=-1, train=30, remove_divergent=True, remove_zero=True, epsilon=1e-4,
+             segment=20)
+    seq = SequentialSoupEngine(spec, 800, p, seed=9).evolve(100)
+    fo = (_fix_other(seq.W[:, :spec.P].clone(), 1e-4).reshape(40, 20) == 2).sum(1)
+    assert (fo <= 13).mean() > 0.01 and (fo >= 13).mean() > 0.01, fo
+    assert fo.mean() > 10
+    assert sum(seq.count().values()) == 800

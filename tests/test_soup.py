@@ -111,6 +111,26 @@ def test_device_soup_records_reference_schema():
     assert p.get_weights()[0].shape == (4, 2)
 
 
+def test_native_sequential_soup_api():
+    """Soup(mode="native"): the sequential algorithm in one native call per evolve, with the
+    same particle views and census as the other modes."""
+    rng.set_seed(5)
+    s = Soup(300, gen, mode="native", seed=3).with_params(remove_divergent=True, remove_zero=True, train=2)
+    s.seed()
+    uids0 = [p.get_uid() for p in s.particles]
+    s.evolve(5)
+    assert s.time == 5 and len(s.particles) == 300
+    assert sum(s.count().values()) == 300
+    uids = [p.get_uid() for p in s.particles]
+    born = [u for u in uids if u not in set(uids0)]
+    assert all(u >= max(uids0) for u in born)  # newborns continue the process-wide counter
+    p = s.particles[0]
+    assert isinstance(p.is_fixpoint(), bool)
+    assert p.get_weights()[0].shape == (4, 2)
+    with pytest.raises(ValueError):
+        Soup(10, gen, mode="native", dist=object())
+
+
 def test_device_vs_sequential_statistics_training_soup():
     """Both modes converge the same way: with train=20 nearly every WW particle becomes a
     non-trivial fixpoint or stays `other` (reference code/results/Soup/log.txt: 13 / 7)."""
