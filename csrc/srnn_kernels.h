@@ -645,10 +645,13 @@ struct Item {
     int8_t rs = 0;
     if ((a.flags & 2) && is_diverged<P>(w)) rs = 1;
     else if ((a.flags & 4) && is_zero<P>(w, a.eps)) rs = 2;
+    if (a.W2) store(rowp(a.W2, j), w);  // recording: the particle's state before any respawn
     if (rs) Net::init(w, rng(a), respawn_key(gen, j));
     store(rowp(a.W, j), w);
     if (a.action) a.action[j] = act;
-    if (a.counterpart) a.counterpart[j] = cp;
+    // recording (W2 set): the counterpart's uid at the time of the action (a slot before j may
+    // already hold a newborn this generation); otherwise its slot
+    if (a.counterpart) a.counterpart[j] = (a.W2 && cp >= 0) ? a.uid_out[cp] : cp;
     if (a.loss) a.loss[j] = loss;
     if (a.respawn) a.respawn[j] = rs;
   }

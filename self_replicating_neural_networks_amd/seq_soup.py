@@ -53,7 +53,7 @@ class SequentialSoupEngine:
         self.counterpart = torch.full((self.n,), -1, dtype=torch.int64)
         self.loss = torch.zeros(self.n, dtype=torch.float32)
         self.respawn = torch.zeros(self.n, dtype=torch.int8)
-        self.recorder = None  # (Soup views: no per-step state recording in the native loop)
+        self.recorder = None  # StateRecorder (Soup record=True): trajectory states per generation
 
     def local_rows(self) -> torch.Tensor:
         return self.W
@@ -70,11 +70,30 @@ class SequentialSoupEngine:
             f |= _lib.FLAG_REMOVE_ZERO
         return f
 
-    def evolve(self, iterations: int = 1) -> "SequentialSoupEngine":
+    def evolve(self, iterations: int = 1, record: bool = False) -> "SequentialSoupEngine":
         """``iterations`` sequential generations in one native call (action / counterpart /
-        loss / respawn describe the last one)."""
+        loss / respawn describe the last one).  With ``record`` (and a ``recorder``) one call
+        per generation that also keeps every particle's pre-respawn state (``rows_out``) and
+        the counterparts' uids at the time of each action, for the reference's trajectory
+        states (code/soup.py:87)."""
         if iterations <= 0:
             return self
+        if record and self.recorder is not None:
+            for _ in range(int(iterations)):
+                old_uid = self.uid.clone()
+                self._run(1, rows_out=self.rows_out)
+                self.recorder.on_sequential_generation(self, self.time, old_uid)
+            return self
+        self._run(int(iterations))
+        return self
+
+    @property
+    def rows_out(self) -> torch.Tensor:
+        if getattr(self, "_rows_out", None) is None:
+            self._rows_out = torch.zeros_like(self.W)
+        return self._rows_out
+
+    def _run(self, iterations: int, rows_out: Optional[torch.Tensor] = None):
         a = _lib.SrnnArgs()
         a.n, a.n_total, a.lo = self.n, self.n, 0
         a.seed = self.seed & 0xFFFFFFFFFFFFFFFF
@@ -86,13 +105,12 @@ class SequentialSoupEngine:
         a.segment = int(self.params.get("segment", 0) or 0)
         a.flags = self._flags()
         a.steps = int(iterations)
-        a.W = _p(self.W)
+        a.W, a.W2 = _p(self.W), _p(rows_out)
         a.gen_ptr = _p(self.gen)
         a.uid_base, a.uid_out = _p(self.next_uid), _p(self.uid)
         a.action, a.counterpart, a.loss, a.respawn = _p(self.action), _p(self.counterpart), _p(self.loss), _p(self.respawn)
         _lib.run(_lib.OP_SOUP_SEQ, self.spec, a, dtype=self.dtype_code)
         self.time += int(iterations)
-        return self
 
     def count(self, with_sec: bool = True) -> Dict[str, int]:
         """Census (reference Soup.count, code/soup.py:89-103)."""

@@ -7,7 +7,7 @@
   Meant for the reference's small soups (10-100 particles).
 * ``mode="native"`` — the sequential algorithm on a weight table in one native call per
   ``evolve`` (``seq_soup.SequentialSoupEngine``, any size; slot-keyed Philox streams instead
-  of the process-wide ``prng``; no per-step state recording).
+  of the process-wide ``prng``; trajectory states recorded like the other modes).
 * ``mode="device"`` — the population lives in a device weight table and every
   generation is one fused kernel pipeline (``SoupEngine``), optionally sharded over the
   ranks of a process group.  Within a generation all reads come from the
@@ -114,7 +114,7 @@ class Soup(object):
             if self.engine is None:
                 self._seed_device()
             if self.mode == "native":
-                self.engine.evolve(iterations)
+                self.engine.evolve(iterations, record=self.record)
                 self.time += iterations
                 ParticleDecorator.next_uid = max(ParticleDecorator.next_uid, int(self.engine.next_uid[0]))
             else:
@@ -209,6 +209,9 @@ class Soup(object):
             self.engine.next_uid.add_(base)
             ParticleDecorator.next_uid += self.size
             self._uid_offset = base
+            if self.record:
+                self.engine.recorder = StateRecorder(spec.class_name)
+                self.engine.recorder.record_init(self.engine, time=0)
             self._refresh_views()
             return
         device = self.device
@@ -264,7 +267,13 @@ class StateRecorder:
         self._snap = (eng.rows_out[:, : eng.spec.P].clone(), eng.action.clone(), eng.counterpart.clone(),
                       eng.loss.clone(), eng.respawn.clone(), uid_slots)
 
+    def on_sequential_generation(self, eng, time, old_uid):
+        """After one generation of a ``SequentialSoupEngine`` (its counterparts are uids)."""
+        self._snap = (eng.rows_out[:, : eng.spec.P], eng.action, eng.counterpart, eng.loss, eng.respawn, old_uid)
+        self.on_generation_end(eng, time, None)
+
     def on_generation_end(self, eng, time, uid_of_slot):
+        """``uid_of_slot`` maps counterpart slots to uids (None: counterparts are uids)."""
         W, act, cp, loss, resp, old_uid = (t.cpu().numpy() for t in self._snap)
         new_uid = eng.uid.cpu().numpy()
         train = int(eng.params.get("train", 0))
@@ -274,7 +283,8 @@ class StateRecorder:
             a = ACTION_NAMES[int(act[j])]
             if a is not None:
                 d["action"] = a
-                d["counterpart"] = None if a == "train_self" else int(uid_of_slot[int(cp[j])])
+                d["counterpart"] = (None if a == "train_self" else
+                                    int(cp[j]) if uid_of_slot is None else int(uid_of_slot[int(cp[j])]))
             if a == "train_self":
                 d["fitted"] = train
                 d["loss"] = float(loss[j])

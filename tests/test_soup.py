@@ -131,6 +131,40 @@ def test_native_sequential_soup_api():
         Soup(10, gen, mode="native", dist=object())
 
 
+def test_native_sequential_soup_records_reference_states():
+    """Recording does not change the soup, and the states follow the reference schema: the
+    old particle's last state names its replacement, counterparts are uids that existed."""
+    def run(record):
+        rng.set_seed(9)
+        s = Soup(200, gen, mode="native", seed=4, record=record).with_params(
+            remove_divergent=True, remove_zero=True, train=1, attacking_rate=0.3, learn_from_rate=0.3)
+        s.seed()
+        s.evolve(6)
+        return s
+    a, b = run(True), run(False)
+    assert np.array_equal(np.stack([p.get_weights_flat() for p in a.particles]),
+                          np.stack([p.get_weights_flat() for p in b.particles]))
+    assert ([p.get_uid() - a._uid_offset for p in a.particles]
+            == [p.get_uid() - b._uid_offset for p in b.particles])  # (process-wide uid counter)
+    known = set(a.historical_particles)
+    n_dead = 0
+    for uid, p in a.historical_particles.items():
+        st = p.get_states()
+        assert st and st[0]["action"] == "init"
+        for d in st[1:]:
+            assert {"class", "weights", "time"} <= set(d)
+            if d.get("action") in ("divergent_dead", "zweo_dead"):
+                n_dead += 1
+                assert d["counterpart"] in known and d["counterpart"] > uid
+            elif d.get("action") in ("attacking", "learn_from"):
+                assert d["counterpart"] in known
+    for p in a.particles:
+        if p.get_uid() < a._uid_offset + 200:  # a founder alive at the end: one state per generation
+            assert [d["time"] for d in p.get_states()] == list(range(7))
+    # (a divergent particle's non-finite last state is not recorded, as in device mode)
+    assert 0 < n_dead <= sum(1 for u in known if u not in {p.get_uid() for p in a.particles})
+
+
 def test_device_vs_sequential_statistics_training_soup():
     """Both modes converge the same way: with train=20 nearly every WW particle becomes a
     non-trivial fixpoint or stays `other` (reference code/results/Soup/log.txt: 13 / 7)."""
