@@ -211,8 +211,56 @@ static std::vector<float> soup(int R, int64_t N, int gens, std::vector<int64_t>*
   return W;
 }
 
+// ---- exact sequential soup (OP_SOUP_SEQ): K steps in one call == K calls of one step,
+// recording on or off (pre-respawn rows in W2, counterpart uids) ----------------------------
+static void seq_soup(const SrnnCfg& c, int64_t n, int steps) {
+  std::vector<float> W[2], rows((size_t)(n * c.pp));
+  std::vector<int64_t> uid[2], next[2], cp((size_t)n);
+  std::vector<int32_t> gen[2];
+  std::vector<int8_t> act((size_t)n), rs((size_t)n);
+  std::vector<float> loss((size_t)n);
+  for (int v = 0; v < 2; ++v) {
+    W[v].assign((size_t)(n * c.pp), 0.f), uid[v].resize((size_t)n), next[v].assign(1, n), gen[v].assign(1, 1);
+    for (int64_t j = 0; j < n; ++j) uid[v][(size_t)j] = j;
+    SrnnArgs a{};
+    a.n = n, a.seed = 11, a.W = W[v].data(), a.uid = uid[v].data();
+    run(OP_INIT, c, a);
+  }
+  auto args = [&](int v) {
+    SrnnArgs a{};
+    a.n = a.n_total = n, a.seed = 11, a.lr = 0.01f, a.eps = 1e-4f;
+    a.attacking_rate = 0.3f, a.learn_from_rate = 0.3f, a.epochs = 2, a.severity = 2, a.flags = 1 | 2 | 4;
+    a.W = W[v].data(), a.gen_ptr = gen[v].data(), a.uid_base = next[v].data(), a.uid_out = uid[v].data();
+    a.action = act.data(), a.counterpart = cp.data(), a.loss = loss.data(), a.respawn = rs.data();
+    return a;
+  };
+  SrnnArgs a = args(0);
+  a.steps = steps;
+  run(OP_SOUP_SEQ, c, a);
+  for (int s = 0; s < steps; ++s) {
+    SrnnArgs b = args(1);
+    b.steps = 1, b.W2 = rows.data();
+    std::vector<int64_t> before = uid[1];
+    run(OP_SOUP_SEQ, c, b);
+    // a particle's recorded state is its row after its own turn: later attackers may still
+    // change the table row, so most (not all) surviving rows match it, the last one always
+    int64_t bad_cp = 0, bad_uid = 0, same = 0, kept = 0;
+    for (int64_t j = 0; j < n; ++j) {
+      bad_cp += cp[(size_t)j] >= next[1][0];  // counterparts are uids that existed
+      const bool eq = std::memcmp(&rows[(size_t)(j * c.pp)], &W[1][(size_t)(j * c.pp)], 4 * (size_t)c.pp) == 0;
+      if (rs[(size_t)j]) bad_uid += uid[1][(size_t)j] == before[(size_t)j];
+      else kept += 1, same += eq;
+    }
+    CHECK(bad_cp == 0 && bad_uid == 0 && 2 * same >= kept);
+    CHECK(rs[(size_t)(n - 1)] || std::memcmp(&rows[(size_t)((n - 1) * c.pp)], &W[1][(size_t)((n - 1) * c.pp)], 4 * (size_t)c.pp) == 0);
+  }
+  CHECK(W[0] == W[1] && uid[0] == uid[1] && next[0] == next[1] && gen[0][0] == 1 + steps && gen[1][0] == 1 + steps);
+}
+
 int main() {
   CHECK(srnn_abi_version() == 14);
+  seq_soup(ww22(), 257, 4);
+  seq_soup(agg422(), 129, 3);
   ops_smoke(ww22(), 1000);
   ops_smoke(agg422(), 777);
   ops_smoke(cfg(2, 2, 2, 0, 17), 300);              // Recurrent(2,2): templated BPTT
