@@ -1383,16 +1383,38 @@ int uid_assign(const SrnnCfg& c, const SrnnArgs& a);
 // definition: a single CPU core runs it ~100x faster than per-particle device launches and
 // faster than one GPU lane).  Newborns get uids from *uid_base in index order; uid_out
 // receives them; the generation counter advances by `steps`.
+// The same serial loop as ONE device lane (measured against the host loop: the dependent
+// chain is slower on a GPU lane than on a CPU core, profiles/r2o_native_sequential_soups.md)
+template <class Net, class S>
+__global__ __launch_bounds__(TB) void k_soup_seq(SrnnCfg c, SrnnArgs a) {
+  using I = Item<Net, S>;
+  constexpr int SAMP = Net::KIND == 0 ? Net::P : 1;
+  constexpr int PERM = (Net::P + 4) & ~3;
+  __shared__ float4 s_samp[TB * SAMP];  // lane 0's slots at s_samp[k * TB] (SAMP_STRIDE)
+  __shared__ uint8_t s_perm[PERM];
+  if (threadIdx.x != 0) return;
+  const int32_t gen0 = I::gen_of(a);
+  int64_t next = a.uid_base[0];
+  for (int32_t s = 0; s < a.steps; ++s) {
+    for (int64_t j = 0; j < a.n; ++j) {
+      I::soup_seq_one(c, a, j, gen0 + s, s_samp, s_perm);
+      if (a.respawn && a.respawn[j]) a.uid_out[j] = next++;
+    }
+  }
+  ((int64_t*)a.uid_base)[0] = next;
+  I::set_gen(a, gen0 + a.steps);
+}
+
 template <class Net, class S>
 int soup_seq(const SrnnCfg& c, const SrnnArgs& a) {
   using I = Item<Net, S>;
-  if (a.dev) {
-    set_error("sequential soups run on the host (their update order is serial)");
-    return -5;
-  }
   if (a.world > 1 || a.lo != 0 || (a.n_total && a.n_total != a.n) || !a.uid_base || !a.uid_out) {
     set_error("sequential soup: one unsharded table, uid_base and uid_out needed");
     return -5;
+  }
+  if (a.dev) {
+    hipLaunchKernelGGL((k_soup_seq<Net, S>), dim3(1), dim3(1), 0, (hipStream_t)a.stream, c, a);
+    return 0;
   }
   float4 samp[Net::P + 1];
   uint8_t perm[Net::P + 4];

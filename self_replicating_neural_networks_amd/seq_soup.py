@@ -34,8 +34,12 @@ def _p(t: Optional[torch.Tensor]):
 
 class SequentialSoupEngine:
     def __init__(self, spec: ArchSpec, n: int, params: Optional[dict] = None, seed: int = 0, lr: float = 0.01,
-                 shuffle: bool = True, dtype: torch.dtype = torch.float32, weights: Optional[torch.Tensor] = None):
+                 shuffle: bool = True, dtype: torch.dtype = torch.float32, weights: Optional[torch.Tensor] = None,
+                 device="cpu"):
+        """``device="cuda"`` runs the same serial loop as one GPU lane (``k_soup_seq``; measured
+        slower than the host loop -- it exists for tables that live on the device)."""
         self.spec, self.n = spec, int(n)
+        self.device = torch.device(device)
         self.params = dict(attacking_rate=0.1, learn_from_rate=0.1, train=0, learn_from_severity=1)
         self.params.update(params or {})
         self.seed, self.lr, self.shuffle = int(seed), float(lr), bool(shuffle)
@@ -53,6 +57,9 @@ class SequentialSoupEngine:
         self.counterpart = torch.full((self.n,), -1, dtype=torch.int64)
         self.loss = torch.zeros(self.n, dtype=torch.float32)
         self.respawn = torch.zeros(self.n, dtype=torch.int8)
+        if self.device.type != "cpu":
+            for k in ("W", "uid", "next_uid", "gen", "action", "counterpart", "loss", "respawn"):
+                setattr(self, k, getattr(self, k).to(self.device))
         self.recorder = None  # StateRecorder (Soup record=True): trajectory states per generation
 
     def local_rows(self) -> torch.Tensor:
@@ -109,6 +116,9 @@ class SequentialSoupEngine:
         a.gen_ptr = _p(self.gen)
         a.uid_base, a.uid_out = _p(self.next_uid), _p(self.uid)
         a.action, a.counterpart, a.loss, a.respawn = _p(self.action), _p(self.counterpart), _p(self.loss), _p(self.respawn)
+        if self.device.type != "cpu":
+            a.dev = 1
+            a.stream = ctypes.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
         _lib.run(_lib.OP_SOUP_SEQ, self.spec, a, dtype=self.dtype_code)
         self.time += int(iterations)
 
