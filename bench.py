@@ -12,88 +12,143 @@ scaling: the population is sharded, every rank owns 100k particles; at N=1 this 
 100k-particle soup).  Random-init weights, fp32 (the reference's dtype; bf16 would make
 the 1e-4 fixpoint test meaningless).
 
-Multi-GPU (N>1): every rank owns 100k particles; one generation is ONE all-to-all on the
-soup's own RCCL communicator (partner rows + per-rank stats rows, over xGMI) -> post-exchange
-launch (received-row index + newborn uids) -> generation kernel (evolve + census + the next
-generation's decisions of every global slot) -> finish launch (counts + packing the next
-exchange).  Single GPU: the generation kernel + finish, 8 generations per hipGraph.
+Multi-GPU (N>1): one process per GPU, every rank owns 100k particles of ONE global soup
+(partners uniform over all N x 100k slots).  Per generation each rank ships the rows other
+ranks need (attackers of their victims, teachers their learners requested one generation
+ahead) in ONE all-to-all on the soup's own RCCL communicator over xGMI, on a comm stream,
+while the slots that need no remote row evolve on the compute stream (soup_engine.py).
+Single GPU: the fused generation kernel, 16/8/4/2 generations per hipGraph.
 
 value = particles x generations / second over the whole job (max time over ranks).
 
 Usage: python bench.py --gpus N --steps K --warmup W
-       (N>1 is launched by torch.distributed.run, one rank per GPU, RCCL over xGMI)
+       N > 1 without torchrun's env: bench.py launches torch.distributed.run itself (one rank
+       per GPU, RCCL over xGMI) as a child process and relays rank 0's JSON line.
 """
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
-import torch
-import torch.distributed as dist
-
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 
-from self_replicating_neural_networks_amd.arch import ArchSpec  # noqa: E402
-from self_replicating_neural_networks_amd.parallel.dist import from_env  # noqa: E402
-from self_replicating_neural_networks_amd.soup_engine import SoupEngine  # noqa: E402
 
-
-def main():
+def parse_args(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--particles-per-gpu", type=int, default=100_000)
     ap.add_argument("--train", type=int, default=20)
+    ap.add_argument("--attacking-rate", type=float, default=0.1)
+    ap.add_argument("--learn-from-rate", type=float, default=0.1)
+    ap.add_argument("--severity", type=int, default=1)
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--no-stats", action="store_true")
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--backend", default="nccl", help="nccl (= RCCL on ROCm) or gloo (rehearsal)")
+    ap.add_argument("--device", default="cuda", choices=["cuda", "cpu"],
+                    help="cpu: host rehearsal of the same engine (gloo backend)")
     ap.add_argument("--share-device", action="store_true",
                     help="rehearsal on a 1-GPU box: every rank uses cuda:0")
     ap.add_argument("--force-sharded", action="store_true",
                     help="rehearsal: run the multi-GPU generation (RCCL all-to-all) even with one rank")
-    args = ap.parse_args()
-    if args.force_sharded:
-        os.environ["SRNN_FORCE_SHARDED"] = "1"
+    return ap.parse_args(argv)
 
+
+def _free_port() -> int:
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(args) -> int:
+    """--gpus N > 1 outside torchrun: start torch.distributed.run as a CHILD process (nothing
+    here has touched the GPU) and relay its output; the exit code is the child's."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(args.gpus),
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+           os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", OMP_NUM_THREADS=os.environ.get("OMP_NUM_THREADS", "4"))
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.run(cmd, env=env).returncode
+
+
+def model_string(args) -> str:
+    parts = [f"train={args.train}"]
+    parts.append(f"attack {args.attacking_rate:g}" if args.attacking_rate > 0 else "no attacks")
+    if args.learn_from_rate > 0:
+        parts.append(f"learn_from {args.learn_from_rate:g}" + (f" x{args.severity}" if args.severity != 1 else ""))
+    else:
+        parts.append("no learn_from")
+    parts.append("remove divergent/zero")
+    return "Soup of WeightwiseNeuralNetwork(width=2, depth=2), " + ", ".join(parts)
+
+
+def main(argv=None):
+    args = parse_args(argv)
+    in_launcher = "WORLD_SIZE" in os.environ
+    if args.gpus > 1 and not in_launcher:
+        sys.exit(launch_ranks(args))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if world != args.gpus:
-        print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}: refusing to report a number for a "
+              "different GPU count", file=sys.stderr)
+        sys.exit(2)
+
+    import torch
+    import torch.distributed as dist
+    from self_replicating_neural_networks_amd.arch import ArchSpec
+    from self_replicating_neural_networks_amd.parallel.dist import from_env
+    from self_replicating_neural_networks_amd.soup_engine import SoupEngine
+
+    if args.force_sharded:
+        os.environ["SRNN_FORCE_SHARDED"] = "1"
     if args.share_device:
         os.environ["SRNN_SHARE_DEVICE"] = "1"
-    d = from_env(backend=args.backend)
-    dev = torch.device("cuda", 0 if args.share_device else d.local_rank)
-    torch.cuda.set_device(dev)
+    on_gpu = args.device == "cuda"
+    backend = args.backend if on_gpu else "gloo"
+    d = from_env(backend=backend, device_type=args.device)
+    if on_gpu:
+        dev = torch.device("cuda", 0 if args.share_device else d.local_rank)
+        torch.cuda.set_device(dev)
+    else:
+        dev = torch.device("cpu")
+
+    def sync():
+        if on_gpu:
+            torch.cuda.synchronize(dev)
 
     spec = ArchSpec.weightwise(2, 2)
-    params = dict(attacking_rate=0.1, learn_from_rate=0.1, learn_from_severity=1, train=args.train,
+    params = dict(attacking_rate=args.attacking_rate, learn_from_rate=args.learn_from_rate,
+                  learn_from_severity=args.severity, train=args.train,
                   remove_divergent=True, remove_zero=True, epsilon=1e-4)
     n_total = args.particles_per_gpu * d.world
     eng = SoupEngine(spec, n_total, params, device=dev, seed=args.seed, dist=d)
     eng.stats = not args.no_stats
     graphed = False
-    if not args.no_graph:
+    if on_gpu and not args.no_graph:
         graphed = eng.capture(warmup=1)
     eng.evolve(args.warmup)
-    torch.cuda.synchronize(dev)
+    sync()
     d.barrier()
-    torch.cuda.synchronize(dev)
+    sync()
     t0 = time.perf_counter()
     eng.evolve(args.steps)
-    torch.cuda.synchronize(dev)
+    sync()
     d.barrier()
-    torch.cuda.synchronize(dev)
+    sync()
     dt = time.perf_counter() - t0
-    t = torch.tensor([dt], dtype=torch.float64, device=dev)
+    t = torch.tensor([dt], dtype=torch.float64, device=dev if backend == "nccl" else "cpu")
     if d.enabled:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     dt = float(t.item())
-    if eng.exchange_overflowed():
-        # rows that did not fit the all-to-all capacity were dropped: the generation is invalid
-        raise SystemExit(f"soup row exchange overflowed its capacity (ovf flags {int(eng.ovf.item())}: 1 rows dropped, "
-                         "2 a wait timed out): the measured generations are invalid")
+    err = eng.exchange_error()
+    if err:
+        # rows that did not fit the exchange capacity were dropped: the generations are invalid
+        raise SystemExit(f"soup row exchange failed ({err}): the measured generations are invalid")
     census = eng.count()
     value = n_total * args.steps / dt
     if d.rank == 0:
@@ -110,13 +165,13 @@ def main():
             "vs_baseline": None,
             "dtype": "fp32",
             "data": "synthetic (random-init particles, Philox seed %d)" % args.seed,
-            "config": {"model": "Soup of WeightwiseNeuralNetwork(width=2, depth=2), train=20, attack 0.1, "
-                                "learn_from 0.1, remove divergent/zero",
+            "config": {"model": model_string(args),
                        "global_batch": n_total, "particles_per_gpu": args.particles_per_gpu, "seq_len": None,
-                       "parallelism": f"population-dp{d.world}", "hip_graph": graphed,
+                       "parallelism": f"population-dp{d.world}", "device": args.device, "hip_graph": graphed,
                        "multi_generation_graph": eng._chunk is not None,
                        "collectives": ("native RCCL communicator (" + d.native.library + ")") if d.native
-                       else ("torch.distributed" if d.enabled else None),
+                       else (f"torch.distributed ({backend})" if d.enabled else None),
+                       "overlap": getattr(eng, "overlap", False),
                        "census_every_step": eng.stats, "final_census": census},
         }), flush=True)
     eng.release_graphs()  # graph executables reference the RCCL communicator

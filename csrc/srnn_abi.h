@@ -1,5 +1,6 @@
 // srnn_abi.h — C ABI of libsrnn.so (mirrored by ctypes structures in
-// self_replicating_neural_networks_amd/ops/_lib.py; keep the field order in sync).
+// self_replicating_neural_networks_amd/ops/_lib.py; keep the field order and the flag
+// values in sync).
 #pragma once
 #include <stdint.h>
 
@@ -17,22 +18,45 @@ struct SrnnCfg {
   int32_t dtype;       // weight-table storage: 0 fp32, 1 bf16, 2 fp16 (arithmetic is fp32)
 };
 
+// ---- SrnnArgs.flags bits (one meaning each; SRNN_F_* below, FLAG_* in ops/_lib.py)
+enum SrnnFlag : uint32_t {
+  SRNN_F_SHUFFLE = 1u << 0,          // SGD sample order shuffled per epoch (Keras fit shuffle=True)
+  SRNN_F_REMOVE_DIVERGENT = 1u << 1, // soup: respawn divergent particles (reference code/soup.py:77-80)
+  SRNN_F_REMOVE_ZERO = 1u << 2,      // soup: respawn zero particles (code/soup.py:81-86)
+  SRNN_F_FIX_SEC = 1u << 3,          // classification tests second-order fixpoints too
+  SRNN_F_ROW_FLAGS = 1u << 4,        // evolve: per-row respawn flags (rowflags[n]) instead of 64-row ballots
+  SRNN_F_RESPAWN_INLINE = 1u << 5,   // evolve re-initialises newborn rows itself
+  SRNN_F_COUNT_RESPAWNS = 1u << 6,   // classify: respawns of this generation into counts[5]
+  SRNN_F_FULL_TABLE = 1u << 7,       // sharded all-gather: recvbuf is the gathered [n_total] table
+  SRNN_F_X2_PRIME = 1u << 8,         // X2 pack / post: first exchange (decisions of THIS generation, no rows)
+  SRNN_F_GEN_ADVANCE = 1u << 9,      // classify advances the generation counter
+  SRNN_F_FUSED_CENSUS = 1u << 10,    // the generation kernel classifies its stored rows (census)
+  SRNN_F_TWO_PHASE = 1u << 11,       // fused generation: block stats for a separate finish launch
+  SRNN_F_MASKS_BS = 1u << 12,        // uid assignment reads ballots from block stats (u64[4] per block)
+  SRNN_F_GEN_COUNTS = 1u << 13,      // fused generation advances the counter itself (finish follows later)
+  SRNN_F_FINISH_BATCH = 1u << 14,    // OP_GEN_FINISH: a ring of `steps` generations' block stats
+  SRNN_F_BORN_TOTAL = 1u << 15,      // fused generation adds its newborn count after its block stats
+  SRNN_F_X2 = 1u << 16,              // sharded all-to-all exchange (srnn_shard.hip): list entries >= n are
+                                     // received rows, teachers of remote learners come from rlist
+  SRNN_F_X2_REMOTE = 1u << 17,       // X2 evolve: the remote-dependent slots of rlist (else: the local slots)
+  SRNN_F_X2_FINISH_ONLY = 1u << 18,  // X2 pack: only the finish of the last generation (flush)
+};
+
+// Attack-list entries (uint32, SRNN_NIL ends a list).  Single rank: the attacker's row
+// (= its slot).  SRNN_F_FULL_TABLE: the attacker's global slot.  SRNN_F_X2: e < n is the
+// local row e, e >= n the received row e - n (its slot in x_rslot[e - n]).
+#define SRNN_NIL 0xFFFFFFFFu
+
 struct SrnnArgs {
   int64_t n;            // work items (rows) of this call
   int64_t n_total;      // soup: global population size
   int64_t lo;           // soup: first global slot owned by this rank
-  int32_t steps;        // fixpoint run: step limit
+  int32_t steps;        // fixpoint run: step limit; batched finish: generations
   int32_t epochs;       // train: epochs; soup: train count
   int32_t severity;     // soup: learn_from_severity
   int32_t early_exit;   // fixpoint run: stop at fixpoint / divergence
-  int32_t flags;        // bit0 shuffle, bit1 remove_divergent, bit2 remove_zero, bit3 fix_sec, bit4 per-row respawn flags, bit5 respawn inline, bit6 count respawns in counts[5], bit7 recvbuf is the all-gathered table,
-                        // bit8 uid_assign reads the per-rank stats from the exchange's stats rows, bit9 classify advances *gen_ptr,
-                        // bit10 fused generation computes the census, bit16 asynchronous finish (OP_SOUP_GEN
-                        // advances the generation counter itself and leaves the finish to OP_GEN_FINISH),
-                        // bit17 precomputed SGD permutations (perm_cur / perm_next, helper waves),
-                        // bit18 OP_GEN_FINISH is a batch of `steps` generations (block stats ring in temp,
-                        // temp_bytes per generation; census = optional [steps][6] history)
-  int32_t gen;          // soup generation (time)
+  uint32_t flags;       // SrnnFlag bits
+  int32_t gen;          // soup generation (time) when gen_ptr is null
   float eps;
   float lr;
   float attacking_rate;
@@ -50,56 +74,71 @@ struct SrnnArgs {
   int8_t* cls;          // per-row class
   int32_t* nsteps;      // per-row steps taken
   float* loss;          // per-row loss
-  uint64_t* counts;     // [5] class histogram (atomic adds)
-  int32_t* i32a;        // soup: attack target per global slot
-  int32_t* i32b;        // soup: teacher per global slot
-  int32_t* i32c;        // soup: per-local-victim attack count; later respawn flags as int32
-  int32_t* i32d;        // soup: exclusive offsets [n+1]
-  int32_t* i32e;        // soup: fill cursor per local victim
-  int32_t* i32f;        // soup: attacker list (CSR payload)
+  uint64_t* counts;     // [6] class histogram (atomic adds) + respawns
+  // ---- soup: decisions and attack lists
+  uint32_t* heads;      // [n] first attacker entry of each local victim this generation (consumed -> NIL)
+  uint32_t* nexts;      // entry -> next entry of the same victim
+  uint32_t* heads_next; // fused generation / X2 pack+post: the NEXT generation's lists
+  uint32_t* nexts_next;
+  int64_t* dec_at;      // OP_SOUP_DECIDE: attack target per global slot (diagnostics, optional)
+  int64_t* dec_te;      // OP_SOUP_DECIDE: teacher per global slot (diagnostics, optional)
+  unsigned long long* ballots;  // evolve: respawn ballot per 64-row block (u64[nb])
+  int32_t* rowflags;    // evolve with SRNN_F_ROW_FLAGS: respawn flag per row
+  int32_t* done;        // fused generation / parallel batched finish: done counter (last-wave hand-off)
   int64_t* uid_out;     // respawn: uid column to update
-  const int64_t* uid_base;  // respawn: device scalar, first uid for this rank
+  int64_t* uid_base;    // respawn: device scalar, next uid (advanced in place)
   const int32_t* gen_ptr;   // soup: device scalar generation (graph replay); null -> gen
-  int64_t segment;          // soup: >0 -> independent sub-soups of this many slots (partners chosen inside)
-  int32_t world;            // soup: ranks sharing the population (<= 1: unsharded)
+  int32_t* gen_out;     // soup: where "advance the generation" writes gen + 1 (null -> *gen_ptr in
+                        // place): a 2-slot ring indexed by the ping-pong parity
+  int64_t segment;      // soup: >0 -> independent sub-soups of this many slots (partners chosen inside)
+  int32_t world;        // soup: ranks sharing the population (<= 1: unsharded)
   int32_t rank;
-  int64_t cap;              // soup: rows per destination rank in the exchange buffers
-  float* sendbuf;           // [world][cap][pp + 4]: row, then (slot, generation) tags
-  const float* recvbuf;     // [world][cap][pp + 4]
-  int32_t* need;            // [n] bitmask of the ranks that need local row j this generation
-  int32_t* sendcnt;         // [world] rows packed per destination
-  int32_t* rmap;            // [n_total] received row index of a remote slot
-  int32_t* ovf;             // [1] exchange overflow flag
-  const int64_t* stats;     // [world][6] gathered (class counts[5], respawns) per rank
-  int64_t* census;          // [5] global class counts (written by OP_UID_ASSIGN)
-  int8_t* action;       // soup: action code per local row
-  int64_t* counterpart; // soup: counterpart slot per local row
+  // ---- sharded soup exchange (srnn_shard.hip).  SRNN_F_FULL_TABLE: recvbuf = the gathered
+  // table, stats = [world][6].  SRNN_F_X2: one all-to-all per generation; per peer a block of
+  // x_blk bytes = header (int64[X2_HDR]) + x_cr rows of (row, int64 slot, int32 gen, pad) +
+  // x_cn notices (int64 attacker, int64 victim) + x_cq requests (int64 teacher)
+  int64_t x_cr, x_cn, x_cq, x_blk;
+  char* sendbuf;
+  const char* recvbuf;
+  const int64_t* stats;       // FULL_TABLE: [world][6] gathered (class counts[5], respawns) per rank
+  int64_t* census;            // [5] global class counts of the previous generation
+  int32_t* err;               // [1] exchange error bits: 1 capacity overflow, 4 row tag mismatch
+  // ---- X2 per-generation state ("this" = the generation being evolved / exchanged, "next" =
+  // the one whose decisions pack and post prepare; the engine swaps them by parity)
+  uint32_t* x_dep;            // [ceil(n/32)] remote-dependent bits of this generation (read, reset)
+  uint32_t* x_dep_next;       // the next generation's (set by pack / post)
+  uint32_t* x_rlist;          // [2n] (row, teacher recv row or NIL) of this generation's remote slots
+  uint32_t* x_rlist_next;
+  int32_t* x_rcount;          // [1] entries of x_rlist (zeroed by the remote evolve's last wave)
+  int32_t* x_rcount_next;
+  int64_t* x_rslot;           // [world * x_cr] attacker slot of received row k (this generation)
+  int64_t* x_rslot_next;
+  uint32_t* x_satt;           // [world * x_cn] local attacker rows noticed to each peer for this generation
+  uint32_t* x_satt_next;
+  int32_t* x_cno;             // [world] notices sent per peer for this generation (zeroed by post)
+  int32_t* x_cno_next;
+  int32_t* x_crq;             // [world] requests sent per peer for this generation (zeroed by post)
+  int32_t* x_crq_next;
+  uint32_t* x_srep;           // [world * x_cq] local rows requested by each peer (this generation)
+  int32_t* x_nsrep;           // [world]
+  int64_t* x_part;            // [x_groups][6] finish partials (born, census[5]) per workgroup
+  int32_t* x_ctl;             // [8] last-workgroup tickets (re-armed by their last workgroup)
+  int32_t x_groups;           // finish / uid workgroups
+  int32_t pad2;
+  int8_t* action;       // soup: action code per local row (optional)
+  int64_t* counterpart; // soup: counterpart slot per local row (optional)
   int8_t* respawn;      // soup: 0 none, 1 divergent_dead, 2 zweo_dead
-  void* temp;           // scratch for device scans
+  void* temp;           // block stats u64[4] per 64-row block (ballot, census): the fused generation /
+                        // X2 evolve write them, the finish / X2 pack + post read them
   int64_t temp_bytes;
   int32_t dev;          // 0 host (CPU tensors), 1 device (HIP)
   int32_t pad1;
   void* stream;         // hipStream_t for dev == 1
-  int32_t* gen_out;     // soup: where "advance the generation" writes gen + 1 (null -> *gen_ptr in
-                        // place).  The engine keeps a 2-slot ring indexed by the ping-pong parity
-                        // so a kernel can advance the counter while its other blocks still read it.
   void* scratch;        // generic (runtime-shape) engine: per-lane vectors, element-major; null ->
   int64_t scratch_bytes;  // the library's own cached device buffer (not inside a graph capture)
-  // fused single-rank generation with precomputed shuffles (flag 131072): the SGD
-  // permutations of generation gen are in perm_cur[k][n] (k < perm_e: learn epochs then
-  // train epochs), helper waves fill perm_next for gen + 1; helper_ctl = work-queue head +
-  // per-SIMD main-wave counts of this parity (re-armed by the finish kernel)
-  uint64_t* perm_cur;
-  uint64_t* perm_next;
-  int32_t* helper_ctl;
-  int32_t perm_e;
-  int32_t helpers;      // helper workgroups appended to the generation grid
-  // sharded fused generation with the post-exchange work folded in (flag 524288): the
-  // respawn ballots of the PREVIOUS generation (block stats, u64[4] per 64 rows; temp holds
-  // this generation's) and the counter the unpack workgroups bump for the generation waves
-  void* temp2;
-  int32_t* xdone;
 };
+
+#define SRNN_X2_HDR 12  // int64 header words of an X2 exchange block (see srnn_shard.hip)
 
 enum SrnnOp {
   OP_INIT = 0,          // W[i] = fresh particle keyed by uid[i]
@@ -109,29 +148,25 @@ enum SrnnOp {
   OP_LEARN = 4,         // `epochs` epochs on samples of W2[idx_t[i]], loss
   OP_CLASSIFY = 5,      // cls + counts
   OP_PERTURB = 6,       // W[i] +-= U(0,1) * eps, p=1/2 each (known-fixpoint variation)
-  OP_SOUP_DECIDE = 7,   // per global slot: decisions; attacks on local victims linked (i32e head, i32f next)
-  OP_RESPAWN_SEQ = 8,   // single rank: scan respawn flags, new uids from *uid_base (updated), re-init, ++*gen_ptr
-  OP_SOUP_EVOLVE = 9,   // fused attack -> learn -> train -> respawn flags for local rows
-  OP_SCAN = 10,         // i32d[0..n] = exclusive scan of i32c[0..n)
-  OP_RESPAWN = 11,      // rows with respawn != 0: uid_out = *uid_base + i32d[i], fresh weights
+  OP_SOUP_DECIDE = 7,   // per global slot: decisions; attacks on local victims linked (heads, nexts)
+  OP_RESPAWN_SEQ = 8,   // single rank: scan respawn ballots, new uids from *uid_base, re-init, ++gen
+  OP_SOUP_EVOLVE = 9,   // attack -> learn -> train -> respawn flags for local rows (X2: local / remote slots)
+  OP_RESPAWN = 11,      // rows with respawn != 0: fresh weights
   OP_VARY_RUN = 12,     // known-fixpoint variation run: nsteps = time to vergence, loss = time as fixpoint
-  OP_SOUP_PACK = 13,    // sharded soup: stats rows + local rows needed by other ranks -> sendbuf (tagged)
-  OP_SOUP_UNPACK = 14,  // sharded soup: index the received rows (rmap), reset sendcnt
-  OP_SOUP_GEN = 16,     // fused generation: evolve + next decisions + census (+ finish; flag 32768: the
-                        // finish launch also packs the next all-to-all = OP_SOUP_PACK)
-  OP_SOUP_PERMS = 18,   // fill perm_next with the SGD permutations of generation *gen_ptr (first generation)
-  OP_SOUP_SEQ = 19,     // host: `steps` sequential (Gauss-Seidel, in-place, index-order) soup generations
-  OP_GEN_FINISH = 17,   // single rank, flag 65536: census + newborn uids of the generation whose block
-                        // stats are in temp (the finish half of OP_SOUP_GEN, on a side stream)
-  OP_UID_ASSIGN = 15,   // sharded soup: uids of the previous generation's newborns from the per-rank stats
-                        // (flag 16384: the same launch also indexes the received rows = OP_SOUP_UNPACK)
+  OP_UID_ASSIGN = 15,   // sharded all-gather soup: uids of the previous generation's newborns from stats
+  OP_SOUP_GEN = 16,     // fused single-rank generation: evolve + next decisions + census (+ finish)
+  OP_GEN_FINISH = 17,   // single rank: census + newborn uids of generations whose block stats are in temp
+  OP_SOUP_SEQ = 19,     // `steps` sequential (Gauss-Seidel, in-place, index-order) soup generations
+  OP_X2_PACK = 20,      // sharded all-to-all soup: finish of the previous generation + next decisions
+                        // (links, notices, requests) + the rows of this generation's exchange
+  OP_X2_POST = 21,      // after the all-to-all: uids of the previous generation's newborns, global
+                        // census, received notices linked for the next generation, requests kept
 };
 
-int srnn_abi_version();  // 14
+int srnn_abi_version();  // 15
 int srnn_has_config(const SrnnCfg* cfg);
 int srnn_run(int op, const SrnnCfg* cfg, const SrnnArgs* args);
 const char* srnn_last_error();
-int64_t srnn_scan_temp_bytes(int64_t n);
 int srnn_is_generic(const SrnnCfg* cfg, int op);
 void srnn_set_force_generic(int on);  // 1: this op of this config runs on the generic engine
 int64_t srnn_generic_scratch_bytes(const SrnnCfg* cfg, int64_t n, int64_t max_lanes);

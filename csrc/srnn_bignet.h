@@ -354,7 +354,7 @@ __global__ __launch_bounds__(TBB) void k_big(SrnnCfg c, SrnnArgs a) {
     } else if constexpr (OP == OP_RUN_FIXPOINT || OP == OP_CLASSIFY) {
       load_row<T>(L.w, a.W + p * T::PP, lane);
       __builtin_amdgcn_wave_barrier();
-      const bool with_sec = (a.flags & 8) != 0;
+      const bool with_sec = (a.flags & SRNN_F_FIX_SEC) != 0;
       int s = 0;
       float st[T::A];
       bool compressed = false;
@@ -472,7 +472,7 @@ __global__ __launch_bounds__(TBB) void k_big_fix1(SrnnCfg c, SrnnArgs a) {
   int8_t* flag = reinterpret_cast<int8_t*>(state + a.n * T::A);
   load_row<T>(L.w, a.W + p * T::PP, lane);
   __builtin_amdgcn_wave_barrier();
-  const bool with_sec = (a.flags & 8) != 0;
+  const bool with_sec = (a.flags & SRNN_F_FIX_SEC) != 0;
   bool stop = a.steps <= 0;
   float g[T::A], h[T::A];
   if (!stop && a.early_exit && !lds_finite<T>(L.w, lane)) stop = true;
@@ -533,7 +533,7 @@ __global__ __launch_bounds__(256) void k_big_fix2(SrnnCfg c, SrnnArgs a) {
         k = zero ? C_FIX_ZERO : C_FIX_OTHER;
       } else {
         k = C_OTHER;
-        if (a.flags & 8) {
+        if (a.flags & SRNN_F_FIX_SEC) {
           mlp_state_lane<T>(st, h1, h2);
           if (finite_all<T>(h2) && close_all<T>(h2, st, a.eps)) k = C_FIX_SEC;
         }
@@ -1007,7 +1007,7 @@ __global__ __launch_bounds__(TBROW) void k_big_fix1_row(SrnnCfg c, SrnnArgs a) {
   if (stop) {  // no step taken: the row is unchanged, classify the general weights
     flag[p] = 0;
     if (a.nsteps) a.nsteps[p] = 0;
-    if (a.cls) a.cls[p] = sclassify<T, StF32>(w, sm, a.eps, (a.flags & 8) != 0, c.aggregator);
+    if (a.cls) a.cls[p] = sclassify<T, StF32>(w, sm, a.eps, (a.flags & SRNN_F_FIX_SEC) != 0, c.aggregator);
   } else {
 #pragma unroll
     for (int i = 0; i < T::A; ++i) state[p * T::A + i] = h[i];
@@ -1025,7 +1025,7 @@ __global__ __launch_bounds__(TBROW) void k_big_row(SrnnCfg c, SrnnArgs a) {
     int8_t k = -1;
     if (p < a.n) {
       lrow_load<T>(a.W + p * T::PP, w);
-      k = lclassify<T>(w, a.eps, (a.flags & 8) != 0, c.aggregator);
+      k = lclassify<T>(w, a.eps, (a.flags & SRNN_F_FIX_SEC) != 0, c.aggregator);
       if (a.cls) a.cls[p] = k;
     }
     if (a.counts) {  // histogram: wave ballots -> LDS -> one atomic per (block, class)
@@ -1183,13 +1183,6 @@ struct BRow {
         g[c] = aggregator == 0 ? (float)(acc[c] / (double)(e - b)) : m[c];
       }
     }
-  }
-  // generation-start row of global slot g: this rank's table (W2) or the exchange buffers
-  // (flag 128: all-gathered [n_total] table; else the all-to-all rows indexed by rmap)
-  __device__ static const char* row_of(const SrnnArgs& a, int64_t g) {
-    if (a.world <= 1 || (g >= a.lo && g < a.lo + a.n)) return at(a.W2, g - a.lo);
-    if (a.flags & 128) return at(a.recvbuf, g);
-    return reinterpret_cast<const char*>(a.recvbuf) + (int64_t)a.rmap[g] * XB;
   }
   // glorot init of a particle straight into its (global) row: the draws and values of
   // glorot_fill / g_glorot, encoded to the storage format
@@ -1479,8 +1472,8 @@ __global__ __launch_bounds__(TBROW) void k_big_rows(SrnnCfg c, SrnnArgs a) {
     R::load_staged(a.W, valid ? (int32_t)p : -1, w, st);
     if (valid) {
       if constexpr (SHUF) cp.draw(rng, a.uid ? (uint64_t)a.uid[p] : (uint64_t)(a.lo + p), a.ctr);
-      if constexpr (SHUF) k = bclassify<T, S, SHUF>(w, a.eps, (a.flags & 8) != 0, c.aggregator, cp);
-      else k = sclassify<T, S>(w, RowSummary<T>(w), a.eps, (a.flags & 8) != 0, c.aggregator);
+      if constexpr (SHUF) k = bclassify<T, S, SHUF>(w, a.eps, (a.flags & SRNN_F_FIX_SEC) != 0, c.aggregator, cp);
+      else k = sclassify<T, S>(w, RowSummary<T>(w), a.eps, (a.flags & SRNN_F_FIX_SEC) != 0, c.aggregator);
       if (a.cls) a.cls[p] = k;
     }
     if (a.counts) {  // wave ballots -> LDS -> one atomic per (block, class)
@@ -1489,15 +1482,15 @@ __global__ __launch_bounds__(TBROW) void k_big_rows(SrnnCfg c, SrnnArgs a) {
         const unsigned long long m = __ballot(k == q);
         if ((threadIdx.x & 63) == 0 && m) atomicAdd(&s_cnt[q], (uint32_t)__popcll(m));
       }
-      if (a.flags & 64) {
+      if (a.flags & SRNN_F_COUNT_RESPAWNS) {
         const unsigned long long m = __ballot(valid && a.respawn[p] != 0);
         if ((threadIdx.x & 63) == 0 && m) atomicAdd(&s_cnt[5], (uint32_t)__popcll(m));
       }
       __syncthreads();
-      if (threadIdx.x < 6 && s_cnt[threadIdx.x] && (threadIdx.x < 5 || (a.flags & 64)))
+      if (threadIdx.x < 6 && s_cnt[threadIdx.x] && (threadIdx.x < 5 || (a.flags & SRNN_F_COUNT_RESPAWNS)))
         atomicAdd(a.counts + threadIdx.x, (uint64_t)s_cnt[threadIdx.x]);
     }
-    if ((a.flags & 512) && blockIdx.x == 0 && threadIdx.x == 0) {
+    if ((a.flags & SRNN_F_GEN_ADVANCE) && blockIdx.x == 0 && threadIdx.x == 0) {
       if (a.gen_out) a.gen_out[0] = a.gen_ptr[0] + 1;
       else ((int32_t*)a.gen_ptr)[0] = a.gen_ptr[0] + 1;
     }
@@ -1583,107 +1576,133 @@ __global__ __launch_bounds__(256) void k_big_lane_s(SrnnCfg c, SrnnArgs a) {
 // Synchronous soup generation of local row j (Item::soup_evolve / GItem::soup_evolve with
 // the row in VGPRs): attacks received in ascending attacker-slot order (generation-start
 // attacker rows), learn_from `severity` epochs on the teacher's aggregated generation-start
-// row, `epochs` self-train steps, respawn flags (+ inline re-init, flag 32), the 64-row
-// respawn ballot (or per-row flags, flag 16).  Only one 280-float row is live at a time:
-// the victim's aggregate is taken before the attacker's row is loaded into the same
-// registers (an attack rewrites every weight of the victim).
+// row, `epochs` self-train steps, respawn flags (+ inline re-init).  Only one 280-float row
+// is live at a time: the victim's aggregate is taken before the attacker's row is loaded
+// into the same registers (an attack rewrites every weight of the victim).  Returns the
+// respawn code; tk = the received row of a remote teacher (SRNN_F_X2).
 template <class T, class S, bool SHUF>
-__global__ __launch_bounds__(TBROW) void k_big_soup_evolve(SrnnCfg c, SrnnArgs a) {
+__device__ __forceinline__ int8_t big_soup_one(const SrnnCfg& c, const SrnnArgs& a, const ChunkPerm<T>& cp,
+                                               int64_t j, uint32_t tk) {
   using R = BRow<T, S>;
-  __shared__ uint32_t s_cw[SHUF ? ChunkPerm<T>::NW * TBROW : 1];
-  const ChunkPerm<T> cp{s_cw + threadIdx.x};
-  const int64_t j = (int64_t)blockIdx.x * TBROW + threadIdx.x;
   const Rng rng{(uint32_t)a.seed, (uint32_t)(a.seed >> 32)};
-  bool rs_any = false;
+  const int64_t g = a.lo + j;
+  const int32_t gen = a.gen_ptr ? a.gen_ptr[0] : a.gen;
+  const bool x2 = (a.flags & SRNN_F_X2) != 0;
   // the own row stays a per-lane load (the generation is SGD-bound: staging it through LDS
   // measured slower, profiles/r2j_staged_rows_finish_par.md)
-  if (j < a.n) {
-    const int64_t g = a.lo + j;
-    const int32_t gen = a.gen_ptr ? a.gen_ptr[0] : a.gen;
-    float w[T::P];
-    R::load(R::at(a.W2, j), w);
-    uint32_t ctr = (uint32_t)gen * 1024u;
-    const int32_t head = a.i32e[j];
-    a.i32e[j] = -1;  // list consumed: reset for the next generation's decide
-    int32_t last = -1;
-    while (head >= 0) {
-      int32_t best = INT_MAX;
-      for (int32_t r = head; r >= 0; r = a.i32f[r]) best = (r > last && r < best) ? r : best;
-      if (best == INT_MAX) break;
-      last = best;
-      float gv[T::A], h[T::A];
-      lrow_aggregate<T>(w, gv, c.aggregator);
-      R::load(R::row_of(a, best), w);
-      lmlp<T>(w, gv, h);
-      R::quant_a(h);
-      if constexpr (SHUF) cp.draw(rng, (uint64_t)g, ctr);
-      expand_out<T, SHUF>(w, h, cp);
-      ctr += 1;
-    }
-    int32_t my_at, te;
-    Item<Weightwise<1, 1>, StF32>::decision(a, g, gen, my_at, te);
-    int8_t act = A_NONE;
-    int64_t cpart = -1;
-    if (my_at >= 0) act = A_ATTACKING, cpart = my_at;
-    // learn_from (`severity` steps on the teacher's aggregate) then self-train (`epochs`
-    // steps on the own aggregate) as ONE step loop: a single inlined SGD step keeps the
-    // register allocation of the 280-float row to one copy
-    float gt[T::A];
-    int nlearn = 0;
-    if (te >= 0) {
-      R::stream_aggregate(R::row_of(a, te), gt, c.aggregator);
-      nlearn = a.severity > 0 ? a.severity : 0;
-      act = A_LEARN_FROM;
-      cpart = te;
-    }
-    if (a.epochs > 0) act = A_TRAIN_SELF, cpart = -1;
-    const int nsteps = nlearn + (a.epochs > 0 ? a.epochs : 0);
-    float loss = 0.f;
-    for (int s = 0; s < nsteps; ++s) {
-      float gs[T::A];
-      if (s < nlearn) {
-#pragma unroll
-        for (int q = 0; q < T::A; ++q) gs[q] = gt[q];
-      } else {
-        lrow_aggregate<T>(w, gs, c.aggregator);
-      }
-      loss = ltrain_step<T>(w, gs, a.lr);
-    }
-    R::quant(w);  // the stored state decides respawn
-    // any non-finite weight <=> NaN in sum(w * 0); all |w| <= eps <=> min / max within
-    // (fminf / fmaxf skip NaNs: a NaN row is never a zero row, as in the per-weight test)
-    // (8 independent partial chains: min / max / NaN propagation are order-free)
-    float nz[8], lo[8], hi[8];
-#pragma unroll
-    for (int q = 0; q < 8; ++q) nz[q] = 0.f, lo[q] = w[0], hi[q] = w[0];
-#pragma unroll
-    for (int k = 0; k < T::P; ++k) {
-      nz[k & 7] = fmaf(w[k], 0.f, nz[k & 7]);
-      lo[k & 7] = fminf(lo[k & 7], w[k]);
-      hi[k & 7] = fmaxf(hi[k & 7], w[k]);
-    }
-#pragma unroll
-    for (int q = 1; q < 8; ++q) nz[0] += nz[q], lo[0] = fminf(lo[0], lo[q]), hi[0] = fmaxf(hi[0], hi[q]);
-    const bool bad = !finitef(nz[0]);
-    const bool zero = !bad && (-a.eps <= lo[0]) && (hi[0] <= a.eps);
-    int8_t rsp = 0;
-    if ((a.flags & 2) && bad) rsp = 1;
-    else if ((a.flags & 4) && zero) rsp = 2;
-    if (rsp && (a.flags & 32)) R::init_row(R::at(a.W, j), rng, respawn_key(gen, g));  // newborn
-    else R::store(R::at(a.W, j), w);
-    if (a.action) a.action[j] = act;
-    if (a.counterpart) a.counterpart[j] = cpart;
-    if (a.loss) a.loss[j] = loss;
-    a.respawn[j] = rsp;
-    rs_any = rsp != 0;
+  float w[T::P];
+  R::load(R::at(a.W2, j), w);
+  uint32_t ctr = (uint32_t)gen * 1024u;
+  for_each_attacker<false>(a, j, [&](uint32_t e, int64_t slot) {
+    float gv[T::A], h[T::A];
+    lrow_aggregate<T>(w, gv, c.aggregator);
+    const char* r = ent_row(a, e, R::RB);
+    if (x2 && (int64_t)e >= a.n) x2_check(a, r, R::RB, slot, gen);
+    R::load(r, w);
+    lmlp<T>(w, gv, h);
+    R::quant_a(h);
+    if constexpr (SHUF) cp.draw(rng, (uint64_t)g, ctr);
+    expand_out<T, SHUF>(w, h, cp);
+    ctr += 1;
+  });
+  int64_t my_at, te;
+  Item<Weightwise<1, 1>, StF32>::decision(a, g, gen, my_at, te);
+  int8_t act = A_NONE;
+  int64_t cpart = -1;
+  if (my_at >= 0) act = A_ATTACKING, cpart = my_at;
+  // learn_from (`severity` steps on the teacher's aggregate) then self-train (`epochs`
+  // steps on the own aggregate) as ONE step loop: a single inlined SGD step keeps the
+  // register allocation of the 280-float row to one copy
+  float gt[T::A];
+  int nlearn = 0;
+  if (te >= 0) {
+    const char* r = teacher_row(a, te, tk, R::RB);
+    if (x2 && tk != SRNN_NIL) x2_check(a, r, R::RB, te, gen);
+    R::stream_aggregate(r, gt, c.aggregator);
+    nlearn = a.severity > 0 ? a.severity : 0;
+    act = A_LEARN_FROM;
+    cpart = te;
   }
-  if (a.i32c) {
-    if (a.flags & 16) {
-      if (j < a.n) a.i32c[j] = rs_any ? 1 : 0;
+  if (a.epochs > 0) act = A_TRAIN_SELF, cpart = -1;
+  const int nsteps = nlearn + (a.epochs > 0 ? a.epochs : 0);
+  float loss = 0.f;
+  for (int s = 0; s < nsteps; ++s) {
+    float gs[T::A];
+    if (s < nlearn) {
+#pragma unroll
+      for (int q = 0; q < T::A; ++q) gs[q] = gt[q];
     } else {
-      const unsigned long long m = __ballot(rs_any);
-      if ((threadIdx.x & 63) == 0) reinterpret_cast<unsigned long long*>(a.i32c)[j >> 6] = m;
+      lrow_aggregate<T>(w, gs, c.aggregator);
     }
+    loss = ltrain_step<T>(w, gs, a.lr);
+  }
+  R::quant(w);  // the stored state decides respawn
+  // any non-finite weight <=> NaN in sum(w * 0); all |w| <= eps <=> min / max within
+  // (fminf / fmaxf skip NaNs: a NaN row is never a zero row, as in the per-weight test)
+  // (8 independent partial chains: min / max / NaN propagation are order-free)
+  float nz[8], lo[8], hi[8];
+#pragma unroll
+  for (int q = 0; q < 8; ++q) nz[q] = 0.f, lo[q] = w[0], hi[q] = w[0];
+#pragma unroll
+  for (int k = 0; k < T::P; ++k) {
+    nz[k & 7] = fmaf(w[k], 0.f, nz[k & 7]);
+    lo[k & 7] = fminf(lo[k & 7], w[k]);
+    hi[k & 7] = fmaxf(hi[k & 7], w[k]);
+  }
+#pragma unroll
+  for (int q = 1; q < 8; ++q) nz[0] += nz[q], lo[0] = fminf(lo[0], lo[q]), hi[0] = fmaxf(hi[0], hi[q]);
+  const bool bad = !finitef(nz[0]);
+  const bool zero = !bad && (-a.eps <= lo[0]) && (hi[0] <= a.eps);
+  int8_t rsp = 0;
+  if ((a.flags & SRNN_F_REMOVE_DIVERGENT) && bad) rsp = 1;
+  else if ((a.flags & SRNN_F_REMOVE_ZERO) && zero) rsp = 2;
+  if (rsp && (a.flags & SRNN_F_RESPAWN_INLINE)) R::init_row(R::at(a.W, j), rng, respawn_key(gen, g));  // newborn
+  else R::store(R::at(a.W, j), w);
+  if (a.action) a.action[j] = act;
+  if (a.counterpart) a.counterpart[j] = cpart;
+  if (a.loss) a.loss[j] = loss;
+  if (a.respawn) a.respawn[j] = rsp;
+  return rsp;
+}
+
+// OP_SOUP_EVOLVE of big nets: rows of this workgroup (single rank / all-gather: 64-row
+// ballots or per-row flags; SRNN_F_X2 local: minus the remote-dependent rows, block stats
+// by atomics) or, with SRNN_F_X2_REMOTE, the remote-dependent list (grid-stride)
+template <class T, class S, bool SHUF>
+__global__ __launch_bounds__(TBROW) void k_big_soup_evolve(SrnnCfg c, SrnnArgs a) {
+  __shared__ uint32_t s_cw[SHUF ? ChunkPerm<T>::NW * TBROW : 1];
+  const ChunkPerm<T> cp{s_cw + threadIdx.x};
+  const bool x2 = (a.flags & SRNN_F_X2) != 0;
+  unsigned long long* bs = reinterpret_cast<unsigned long long*>(a.temp);
+  if (x2 && (a.flags & SRNN_F_X2_REMOTE)) {
+    const int64_t cnt = *(volatile const int32_t*)a.x_rcount;
+    for (int64_t q = (int64_t)blockIdx.x * TBROW + threadIdx.x; q - threadIdx.x < cnt;
+         q += (int64_t)gridDim.x * TBROW) {
+      if (q < cnt) {
+        const int64_t j = a.x_rlist[2 * q];
+        const bool rs = big_soup_one<T, S, SHUF>(c, a, cp, j, a.x_rlist[2 * q + 1]) != 0;
+        bs_publish_lane(bs, j, rs, -1);
+      }
+    }
+    __syncthreads();
+    if (threadIdx.x == 0 && atomicAdd(a.x_ctl + 3, 1) == (int32_t)gridDim.x - 1) {
+      *a.x_rcount = 0;
+      a.x_ctl[3] = 0;
+    }
+    return;
+  }
+  const int64_t j = (int64_t)blockIdx.x * TBROW + threadIdx.x;
+  bool rs = false;
+  if (j < a.n && !(x2 && x2_dep(a, j))) rs = big_soup_one<T, S, SHUF>(c, a, cp, j, SRNN_NIL) != 0;
+  if (x2) {
+    const int64_t wd = (j >> 6) * 2 + (threadIdx.x & 63);
+    if ((threadIdx.x & 63) < 2 && wd * 32 < a.n) a.x_dep[wd] = 0u;
+    bs_publish_wave(bs, j >> 6, rs, -1);
+  } else if (a.flags & SRNN_F_ROW_FLAGS) {
+    if (j < a.n && a.rowflags) a.rowflags[j] = rs ? 1 : 0;
+  } else if (a.ballots) {
+    const unsigned long long m = __ballot(rs);
+    if ((threadIdx.x & 63) == 0) a.ballots[j >> 6] = m;
   }
 }
 
@@ -1694,7 +1713,7 @@ template <class T, class S>
 __global__ __launch_bounds__(TBR) void k_big_respawn_seq(SrnnCfg c, SrnnArgs a) {
   using R = BRow<T, S>;
   __shared__ int32_t s_wave[TBR / 64];
-  const unsigned long long* masks = reinterpret_cast<const unsigned long long*>(a.i32c);
+  const unsigned long long* masks = a.ballots;
   const int64_t nb = (a.n + 63) / 64;
   const int64_t ch = (nb + TBR - 1) / TBR;
   const int64_t b0 = (int64_t)threadIdx.x * ch;
@@ -1714,12 +1733,12 @@ __global__ __launch_bounds__(TBR) void k_big_respawn_seq(SrnnCfg c, SrnnArgs a) 
       m &= m - 1;
       const int64_t r = b * 64 + bit;
       a.uid_out[r] = k++;
-      if (!(a.flags & 32)) R::init_row(R::at(a.W, r), rng, respawn_key(gen, a.lo + r));  // else done inline
+      if (!(a.flags & SRNN_F_RESPAWN_INLINE)) R::init_row(R::at(a.W, r), rng, respawn_key(gen, a.lo + r));  // else inline
     }
   }
   __syncthreads();
   if (threadIdx.x == 0) {
-    ((int64_t*)a.uid_base)[0] = base + total;
+    a.uid_base[0] = base + total;
     if (a.gen_out) a.gen_out[0] = gen + 1;
     else if (a.gen_ptr) ((int32_t*)a.gen_ptr)[0] = gen + 1;
   }
@@ -1741,9 +1760,13 @@ int big_run_s(int op, const SrnnCfg& c, const SrnnArgs& a) {
       break;
     case OP_TRAIN: hipLaunchKernelGGL((k_big_rows<T, S, SHUF, OP_TRAIN>), dim3(g64), dim3(TBROW), 0, st, c, a); break;
     case OP_LEARN: hipLaunchKernelGGL((k_big_rows<T, S, SHUF, OP_LEARN>), dim3(g64), dim3(TBROW), 0, st, c, a); break;
-    case OP_SOUP_EVOLVE:
-      hipLaunchKernelGGL((k_big_soup_evolve<T, S, SHUF>), dim3(g64), dim3(TBROW), 0, st, c, a);
+    case OP_SOUP_EVOLVE: {
+      unsigned g = g64;
+      if ((a.flags & SRNN_F_X2) && (a.flags & SRNN_F_X2_REMOTE))  // bounded grid over the remote list
+        g = g < (unsigned)(X2_REMOTE_WAVES / 4) ? g : (unsigned)(X2_REMOTE_WAVES / 4);
+      hipLaunchKernelGGL((k_big_soup_evolve<T, S, SHUF>), dim3(g), dim3(TBROW), 0, st, c, a);
       break;
+    }
     case OP_RESPAWN_SEQ: hipLaunchKernelGGL((k_big_respawn_seq<T, S>), dim3(1), dim3(TBR), 0, st, c, a); break;
     case OP_SOUP_DECIDE: {
       // decisions are shape independent: every global slot

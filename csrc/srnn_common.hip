@@ -1,6 +1,5 @@
 // srnn_common.hip — ABI entry points, error handling and device scans of libsrnn.so.
 #include "srnn_kernels.h"
-#include <hipcub/hipcub.hpp>
 #include <cstring>
 #include <cstdlib>
 #include <string>
@@ -20,6 +19,7 @@ extern "C" int srnn_aggbig_serves(int op, int dtype, int shuffler);
 extern "C" int srnn_dispatch_lowp(int op, const SrnnCfg* c, const SrnnArgs* a);
 
 extern "C" int srnn_dispatch_generic(int op, const SrnnCfg* c, const SrnnArgs* a);
+extern "C" int srnn_x2_run(int op, const SrnnCfg* c, const SrnnArgs* a);
 
 // ---- tracing / checking hooks, read once from the environment:
 //   SRNN_ROCTX=1       one roctx range per operator launch (rocprofv3 --marker-trace),
@@ -57,12 +57,27 @@ const Hooks& hooks() {
   return h;
 }
 const char* op_name(int op) {
-  static const char* names[] = {"srnn:init",       "srnn:apply",        "srnn:run_fixpoint", "srnn:train",
-                                "srnn:learn",      "srnn:classify",     "srnn:perturb",      "srnn:soup_decide",
-                                "srnn:respawn_seq", "srnn:soup_evolve", "srnn:scan",         "srnn:respawn",
-                                "srnn:vary_run",   "srnn:soup_pack",    "srnn:soup_unpack",  "srnn:uid_assign",
-                                "srnn:soup_gen",   "srnn:gen_finish",   "srnn:soup_perms"};
-  return (op >= 0 && op < (int)(sizeof(names) / sizeof(names[0]))) ? names[op] : "srnn:op";
+  switch (op) {
+    case OP_INIT: return "srnn:init";
+    case OP_APPLY: return "srnn:apply";
+    case OP_RUN_FIXPOINT: return "srnn:run_fixpoint";
+    case OP_TRAIN: return "srnn:train";
+    case OP_LEARN: return "srnn:learn";
+    case OP_CLASSIFY: return "srnn:classify";
+    case OP_PERTURB: return "srnn:perturb";
+    case OP_SOUP_DECIDE: return "srnn:soup_decide";
+    case OP_RESPAWN_SEQ: return "srnn:respawn_seq";
+    case OP_SOUP_EVOLVE: return "srnn:soup_evolve";
+    case OP_RESPAWN: return "srnn:respawn";
+    case OP_VARY_RUN: return "srnn:vary_run";
+    case OP_UID_ASSIGN: return "srnn:uid_assign";
+    case OP_SOUP_GEN: return "srnn:soup_gen";
+    case OP_GEN_FINISH: return "srnn:gen_finish";
+    case OP_SOUP_SEQ: return "srnn:soup_seq";
+    case OP_X2_PACK: return "srnn:x2_pack";
+    case OP_X2_POST: return "srnn:x2_post";
+    default: return "srnn:op";
+  }
 }
 }  // namespace
 
@@ -143,8 +158,7 @@ static void* g_scratch[64] = {nullptr};
 static int64_t g_scratch_bytes[64] = {0};
 
 static int with_scratch(int op, const SrnnCfg* c, const SrnnArgs* a) {
-  if (!a->dev || a->scratch || route(op, c, a) != 1 || op == OP_SOUP_DECIDE || op == OP_SOUP_PACK ||
-      op == OP_SOUP_UNPACK || op == OP_UID_ASSIGN)
+  if (!a->dev || a->scratch || route(op, c, a) != 1 || op == OP_SOUP_DECIDE)
     return dispatch(op, c, a);
   const int64_t want = srnn_generic_scratch_bytes(c, a->n, 65536);
   int dev = 0;
@@ -177,7 +191,7 @@ static int with_scratch(int op, const SrnnCfg* c, const SrnnArgs* a) {
 
 extern "C" {
 
-int srnn_abi_version() { return 14; }
+int srnn_abi_version() { return 15; }
 
 const char* srnn_last_error() { return srnn::g_err.c_str(); }
 
@@ -195,44 +209,16 @@ int srnn_is_generic(const SrnnCfg* cfg, int op) {
   return route(op, cfg, &probe) == 1 ? 1 : 0;
 }
 
-int64_t srnn_scan_temp_bytes(int64_t n) {
-  size_t bytes = 0;
-  (void)hipcub::DeviceScan::InclusiveSum(nullptr, bytes, (const int32_t*)nullptr, (int32_t*)nullptr, (int)n);
-  return (int64_t)bytes;
-}
-
 int srnn_run(int op, const SrnnCfg* cfg, const SrnnArgs* a) {
   srnn::set_error("");
-  if (op == OP_SCAN) {
-    // i32d[0] = 0, i32d[k+1] = sum_{q<=k} i32c[q]
-    if (!a->dev) {
-      int64_t acc = 0;
-      a->i32d[0] = 0;
-      for (int64_t k = 0; k < a->n; ++k) {
-        acc += a->i32c[k];
-        a->i32d[k + 1] = (int32_t)acc;
-      }
-      return 0;
-    }
-    hipStream_t st = (hipStream_t)a->stream;
-    if (a->n > 0) {
-      size_t bytes = (size_t)a->temp_bytes;
-      hipError_t e = hipcub::DeviceScan::InclusiveSum(a->temp, bytes, a->i32c, a->i32d + 1, (int)a->n, st);
-      if (e != hipSuccess) {
-        srnn::set_error(hipGetErrorString(e));
-        return -3;
-      }
-    }
-    // i32d[0] = 0 (the inclusive scan went to i32d + 1)
-    hipError_t e = hipMemsetAsync(a->i32d, 0, sizeof(int32_t), st);
-    if (e == hipSuccess) e = hipGetLastError();
-    if (e != hipSuccess) {
-      srnn::set_error(hipGetErrorString(e));
-      return -3;
-    }
-    return 0;
-  }
   const Hooks& h = hooks();
+  if (op == OP_X2_PACK || op == OP_X2_POST || op == OP_UID_ASSIGN) {
+    // the exchange protocol is shape independent (srnn_shard.hip)
+    if (h.push) h.push(op_name(op));
+    const int r = srnn_x2_run(op, cfg, a);
+    if (h.pop) h.pop();
+    return r;
+  }
   if (h.push) h.push(op_name(op));
   int r = with_scratch(op, cfg, a);
   if (r == 1) srnn::set_error("not a valid network shape for libsrnn");

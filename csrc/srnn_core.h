@@ -55,6 +55,7 @@ enum Purpose : uint32_t {
   P_AGGSHUF = 4,     // aggregating shuffle_random   ctr=(uid, op_ctr)
   P_SOUP = 5,        // soup decisions               ctr=(slot, generation)
   P_PERTURB = 6,     // known-fixpoint variation     ctr=(uid, op_ctr)
+  P_SOUP_WIDE = 7,   // soup partners of populations > 2^32 slots (64-bit draws) ctr=(slot, generation)
 };
 
 struct Rng {

@@ -595,8 +595,6 @@ struct GItem {
   SRNN_HD static const char* rowp(const GShape& s, const float* b, int64_t i) {
     return reinterpret_cast<const char*>(b) + i * g_rb(s);
   }
-  SRNN_HD static int64_t xb(const GShape& s) { return g_rb(s) + 16; }
-  SRNN_HD static int64_t sr(const GShape& s) { return (48 + xb(s) - 1) / xb(s); }
   SRNN_HD static ApplyCtx actx(const SrnnArgs& a, const GShape& s, uint64_t uid, uint32_t ctr) {
     ApplyCtx x;
     x.rng = rng(a);
@@ -615,18 +613,11 @@ struct GItem {
     tc.ctr = ctr;
     tc.samp = nullptr;
     tc.perm = nullptr;
-    tc.shuffle = (a.flags & 1) != 0;
+    tc.shuffle = (a.flags & SRNN_F_SHUFFLE) != 0;
     tc.stride = 1;
     tc.aggregator = s.aggregator;
     return tc;
   }
-  // generation-start row of global slot g (local table, or the exchange buffers)
-  SRNN_HD static const char* row_of(const GShape& s, const SrnnArgs& a, int64_t g) {
-    if (a.world <= 1 || (g >= a.lo && g < a.lo + a.n)) return rowp(s, a.W2, g - a.lo);
-    if (a.flags & 128) return rowp(s, a.recvbuf, g);
-    return reinterpret_cast<const char*>(a.recvbuf) + (int64_t)a.rmap[g] * xb(s);
-  }
-
   SRNN_HD static void init(const GCtx& x, const SrnnArgs& a, int64_t i) {
     SV w = x.v(x.s->o_w);
     g_init(x, w, rng(a), uid_of(a, i));
@@ -666,7 +657,7 @@ struct GItem {
     }
     g_store(s, rowp(s, a.W, i), w);
     if (a.nsteps) a.nsteps[i] = st;
-    if (a.cls) a.cls[i] = g_classify_w(x, w, a.eps, (a.flags & 8) != 0, ac);
+    if (a.cls) a.cls[i] = g_classify_w(x, w, a.eps, (a.flags & SRNN_F_FIX_SEC) != 0, ac);
   }
   SRNN_HD static void vary_run(const GCtx& x, const SrnnArgs& a, int64_t i) {
     const GShape& s = *x.s;
@@ -722,76 +713,35 @@ struct GItem {
     const GShape& s = *x.s;
     SV w = x.v(s.o_w);
     g_load(s, rowp(s, a.W, i), w);
-    const int8_t k = g_classify_w(x, w, a.eps, (a.flags & 8) != 0, actx(a, s, uid_of(a, i), a.ctr));
+    const int8_t k = g_classify_w(x, w, a.eps, (a.flags & SRNN_F_FIX_SEC) != 0, actx(a, s, uid_of(a, i), a.ctr));
     if (a.cls) a.cls[i] = k;
     return k;
   }
 
-  // ---------------------------------------------------------------- soup (sharded-safe)
-  SRNN_HD static void soup_pack(const GShape& s, const SrnnArgs& a, int64_t j) {
-    int32_t m = a.need[j];
-    if (!m) return;
-    a.need[j] = 0;
-    const int32_t gen = a.gen_ptr ? a.gen_ptr[0] : a.gen;
-    const char* src = rowp(s, a.W2, j);
-    const int64_t RB = g_rb(s), XB = xb(s);
-    while (m) {
-      const int r = __builtin_ctz((unsigned)m);
-      m &= m - 1;
-      const int32_t pos = atomic_add_i32(a.sendcnt + r, 1);
-      if (pos >= a.cap) {
-        atomic_or_i32(a.ovf, 1);
-        continue;
-      }
-      char* dst = reinterpret_cast<char*>(a.sendbuf) + ((int64_t)r * a.cap + pos) * XB;
-      const uint2* s2 = reinterpret_cast<const uint2*>(src);
-      uint2* d2 = reinterpret_cast<uint2*>(dst);
-      for (int64_t q = 0; q < RB / 8; ++q) d2[q] = s2[q];
-      d2[RB / 8] = make_uint2((uint32_t)(a.lo + j), (uint32_t)gen);
-      d2[RB / 8 + 1] = make_uint2(0u, 0u);
-    }
-  }
-  SRNN_HD static void pack_stats(const GShape& s, const SrnnArgs& a) {
-    for (int r = 0; r < a.world; ++r) {
-      int64_t* d = reinterpret_cast<int64_t*>(reinterpret_cast<char*>(a.sendbuf) + (int64_t)r * a.cap * xb(s));
-      for (int q = 0; q < 6; ++q) d[q] = (int64_t)a.counts[q];
-    }
-  }
-  SRNN_HD static void soup_unpack(const GShape& s, const SrnnArgs& a, int64_t k) {
-    if (k % a.cap < sr(s)) return;
-    const int32_t* tag = reinterpret_cast<const int32_t*>(reinterpret_cast<const char*>(a.recvbuf) + k * xb(s) + g_rb(s));
-    if (tag[1] == (a.gen_ptr ? a.gen_ptr[0] : a.gen)) a.rmap[tag[0]] = (int32_t)k;
-  }
-  SRNN_HD static int64_t stat(const GShape& s, const SrnnArgs& a, int r, int q) {
-    if (a.flags & 256)
-      return reinterpret_cast<const int64_t*>(reinterpret_cast<const char*>(a.recvbuf) + (int64_t)r * a.cap * xb(s))[q];
-    return a.stats[r * 6 + q];
-  }
-
-  // synchronous generation of local row j (Item::soup_evolve)
-  SRNN_HD static void soup_evolve(const GCtx& x, const SrnnArgs& a, int64_t j) {
+  // ---------------------------------------------------------------- soup
+  // synchronous generation of local row j (Item::soup_evolve): attacks received in
+  // ascending attacker-slot order, learn_from, self-train, respawn; tk: the received row of
+  // a remote teacher (SRNN_F_X2).  Returns the respawn code.
+  SRNN_HD static int8_t soup_evolve(const GCtx& x, const SrnnArgs& a, int64_t j, uint32_t tk = SRNN_NIL) {
     const GShape& s = *x.s;
     const int64_t g = a.lo + j;
+    const int64_t rb = g_rb(s);
     SV w = x.v(s.o_w), f = x.v(s.o_t), o = x.v(s.o_o);
     g_load(s, rowp(s, a.W2, j), w);
     const uint64_t uid = (uint64_t)g;  // stream key of this slot (Item::soup_evolve)
     const int32_t gen = a.gen_ptr ? a.gen_ptr[0] : a.gen;
+    const bool x2 = (a.flags & SRNN_F_X2) != 0;
     ApplyCtx ac = actx(a, s, uid, (uint32_t)gen * 1024u);
-    const int32_t head = a.i32e[j];
-    a.i32e[j] = -1;
-    int32_t last = -1;
-    while (head >= 0) {
-      int32_t best = INT_MAX;
-      for (int32_t r = head; r >= 0; r = a.i32f[r]) best = (r > last && r < best) ? r : best;
-      if (best == INT_MAX) break;
-      last = best;
-      g_load(s, row_of(s, a, best), f);
+    for_each_attacker<false>(a, j, [&](uint32_t e, int64_t slot) {
+      const char* r = ent_row(a, e, rb);
+      if (x2 && (int64_t)e >= a.n) x2_check(a, r, rb, slot, gen);
+      g_load(s, r, f);
       g_apply(x, f, w, o, ac);
       g_quant(s, o);
       ac.ctr += 1;
       g_copy(s, w, o);
-    }
-    int32_t my_at, te;
+    });
+    int64_t my_at, te;
     Item<Weightwise<1, 1>, StF32>::decision(a, g, gen, my_at, te);
     int8_t act = A_NONE;
     int64_t cp = -1;
@@ -799,7 +749,9 @@ struct GItem {
     TrainCtx tc = tctx(a, s, uid, (uint32_t)gen * 1024u + 512u);
     float loss = 0.f;
     if (te >= 0) {
-      g_load(s, row_of(s, a, te), f);
+      const char* r = teacher_row(a, te, tk, rb);
+      if (x2 && tk != SRNN_NIL) x2_check(a, r, rb, te, gen);
+      g_load(s, r, f);
       if (a.severity > 0) loss = g_train_epochs(x, w, f, a.severity, false, tc);
       act = A_LEARN_FROM;
       cp = te;
@@ -811,14 +763,65 @@ struct GItem {
     }
     g_quant(s, w);
     int8_t rs = 0;
-    if ((a.flags & 2) && g_diverged(s, w)) rs = 1;
-    else if ((a.flags & 4) && g_zero(s, w, a.eps)) rs = 2;
-    if (rs && (a.flags & 32)) g_init(x, w, rng(a), respawn_key(gen, g));
+    if ((a.flags & SRNN_F_REMOVE_DIVERGENT) && g_diverged(s, w)) rs = 1;
+    else if ((a.flags & SRNN_F_REMOVE_ZERO) && g_zero(s, w, a.eps)) rs = 2;
+    if (rs && (a.flags & SRNN_F_RESPAWN_INLINE)) g_init(x, w, rng(a), respawn_key(gen, g));
     g_store(s, rowp(s, a.W, j), w);
     if (a.action) a.action[j] = act;
     if (a.counterpart) a.counterpart[j] = cp;
     if (a.loss) a.loss[j] = loss;
-    a.respawn[j] = rs;
+    if (a.respawn) a.respawn[j] = rs;
+    return rs;
+  }
+  // census class of the stored row j (the fused census key: slot, counter 0x7FFFFFF0)
+  SRNN_HD static int8_t census_class(const GCtx& x, const SrnnArgs& a, int64_t j) {
+    const GShape& s = *x.s;
+    SV w = x.v(s.o_w);
+    g_load(s, rowp(s, a.W, j), w);
+    return g_classify_w(x, w, a.eps, (a.flags & SRNN_F_FIX_SEC) != 0, actx(a, s, (uint64_t)(a.lo + j), 0x7FFFFFF0u));
+  }
+  // sequential (Gauss-Seidel) step of particle j in generation gen (Item::soup_seq_one)
+  SRNN_HD static void soup_seq_one(const GCtx& x, const SrnnArgs& a, int64_t j, int32_t gen) {
+    const GShape& s = *x.s;
+    SV w = x.v(s.o_w), f = x.v(s.o_t), o = x.v(s.o_o);
+    int64_t at, te;
+    Item<Weightwise<1, 1>, StF32>::decision(a, j, gen, at, te);
+    int8_t act = A_NONE;
+    int64_t cp = -1;
+    if (at >= 0) {  // the victim's weights become f_j(victim)
+      g_load(s, rowp(s, a.W, j), w);
+      g_load(s, rowp(s, a.W, at), f);
+      g_apply(x, w, f, o, actx(a, s, (uint64_t)j, (uint32_t)gen * 1024u + 1u));
+      g_quant(s, o);
+      g_store(s, rowp(s, a.W, at), o);
+      act = A_ATTACKING;
+      cp = at;
+    }
+    g_load(s, rowp(s, a.W, j), w);
+    TrainCtx tc = tctx(a, s, (uint64_t)j, (uint32_t)gen * 1024u + 512u);
+    float loss = 0.f;
+    if (te >= 0) {
+      g_load(s, rowp(s, a.W, te), f);
+      if (a.severity > 0) loss = g_train_epochs(x, w, f, a.severity, false, tc);
+      act = A_LEARN_FROM;
+      cp = te;
+    }
+    if (a.epochs > 0) {
+      loss = g_train_epochs(x, w, f, a.epochs, true, tc);
+      act = A_TRAIN_SELF;
+      cp = -1;
+    }
+    g_quant(s, w);
+    int8_t rs = 0;
+    if ((a.flags & SRNN_F_REMOVE_DIVERGENT) && g_diverged(s, w)) rs = 1;
+    else if ((a.flags & SRNN_F_REMOVE_ZERO) && g_zero(s, w, a.eps)) rs = 2;
+    if (a.W2) g_store(s, rowp(s, a.W2, j), w);  // recording: the state before any respawn
+    if (rs) g_init(x, w, rng(a), respawn_key(gen, j));
+    g_store(s, rowp(s, a.W, j), w);
+    if (a.action) a.action[j] = act;
+    if (a.counterpart) a.counterpart[j] = (a.W2 && cp >= 0) ? a.uid_out[cp] : cp;
+    if (a.loss) a.loss[j] = loss;
+    if (a.respawn) a.respawn[j] = rs;
   }
   SRNN_HD static void respawn(const GCtx& x, const SrnnArgs& a, int64_t j) {
     if (a.respawn[j] == 0) return;
@@ -832,7 +835,7 @@ struct GItem {
 // ==================================================================================
 // Device kernels (grid-stride, lane per row; scratch element-major over all lanes)
 // ==================================================================================
-constexpr int GOP_CLASSIFY_COUNT = 100, GOP_EVOLVE = 101;
+constexpr int GOP_CLASSIFY_COUNT = 100, GOP_EVOLVE = 101, GOP_X2_REMOTE = 102;
 
 template <int OP>
 __global__ __launch_bounds__(GTB) void k_generic(GShape s, SrnnArgs a, int64_t lanes) {
@@ -843,7 +846,7 @@ __global__ __launch_bounds__(GTB) void k_generic(GShape s, SrnnArgs a, int64_t l
   const int64_t lane_id = (int64_t)blockIdx.x * GTB + threadIdx.x;
   GCtx x{&s, reinterpret_cast<float*>(a.scratch) + lane_id, lanes, s_coords, g_orth(s, a.scratch, lanes, lane_id)};
   const int64_t stride = (int64_t)gridDim.x * GTB;
-  const int64_t items = a.n;
+  const int64_t items = OP == GOP_X2_REMOTE ? (int64_t)*(volatile const int32_t*)a.x_rcount : a.n;
   for (int64_t base = (int64_t)blockIdx.x * GTB; base < items; base += stride) {
     const int64_t i = base + threadIdx.x;
     const bool on = i < items;
@@ -869,48 +872,59 @@ __global__ __launch_bounds__(GTB) void k_generic(GShape s, SrnnArgs a, int64_t l
           const unsigned long long m = __ballot(k == q);
           if (threadIdx.x == 0 && m) s_cnt[q] += (uint32_t)__popcll(m);
         }
-        if (a.flags & 64) {
+        if (a.flags & SRNN_F_COUNT_RESPAWNS) {
           const unsigned long long m = __ballot(on && a.respawn[i] != 0);
           if (threadIdx.x == 0) s_cnt[5] += (uint32_t)__popcll(m);
         }
       }
     } else if constexpr (OP == GOP_EVOLVE) {
+      // single rank / all-gather: 64-row ballots (or per-row flags); X2 local: the rows that
+      // need no remote row (x_dep), block stats by atomics (srnn_kernels.h bs_publish_*)
+      const bool x2 = (a.flags & SRNN_F_X2) != 0;
+      const bool act = on && !(x2 && x2_dep(a, i));
       bool rs = false;
-      if (on) {
-        GItem::soup_evolve(x, a, i);
-        rs = a.respawn[i] != 0;
+      int8_t k = -1;
+      if (act) {
+        rs = GItem::soup_evolve(x, a, i) != 0;
+        if (x2 && (a.flags & SRNN_F_FUSED_CENSUS)) k = GItem::census_class(x, a, i);
       }
-      if (a.i32c) {
-        if (a.flags & 16) {
-          if (on) a.i32c[i] = rs ? 1 : 0;
-        } else {
-          const unsigned long long m = __ballot(rs);  // the 64 rows of this block: one ballot word
-          if (threadIdx.x == 0) reinterpret_cast<unsigned long long*>(a.i32c)[base / GTB] = m;
-        }
+      if (x2) {
+        const int64_t wd = (base / GTB) * 2 + threadIdx.x;
+        if (threadIdx.x < 2 && wd * 32 < a.n) a.x_dep[wd] = 0u;
+        bs_publish_wave(reinterpret_cast<unsigned long long*>(a.temp), base / GTB, rs, k);
+      } else if (a.flags & SRNN_F_ROW_FLAGS) {
+        if (on && a.rowflags) a.rowflags[i] = rs ? 1 : 0;
+      } else if (a.ballots) {
+        const unsigned long long m = __ballot(rs);  // the 64 rows of this block: one ballot word
+        if (threadIdx.x == 0) a.ballots[base / GTB] = m;
+      }
+    } else if constexpr (OP == GOP_X2_REMOTE) {
+      // items = the remote-dependent list (x_rlist, length x_rcount on the device)
+      if (on) {
+        const int64_t j = a.x_rlist[2 * i];
+        const bool rs = GItem::soup_evolve(x, a, j, a.x_rlist[2 * i + 1]) != 0;
+        const int8_t k = (a.flags & SRNN_F_FUSED_CENSUS) ? GItem::census_class(x, a, j) : (int8_t)-1;
+        bs_publish_lane(reinterpret_cast<unsigned long long*>(a.temp), j, rs, k);
       }
     }
   }
+  if constexpr (OP == GOP_X2_REMOTE) {
+    int32_t prev = 0;
+    if (threadIdx.x == 0) prev = atomicAdd(a.x_ctl + 3, 1);
+    prev = __shfl(prev, 0);
+    if (prev == (int32_t)gridDim.x - 1 && threadIdx.x == 0) {
+      *a.x_rcount = 0;
+      a.x_ctl[3] = 0;
+    }
+  }
   if constexpr (OP == GOP_CLASSIFY_COUNT) {
-    if (threadIdx.x < 6 && s_cnt[threadIdx.x] && (threadIdx.x < 5 || (a.flags & 64)))
+    if (threadIdx.x < 6 && s_cnt[threadIdx.x] && (threadIdx.x < 5 || (a.flags & SRNN_F_COUNT_RESPAWNS)))
       atomicAdd(a.counts + threadIdx.x, (uint64_t)s_cnt[threadIdx.x]);
-    if ((a.flags & 512) && blockIdx.x == 0 && threadIdx.x == 0) {
+    if ((a.flags & SRNN_F_GEN_ADVANCE) && blockIdx.x == 0 && threadIdx.x == 0) {
       if (a.gen_out) a.gen_out[0] = a.gen_ptr[0] + 1;
       else ((int32_t*)a.gen_ptr)[0] = a.gen_ptr[0] + 1;
     }
   }
-}
-
-// sharded-soup byte movers with the runtime row size
-__global__ __launch_bounds__(256) void k_g_pack(GShape s, SrnnArgs a) {
-  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (i == 0) GItem::pack_stats(s, a);
-  if (i < a.n) GItem::soup_pack(s, a, i);
-}
-__global__ __launch_bounds__(256) void k_g_unpack(GShape s, SrnnArgs a) {
-  const int64_t k = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (k == 0)
-    for (int r = 0; r < a.world; ++r) a.sendcnt[r] = (int32_t)GItem::sr(s);
-  if (k < (int64_t)a.world * a.cap) GItem::soup_unpack(s, a, k);
 }
 
 // Single-rank respawn (k_respawn_seq with runtime shapes): one workgroup scans the 64-row
@@ -919,7 +933,7 @@ __global__ __launch_bounds__(256) void k_g_unpack(GShape s, SrnnArgs a) {
 constexpr int GTBR = 1024;
 __global__ __launch_bounds__(GTBR) void k_g_respawn_seq(GShape s, SrnnArgs a) {
   __shared__ int32_t s_wave[GTBR / 64];
-  const unsigned long long* masks = reinterpret_cast<const unsigned long long*>(a.i32c);
+  const unsigned long long* masks = a.ballots;
   const int64_t nb = (a.n + GTB - 1) / GTB, ch = (nb + GTBR - 1) / GTBR;
   const int64_t b0 = (int64_t)threadIdx.x * ch, b1 = b0 + ch < nb ? b0 + ch : nb;
   int32_t cnt = 0;
@@ -937,7 +951,7 @@ __global__ __launch_bounds__(GTBR) void k_g_respawn_seq(GShape s, SrnnArgs a) {
       m &= m - 1;
       const int64_t r = b * GTB + bit;
       a.uid_out[r] = k++;
-      if (a.flags & 32) continue;  // re-initialised inline by the evolve kernel
+      if (a.flags & SRNN_F_RESPAWN_INLINE) continue;  // re-initialised inline by the evolve kernel
       SV w = x.v(s.o_w);
       g_init(x, w, GItem::rng(a), respawn_key(gen, a.lo + r));
       g_store(s, GItem::rowp(s, a.W, r), w);
@@ -945,52 +959,11 @@ __global__ __launch_bounds__(GTBR) void k_g_respawn_seq(GShape s, SrnnArgs a) {
   }
   __syncthreads();
   if (threadIdx.x == 0) {
-    ((int64_t*)a.uid_base)[0] = base + total;
+    a.uid_base[0] = base + total;
     if (a.gen_out) a.gen_out[0] = gen + 1;
     else if (a.gen_ptr) ((int32_t*)a.gen_ptr)[0] = gen + 1;
   }
   if (a.counts && threadIdx.x < 5) a.counts[threadIdx.x] = 0;
-}
-
-// Sharded soup: uids of the previous generation's newborns (k_uid_assign, runtime rows)
-__global__ __launch_bounds__(GTBR) void k_g_uid_assign(GShape s, SrnnArgs a) {
-  __shared__ int32_t s_wave[GTBR / 64];
-  __shared__ int64_t s_prefix, s_total;
-  if (threadIdx.x == 0) {
-    int64_t pre = 0, tot = 0, cen[5] = {0, 0, 0, 0, 0}, all = 0;
-    for (int r = 0; r < a.world; ++r) {
-      const int64_t k = GItem::stat(s, a, r, 5);
-      if (r < a.rank) pre += k;
-      tot += k;
-      for (int q = 0; q < 5; ++q) cen[q] += GItem::stat(s, a, r, q);
-    }
-    for (int q = 0; q < 5; ++q) all += cen[q];
-    s_prefix = pre;
-    s_total = tot;
-    if (a.census && all > 0)
-      for (int q = 0; q < 5; ++q) a.census[q] = cen[q];
-  }
-  unsigned long long* masks = reinterpret_cast<unsigned long long*>(a.i32c);
-  const int64_t nb = (a.n + GTB - 1) / GTB, ch = (nb + GTBR - 1) / GTBR;
-  const int64_t b0 = (int64_t)threadIdx.x * ch, b1 = b0 + ch < nb ? b0 + ch : nb;
-  int32_t cnt = 0;
-  for (int64_t b = b0; b < b1; ++b) cnt += __popcll(masks[b]);
-  int32_t total_local;
-  const int32_t incl = block_incl_scan<GTBR>(cnt, s_wave, &total_local);
-  const int64_t base = *(volatile const int64_t*)a.uid_base;
-  int64_t k = base + s_prefix + incl - cnt;
-  for (int64_t b = b0; b < b1 && cnt; ++b) {
-    unsigned long long m = masks[b];
-    masks[b] = 0ull;
-    while (m) {
-      const int bit = __ffsll((long long)m) - 1;
-      m &= m - 1;
-      a.uid_out[b * GTB + bit] = k++;
-    }
-  }
-  __syncthreads();
-  if (threadIdx.x == 0) ((int64_t*)a.uid_base)[0] = base + s_total;
-  if (a.counts && threadIdx.x < 6) a.counts[threadIdx.x] = 0;
 }
 
 // ==================================================================================
@@ -1020,11 +993,57 @@ static void host_generic(int op, const GShape& s, const SrnnArgs& a) {
     case OP_PERTURB: host_parallel(a.n, with_ctx([&](const GCtx& x, int64_t i) { GItem::perturb(x, a, i); })); break;
     case OP_VARY_RUN: host_parallel(a.n, with_ctx([&](const GCtx& x, int64_t i) { GItem::vary_run(x, a, i); })); break;
     case OP_RESPAWN: host_parallel(a.n, with_ctx([&](const GCtx& x, int64_t i) { GItem::respawn(x, a, i); })); break;
-    case OP_SOUP_EVOLVE:
+    case OP_SOUP_EVOLVE: {
+      if (a.flags & SRNN_F_X2) {
+        const bool census = (a.flags & SRNN_F_FUSED_CENSUS) != 0;
+        unsigned long long* bs = reinterpret_cast<unsigned long long*>(a.temp);
+        if (a.flags & SRNN_F_X2_REMOTE) {
+          host_parallel(*a.x_rcount, with_ctx([&](const GCtx& x, int64_t q) {
+            const int64_t j = a.x_rlist[2 * q];
+            const bool rs = GItem::soup_evolve(x, a, j, a.x_rlist[2 * q + 1]) != 0;
+            bs_publish_host(bs, j, rs, census ? GItem::census_class(x, a, j) : (int8_t)-1);
+          }));
+          *a.x_rcount = 0;
+        } else {
+          host_parallel(a.n, with_ctx([&](const GCtx& x, int64_t i) {
+            if (x2_dep(a, i)) return;
+            const bool rs = GItem::soup_evolve(x, a, i) != 0;
+            bs_publish_host(bs, i, rs, census ? GItem::census_class(x, a, i) : (int8_t)-1);
+          }));
+          for (int64_t w = 0; w < (a.n + 31) / 32; ++w) a.x_dep[w] = 0u;
+        }
+        break;
+      }
       host_parallel(a.n, with_ctx([&](const GCtx& x, int64_t i) { GItem::soup_evolve(x, a, i); }));
-      if (a.i32c)
-        for (int64_t i = 0; i < a.n; ++i) a.i32c[i] = a.respawn[i] != 0 ? 1 : 0;
+      if ((a.flags & SRNN_F_ROW_FLAGS) && a.rowflags) {
+        for (int64_t i = 0; i < a.n; ++i) a.rowflags[i] = a.respawn[i] != 0 ? 1 : 0;
+      } else if (a.ballots) {
+        for (int64_t b = 0; b < (a.n + GTB - 1) / GTB; ++b) {
+          unsigned long long m = 0;
+          for (int64_t i = b * GTB; i < a.n && i < (b + 1) * GTB; ++i)
+            if (a.respawn[i]) m |= 1ull << (i - b * GTB);
+          a.ballots[b] = m;
+        }
+      }
       break;
+    }
+    case OP_SOUP_SEQ: {
+      // sequential soups of runtime shapes (Item soup_seq): serial by definition, host only
+      std::vector<float> buf((size_t)s.sfloats);
+      std::vector<double> orth((size_t)s.orthd + 1);
+      GCtx x{&s, buf.data(), 1, coords.data(), orth.data()};
+      const int32_t gen0 = a.gen_ptr ? a.gen_ptr[0] : a.gen;
+      int64_t next = a.uid_base[0];
+      for (int32_t st = 0; st < a.steps; ++st)
+        for (int64_t j = 0; j < a.n; ++j) {
+          GItem::soup_seq_one(x, a, j, gen0 + st);
+          if (a.respawn && a.respawn[j]) a.uid_out[j] = next++;
+        }
+      a.uid_base[0] = next;
+      if (a.gen_out) a.gen_out[0] = gen0 + a.steps;
+      else if (a.gen_ptr) ((int32_t*)a.gen_ptr)[0] = gen0 + a.steps;
+      break;
+    }
     case OP_CLASSIFY: {
       std::vector<int8_t> ks((size_t)a.n);
       host_parallel(a.n, with_ctx([&](const GCtx& x, int64_t i) { ks[(size_t)i] = GItem::classify(x, a, i); }));
@@ -1032,9 +1051,9 @@ static void host_generic(int op, const GShape& s, const SrnnArgs& a) {
         uint64_t local[5] = {0, 0, 0, 0, 0};
         for (int64_t i = 0; i < a.n; ++i) local[ks[(size_t)i]]++;
         for (int q = 0; q < 5; ++q) a.counts[q] += local[q];
-        if (a.flags & 64)
+        if (a.flags & SRNN_F_COUNT_RESPAWNS)
           for (int64_t i = 0; i < a.n; ++i) a.counts[5] += a.respawn[i] != 0;
-        if (a.flags & 512) {
+        if (a.flags & SRNN_F_GEN_ADVANCE) {
           if (a.gen_out) a.gen_out[0] = a.gen_ptr[0] + 1;
           else ((int32_t*)a.gen_ptr)[0] = a.gen_ptr[0] + 1;
         }
@@ -1050,50 +1069,16 @@ static void host_generic(int op, const GShape& s, const SrnnArgs& a) {
       for (int64_t i = 0; i < a.n; ++i) {
         if (a.respawn[i] == 0) continue;
         a.uid_out[i] = k++;
-        if (a.flags & 32) continue;  // re-initialised inline by the evolve
+        if (a.flags & SRNN_F_RESPAWN_INLINE) continue;  // re-initialised inline by the evolve
         SV w = x.v(s.o_w);
         g_init(x, w, GItem::rng(a), respawn_key(gen, a.lo + i));
         g_store(s, GItem::rowp(s, a.W, i), w);
       }
-      ((int64_t*)a.uid_base)[0] = k;
+      a.uid_base[0] = k;
       if (a.gen_out) a.gen_out[0] = gen + 1;
       else if (a.gen_ptr) ((int32_t*)a.gen_ptr)[0] = gen + 1;
       if (a.counts)
         for (int q = 0; q < 5; ++q) a.counts[q] = 0;
-      break;
-    }
-    case OP_SOUP_PACK:
-      GItem::pack_stats(s, a);
-      for (int64_t j = 0; j < a.n; ++j) GItem::soup_pack(s, a, j);
-      break;
-    case OP_SOUP_UNPACK:
-      for (int r = 0; r < a.world; ++r) a.sendcnt[r] = (int32_t)GItem::sr(s);
-      for (int64_t k = 0; k < (int64_t)a.world * a.cap; ++k) GItem::soup_unpack(s, a, k);
-      break;
-    case OP_UID_ASSIGN: {
-      if (a.flags & 16384) {
-        for (int64_t k = 0; k < (int64_t)a.world * a.cap; ++k) GItem::soup_unpack(s, a, k);
-        for (int r = 0; r < a.world; ++r) a.sendcnt[r] = (int32_t)GItem::sr(s);
-      }
-      int64_t pre = 0, tot = 0, cen[5] = {0, 0, 0, 0, 0}, all = 0;
-      for (int r = 0; r < a.world; ++r) {
-        const int64_t k = GItem::stat(s, a, r, 5);
-        if (r < a.rank) pre += k;
-        tot += k;
-        for (int q = 0; q < 5; ++q) cen[q] += GItem::stat(s, a, r, q);
-      }
-      for (int q = 0; q < 5; ++q) all += cen[q];
-      if (a.census && all > 0)
-        for (int q = 0; q < 5; ++q) a.census[q] = cen[q];
-      int64_t k = a.uid_base[0] + pre;
-      for (int64_t i = 0; i < a.n; ++i)
-        if (a.i32c[i]) {
-          a.uid_out[i] = k++;
-          a.i32c[i] = 0;
-        }
-      ((int64_t*)a.uid_base)[0] += tot;
-      if (a.counts)
-        for (int q = 0; q < 6; ++q) a.counts[q] = 0;
       break;
     }
     default: break;
@@ -1350,7 +1335,7 @@ __global__ __launch_bounds__(64) void k_rnn_wave(GShape s, SrnnArgs a) {
       rw_store(s, GItem::rowp(s, a.W, i), r.w);
       if (a.nsteps && lane == 0) a.nsteps[i] = st;
       if (a.cls) {
-        const int8_t k = rw_classify(s, r, a.eps, (a.flags & 8) != 0);
+        const int8_t k = rw_classify(s, r, a.eps, (a.flags & SRNN_F_FIX_SEC) != 0);
         if (lane == 0) a.cls[i] = k;
       }
     }
@@ -1406,7 +1391,7 @@ static bool generic_op_supported(int op) {
   switch (op) {
     case OP_INIT: case OP_APPLY: case OP_RUN_FIXPOINT: case OP_TRAIN: case OP_LEARN: case OP_CLASSIFY:
     case OP_PERTURB: case OP_SOUP_DECIDE: case OP_RESPAWN_SEQ: case OP_SOUP_EVOLVE: case OP_RESPAWN:
-    case OP_VARY_RUN: case OP_SOUP_PACK: case OP_SOUP_UNPACK: case OP_UID_ASSIGN:
+    case OP_VARY_RUN:
       return true;
     default: return false;
   }
@@ -1428,19 +1413,7 @@ static int generic_launch(int op, const GShape& s, const SrnnArgs& a) {
     SrnnCfg dummy{};
     return launch<Weightwise<1, 1>, OP_SOUP_DECIDE, StF32>(dummy, a);
   }
-  if (op == OP_SOUP_PACK) {
-    const int64_t items = a.n > 0 ? a.n : 1;
-    hipLaunchKernelGGL(k_g_pack, dim3((unsigned)((items + 255) / 256)), dim3(256), 0, st, s, a);
-  } else if (op == OP_SOUP_UNPACK) {
-    const int64_t items = (int64_t)a.world * a.cap;
-    if (items > 0) hipLaunchKernelGGL(k_g_unpack, dim3((unsigned)((items + 255) / 256)), dim3(256), 0, st, s, a);
-  } else if (op == OP_UID_ASSIGN) {
-    if (a.flags & 16384) {
-      const int64_t items = (int64_t)a.world * a.cap;
-      if (items > 0) hipLaunchKernelGGL(k_g_unpack, dim3((unsigned)((items + 255) / 256)), dim3(256), 0, st, s, a);
-    }
-    hipLaunchKernelGGL(k_g_uid_assign, dim3(1), dim3(GTBR), 0, st, s, a);
-  } else if (op == OP_RESPAWN_SEQ) {
+  if (op == OP_RESPAWN_SEQ) {
     if (!a.scratch || a.scratch_bytes < (int64_t)GTBR * g_lane_bytes(s)) {
       set_error("generic respawn_seq needs scratch >= 1024 lanes (srnn_generic_scratch_bytes)");
       return -5;
@@ -1471,7 +1444,14 @@ static int generic_launch(int op, const GShape& s, const SrnnArgs& a) {
       case OP_PERTURB: SRNN_GK(OP_PERTURB)
       case OP_VARY_RUN: SRNN_GK(OP_VARY_RUN)
       case OP_RESPAWN: SRNN_GK(OP_RESPAWN)
-      case OP_SOUP_EVOLVE: SRNN_GK(GOP_EVOLVE)
+      case OP_SOUP_EVOLVE:
+        if ((a.flags & SRNN_F_X2) && (a.flags & SRNN_F_X2_REMOTE)) {
+          // the list length is on the device: a bounded grid-stride launch over the list
+          const int64_t rl = lanes < X2_REMOTE_WAVES * GTB ? lanes : X2_REMOTE_WAVES * GTB;
+          hipLaunchKernelGGL((k_generic<GOP_X2_REMOTE>), dim3((unsigned)(rl / GTB)), block, lds, st, s, a, rl);
+          break;
+        }
+        SRNN_GK(GOP_EVOLVE)
       case OP_CLASSIFY:
         if (a.counts) {
           SRNN_GK(GOP_CLASSIFY_COUNT)
@@ -1501,6 +1481,10 @@ extern "C" int srnn_dispatch_generic(int op, const SrnnCfg* c, const SrnnArgs* a
     return 1;
   }
   if (op < 0) return 0;
+  if (op == OP_SOUP_SEQ && !a->dev) {  // sequential soups: host only (a serial chain)
+    srnn::host_generic(op, s, *a);
+    return 0;
+  }
   if (!srnn::generic_op_supported(op)) return 2;
   if (!a->dev) {
     if (op == OP_SOUP_DECIDE) {

@@ -21,6 +21,9 @@ namespace srnn {
 void set_error(const char* msg);
 
 constexpr int TB = 64;  // threads per block: one wave; lane-private LDS scratch per thread
+// waves of the X2 remote evolve (grid-stride over the remote-dependent list, whose length is
+// only known on the device): 4 per SIMD of a 256-CU MI355X
+constexpr int64_t X2_REMOTE_WAVES = 4096;
 
 enum Action : int8_t { A_NONE = 0, A_ATTACKING = 1, A_LEARN_FROM = 2, A_TRAIN_SELF = 3 };
 
@@ -71,15 +74,98 @@ SRNN_HD int32_t atomic_or_i32(int32_t* p, int32_t v) {
 
 // rank owning global slot g under the contiguous sharding lo_r = floor(r * N / R)
 SRNN_HD int32_t shard_of(int64_t g, int64_t n_total, int32_t world) {
+  // g * world < 2^63 for any population that fits a node (< 2^58 slots)
   int32_t r = (int32_t)((g * world) / n_total);
   while (r + 1 < world && ((int64_t)(r + 1) * n_total) / world <= g) ++r;
   while (r > 0 && ((int64_t)r * n_total) / world > g) --r;
   return r;
 }
+SRNN_HD int64_t shard_lo(int32_t r, int64_t n_total, int32_t world) { return ((int64_t)r * n_total) / world; }
 
-// init key of the particle born in slot g at generation `gen` (rank-count invariant)
+// init key of the particle born in slot g at generation `gen` (rank-count invariant).
+// Slots below 2^32: bit 62 | gen << 32 | slot; larger slots (HBM-filling sharded soups):
+// bit 63 | (gen mod 2^23) << 40 | slot.  Initial particles are keyed by their uid (< 2^62).
 SRNN_HD uint64_t respawn_key(int32_t gen, int64_t g) {
-  return (1ull << 62) | ((uint64_t)(uint32_t)gen << 32) | (uint64_t)g;
+  if ((uint64_t)g < (1ull << 32)) return (1ull << 62) | ((uint64_t)(uint32_t)gen << 32) | (uint64_t)g;
+  return (1ull << 63) | ((uint64_t)((uint32_t)gen & 0x7FFFFFu) << 40) | ((uint64_t)g & ((1ull << 40) - 1));
+}
+
+// ----------------------------------------------------------------------------------
+// Soup row sources and attack lists, shape independent (rb = bytes of a table row).
+// A victim's list holds its attackers' entries (SRNN_NIL-terminated, see srnn_abi.h):
+//   single rank       entry = the attacker's row (= slot, lo = 0), row in W2
+//   SRNN_F_FULL_TABLE entry = global slot, row in W2 (own shard) or the gathered table
+//   SRNN_F_X2         entry < n: local row in W2; entry >= n: received row e - n of the
+//                     all-to-all (block q = k / x_cr, position k % x_cr), slot in x_rslot
+// ----------------------------------------------------------------------------------
+constexpr int64_t X2_HB = (int64_t)SRNN_X2_HDR * 8;  // header bytes of an exchange block
+SRNN_HD int64_t x2_xb(int64_t rb) { return rb + 16; }  // exchange row: weights + (int64 slot, int64 gen)
+SRNN_HD const char* x2_row(const SrnnArgs& a, int64_t k, int64_t rb) {
+  const int64_t q = k / a.x_cr, pos = k - q * a.x_cr;
+  return a.recvbuf + q * a.x_blk + X2_HB + pos * x2_xb(rb);
+}
+SRNN_HD uint64_t ent_slot(const SrnnArgs& a, uint32_t e) {
+  if (a.flags & SRNN_F_FULL_TABLE) return e;
+  if ((int64_t)e < a.n) return (uint64_t)(a.lo + (int64_t)e);
+  return (uint64_t)a.x_rslot[(int64_t)e - a.n];
+}
+SRNN_HD const char* ent_row(const SrnnArgs& a, uint32_t e, int64_t rb) {
+  if (a.flags & SRNN_F_FULL_TABLE) {
+    const int64_t g = (int64_t)e;
+    if (g >= a.lo && g < a.lo + a.n) return reinterpret_cast<const char*>(a.W2) + (g - a.lo) * rb;
+    return a.recvbuf + g * rb;
+  }
+  if ((int64_t)e < a.n) return reinterpret_cast<const char*>(a.W2) + (int64_t)e * rb;
+  return x2_row(a, (int64_t)e - a.n, rb);
+}
+// generation-start row of teacher slot te (tk: its received row under SRNN_F_X2)
+SRNN_HD const char* teacher_row(const SrnnArgs& a, int64_t te, uint32_t tk, int64_t rb) {
+  if (te >= a.lo && te < a.lo + a.n) return reinterpret_cast<const char*>(a.W2) + (te - a.lo) * rb;
+  if (a.flags & SRNN_F_FULL_TABLE) return a.recvbuf + te * rb;
+  return x2_row(a, (int64_t)tk, rb);
+}
+SRNN_HD void err_or(int32_t* p, int32_t v) {
+  if (!p) return;
+#if defined(__HIP_DEVICE_COMPILE__)
+  atomicOr(p, v);
+#else
+  __atomic_fetch_or(p, v, __ATOMIC_RELAXED);
+#endif
+}
+// a received row must carry the slot and generation the receiver expects (protocol check)
+SRNN_HD void x2_check(const SrnnArgs& a, const char* row, int64_t rb, int64_t slot, int32_t gen) {
+  const int64_t* t = reinterpret_cast<const int64_t*>(row + rb);
+  if (t[0] != slot || t[1] != (int64_t)gen) err_or(a.err, 4);
+}
+// Visit the attackers of local victim j in ascending attacker-slot order (the list is in
+// arrival order; lists are short: Poisson(attacking_rate)).  Consumes the list head.
+// SINGLE: single-rank lists (entry = slot = row): no flag tests on the hot path.
+// Sharded lists (!SINGLE) are bounded: a list that does not end within 2^16 steps (a
+// protocol bug) sets error bit 4 and ends the walk instead of hanging the GPU.
+template <bool SINGLE, class F>
+SRNN_HD void for_each_attacker(const SrnnArgs& a, int64_t j, F&& f) {
+  const uint32_t head = a.heads[j];
+  if (head == SRNN_NIL) return;
+  a.heads[j] = SRNN_NIL;  // consumed: NIL for the generation after next
+  uint64_t last = 0;
+  bool first = true;
+  uint32_t steps = 0;
+  for (;;) {
+    uint64_t best = ~0ull;
+    uint32_t be = SRNN_NIL;
+    for (uint32_t e = head; e != SRNN_NIL; e = a.nexts[e]) {
+      if (!SINGLE && ++steps > (1u << 16)) {
+        err_or(a.err, 4);
+        return;
+      }
+      const uint64_t sl = SINGLE ? (uint64_t)e : ent_slot(a, e);
+      if ((first || sl > last) && sl < best) best = sl, be = e;
+    }
+    if (be == SRNN_NIL) break;
+    first = false;
+    last = best;
+    f(be, (int64_t)best);
+  }
 }
 
 // ----------------------------------------------------------------------------------
@@ -149,42 +235,8 @@ struct Item {
   static constexpr int P = Net::P;
   static constexpr int PP = Net::PP;
   static constexpr int RB = PP * S::BYTES;  // bytes per table row
-  static constexpr int XB = RB + 16;        // exchange row: weights + (slot, gen, -, -) int32 tags
-  // the first SR rows of every destination block of the all-to-all carry the sender's
-  // int64[6] stats (census of its previous generation + respawn count): the per-rank
-  // stats all-gather rides on the row exchange (one collective per generation)
-  static constexpr int SR = (48 + XB - 1) / XB;
-
-  // stats word q of rank r: from the exchange receive buffer (flag 256) or the gathered
-  // [world][6] array
-  SRNN_HD static int64_t stat(const SrnnArgs& a, int r, int q) {
-    if (a.flags & 256)
-      return reinterpret_cast<const int64_t*>(reinterpret_cast<const char*>(a.recvbuf) + (int64_t)r * a.cap * XB)[q];
-    return a.stats[r * 6 + q];
-  }
-  SRNN_HD static void pack_stats(const SrnnArgs& a) {
-    for (int r = 0; r < a.world; ++r) {
-      int64_t* d = reinterpret_cast<int64_t*>(reinterpret_cast<char*>(a.sendbuf) + (int64_t)r * a.cap * XB);
-      for (int q = 0; q < 6; ++q) d[q] = (int64_t)a.counts[q];
-    }
-  }
-
   SRNN_HD static char* rowp(float* base, int64_t i) { return reinterpret_cast<char*>(base) + i * RB; }
   SRNN_HD static const char* rowp(const float* base, int64_t i) { return reinterpret_cast<const char*>(base) + i * RB; }
-
-  // generation-start row of global slot g: local table (W2, this rank's rows) or the
-  // exchange receive buffer for slots of other ranks
-  // (flag 128: recvbuf is the all-gathered [n_total] table of every rank's rows)
-  SRNN_HD static const char* row_of(const SrnnArgs& a, int64_t g) {
-    if (a.world <= 1 || (g >= a.lo && g < a.lo + a.n)) return rowp(a.W2, g - a.lo);
-    if (a.flags & 128) return rowp(a.recvbuf, g);
-#if defined(__HIP_DEVICE_COMPILE__)
-    if (a.flags & 524288)  // indexed by unpack workgroups of this same launch: memory-side read
-      return reinterpret_cast<const char*>(a.recvbuf) +
-             (int64_t)__hip_atomic_load(a.rmap + g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) * XB;
-#endif
-    return reinterpret_cast<const char*>(a.recvbuf) + (int64_t)a.rmap[g] * XB;
-  }
 
   SRNN_HD static void q(float* w) {
     if constexpr (S::ID != 0) {
@@ -319,7 +371,7 @@ struct Item {
     }
     store(rowp(a.W, i), w);
     if (a.nsteps) a.nsteps[i] = s;
-    if (a.cls) a.cls[i] = classify_w(w, a.eps, (a.flags & 8) != 0, x);
+    if (a.cls) a.cls[i] = classify_w(w, a.eps, (a.flags & SRNN_F_FIX_SEC) != 0, x);
   }
 
   // ---------------------------------------------------------------- known-fixpoint variation
@@ -378,7 +430,7 @@ struct Item {
     tc.ctr = a.ctr;
     tc.samp = samp;
     tc.perm = perm;
-    tc.shuffle = (a.flags & 1) != 0;
+    tc.shuffle = (a.flags & SRNN_F_SHUFFLE) != 0;
     tc.stride = SAMP_STRIDE;
     tc.aggregator = c.aggregator;
     float loss = 0.f;
@@ -399,7 +451,7 @@ struct Item {
   SRNN_HD static int8_t classify(const SrnnCfg& c, const SrnnArgs& a, int64_t i, uint8_t* perm) {
     float w[P];
     load(rowp(a.W, i), w);
-    int8_t k = classify_w(w, a.eps, (a.flags & 8) != 0, actx(a, c, uid_of(a, i), a.ctr, perm));
+    int8_t k = classify_w(w, a.eps, (a.flags & SRNN_F_FIX_SEC) != 0, actx(a, c, uid_of(a, i), a.ctr, perm));
     if (a.cls) a.cls[i] = k;
     return k;
   }
@@ -407,15 +459,32 @@ struct Item {
   // ---------------------------------------------------------------- soup
   // Decisions of global slot g in generation `gen` (reference code/soup.py:56-63): a pure
   // function of (seed, slot, generation), so any rank can recompute any slot's decision.
-  SRNN_HD static void decision(const SrnnArgs& a, int64_t g, int32_t gen, int32_t& at, int32_t& te) {
-    U4 d = rng(a).draw((uint64_t)g, (uint32_t)gen, P_SOUP);
+  // Partners are uniform over the slot's sub-soup (segment) or the whole population; spans
+  // above 2^32 slots take 64-bit partner draws from a second stream.
+  SRNN_HD static void decision(const SrnnArgs& a, int64_t g, int32_t gen, int64_t& at, int64_t& te) {
+    const Rng r = rng(a);
+    const U4 d = r.draw((uint64_t)g, (uint32_t)gen, P_SOUP);
     at = -1;
     te = -1;
-    // partners are drawn inside the slot's sub-soup (segment) or the whole population
     const int64_t span = a.segment > 0 ? a.segment : a.n_total;
     const int64_t base = a.segment > 0 ? (g / a.segment) * a.segment : 0;
-    if (u01(d.x) < a.attacking_rate) at = (int32_t)(base + (int64_t)(((uint64_t)d.y * (uint64_t)span) >> 32));
-    if (u01(d.z) < a.learn_from_rate) te = (int32_t)(base + (int64_t)(((uint64_t)d.w * (uint64_t)span) >> 32));
+    const bool atk = u01(d.x) < a.attacking_rate, lrn = u01(d.z) < a.learn_from_rate;
+    if (!atk && !lrn) return;
+    if ((uint64_t)span <= 0xFFFFFFFFull) {
+      if (atk) at = base + (int64_t)(((uint64_t)d.y * (uint64_t)span) >> 32);
+      if (lrn) te = base + (int64_t)(((uint64_t)d.w * (uint64_t)span) >> 32);
+    } else {
+      const U4 e = r.draw((uint64_t)g, (uint32_t)gen, P_SOUP_WIDE);
+      if (atk) at = base + (int64_t)mulhi64((((uint64_t)e.x) << 32) | e.y, (uint64_t)span);
+      if (lrn) te = base + (int64_t)mulhi64((((uint64_t)e.z) << 32) | e.w, (uint64_t)span);
+    }
+  }
+  SRNN_HD static uint64_t mulhi64(uint64_t x, uint64_t y) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return __umul64hi(x, y);
+#else
+    return (uint64_t)(((unsigned __int128)x * y) >> 64);
+#endif
   }
   SRNN_HD static int32_t gen_of(const SrnnArgs& a) { return a.gen_ptr ? a.gen_ptr[0] : a.gen; }
   // the next generation's counter: the other ring slot (gen_out) or in place
@@ -424,96 +493,53 @@ struct Item {
     else if (a.gen_ptr) ((int32_t*)a.gen_ptr)[0] = g;
   }
 
-  // Every global slot: link attacks on this rank's victims into per-victim lists
-  // (head[victim] in i32e, pre-set to -1; next[attacker] in i32f).  Optional i32a/i32b
-  // receive the decisions (diagnostics/tests).
+  // Every global slot (single rank or all-gather exchange): link attacks on this rank's
+  // victims into per-victim lists (heads pre-set to NIL).  Entries are global slots (single
+  // rank: lo = 0, slot = row).  Optional dec_at / dec_te receive the decisions.
   SRNN_HD static void soup_decide(const SrnnArgs& a, int64_t i) {
-    int32_t at, te;
+    int64_t at, te;
     decision(a, i, gen_of(a), at, te);
-    if (a.i32a) a.i32a[i] = at;
-    if (a.i32b) a.i32b[i] = te;
-    link_decision(a, i, at, te, a.i32e, a.i32f);
+    if (a.dec_at) a.dec_at[i] = at;
+    if (a.dec_te) a.dec_te[i] = te;
+    if (at >= a.lo && at < a.lo + a.n) link(a.heads, a.nexts, at - a.lo, (uint32_t)i);
   }
-  // attacks on this rank's victims -> lists (head, next); rows other ranks will need ->
-  // need masks (sharded)
-  SRNN_HD static void link_decision(const SrnnArgs& a, int64_t i, int32_t at, int32_t te, int32_t* head,
-                                    int32_t* next) {
-    const bool i_local = i >= a.lo && i < a.lo + a.n;
-    if (at >= a.lo && at < a.lo + a.n) {
+  // entry e joins the list of local victim v
+  SRNN_HD static void link(uint32_t* heads, uint32_t* nexts, int64_t v, uint32_t e) {
 #if defined(__HIP_DEVICE_COMPILE__)
-      next[i] = atomicExch(head + (at - a.lo), (int32_t)i);
+    nexts[e] = atomicExch(heads + v, e);
 #else
-      next[i] = __atomic_exchange_n(head + (at - a.lo), (int32_t)i, __ATOMIC_RELAXED);
+    nexts[e] = __atomic_exchange_n(heads + v, e, __ATOMIC_RELAXED);
 #endif
-    } else if (a.need && a.world > 1 && at >= 0 && i_local) {
-      // my particle attacks a victim owned by another rank: ship my row there
-      atomic_or_i32(a.need + (i - a.lo), 1 << shard_of(at, a.n_total, a.world));
-    }
-    if (a.need && a.world > 1 && te >= a.lo && te < a.lo + a.n && !i_local) {
-      // a remote learner picked one of my particles as teacher
-      atomic_or_i32(a.need + (te - a.lo), 1 << shard_of(i, a.n_total, a.world));
-    }
-  }
-
-  // sharded soup: copy local row j to every rank that needs it this generation
-  SRNN_HD static void soup_pack(const SrnnArgs& a, int64_t j) {
-    int32_t m = a.need[j];
-    if (!m) return;
-    a.need[j] = 0;
-    const int32_t gen = gen_of(a);
-    const char* src = rowp(a.W2, j);
-    while (m) {
-      const int r = __builtin_ctz((unsigned)m);
-      m &= m - 1;
-      const int32_t pos = atomic_add_i32(a.sendcnt + r, 1);
-      if (pos >= a.cap) {
-        atomic_or_i32(a.ovf, 1);
-        continue;
-      }
-      char* dst = reinterpret_cast<char*>(a.sendbuf) + ((int64_t)r * a.cap + pos) * XB;
-      const uint2* s2 = reinterpret_cast<const uint2*>(src);
-      uint2* d2 = reinterpret_cast<uint2*>(dst);
-#pragma unroll
-      for (int q = 0; q < RB / 8; ++q) d2[q] = s2[q];
-      d2[RB / 8] = make_uint2((uint32_t)(a.lo + j), (uint32_t)gen);
-      d2[RB / 8 + 1] = make_uint2(0u, 0u);
-    }
-  }
-  // sharded soup: received row k -> rmap[slot]; rows of older generations are ignored
-  SRNN_HD static void soup_unpack(const SrnnArgs& a, int64_t k) {
-    if (k % a.cap < SR) return;  // stats rows
-    const int32_t* tag = reinterpret_cast<const int32_t*>(reinterpret_cast<const char*>(a.recvbuf) + k * XB + RB);
-    if (tag[1] == gen_of(a)) a.rmap[tag[0]] = (int32_t)k;
   }
 
   // Synchronous (Jacobi) generation for local row j: every read is from the
-  // generation-start table W2 (global rows), the result goes to W (local rows).  The
-  // particle's random streams (SGD shuffles, shuffle_random) are keyed by its global SLOT
-  // and the generation -- not by its uid -- so a generation never waits for the uids of
-  // the previous generation's newborns (their uid assignment overlaps the next generation).
-  SRNN_HD static void soup_evolve(const SrnnCfg& c, const SrnnArgs& a, int64_t j, float4* samp, uint8_t* perm) {
+  // generation-start table W2 (own rows) or received / gathered rows of other ranks, the
+  // result goes to W (local rows).  The particle's random streams (SGD shuffles,
+  // shuffle_random) are keyed by its global SLOT and the generation -- not by its uid -- so
+  // a generation never waits for the uids of the previous generation's newborns.
+  // SINGLE: single-rank source rows (no exchange); tk: the received row of a remote teacher
+  // (SRNN_F_X2).  Returns the respawn code (also in respawn[j]).
+  template <bool SINGLE = false>
+  SRNN_HD static int8_t soup_evolve(const SrnnCfg& c, const SrnnArgs& a, int64_t j, float4* samp, uint8_t* perm,
+                                    uint32_t tk = SRNN_NIL) {
     const int64_t g = a.lo + j;
     float w[P], f[P], o[P];
     load(rowp(a.W2, j), w);
     const uint64_t uid = (uint64_t)g;  // stream key of this slot
     const int32_t gen = gen_of(a);
     ApplyCtx x = actx(a, c, uid, (uint32_t)gen * 1024u, perm);
-    // 1. attacks received, in ascending attacker slot order (the list is in arrival order)
-    const int32_t head = a.i32e[j];
-    a.i32e[j] = -1;  // list consumed: reset for the next generation's decide
-    int32_t last = -1;
-    while (head >= 0) {
-      int32_t best = INT_MAX;
-      for (int32_t r = head; r >= 0; r = a.i32f[r]) best = (r > last && r < best) ? r : best;
-      if (best == INT_MAX) break;
-      last = best;
-      load(row_of(a, best), f);
+    const bool x2 = !SINGLE && (a.flags & SRNN_F_X2);
+    // 1. attacks received, in ascending attacker slot order (generation-start attacker rows)
+    for_each_attacker<SINGLE>(a, j, [&](uint32_t e, int64_t slot) {
+      const char* r = SINGLE ? rowp(a.W2, (int64_t)e) : ent_row(a, e, RB);
+      if (x2 && (int64_t)e >= a.n) x2_check(a, r, RB, slot, gen);
+      load(r, f);
       Net::apply(f, w, o, x);
       q(o);
       x.ctr += 1;
       copy(w, o);
-    }
-    int32_t my_at, te;
+    });
+    int64_t my_at, te;
     decision(a, g, gen, my_at, te);
     int8_t act = A_NONE;
     int64_t cp = -1;
@@ -528,19 +554,15 @@ struct Item {
     tc.ctr = (uint32_t)gen * 1024u + 512u;
     tc.samp = samp;
     tc.perm = perm;
-    tc.shuffle = (a.flags & 1) != 0;
+    tc.shuffle = (a.flags & SRNN_F_SHUFFLE) != 0;
     tc.stride = SAMP_STRIDE;
     tc.aggregator = c.aggregator;
-    if ((a.flags & 131072) && a.perm_cur) {  // SGD permutations precomputed by helper waves
-      tc.pre = reinterpret_cast<const unsigned long long*>(a.perm_cur) + j;
-      tc.pre_stride = a.n;
-      tc.pre_ctr0 = (uint32_t)gen * 1024u + 512u;
-      tc.pre_n = a.perm_e;
-    }
     float loss = 0.f;
     // 2. learn_from a teacher (its generation-start weights)
     if (te >= 0) {
-      load(row_of(a, te), f);
+      const char* r = SINGLE ? rowp(a.W2, te) : teacher_row(a, te, tk, RB);
+      if (x2 && tk != SRNN_NIL) x2_check(a, r, RB, te, gen);
+      load(r, f);
       if constexpr (Net::KIND == 0) {
         if (a.severity > 0) loss = Net::template train_epochs<false>(w, f, a.severity, tc);
       } else {
@@ -565,22 +587,15 @@ struct Item {
     // 4. respawn flags (reference code/soup.py:77-86; zero test on the old particle)
     q(w);  // the stored state decides respawn
     int8_t rs = 0;
-    if ((a.flags & 2) && is_diverged<P>(w)) rs = 1;
-    else if ((a.flags & 4) && is_zero<P>(w, a.eps)) rs = 2;
-    if (rs && (a.flags & 32)) Net::init(w, rng(a), respawn_key(gen, g));  // newborn, uid assigned later
+    if ((a.flags & SRNN_F_REMOVE_DIVERGENT) && is_diverged<P>(w)) rs = 1;
+    else if ((a.flags & SRNN_F_REMOVE_ZERO) && is_zero<P>(w, a.eps)) rs = 2;
+    if (rs && (a.flags & SRNN_F_RESPAWN_INLINE)) Net::init(w, rng(a), respawn_key(gen, g));  // newborn
     store(rowp(a.W, j), w);
     if (a.action) a.action[j] = act;
     if (a.counterpart) a.counterpart[j] = cp;
     if (a.loss) a.loss[j] = loss;
-    a.respawn[j] = rs;
-    if (a.i32c) {
-#if defined(__HIP_DEVICE_COMPILE__)
-      // one wave per block (TB == 64): per-block respawn count for k_respawn_seq
-      (void)0;
-#else
-      a.i32c[j] = rs != 0 ? 1 : 0;
-#endif
-    }
+    if (a.respawn) a.respawn[j] = rs;
+    return rs;
   }
 
   // Sequential (Gauss-Seidel) generation step of particle j (reference Soup.evolve,
@@ -594,7 +609,7 @@ struct Item {
   SRNN_HD static void soup_seq_one(const SrnnCfg& c, const SrnnArgs& a, int64_t j, int32_t gen, float4* samp,
                                    uint8_t* perm) {
     float w[P], f[P], o[P];
-    int32_t at, te;
+    int64_t at, te;
     decision(a, j, gen, at, te);
     int8_t act = A_NONE;
     int64_t cp = -1;
@@ -615,7 +630,7 @@ struct Item {
     tc.ctr = (uint32_t)gen * 1024u + 512u;
     tc.samp = samp;
     tc.perm = perm;
-    tc.shuffle = (a.flags & 1) != 0;
+    tc.shuffle = (a.flags & SRNN_F_SHUFFLE) != 0;
     tc.stride = SAMP_STRIDE;
     tc.aggregator = c.aggregator;
     float loss = 0.f;
@@ -643,8 +658,8 @@ struct Item {
     }
     q(w);  // 4. respawn (the zero test on the old particle: at most one of the two)
     int8_t rs = 0;
-    if ((a.flags & 2) && is_diverged<P>(w)) rs = 1;
-    else if ((a.flags & 4) && is_zero<P>(w, a.eps)) rs = 2;
+    if ((a.flags & SRNN_F_REMOVE_DIVERGENT) && is_diverged<P>(w)) rs = 1;
+    else if ((a.flags & SRNN_F_REMOVE_ZERO) && is_zero<P>(w, a.eps)) rs = 2;
     if (a.W2) store(rowp(a.W2, j), w);  // recording: the particle's state before any respawn
     if (rs) Net::init(w, rng(a), respawn_key(gen, j));
     store(rowp(a.W, j), w);
@@ -662,54 +677,7 @@ struct Item {
     Net::init(w, rng(a), respawn_key(gen_of(a), a.lo + j));
     store(rowp(a.W, j), w);
   }
-
-  // SGD permutations of local row j for generation `gen` (epoch counters gen*1024+512+k,
-  // k < perm_e, keyed by the slot): exactly what train_epochs would draw, into
-  // out[k * n + j] (k-major: the lanes of a wave write consecutive words)
-  SRNN_HD static void perm_fill(const SrnnArgs& a, int64_t j, int32_t gen, uint64_t* out) {
-    if constexpr (Net::KIND == 0 && P <= 16) {
-      const uint64_t key = (uint64_t)(a.lo + j);
-      const uint32_t c0 = (uint32_t)gen * 1024u + 512u;  // even: epochs (k, k+1) share a draw
-      const Rng r = rng(a);
-      for (int32_t k = 0; k < a.perm_e; k += 2) {
-        const U4 d = perm_draw(r, key, c0 + (uint32_t)k, P_SHUFFLE);
-        out[(int64_t)k * a.n + j] = perm_from_bits<P>(perm_bits(d, c0 + (uint32_t)k));
-        if (k + 1 < a.perm_e) out[(int64_t)(k + 1) * a.n + j] = perm_from_bits<P>(perm_bits(d, c0 + (uint32_t)k + 1u));
-      }
-    }
-  }
 };
-
-// ----------------------------------------------------------------------------------
-// Helper waves of the fused generation (flag 131072).  At ~1.5 waves per SIMD the SIMDs
-// carrying two generation waves are issue-saturated while the others run one wave at half
-// issue rate.  The next generation's SGD permutations (the Philox + Fisher-Yates integer
-// work, ~30 % of an epoch's instructions) are computed by extra workgroups that keep
-// going only on SIMDs holding fewer than two generation waves, pulling 64-slot chunks from
-// a work queue; generation waves drain whatever is left when they finish, so the queue
-// always empties inside the launch.  Placement only affects speed, never the result.
-// ----------------------------------------------------------------------------------
-__device__ __forceinline__ int simd_slot() {
-  const uint32_t hw = __builtin_amdgcn_s_getreg((31 << 11) | 4);  // HW_REG_HW_ID
-  const uint32_t xcc = __builtin_amdgcn_s_getreg((3 << 11) | 20);  // HW_REG_XCC_ID[3:0]
-  const uint32_t simd = (hw >> 4) & 3u, cu = (hw >> 8) & 15u, sh = (hw >> 12) & 1u, se = (hw >> 13) & 7u;
-  return (int)((((((xcc & 7u) * 8u + se) * 2u + sh) * 16u + cu) * 4u) + simd);  // < 8192
-}
-constexpr int HELPER_CTL = 1 + 8192;  // queue head + per-SIMD generation-wave counts
-
-template <class Net, class S>
-__device__ void perm_drain(const SrnnArgs& a, int32_t gen_next) {
-  using I = Item<Net, S>;
-  const int64_t nch = (a.n + TB - 1) / TB;
-  for (;;) {
-    int32_t ch = 0;
-    if (threadIdx.x == 0) ch = atomicAdd(a.helper_ctl, 1);
-    ch = __shfl(ch, 0);
-    if ((int64_t)ch >= nch) break;
-    const int64_t j = (int64_t)ch * TB + threadIdx.x;
-    if (j < a.n) I::perm_fill(a, j, gen_next, a.perm_next);
-  }
-}
 
 // ==================================================================================
 // Device kernels
@@ -718,7 +686,7 @@ template <class Net, int OP, class S>
 __global__ __launch_bounds__(TB) void k_op(SrnnCfg c, SrnnArgs a) {
   using I = Item<Net, S>;
   constexpr int P = Net::P;
-  constexpr bool NEED_SAMP = (OP == OP_TRAIN || OP == OP_LEARN || OP == OP_SOUP_EVOLVE) && Net::KIND == 0;
+  constexpr bool NEED_SAMP = (OP == OP_TRAIN || OP == OP_LEARN) && Net::KIND == 0;
   constexpr int SAMP = NEED_SAMP ? P : 1;  // slot-major [P][TB]: lane fastest
   constexpr int PERM = (P + 4) & ~3;
   __shared__ float4 s_samp[TB * SAMP];
@@ -729,15 +697,6 @@ __global__ __launch_bounds__(TB) void k_op(SrnnCfg c, SrnnArgs a) {
 
   if constexpr (OP == OP_SOUP_DECIDE) {
     if (i < a.n_total) I::soup_decide(a, i);
-    return;
-  } else if constexpr (OP == OP_SOUP_UNPACK) {
-    if (i == 0)  // packing of this generation is complete; data rows follow the stats rows
-      for (int r = 0; r < a.world; ++r) a.sendcnt[r] = I::SR;
-    if (i < (int64_t)a.world * a.cap) I::soup_unpack(a, i);
-    return;
-  } else if constexpr (OP == OP_SOUP_PACK) {
-    if (i == 0) I::pack_stats(a);
-    if (i < a.n) I::soup_pack(a, i);
     return;
   } else if constexpr (OP == OP_CLASSIFY) {
     if (i < a.n) I::classify(c, a, i, perm);  // histogram: k_classify_count
@@ -755,9 +714,49 @@ __global__ __launch_bounds__(TB) void k_op(SrnnCfg c, SrnnArgs a) {
   }
 }
 
-// Fused soup generation body: one wave per block; after the per-particle work the wave
-// publishes its 64-bit respawn ballot (i32c as u64[block]) for the single-rank respawn scan, or per-row
-// flags (i32c[row]) when OP_SCAN follows (sharded path, a.i32d != null flags that mode).
+// ----------------------------------------------------------------------------------
+// X2 block stats (u64[4] per 64-row block of a generation: respawn ballot; class counts
+// c0 | c1 << 32, c2 | c3 << 32, c4) are accumulated with atomics: the local and the remote
+// evolve of a sharded generation run at the same time and share blocks.
+// ----------------------------------------------------------------------------------
+__device__ __forceinline__ void bs_publish_wave(unsigned long long* bs, int64_t b, bool rs, int8_t k) {
+  const unsigned long long m = __ballot(rs);
+  uint32_t cnt[5];
+#pragma unroll
+  for (int q = 0; q < 5; ++q) cnt[q] = (uint32_t)__popcll(__ballot(k == q));
+  if (threadIdx.x % TB == 0) {
+    unsigned long long* st = bs + b * 4;
+    if (m) atomicOr(st, m);
+    const unsigned long long c01 = (unsigned long long)cnt[0] | ((unsigned long long)cnt[1] << 32);
+    const unsigned long long c23 = (unsigned long long)cnt[2] | ((unsigned long long)cnt[3] << 32);
+    if (c01) atomicAdd(st + 1, c01);
+    if (c23) atomicAdd(st + 2, c23);
+    if (cnt[4]) atomicAdd(st + 3, (unsigned long long)cnt[4]);
+  }
+}
+__device__ __forceinline__ void bs_publish_lane(unsigned long long* bs, int64_t row, bool rs, int8_t k) {
+  unsigned long long* st = bs + (row >> 6) * 4;
+  if (rs) atomicOr(st, 1ull << (row & 63));
+  if (k >= 0) atomicAdd(st + 1 + (k >> 1), 1ull << (32 * (k & 1)));
+}
+// host form of the same accumulation (the X2 evolve on CPU tensors)
+inline void bs_publish_host(unsigned long long* bs, int64_t row, bool rs, int8_t k) {
+  unsigned long long* st = bs + (row >> 6) * 4;
+  if (rs) __atomic_fetch_or(st, 1ull << (row & 63), __ATOMIC_RELAXED);
+  if (k >= 0) __atomic_fetch_add(st + 1 + (k >> 1), 1ull << (32 * (k & 1)), __ATOMIC_RELAXED);
+}
+// X2 local evolve: is row i remote-dependent this generation?
+SRNN_HD bool x2_dep(const SrnnArgs& a, int64_t i) { return (a.x_dep[i >> 5] >> (i & 31)) & 1u; }
+
+// Soup evolve (OP_SOUP_EVOLVE), one wave per block, lane per slot:
+//  * single rank / all-gather exchange: rows blockIdx * 64 + lane; each wave publishes its
+//    64-bit respawn ballot (ballots[block]) or per-row flags (rowflags, SRNN_F_ROW_FLAGS)
+//  * SRNN_F_X2, local: the same rows minus the remote-dependent ones (x_dep bits, reset
+//    here for the generation after next)
+//  * SRNN_F_X2 | SRNN_F_X2_REMOTE: the (row, teacher row) entries of x_rlist, grid-stride
+//    over a bounded grid; the last wave re-arms the list counter
+//  X2 evolves accumulate the generation's block stats (temp), with SRNN_F_FUSED_CENSUS the
+//  census class of each stored row too.
 template <class Net, class S>
 __global__ __launch_bounds__(TB) void k_soup_evolve(SrnnCfg c, SrnnArgs a) {
   using I = Item<Net, S>;
@@ -766,102 +765,63 @@ __global__ __launch_bounds__(TB) void k_soup_evolve(SrnnCfg c, SrnnArgs a) {
   constexpr int PERM = (P + 4) & ~3;
   __shared__ float4 s_samp[TB * SAMP];
   __shared__ uint8_t s_perm[TB * PERM];
-  const int64_t i = (int64_t)blockIdx.x * TB + threadIdx.x;
-  bool rs = false;
-  if (i < a.n) {
-    I::soup_evolve(c, a, i, s_samp + threadIdx.x, s_perm + threadIdx.x * PERM);
-    rs = a.respawn[i] != 0;
-  }
-  if (a.i32c) {
-    if (a.flags & 16) {
-      if (i < a.n) a.i32c[i] = rs ? 1 : 0;
-    } else {
-      unsigned long long m = __ballot(rs);
-      if (threadIdx.x == 0) reinterpret_cast<unsigned long long*>(a.i32c)[blockIdx.x] = m;
-    }
-  }
-}
-
-// ----------------------------------------------------------------------------------
-// Post-exchange work of a sharded generation folded into its generation launch (flag
-// 524288) instead of a separate launch between the all-to-all and the generation:
-//   workgroup 0        -- uids of the previous generation's newborns (stats rows of the
-//                         exchange: lower ranks' respawn counts; the previous generation's
-//                         ballots in temp2) + the global census + send-counter reset;
-//   workgroups 1..U    -- index the received rows (rmap[slot] = row, memory-side atomic
-//                         stores), then bump xdone;
-//   the rest           -- generation waves: the next generation's decisions first (they do
-//                         not need the received rows), then wait for xdone == U (bounded
-//                         spin, overflow flag 2 on timeout: never a hang), then evolve.
-// The unpack workgroups have the lowest block ids, so they are dispatched before any
-// generation wave can occupy the machine: the wait always ends.
-// ----------------------------------------------------------------------------------
-template <class Net, class S>
-__device__ void post_uids(const SrnnArgs& a) {
-  using I = Item<Net, S>;
   const int lane = threadIdx.x;
-  if (lane < a.world) a.sendcnt[lane] = I::SR;  // the finish launch packs the next exchange
-  int64_t pre = 0, tot = 0;
-  if (lane == 0) {
-    int64_t cen[5] = {0, 0, 0, 0, 0}, all = 0;
-    for (int r = 0; r < a.world; ++r) {
-      const int64_t k = I::stat(a, r, 5);
-      if (r < a.rank) pre += k;
-      tot += k;
-      for (int q = 0; q < 5; ++q) cen[q] += I::stat(a, r, q);
+  float4* samp = s_samp + lane;
+  uint8_t* perm = s_perm + lane * PERM;
+  const bool census = (a.flags & SRNN_F_FUSED_CENSUS) != 0;
+  auto classify_stored = [&](int64_t i) -> int8_t {
+    float w[P];
+    I::load(I::rowp(a.W, i), w);
+    return I::classify_w(w, a.eps, (a.flags & SRNN_F_FIX_SEC) != 0,
+                         I::actx(a, c, (uint64_t)(a.lo + i), 0x7FFFFFF0u, perm));
+  };
+  if (!(a.flags & SRNN_F_X2)) {
+    const int64_t i = (int64_t)blockIdx.x * TB + lane;
+    bool rs = false;
+    if (i < a.n) rs = I::soup_evolve(c, a, i, samp, perm) != 0;
+    if (a.flags & SRNN_F_ROW_FLAGS) {
+      if (i < a.n && a.rowflags) a.rowflags[i] = rs ? 1 : 0;
+    } else if (a.ballots) {
+      const unsigned long long m = __ballot(rs);
+      if (lane == 0) a.ballots[blockIdx.x] = m;
     }
-    for (int q = 0; q < 5; ++q) all += cen[q];
-    if (a.census && all > 0)
-      for (int q = 0; q < 5; ++q) a.census[q] = cen[q];
+    return;
   }
-  pre = __shfl(pre, 0);
-  tot = __shfl(tot, 0);
-  unsigned long long* masks = reinterpret_cast<unsigned long long*>(a.temp2);
-  const int64_t nb = (a.n + TB - 1) / TB, ch = (nb + TB - 1) / TB;
-  const int64_t b0 = (int64_t)lane * ch, b1 = b0 + ch < nb ? b0 + ch : nb;
-  int32_t cnt = 0;
-  for (int64_t b = b0; b < b1; ++b) cnt += __popcll(masks[b * 4]);
-  int32_t incl = cnt;
-#pragma unroll
-  for (int off = 1; off < TB; off <<= 1) {
-    const int32_t v = __shfl_up(incl, off);
-    if (lane >= off) incl += v;
+  unsigned long long* bs = reinterpret_cast<unsigned long long*>(a.temp);
+  if (!(a.flags & SRNN_F_X2_REMOTE)) {
+    const int64_t i = (int64_t)blockIdx.x * TB + lane;
+    const bool on = i < a.n && !x2_dep(a, i);
+    bool rs = false;
+    int8_t k = -1;
+    if (on) {
+      rs = I::soup_evolve(c, a, i, samp, perm) != 0;
+      if (census) k = classify_stored(i);
+    }
+    // this wave's two dependency words are consumed (every lane read its bit above)
+    const int64_t wd = (int64_t)blockIdx.x * 2 + lane;
+    if (lane < 2 && wd * 32 < a.n) a.x_dep[wd] = 0u;
+    bs_publish_wave(bs, blockIdx.x, rs, k);
+    return;
   }
-  const int64_t base = *(volatile const int64_t*)a.uid_base;
-  int64_t u = base + pre + incl - cnt;
-  for (int64_t b = b0; b < b1 && cnt; ++b) {
-    unsigned long long m = masks[b * 4];
-    masks[b * 4] = 0ull;
-    while (m) {
-      const int bit = __ffsll((long long)m) - 1;
-      m &= m - 1;
-      a.uid_out[b * TB + bit] = u++;
+  const int64_t cnt = *(volatile const int32_t*)a.x_rcount;
+  for (int64_t base = (int64_t)blockIdx.x * TB; base < cnt; base += (int64_t)gridDim.x * TB) {
+    const int64_t q = base + lane;
+    if (q < cnt) {
+      const int64_t j = a.x_rlist[2 * q];
+      const uint32_t tk = a.x_rlist[2 * q + 1];
+      const bool rs = I::soup_evolve(c, a, j, samp, perm, tk) != 0;
+      const int8_t k = census ? classify_stored(j) : (int8_t)-1;
+      bs_publish_lane(bs, j, rs, k);
     }
   }
-  if (lane == 0) ((int64_t*)a.uid_base)[0] = base + tot;
-}
-template <class Net, class S>
-__device__ void post_unpack(const SrnnArgs& a, int64_t k) {
-  using I = Item<Net, S>;
-  if (k < (int64_t)a.world * a.cap && k % a.cap >= I::SR) {
-    const int32_t* tag = reinterpret_cast<const int32_t*>(reinterpret_cast<const char*>(a.recvbuf) + k * I::XB + I::RB);
-    if (tag[1] == I::gen_of(a)) __hip_atomic_store(a.rmap + tag[0], (int32_t)k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's index stores are at memory
-  if (threadIdx.x == 0) __hip_atomic_fetch_add(a.xdone, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ void post_wait(const SrnnArgs& a, int32_t want) {
-  int32_t ok = 1;
-  if (threadIdx.x == 0) {
-    uint32_t it = 0;
-    while (__hip_atomic_load(a.xdone, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < want) {
-      __builtin_amdgcn_s_sleep(2);
-      if (++it > (1u << 24)) {  // ~1 s: report instead of hanging the GPU
-        ok = 0;
-        break;
-      }
-    }
-    if (!ok) atomic_or_i32(a.ovf, 2);
+  // last wave: the counter is free again (the list of the generation after next appends to it;
+  // no data is handed over, every wave read the counter before its ticket)
+  int32_t prev = 0;
+  if (lane == 0) prev = atomicAdd(a.x_ctl + 3, 1);
+  prev = __shfl(prev, 0);
+  if (prev == (int32_t)gridDim.x - 1 && lane == 0) {
+    *a.x_rcount = 0;
+    a.x_ctl[3] = 0;
   }
 }
 
@@ -869,14 +829,16 @@ __device__ __forceinline__ void post_wait(const SrnnArgs& a, int32_t want) {
 // Fused single-rank soup generation (OP_SOUP_GEN): ONE launch per generation instead of
 // decide -> evolve -> respawn -> classify.  Per lane: the generation (attacks received,
 // learn_from, self-train, respawn + inline re-init), then the NEXT generation's decision
-// for its slot linked into the other list buffer (i32a = head, i32b = next; the decisions
+// for its slot linked into the other list buffer (heads_next / nexts_next; the decisions
 // are a pure function of (seed, slot, generation)), then the census class of the stored
-// row.  Each wave publishes its respawn ballot + class counts (temp: u64[4] per block)
-// and bumps a done counter (i32d[0]) with an agent-scope atomic; the LAST wave to
-// finish (no waiting anywhere: every wave exits) scans the ballots in slot order, assigns
-// the globally sequential uids of the newborns, writes the census (counts[0..4]),
-// advances next_uid and the generation counter and re-arms the done counter.
-// flags: 1024 = census on (FIX_SEC bit 8 = with second-order fixpoints).
+// row.  Each wave publishes its respawn ballot + class counts (temp: u64[4] per block).
+//  * SRNN_F_TWO_PHASE: plain stores; a finish launch (k_gen_finish / the batched finish)
+//    numbers the newborns and reduces the census after the kernel boundary
+//    (SRNN_F_GEN_COUNTS: this launch advances the generation counter itself;
+//    SRNN_F_BORN_TOTAL: it also adds its newborn count after the block stats)
+//  * otherwise the LAST wave to finish (done ticket, no waiting anywhere) scans the
+//    ballots in slot order, assigns the newborns' uids, writes the census (counts[0..4]),
+//    advances next_uid and the generation counter and re-arms the ticket.
 // ----------------------------------------------------------------------------------
 template <class Net, class S>
 __global__ __launch_bounds__(TB) void k_soup_gen(SrnnCfg c, SrnnArgs a) {
@@ -886,71 +848,29 @@ __global__ __launch_bounds__(TB) void k_soup_gen(SrnnCfg c, SrnnArgs a) {
   constexpr int PERM = (P + 4) & ~3;
   __shared__ float4 s_samp[TB * SAMP];
   __shared__ uint8_t s_perm[TB * PERM];
-  const bool post = (a.flags & 524288) != 0;
-  int64_t xoff = 0;
-  int32_t nunpack = 0;
-  if (post) {
-    nunpack = (int32_t)(((int64_t)a.world * a.cap + TB - 1) / TB);
-    if (blockIdx.x == 0) {
-      post_uids<Net, S>(a);
-      return;
-    }
-    if ((int64_t)blockIdx.x <= nunpack) {
-      post_unpack<Net, S>(a, (int64_t)(blockIdx.x - 1) * TB + threadIdx.x);
-      return;
-    }
-    xoff = 1 + nunpack;
-  }
-  const int64_t gb = (int64_t)blockIdx.x - xoff;  // generation block: rows gb*64 ..
+  const int64_t gb = blockIdx.x;  // rows gb*64 ..
   const int64_t i = gb * TB + threadIdx.x;
   const int lane = threadIdx.x;
   uint8_t* perm = s_perm + lane * PERM;
   const int32_t gen = I::gen_of(a);
-  const bool census = (a.flags & 1024) != 0;
-  const bool pre = (a.flags & 131072) != 0;
-  if (pre) {
-    const int64_t nb_main = (a.n + TB - 1) / TB;
-    if (gb >= nb_main) {
-      // helper workgroup: work only where fewer than two generation waves share the SIMD
-      int32_t cnt = 0;
-      if (lane == 0) cnt = __hip_atomic_load(a.helper_ctl + 1 + simd_slot(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      cnt = __shfl(cnt, 0);
-      if (cnt < 2) perm_drain<Net, S>(a, gen + 1);
-      return;
-    }
-    if (lane == 0) atomicAdd(a.helper_ctl + 1 + simd_slot(), 1);
-  }
+  const bool census = (a.flags & SRNN_F_FUSED_CENSUS) != 0;
   bool rs = false;
   int8_t k = -1;
-  if (i < a.n && (a.flags & 4096)) {
-    // sharded: the next generation's decisions of EVERY global slot (this lane takes
-    // slots i, i + n, ...): attack lists of local victims + need masks for the pack.
-    // First: they need nothing from the exchange, so they overlap the unpack workgroups
-    for (int64_t g = i; g < a.n_total; g += a.n) {
-      int32_t at, te;
-      I::decision(a, g, gen + 1, at, te);
-      I::link_decision(a, g, at, te, a.i32a, a.i32b);
-    }
-  }
-  if (post) post_wait(a, nunpack);
   if (i < a.n) {
-    I::soup_evolve(c, a, i, s_samp + lane, perm);
-    rs = a.respawn[i] != 0;
-    if (!(a.flags & 4096)) {
-      int32_t at, te;
-      I::decision(a, i, gen + 1, at, te);
-      if (at >= 0) a.i32b[i] = atomicExch(a.i32a + at, (int32_t)i);
-    }
+    rs = I::template soup_evolve<true>(c, a, i, s_samp + lane, perm) != 0;
+    int64_t at, te;
+    I::decision(a, i, gen + 1, at, te);
+    if (at >= 0) I::link(a.heads_next, a.nexts_next, at, (uint32_t)i);
     if (census) {
       float w[P];
       I::load(I::rowp(a.W, i), w);
-      k = I::classify_w(w, a.eps, (a.flags & 8) != 0, I::actx(a, c, (uint64_t)(a.lo + i), 0x7FFFFFF0u, perm));
+      k = I::classify_w(w, a.eps, (a.flags & SRNN_F_FIX_SEC) != 0,
+                        I::actx(a, c, (uint64_t)(a.lo + i), 0x7FFFFFF0u, perm));
     }
   }
-  if ((a.flags & 65536) && gb == 0 && threadIdx.x == 0) {
-    // asynchronous finish: this launch advances the generation counter (the other ring
-    // slot: no block of this launch reads it) so the next generation needs nothing from
-    // the finish kernel, which runs beside it on a side stream
+  if ((a.flags & SRNN_F_GEN_COUNTS) && gb == 0 && threadIdx.x == 0) {
+    // this launch advances the generation counter (the other ring slot: no block of this
+    // launch reads it), so the next generation needs nothing from the finish launch
     I::set_gen(a, gen + 1);
   }
   const unsigned long long m = __ballot(rs);
@@ -963,17 +883,16 @@ __global__ __launch_bounds__(TB) void k_soup_gen(SrnnCfg c, SrnnArgs a) {
   // s_waitcnt vmcnt(0) before the relaxed ticket add; the last wave acquires once and
   // reads them with agent-scope atomic loads (MI355X_MICROARCH "Valid forms").
   unsigned long long* bs = reinterpret_cast<unsigned long long*>(a.temp);
-  if (a.flags & 2048) {  // two-phase: plain stores, k_gen_finish reads them after the kernel boundary
+  if (a.flags & SRNN_F_TWO_PHASE) {  // plain stores, the finish reads them after the kernel boundary
     if (lane == 0) {
       unsigned long long* mine = bs + gb * 4;
       mine[0] = m;
       mine[1] = (unsigned long long)cnt[0] | ((unsigned long long)cnt[1] << 32);
       mine[2] = (unsigned long long)cnt[2] | ((unsigned long long)cnt[3] << 32);
       mine[3] = (unsigned long long)cnt[4];
-      // flag 1048576: the generation's newborn count after the block stats (batched finish)
-      if ((a.flags & 1048576) && m) atomicAdd(bs + ((a.n + TB - 1) / TB) * 4, (unsigned long long)__popcll(m));
+      // the generation's newborn count after the block stats (batched finish)
+      if ((a.flags & SRNN_F_BORN_TOTAL) && m) atomicAdd(bs + ((a.n + TB - 1) / TB) * 4, (unsigned long long)__popcll(m));
     }
-    if (pre) perm_drain<Net, S>(a, gen + 1);  // whatever the helpers left
     return;
   }
   int32_t prev = 0;
@@ -986,10 +905,10 @@ __global__ __launch_bounds__(TB) void k_soup_gen(SrnnCfg c, SrnnArgs a) {
                        __HIP_MEMORY_SCOPE_AGENT);
     __hip_atomic_store(mine + 3, (unsigned long long)cnt[4], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    prev = __hip_atomic_fetch_add(a.i32d, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    prev = __hip_atomic_fetch_add(a.done, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   prev = __shfl(prev, 0);
-  const int32_t nb = (int32_t)(gridDim.x - xoff);
+  const int32_t nb = (int32_t)gridDim.x;
   if (prev != nb - 1) return;
   // ---- last wave: census + sequential uids of the newborns (blocks in slot order)
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
@@ -1033,35 +952,35 @@ __global__ __launch_bounds__(TB) void k_soup_gen(SrnnCfg c, SrnnArgs a) {
     }
   }
   if (lane == 0) {
-    ((int64_t*)a.uid_base)[0] = base + total;
+    a.uid_base[0] = base + total;
     I::set_gen(a, gen + 1);
     if (a.counts) {
 #pragma unroll
       for (int q = 0; q < 5; ++q) a.counts[q] = census ? cs[q] : 0ull;
       a.counts[5] = (uint64_t)total;
     }
-    __hip_atomic_store(a.i32d, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // re-armed for the next launch
+    __hip_atomic_store(a.done, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // re-armed for the next launch
   }
 }
 
 // Inclusive scan over an NT-thread block: wave shuffles (no barrier) + one LDS pass over
 // the NT/64 wave totals (one barrier) instead of a log2(NT)-round Hillis-Steele scan with
 // two barriers per round.  *total receives the block sum.
-template <int NT>
-__device__ __forceinline__ int32_t block_incl_scan(int32_t v, int32_t* s_wave, int32_t* total) {
+template <int NT, class T = int32_t>
+__device__ __forceinline__ T block_incl_scan(T v, T* s_wave, T* total) {
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  int32_t x = v;
+  T x = v;
 #pragma unroll
   for (int off = 1; off < 64; off <<= 1) {
-    const int32_t y = __shfl_up(x, off);
+    const T y = __shfl_up(x, off);
     if (lane >= off) x += y;
   }
   if (lane == 63) s_wave[wv] = x;
   __syncthreads();
-  int32_t pre = 0, tot = 0;
+  T pre = 0, tot = 0;
 #pragma unroll
   for (int w = 0; w < NT / 64; ++w) {
-    const int32_t sw = s_wave[w];
+    const T sw = s_wave[w];
     pre += (w < wv) ? sw : 0;
     tot += sw;
   }
@@ -1069,41 +988,25 @@ __device__ __forceinline__ int32_t block_incl_scan(int32_t v, int32_t* s_wave, i
   return x + pre;
 }
 
-// Second phase of the two-phase fused generation: one SRNN_FINISH_NT-thread workgroup reduces the
-// per-wave census counts, scans the respawn ballots in slot order, assigns the newborns'
-// uids and advances next_uid / the generation counter.  Sharded (flag 4096): only the
-// counts (census + respawns, sent with the next exchange); uids wait for k_uid_assign.
+// Second phase of the two-phase fused single-rank generation: one SRNN_FINISH_NT-thread
+// workgroup reduces the per-wave census counts, scans the respawn ballots in slot order,
+// assigns the newborns' uids and advances next_uid / the generation counter.
 #ifndef SRNN_FINISH_NT
-#define SRNN_FINISH_NT 1024  // threads of the finish workgroup and its pack blocks (256: 7.27 us vs 6.68 us)
+#define SRNN_FINISH_NT 1024  // threads of the finish workgroup (256: 7.27 us vs 6.68 us)
 #endif
 template <class Net, class S, int NT>
 __global__ __launch_bounds__(NT) void k_gen_finish(SrnnArgs a, int32_t nb) {
   using I = Item<Net, S>;
-  if (blockIdx.x > 0) {
-    // flag 32768, blocks >= 1: pack the next generation's all-to-all (rows other ranks
-    // need; generation-start rows of gen + 1 = this generation's output).  Block 0 only
-    // writes the OTHER ring slot of the counter, so the gen read here is stable.
-    SrnnArgs pa = a;
-    pa.W2 = a.W;
-    pa.gen_ptr = nullptr;
-    pa.gen = I::gen_of(a) + 1;
-    const int64_t j = (int64_t)(blockIdx.x - 1) * NT + threadIdx.x;
-    if (j < a.n) I::soup_pack(pa, j);
-    return;
-  }
   __shared__ int32_t s_wave[NT / 64];
   __shared__ unsigned long long s_cs[5];
   const int t = threadIdx.x;
   if (t < 5) s_cs[t] = 0;
-  if (t == 0 && a.xdone) *a.xdone = 0;  // re-armed for the next generation's unpack workgroups
-  if ((a.flags & 131072) && a.helper_ctl)  // re-arm this parity's helper queue / SIMD counts
-    for (int q = t; q < HELPER_CTL; q += NT) a.helper_ctl[q] = 0;
   const unsigned long long* bs = reinterpret_cast<const unsigned long long*>(a.temp);
   // the uid base and the generation counter are only written by thread 0 after the last
   // barrier: load them up front so their latency overlaps the per-block stats loads
   const int64_t base = *(volatile const int64_t*)a.uid_base;
-  const bool async = (a.flags & 65536) != 0;  // the generation kernel advanced the counter
-  const int32_t gen = async ? 0 : I::gen_of(a);
+  const bool advanced = (a.flags & SRNN_F_GEN_COUNTS) != 0;  // the generation kernel advanced the counter
+  const int32_t gen = advanced ? 0 : I::gen_of(a);
   const int32_t ch = (nb + NT - 1) / NT;
   const int32_t b0 = t * ch, b1 = b0 + ch < nb ? b0 + ch : nb;
   int32_t born = 0;
@@ -1125,9 +1028,8 @@ __global__ __launch_bounds__(NT) void k_gen_finish(SrnnArgs a, int32_t nb) {
     for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
     if ((t & 63) == 0 && v) atomicAdd(&s_cs[q], v);
   }
-  const bool sharded = (a.flags & 4096) != 0;  // uids come after the exchange (k_uid_assign)
   int64_t u = base + incl - born;
-  for (int32_t b = b0; b < b1 && born && !sharded; ++b) {
+  for (int32_t b = b0; b < b1 && born; ++b) {
     unsigned long long mm = bs[(int64_t)b * 4];
     while (mm) {
       const int bit = __ffsll((long long)mm) - 1;
@@ -1137,14 +1039,12 @@ __global__ __launch_bounds__(NT) void k_gen_finish(SrnnArgs a, int32_t nb) {
   }
   __syncthreads();
   if (t == 0) {
-    const int32_t total = total_born;
-    if (!sharded) ((int64_t*)a.uid_base)[0] = base + total;
-    if (!async) I::set_gen(a, gen + 1);
+    a.uid_base[0] = base + total_born;
+    if (!advanced) I::set_gen(a, gen + 1);
     if (a.counts) {
-      for (int q = 0; q < 5; ++q) a.counts[q] = (a.flags & 1024) ? s_cs[q] : 0ull;
-      a.counts[5] = (uint64_t)total;
+      for (int q = 0; q < 5; ++q) a.counts[q] = (a.flags & SRNN_F_FUSED_CENSUS) ? s_cs[q] : 0ull;
+      a.counts[5] = (uint64_t)total_born;
     }
-    if (a.flags & 32768) I::pack_stats(a);  // this generation's stats ride on the next exchange
   }
 }
 
@@ -1199,7 +1099,7 @@ __global__ __launch_bounds__(NT) void k_gen_finish_batch(SrnnArgs a, int32_t nb,
     __syncthreads();
     if (t == 0) {
       s_base = base + total_born;
-      const bool census = (a.flags & 1024) != 0;
+      const bool census = (a.flags & SRNN_F_FUSED_CENSUS) != 0;
       if (a.counts && g == m - 1) {
         for (int q = 0; q < 5; ++q) a.counts[q] = census ? s_cs[q] : 0ull;
         a.counts[5] = (uint64_t)total_born;
@@ -1212,10 +1112,10 @@ __global__ __launch_bounds__(NT) void k_gen_finish_batch(SrnnArgs a, int32_t nb,
     // the next generation's scan reuses s_wave / s_cs: every thread past this iteration's reads
     __syncthreads();
   }
-  if (t == 0) ((int64_t*)a.uid_base)[0] = s_base;
+  if (t == 0) a.uid_base[0] = s_base;
 }
 
-// Parallel form of k_gen_finish_batch (a.i32d given: a zeroed done counter): ONE workgroup
+// Parallel form of k_gen_finish_batch (a.done given: a zeroed done counter): ONE workgroup
 // per generation of the batch.  Workgroup g counts the newborns of generations < g (its uid
 // base), reduces its own generation's census and numbers its newborns in slot order exactly
 // as the sequential walk does, but writes a uid only where no later generation of the batch
@@ -1236,7 +1136,7 @@ __global__ __launch_bounds__(NT) void k_gen_finish_par(SrnnArgs a, int32_t nb, i
   auto ring = [&](int32_t k) {
     return reinterpret_cast<const unsigned long long*>(reinterpret_cast<const char*>(a.temp) + (int64_t)k * a.temp_bytes);
   };
-  const bool totals = (a.flags & 1048576) != 0 && m <= NT;  // newborn count of generation k at ring(k)[4 nb]
+  const bool totals = (a.flags & SRNN_F_BORN_TOTAL) != 0 && m <= NT;  // newborns of generation k at ring(k)[4 nb]
   int32_t before = 0, all = 0;
   if (totals) {
     // thread k < m loads generation k's count: m loads in flight at once (a loop over k in
@@ -1293,7 +1193,7 @@ __global__ __launch_bounds__(NT) void k_gen_finish_par(SrnnArgs a, int32_t nb, i
   }
   __syncthreads();
   if (t == 0) {
-    const bool census = (a.flags & 1024) != 0;
+    const bool census = (a.flags & SRNN_F_FUSED_CENSUS) != 0;
     if (a.counts && g == m - 1) {
       for (int q = 0; q < 5; ++q) a.counts[q] = census ? s_cs[q] : 0ull;
       a.counts[5] = (uint64_t)total_born;
@@ -1304,61 +1204,30 @@ __global__ __launch_bounds__(NT) void k_gen_finish_par(SrnnArgs a, int32_t nb, i
     }
     // every workgroup read next_uid before its ticket: the last one may overwrite it
     __threadfence();
-    const int32_t prev = atomicAdd(a.i32d, 1);
+    const int32_t prev = atomicAdd(a.done, 1);
     if (prev == m - 1) {
-      ((int64_t*)a.uid_base)[0] = base + total_all;
+      a.uid_base[0] = base + total_all;
       if (totals)  // every workgroup has read the counts: re-armed for the next batch
         for (int32_t k = 0; k < m; ++k) const_cast<unsigned long long*>(ring(k))[(int64_t)nb * 4] = 0ull;
-      __hip_atomic_store(a.i32d, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(a.done, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
 }
 
-// SGD permutations of generation *gen_ptr for every local row into perm_next (OP_SOUP_PERMS:
-// the first precomputed generation; later ones come from the helper waves)
-template <class Net, class S>
-__global__ __launch_bounds__(256) void k_soup_perms(SrnnArgs a) {
-  using I = Item<Net, S>;
-  const int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (j < a.n) I::perm_fill(a, j, I::gen_of(a), a.perm_next);
-}
-template <class Net, class S>
-int soup_perms(const SrnnCfg&, const SrnnArgs& a) {
-  using I = Item<Net, S>;
-  if (!(Net::KIND == 0 && Net::P <= 16)) return 0;  // no per-epoch permutations to precompute
-  if (!a.perm_next || a.perm_e < 1) {
-    set_error("soup_perms needs perm_next and perm_e >= 1");
-    return -5;
-  }
-  if (!a.dev) {
-    for (int64_t j = 0; j < a.n; ++j) I::perm_fill(a, j, I::gen_of(a), a.perm_next);
-    return 0;
-  }
-  if (a.n <= 0) return 0;
-  hipLaunchKernelGGL((k_soup_perms<Net, S>), dim3((unsigned)((a.n + 255) / 256)), dim3(256), 0, (hipStream_t)a.stream, a);
-  hipError_t e = hipGetLastError();
-  if (e != hipSuccess) {
-    set_error(hipGetErrorString(e));
-    return -3;
-  }
-  return 0;
-}
-
-// Asynchronous finish of a single-rank fused generation (OP_GEN_FINISH, flag 65536): the
-// census reduction + uids of the generation whose block stats are in a.temp, launched on a
-// side stream after that generation and beside the next one (host: no-op, soup_gen did it).
+// Finish of single-rank fused generations (OP_GEN_FINISH): census + newborn uids of the
+// generation(s) whose block stats are in a.temp (host: no-op, soup_gen did it).
 template <class Net, class S>
 int gen_finish(const SrnnCfg&, const SrnnArgs& a) {
   if (!a.dev) return 0;
   const int64_t blocks = (a.n + TB - 1) / TB;
   if (blocks <= 0) return 0;
   constexpr int FNT = SRNN_FINISH_NT;
-  if (a.steps > 1 || (a.flags & 262144)) {  // batch of a.steps generations (ring in temp)
+  if (a.steps > 1 || (a.flags & SRNN_F_FINISH_BATCH)) {  // batch of a.steps generations (ring in temp)
     if (a.steps < 1 || a.temp_bytes < blocks * 32) {
       set_error("batched finish needs steps >= 1 generations and temp_bytes >= 32 per block");
       return -5;
     }
-    if (a.i32d)  // a zeroed done counter: one workgroup per generation
+    if (a.done)  // a zeroed done counter: one workgroup per generation
       hipLaunchKernelGGL((k_gen_finish_par<Net, S, FNT>), dim3((unsigned)a.steps), dim3(FNT), 0,
                          (hipStream_t)a.stream, a, (int32_t)blocks, a.steps);
     else
@@ -1374,9 +1243,6 @@ int gen_finish(const SrnnCfg&, const SrnnArgs& a) {
   }
   return 0;
 }
-
-template <class Net, class S>
-int uid_assign(const SrnnCfg& c, const SrnnArgs& a);
 
 // OP_SOUP_SEQ: `steps` sequential soup generations starting at generation *gen_ptr (or
 // a.gen) on a host table, one particle after another (the reference order is serial by
@@ -1401,7 +1267,7 @@ __global__ __launch_bounds__(TB) void k_soup_seq(SrnnCfg c, SrnnArgs a) {
       if (a.respawn && a.respawn[j]) a.uid_out[j] = next++;
     }
   }
-  ((int64_t*)a.uid_base)[0] = next;
+  a.uid_base[0] = next;
   I::set_gen(a, gen0 + a.steps);
 }
 
@@ -1426,7 +1292,7 @@ int soup_seq(const SrnnCfg& c, const SrnnArgs& a) {
       if (a.respawn && a.respawn[j]) a.uid_out[j] = next++;
     }
   }
-  ((int64_t*)a.uid_base)[0] = next;
+  a.uid_base[0] = next;
   I::set_gen(a, gen0 + a.steps);
   return 0;
 }
@@ -1434,80 +1300,49 @@ int soup_seq(const SrnnCfg& c, const SrnnArgs& a) {
 template <class Net, class S>
 int soup_gen(const SrnnCfg& c, const SrnnArgs& a) {
   using I = Item<Net, S>;
+  if (a.world > 1 || a.lo != 0 || a.n_total != a.n || a.n >= (int64_t)SRNN_NIL) {
+    set_error("fused soup generation: one unsharded table of < 2^32 rows");
+    return -5;
+  }
   if (!a.dev) {
     // host: the same steps in order (evolve all rows, link next decisions, census, uids)
-    if (a.flags & 524288) {
-      // post-exchange work first: previous generation's uids (ballots in temp2), received-row
-      // index, send-counter reset -- the device's workgroup 0 and unpack workgroups
-      SrnnArgs ua = a;
-      ua.flags = (a.flags & ~524288) | 16384 | 8192;
-      ua.temp = a.temp2;
-      ua.counts = nullptr;
-      uid_assign<Net, S>(c, ua);
-    }
     const int32_t gen = I::gen_of(a);
     host_parallel(a.n, [&](int64_t i) {
       float4 samp[Net::P + 1];
       uint8_t perm[Net::P + 4];
-      I::soup_evolve(c, a, i, samp, perm);
+      I::template soup_evolve<true>(c, a, i, samp, perm);
     });
-    if (a.flags & 4096) {
-      for (int64_t g = 0; g < a.n_total; ++g) {
-        int32_t at, te;
-        I::decision(a, g, gen + 1, at, te);
-        I::link_decision(a, g, at, te, a.i32a, a.i32b);
-      }
-    } else {
-      for (int64_t i = 0; i < a.n; ++i) {
-        int32_t at, te;
-        I::decision(a, i, gen + 1, at, te);
-        if (at >= 0) {
-          a.i32b[i] = a.i32a[at];
-          a.i32a[at] = (int32_t)i;
-        }
+    for (int64_t i = 0; i < a.n; ++i) {
+      int64_t at, te;
+      I::decision(a, i, gen + 1, at, te);
+      if (at >= 0) {
+        a.nexts_next[i] = a.heads_next[at];
+        a.heads_next[at] = (uint32_t)i;
       }
     }
     uint64_t cs[5] = {0, 0, 0, 0, 0};
-    if (a.flags & 1024) {
+    if (a.flags & SRNN_F_FUSED_CENSUS) {
       std::vector<int8_t> ks((size_t)a.n);
       host_parallel(a.n, [&](int64_t i) {
         float w[Net::P];
         uint8_t perm[Net::P + 4];
         I::load(I::rowp(a.W, i), w);
-        ks[(size_t)i] = I::classify_w(w, a.eps, (a.flags & 8) != 0, I::actx(a, c, (uint64_t)(a.lo + i), 0x7FFFFFF0u, perm));
+        ks[(size_t)i] = I::classify_w(w, a.eps, (a.flags & SRNN_F_FIX_SEC) != 0,
+                                      I::actx(a, c, (uint64_t)(a.lo + i), 0x7FFFFFF0u, perm));
       });
       for (int64_t i = 0; i < a.n; ++i) cs[ks[(size_t)i]]++;
     }
     int64_t u = a.uid_base[0], total = 0;
-    if (a.flags & 4096) {
-      // sharded: respawn ballots per 64-row block for k_uid_assign after the next exchange
-      unsigned long long* bs = reinterpret_cast<unsigned long long*>(a.temp);
-      for (int64_t b = 0; b < (a.n + TB - 1) / TB; ++b) bs[b * 4] = 0ull;
-      for (int64_t i = 0; i < a.n; ++i)
-        if (a.respawn[i]) {
-          bs[(i / TB) * 4] |= 1ull << (i % TB);
-          ++total;
-        }
-    } else {
-      for (int64_t i = 0; i < a.n; ++i)
-        if (a.respawn[i]) {
-          a.uid_out[i] = u++;
-          ++total;
-        }
-      ((int64_t*)a.uid_base)[0] = u;
-    }
+    for (int64_t i = 0; i < a.n; ++i)
+      if (a.respawn[i]) {
+        a.uid_out[i] = u++;
+        ++total;
+      }
+    a.uid_base[0] = u;
     I::set_gen(a, gen + 1);
     if (a.counts) {
       for (int q = 0; q < 5; ++q) a.counts[q] = cs[q];
       a.counts[5] = (uint64_t)total;
-    }
-    if (a.flags & 32768) {
-      I::pack_stats(a);
-      SrnnArgs pa = a;
-      pa.W2 = a.W;
-      pa.gen_ptr = nullptr;
-      pa.gen = gen + 1;
-      for (int64_t j = 0; j < a.n; ++j) I::soup_pack(pa, j);
     }
     return 0;
   }
@@ -1517,26 +1352,14 @@ int soup_gen(const SrnnCfg& c, const SrnnArgs& a) {
     set_error("grid too large");
     return -2;
   }
-  const int64_t helpers = (a.flags & 131072) ? (a.helpers > 0 ? a.helpers : 0) : 0;
-  int64_t xblocks = 0;
-  if (a.flags & 524288) {
-    if (!(a.flags & 4096) || !(a.flags & 2048) || !a.temp2 || !a.xdone || !a.rmap || !a.recvbuf || a.world > 64) {
-      set_error("post-exchange generation needs a sharded two-phase generation, temp2, xdone, rmap, recvbuf");
-      return -5;
-    }
-    xblocks = 1 + ((int64_t)a.world * a.cap + TB - 1) / TB;
-  }
-  if ((a.flags & 131072) && (!a.perm_cur || !a.perm_next || !a.helper_ctl || !(a.flags & 2048) || a.perm_e < 1)) {
-    set_error("precomputed permutations need perm_cur / perm_next / helper_ctl, perm_e >= 1 and a two-phase generation");
+  if (!a.temp || !a.heads_next || !a.nexts_next || (!(a.flags & SRNN_F_TWO_PHASE) && !a.done)) {
+    set_error("fused soup generation needs block stats (temp), the next lists and a done counter");
     return -5;
   }
-  hipLaunchKernelGGL((k_soup_gen<Net, S>), dim3((unsigned)(xblocks + blocks + helpers)), dim3(TB), 0,
-                     (hipStream_t)a.stream, c, a);
-  if ((a.flags & 2048) && !(a.flags & 65536)) {
+  hipLaunchKernelGGL((k_soup_gen<Net, S>), dim3((unsigned)blocks), dim3(TB), 0, (hipStream_t)a.stream, c, a);
+  if ((a.flags & SRNN_F_TWO_PHASE) && !(a.flags & SRNN_F_GEN_COUNTS)) {
     constexpr int FNT = SRNN_FINISH_NT;
-    const int64_t pack_blocks = (a.flags & 32768) ? (a.n + FNT - 1) / FNT : 0;
-    hipLaunchKernelGGL((k_gen_finish<Net, S, FNT>), dim3((unsigned)(1 + pack_blocks)), dim3(FNT), 0,
-                       (hipStream_t)a.stream, a, (int32_t)blocks);
+    hipLaunchKernelGGL((k_gen_finish<Net, S, FNT>), dim3(1), dim3(FNT), 0, (hipStream_t)a.stream, a, (int32_t)blocks);
   }
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) {
@@ -1568,13 +1391,13 @@ __global__ __launch_bounds__(TBC) void k_classify_count(SrnnCfg c, SrnnArgs a) {
   }
   __syncthreads();
   if (threadIdx.x < 5 && s_cnt[threadIdx.x]) atomicAdd(a.counts + threadIdx.x, (uint64_t)s_cnt[threadIdx.x]);
-  if (a.flags & 64) {  // respawns of this generation (sharded soup: uid prefix)
+  if (a.flags & SRNN_F_COUNT_RESPAWNS) {  // respawns of this generation (sharded soup: uid prefix)
     unsigned long long m = __ballot(i < a.n && a.respawn[i] != 0);
     if ((threadIdx.x & 63) == 0 && m) atomicAdd(a.counts + 5, (uint64_t)__popcll(m));
   }
   // sharded soup: the census closes the generation (no later kernel of this generation
   // reads the counter)
-  if ((a.flags & 512) && blockIdx.x == 0 && threadIdx.x == 0) I::set_gen(a, I::gen_of(a) + 1);
+  if ((a.flags & SRNN_F_GEN_ADVANCE) && blockIdx.x == 0 && threadIdx.x == 0) I::set_gen(a, I::gen_of(a) + 1);
 }
 
 // ----------------------------------------------------------------------------------
@@ -1654,7 +1477,7 @@ __global__ __launch_bounds__(TBG) void k_fix_group(SrnnCfg c, SrnnArgs a) {
         cl = all_of((-a.eps <= wk) && (wk <= a.eps)) ? C_FIX_ZERO : C_FIX_OTHER;
       } else {
         cl = C_OTHER;
-        if (a.flags & 8) {
+        if (a.flags & SRNN_F_FIX_SEC) {
           float x2[4] = {f1, c0, c1, c2};
           Net::Net::forward_only(w, x2, y);
           const float f2 = S::q(y[0]);
@@ -1668,8 +1491,7 @@ __global__ __launch_bounds__(TBG) void k_fix_group(SrnnCfg c, SrnnArgs a) {
 
 template <class Net, int OP, class S>
 int launch(const SrnnCfg& c, const SrnnArgs& a) {
-  int64_t items = (OP == OP_SOUP_DECIDE) ? a.n_total : (OP == OP_SOUP_UNPACK) ? (int64_t)a.world * a.cap : a.n;
-  if (OP == OP_SOUP_PACK && items < 1) items = 1;  // the stats rows are always written
+  const int64_t items = (OP == OP_SOUP_DECIDE) ? a.n_total : a.n;
   if (items <= 0) return 0;
   int64_t blocks = (items + TB - 1) / TB;
   if (blocks > 0x7fffffffLL) {
@@ -1693,6 +1515,14 @@ int launch(const SrnnCfg& c, const SrnnArgs& a) {
     }
   }
   if (OP == OP_SOUP_EVOLVE) {
+    if ((a.flags & SRNN_F_X2) && (a.flags & SRNN_F_X2_REMOTE)) {
+      // bounded grid over the remote-dependent list (its length is on the device)
+      blocks = blocks < X2_REMOTE_WAVES ? blocks : X2_REMOTE_WAVES;
+    }
+    if ((a.flags & SRNN_F_X2) && (!a.temp || !a.x_dep || !a.x_rlist || !a.x_rcount || !a.x_ctl)) {
+      set_error("X2 evolve needs block stats (temp), x_dep, x_rlist, x_rcount and x_ctl");
+      return -5;
+    }
     hipLaunchKernelGGL((k_soup_evolve<Net, S>), dim3((unsigned)blocks), dim3(TB), 0, st, c, a);
   } else if (OP == OP_CLASSIFY && a.counts) {
     hipLaunchKernelGGL((k_classify_count<Net, S>), dim3((unsigned)((items + TBC - 1) / TBC)), dim3(TBC), 0, st, c, a);
@@ -1710,13 +1540,35 @@ int launch(const SrnnCfg& c, const SrnnArgs& a) {
 // ==================================================================================
 // Host execution of the same per-item code (CPU tensors)
 // ==================================================================================
+// X2 evolve on the host: the local rows minus the remote-dependent ones, or the remote list;
+// same block-stats accumulation as the device kernels (census with SRNN_F_FUSED_CENSUS)
+template <class Net, class S, class EvolveFn, class ClassifyFn>
+void host_x2_evolve(const SrnnArgs& a, EvolveFn&& evolve, ClassifyFn&& classify) {
+  unsigned long long* bs = reinterpret_cast<unsigned long long*>(a.temp);
+  const bool census = (a.flags & SRNN_F_FUSED_CENSUS) != 0;
+  if (!(a.flags & SRNN_F_X2_REMOTE)) {
+    host_parallel(a.n, [&](int64_t i) {
+      if (x2_dep(a, i)) return;
+      const bool rs = evolve(i, SRNN_NIL) != 0;
+      bs_publish_host(bs, i, rs, census ? classify(i) : (int8_t)-1);
+    });
+    for (int64_t w = 0; w < (a.n + 31) / 32; ++w) a.x_dep[w] = 0u;
+    return;
+  }
+  const int64_t cnt = *a.x_rcount;
+  host_parallel(cnt, [&](int64_t q) {
+    const int64_t j = a.x_rlist[2 * q];
+    const bool rs = evolve(j, a.x_rlist[2 * q + 1]) != 0;
+    bs_publish_host(bs, j, rs, census ? classify(j) : (int8_t)-1);
+  });
+  *a.x_rcount = 0;
+}
+
 template <class Net, int OP, class S>
 int host_run(const SrnnCfg& c, const SrnnArgs& a) {
   using I = Item<Net, S>;
   constexpr int P = Net::P;
-  int64_t items = (OP == OP_SOUP_DECIDE) ? a.n_total : (OP == OP_SOUP_UNPACK) ? (int64_t)a.world * a.cap : a.n;
-  if (OP == OP_SOUP_UNPACK)
-    for (int r = 0; r < a.world; ++r) a.sendcnt[r] = I::SR;
+  const int64_t items = (OP == OP_SOUP_DECIDE) ? a.n_total : a.n;
   if (OP == OP_CLASSIFY && a.counts) {
     uint64_t local[5] = {0, 0, 0, 0, 0};
     std::vector<int8_t> ks((size_t)items);
@@ -1726,14 +1578,40 @@ int host_run(const SrnnCfg& c, const SrnnArgs& a) {
     });
     for (int64_t i = 0; i < items; ++i) local[ks[(size_t)i]]++;
     for (int q = 0; q < 5; ++q) a.counts[q] += local[q];
-    if (a.flags & 64)
+    if (a.flags & SRNN_F_COUNT_RESPAWNS)
       for (int64_t i = 0; i < items; ++i) a.counts[5] += a.respawn[i] != 0;
-    if (a.flags & 512) I::set_gen(a, I::gen_of(a) + 1);
+    if (a.flags & SRNN_F_GEN_ADVANCE) I::set_gen(a, I::gen_of(a) + 1);
     return 0;
   }
-  if (OP == OP_SOUP_PACK) {
-    I::pack_stats(a);
-    host_parallel(a.n, [&](int64_t i) { I::soup_pack(a, i); });
+  if (OP == OP_SOUP_EVOLVE) {
+    auto evolve = [&](int64_t i, uint32_t tk) -> int8_t {
+      float4 samp[P + 1];
+      uint8_t perm[P + 4];
+      return I::soup_evolve(c, a, i, samp, perm, tk);
+    };
+    if (a.flags & SRNN_F_X2) {
+      auto classify = [&](int64_t i) -> int8_t {
+        float w[P];
+        uint8_t perm[P + 4];
+        I::load(I::rowp(a.W, i), w);
+        return I::classify_w(w, a.eps, (a.flags & SRNN_F_FIX_SEC) != 0,
+                             I::actx(a, c, (uint64_t)(a.lo + i), 0x7FFFFFF0u, perm));
+      };
+      host_x2_evolve<Net, S>(a, evolve, classify);
+      return 0;
+    }
+    host_parallel(a.n, [&](int64_t i) { evolve(i, SRNN_NIL); });
+    if (a.flags & SRNN_F_ROW_FLAGS) {
+      if (a.rowflags)
+        for (int64_t i = 0; i < a.n; ++i) a.rowflags[i] = a.respawn[i] != 0 ? 1 : 0;
+    } else if (a.ballots) {
+      for (int64_t b = 0; b < (a.n + TB - 1) / TB; ++b) {
+        unsigned long long m = 0;
+        for (int64_t i = b * TB; i < a.n && i < (b + 1) * TB; ++i)
+          if (a.respawn[i]) m |= 1ull << (i - b * TB);
+        a.ballots[b] = m;
+      }
+    }
     return 0;
   }
   host_parallel(items, [&](int64_t i) {
@@ -1747,16 +1625,13 @@ int host_run(const SrnnCfg& c, const SrnnArgs& a) {
     else if constexpr (OP == OP_TRAIN) I::train(c, a, i, samp, perm, false);
     else if constexpr (OP == OP_LEARN) I::train(c, a, i, samp, perm, true);
     else if constexpr (OP == OP_PERTURB) I::perturb(c, a, i, samp, perm);
-    else if constexpr (OP == OP_SOUP_EVOLVE) I::soup_evolve(c, a, i, samp, perm);
     else if constexpr (OP == OP_RESPAWN) I::respawn(a, i);
     else if constexpr (OP == OP_VARY_RUN) I::vary_run(c, a, i, samp, perm);
-    else if constexpr (OP == OP_SOUP_PACK) I::soup_pack(a, i);
-    else if constexpr (OP == OP_SOUP_UNPACK) I::soup_unpack(a, i);
   });
   return 0;
 }
 
-// Single-rank respawn: one 1024-thread workgroup scans the respawn flags in slot
+// Single-rank respawn: one 1024-thread workgroup scans the respawn ballots in slot
 // order, assigns the new uids (*uid_base is next_uid), re-initialises those rows, then
 // advances next_uid and the generation counter -- replacing scan + torch bookkeeping
 // kernels with one launch (the flags are sparse; each thread walks a contiguous chunk).
@@ -1765,9 +1640,9 @@ template <class Net, class S>
 __global__ __launch_bounds__(TBR) void k_respawn_seq(SrnnCfg c, SrnnArgs a) {
   using I = Item<Net, S>;
   __shared__ int32_t s_wave[TBR / 64];
-  // i32c as u64[b] = respawn ballot of evolve block b (64 rows); thread t owns blocks
+  // ballots[b] = respawn ballot of evolve block b (64 rows); thread t owns blocks
   // [t*ch, (t+1)*ch): no per-row memory traffic, bits give the rows in slot order.
-  const unsigned long long* masks = reinterpret_cast<const unsigned long long*>(a.i32c);
+  const unsigned long long* masks = a.ballots;
   const int64_t nb = (a.n + TB - 1) / TB;
   const int64_t ch = (nb + TBR - 1) / TBR;
   const int64_t b0 = (int64_t)threadIdx.x * ch;
@@ -1786,7 +1661,7 @@ __global__ __launch_bounds__(TBR) void k_respawn_seq(SrnnCfg c, SrnnArgs a) {
         m &= m - 1;
         const int64_t r = b * TB + bit;
         a.uid_out[r] = k;
-        if (!(a.flags & 32)) {  // flag 32: re-initialised inline by the evolve kernel
+        if (!(a.flags & SRNN_F_RESPAWN_INLINE)) {
           float w[Net::P];
           Net::init(w, I::rng(a), respawn_key(I::gen_of(a), a.lo + r));
           I::store(I::rowp(a.W, r), w);
@@ -1797,7 +1672,7 @@ __global__ __launch_bounds__(TBR) void k_respawn_seq(SrnnCfg c, SrnnArgs a) {
   }
   __syncthreads();
   if (threadIdx.x == 0) {
-    ((int64_t*)a.uid_base)[0] = base + total;
+    a.uid_base[0] = base + total;
     I::set_gen(a, I::gen_of(a) + 1);
   }
   if (a.counts && threadIdx.x < 5) a.counts[threadIdx.x] = 0;  // fresh histogram for the census
@@ -1819,133 +1694,17 @@ int respawn_seq(const SrnnCfg& c, const SrnnArgs& a) {
   for (int64_t i = 0; i < a.n; ++i) {
     if (a.respawn[i] == 0) continue;
     a.uid_out[i] = k;
-    if (!(a.flags & 32)) {
+    if (!(a.flags & SRNN_F_RESPAWN_INLINE)) {
       float w[Net::P];
       Net::init(w, I::rng(a), respawn_key(I::gen_of(a), a.lo + i));
       I::store(I::rowp(a.W, i), w);
     }
     ++k;
   }
-  ((int64_t*)a.uid_base)[0] = k;
+  a.uid_base[0] = k;
   I::set_gen(a, I::gen_of(a) + 1);
   if (a.counts)
     for (int q = 0; q < 5; ++q) a.counts[q] = 0;
-  return 0;
-}
-
-// Sharded soup: uids of the newborns of the previous generation.  The per-rank stats
-// (the exchange's stats rows, flag 256, or the gathered [world][6] array) give the
-// respawn counts of lower ranks (globally sequential uids, reference S13) and the global
-// census; the 64-bit respawn ballots of the evolve waves give the local order.  Consumes
-// the ballots (zeroed), advances next_uid (*uid_base) and zeroes counts[0..5]; with no
-// stats pending (all zero) it is a no-op apart from that.
-template <class Net, class S>
-__global__ __launch_bounds__(TBR) void k_uid_assign(SrnnCfg c, SrnnArgs a) {
-  using I = Item<Net, S>;
-  __shared__ int32_t s_wave[TBR / 64];
-  __shared__ int64_t s_prefix, s_total;
-  if (blockIdx.x > 0) {
-    // flag 16384, blocks >= 1: index the received rows (OP_SOUP_UNPACK); block 0 resets
-    // the send counters (the pack that used them ran in an earlier launch)
-    const int64_t k = (int64_t)(blockIdx.x - 1) * TBR + threadIdx.x;
-    if (k < (int64_t)a.world * a.cap) I::soup_unpack(a, k);
-    return;
-  }
-  if ((a.flags & 16384) && threadIdx.x < a.world) a.sendcnt[threadIdx.x] = I::SR;
-  if (threadIdx.x == 0) {
-    int64_t pre = 0, tot = 0, cen[5] = {0, 0, 0, 0, 0}, all = 0;
-    for (int r = 0; r < a.world; ++r) {
-      const int64_t k = I::stat(a, r, 5);
-      if (r < a.rank) pre += k;
-      tot += k;
-      for (int q = 0; q < 5; ++q) cen[q] += I::stat(a, r, q);
-    }
-    for (int q = 0; q < 5; ++q) all += cen[q];
-    s_prefix = pre;
-    s_total = tot;
-    if (a.census && all > 0)
-      for (int q = 0; q < 5; ++q) a.census[q] = cen[q];
-  }
-  // 64-bit respawn ballot of evolve wave b: i32c as u64[b], or the fused generation's
-  // block stats (flag 8192: u64[4] per block, ballot first)
-  unsigned long long* masks = reinterpret_cast<unsigned long long*>((a.flags & 8192) ? a.temp : (void*)a.i32c);
-  const int mstride = (a.flags & 8192) ? 4 : 1;
-  const int64_t nb = (a.n + TB - 1) / TB;
-  const int64_t ch = (nb + TBR - 1) / TBR;
-  const int64_t b0 = (int64_t)threadIdx.x * ch;
-  const int64_t b1 = b0 + ch < nb ? b0 + ch : nb;
-  int32_t cnt = 0;
-  for (int64_t b = b0; b < b1; ++b) cnt += __popcll(masks[b * mstride]);
-  int32_t total_local;
-  const int32_t incl = block_incl_scan<TBR>(cnt, s_wave, &total_local);  // barrier inside
-  const int64_t base = *(volatile const int64_t*)a.uid_base;
-  int64_t k = base + s_prefix + incl - cnt;
-  for (int64_t b = b0; b < b1 && cnt; ++b) {
-    unsigned long long m = masks[b * mstride];
-    masks[b * mstride] = 0ull;
-    while (m) {
-      const int bit = __ffsll((long long)m) - 1;
-      m &= m - 1;
-      a.uid_out[b * TB + bit] = k++;
-    }
-  }
-  __syncthreads();
-  if (threadIdx.x == 0) ((int64_t*)a.uid_base)[0] = base + s_total;
-  if (a.counts && threadIdx.x < 6) a.counts[threadIdx.x] = 0;
-}
-
-template <class Net, class S>
-int uid_assign(const SrnnCfg& c, const SrnnArgs& a) {
-  using I = Item<Net, S>;
-  if (a.dev) {
-    const int64_t unpack_blocks = (a.flags & 16384) ? ((int64_t)a.world * a.cap + TBR - 1) / TBR : 0;
-    hipLaunchKernelGGL((k_uid_assign<Net, S>), dim3((unsigned)(1 + unpack_blocks)), dim3(TBR), 0,
-                       (hipStream_t)a.stream, c, a);
-    hipError_t e = hipGetLastError();
-    if (e != hipSuccess) {
-      set_error(hipGetErrorString(e));
-      return -3;
-    }
-    return 0;
-  }
-  if (a.flags & 16384) {  // post-exchange: index the received rows too
-    for (int64_t k = 0; k < (int64_t)a.world * a.cap; ++k) I::soup_unpack(a, k);
-    for (int r = 0; r < a.world; ++r) a.sendcnt[r] = I::SR;
-  }
-  int64_t pre = 0, tot = 0, cen[5] = {0, 0, 0, 0, 0}, all = 0;
-  for (int r = 0; r < a.world; ++r) {
-    const int64_t k = I::stat(a, r, 5);
-    if (r < a.rank) pre += k;
-    tot += k;
-    for (int q = 0; q < 5; ++q) cen[q] += I::stat(a, r, q);
-  }
-  for (int q = 0; q < 5; ++q) all += cen[q];
-  if (a.census && all > 0)
-    for (int q = 0; q < 5; ++q) a.census[q] = cen[q];
-  // host path: per-row respawn flags in i32c (evolve with flag 16) or the fused
-  // generation's block ballots (flag 8192), consumed here
-  int64_t k = a.uid_base[0] + pre;
-  if (a.flags & 8192) {
-    unsigned long long* bs = reinterpret_cast<unsigned long long*>(a.temp);
-    for (int64_t b = 0; b < (a.n + TB - 1) / TB; ++b) {
-      unsigned long long m = bs[b * 4];
-      bs[b * 4] = 0ull;
-      while (m) {
-        const int bit = __builtin_ctzll(m);
-        m &= m - 1;
-        a.uid_out[b * TB + bit] = k++;
-      }
-    }
-  } else {
-    for (int64_t i = 0; i < a.n; ++i)
-      if (a.i32c[i]) {
-        a.uid_out[i] = k++;
-        a.i32c[i] = 0;
-      }
-  }
-  ((int64_t*)a.uid_base)[0] += tot;
-  if (a.counts)
-    for (int q = 0; q < 6; ++q) a.counts[q] = 0;
   return 0;
 }
 
@@ -1966,15 +1725,11 @@ int run_net_op(int op, const SrnnCfg& c, const SrnnArgs& a) {
     case OP_PERTURB: return run_one<Net, OP_PERTURB, S>(c, a);
     case OP_SOUP_DECIDE: return run_one<Net, OP_SOUP_DECIDE, S>(c, a);
     case OP_RESPAWN_SEQ: return respawn_seq<Net, S>(c, a);
-    case OP_SOUP_PACK: return run_one<Net, OP_SOUP_PACK, S>(c, a);
-    case OP_SOUP_UNPACK: return run_one<Net, OP_SOUP_UNPACK, S>(c, a);
-    case OP_UID_ASSIGN: return uid_assign<Net, S>(c, a);
     case OP_SOUP_EVOLVE: return run_one<Net, OP_SOUP_EVOLVE, S>(c, a);
     case OP_RESPAWN: return run_one<Net, OP_RESPAWN, S>(c, a);
     case OP_VARY_RUN: return run_one<Net, OP_VARY_RUN, S>(c, a);
     case OP_SOUP_GEN: return soup_gen<Net, S>(c, a);
     case OP_GEN_FINISH: return gen_finish<Net, S>(c, a);
-    case OP_SOUP_PERMS: return soup_perms<Net, S>(c, a);
     case OP_SOUP_SEQ: return soup_seq<Net, S>(c, a);
     default: set_error("unknown op"); return -1;
   }

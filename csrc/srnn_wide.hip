@@ -233,13 +233,13 @@ __global__ __launch_bounds__(WTB) void k_wide(SrnnCfg c, SrnnArgs a) {
       lds_store<T>(a.W + p * T::PP, L.f, lane);
       if (a.nsteps && lane == 0) a.nsteps[p] = s;
       if (a.cls) {
-        cls = wide_classify<T>(L, a.eps, (a.flags & 8) != 0, lane);
+        cls = wide_classify<T>(L, a.eps, (a.flags & SRNN_F_FIX_SEC) != 0, lane);
         if (lane == 0) a.cls[p] = cls;
       }
     } else if constexpr (OP == OP_CLASSIFY) {
       lds_load<T>(L.f, a.W + p * T::PP, lane);
       __builtin_amdgcn_wave_barrier();
-      cls = wide_classify<T>(L, a.eps, (a.flags & 8) != 0, lane);
+      cls = wide_classify<T>(L, a.eps, (a.flags & SRNN_F_FIX_SEC) != 0, lane);
       if (a.cls && lane == 0) a.cls[p] = cls;
     }
   }

@@ -2,9 +2,9 @@
 // under AddressSanitizer+UBSan (`make -C csrc asan`) or ThreadSanitizer (`make -C csrc
 // tsan`) (sanitizers on host code; GPU sanitizers are not available on the
 // pool).  It exercises every operator on host tables with the host thread pool, and
-// rehearses the sharded soup generation for R = 2 and 3 in one process (the all-to-all is
-// a memcpy between the ranks' buffers), checking bitwise equality with the single-rank
-// generation (the R-invariance the multi-GPU path relies on).
+// rehearses the sharded soup protocol (srnn_shard.hip) for R = 2 and 3 in one process (the
+// all-to-all is a memcpy between the ranks' buffers), checking bitwise equality with the
+// single-rank generation (the R-invariance the multi-GPU path relies on).
 #include "../srnn_abi.h"
 
 #include <cmath>
@@ -79,16 +79,16 @@ static void ops_smoke(const SrnnCfg& c, int64_t n) {
   b.W2 = O.data(), b.idx_f = idx.data();
   run(OP_APPLY, c, b);
   SrnnArgs t = a;
-  t.epochs = 3, t.flags = 1, t.loss = loss.data();
+  t.epochs = 3, t.flags = SRNN_F_SHUFFLE, t.loss = loss.data();
   run(OP_TRAIN, c, t);
   SrnnArgs l = t;
   l.W2 = O.data(), l.idx_t = idx.data();
   run(OP_LEARN, c, l);
   SrnnArgs f = a;
-  f.steps = 20, f.early_exit = 1, f.flags = 8, f.cls = cls.data(), f.nsteps = nsteps.data();
+  f.steps = 20, f.early_exit = 1, f.flags = SRNN_F_FIX_SEC, f.cls = cls.data(), f.nsteps = nsteps.data();
   run(OP_RUN_FIXPOINT, c, f);
   SrnnArgs k = a;
-  k.flags = 8, k.cls = cls.data(), k.counts = counts;
+  k.flags = SRNN_F_FIX_SEC, k.cls = cls.data(), k.counts = counts;
   run(OP_CLASSIFY, c, k);
   CHECK((int64_t)(counts[0] + counts[1] + counts[2] + counts[3] + counts[4]) == n);
   SrnnArgs p = a;
@@ -99,37 +99,49 @@ static void ops_smoke(const SrnnCfg& c, int64_t n) {
   run(OP_VARY_RUN, c, v);
 }
 
-// ---- one soup over R ranks (R = 1: the single-rank pipeline) --------------------------
+// ---- one soup over R ranks (R = 1: the single-rank pipeline; R > 1: the sharded
+// all-to-all protocol of srnn_shard.hip, the collective a memcpy between the ranks) -------
 struct RankSoup {
   int64_t lo, hi, n;
   std::vector<float> buf[2];
-  std::vector<int64_t> uid;
-  std::vector<int32_t> head, next_att, flags, need, sendcnt, rmap, ovf;
+  std::vector<int64_t> uid, census, next_uid, part, rslot[2], bstat[2];
+  std::vector<uint32_t> heads[2], nexts[2], dep[2], rlist[2], satt[2], srep;
+  std::vector<int32_t> rcount[2], cno[2], crq[2], nsrep, ctl, err, gen;
+  std::vector<unsigned long long> ballots;
   std::vector<int8_t> action, respawn;
-  std::vector<int64_t> counterpart, census, next_uid, stats;
-  std::vector<float> loss, sendbuf, recvbuf;
-  std::vector<int32_t> gen;
+  std::vector<int64_t> counterpart;
+  std::vector<float> loss;
+  std::vector<char> sendbuf, recvbuf;
   std::vector<uint64_t> counts;
 };
 
 static std::vector<float> soup(int R, int64_t N, int gens, std::vector<int64_t>* uids_out, int64_t* next_out) {
   const SrnnCfg c = ww22();
   const int PP = c.pp;
-  const int XB = PP * 4 + 16, SR = (48 + XB - 1) / XB, XW = XB / 4;
-  const int64_t cap = SR + N;  // generous: no overflow
+  const int64_t XB = PP * 4 + 16;
+  const int64_t cr = N, cn = N, cq = N;  // generous: no overflow
+  const int64_t blk = ((SRNN_X2_HDR * 8 + cr * XB + cn * 16 + cq * 8) + 15) / 16 * 16;
+  const int G = 2;
   std::vector<RankSoup> rk((size_t)R);
   for (int r = 0; r < R; ++r) {
     RankSoup& s = rk[(size_t)r];
     s.lo = r * N / R, s.hi = (r + 1) * N / R, s.n = s.hi - s.lo;
-    s.buf[0].assign((size_t)(s.n * PP), 0.f), s.buf[1].assign((size_t)(s.n * PP), 0.f);
+    const size_t nb = (size_t)((s.n + 63) / 64);
+    for (int q = 0; q < 2; ++q) {
+      s.buf[q].assign((size_t)(s.n * PP), 0.f);
+      s.heads[q].assign((size_t)s.n, SRNN_NIL), s.nexts[q].assign((size_t)(s.n + R * cr), SRNN_NIL);
+      s.dep[q].assign((size_t)(s.n / 32 + 1), 0u), s.rlist[q].assign((size_t)(2 * s.n + 2), 0u);
+      s.rcount[q].assign(1, 0), s.rslot[q].assign((size_t)(R * cr), 0), s.satt[q].assign((size_t)(R * cn), 0u);
+      s.cno[q].assign((size_t)R, 0), s.crq[q].assign((size_t)R, 0), s.bstat[q].assign(nb * 4, 0);
+    }
     s.uid.resize((size_t)s.n);
     for (int64_t j = 0; j < s.n; ++j) s.uid[(size_t)j] = s.lo + j;
-    s.head.assign((size_t)s.n, -1), s.next_att.assign((size_t)N, -1), s.flags.assign((size_t)(s.n + 2), 0);
-    s.need.assign((size_t)s.n, 0), s.sendcnt.assign((size_t)R, SR), s.rmap.assign((size_t)N, 0), s.ovf.assign(1, 0);
+    s.srep.assign((size_t)(R * cq), 0u), s.nsrep.assign((size_t)R, 0), s.ctl.assign(8, 0), s.err.assign(1, 0);
+    s.part.assign((size_t)(G * 6), 0), s.ballots.assign(nb + 1, 0ull);
     s.action.assign((size_t)s.n, 0), s.respawn.assign((size_t)s.n, 0), s.counterpart.assign((size_t)s.n, -1);
-    s.census.assign(5, 0), s.next_uid.assign(1, N), s.stats.assign((size_t)(6 * R), 0), s.loss.assign((size_t)s.n, 0.f);
-    s.sendbuf.assign((size_t)(R * cap * XW), 0.f), s.recvbuf.assign((size_t)(R * cap * XW), 0.f);
-    s.gen.assign(1, 1), s.counts.assign(6, 0);
+    s.census.assign(5, 0), s.next_uid.assign(1, N), s.loss.assign((size_t)s.n, 0.f);
+    s.sendbuf.assign((size_t)(R * blk), 0), s.recvbuf.assign((size_t)(R * blk), 0);
+    s.gen.assign(2, 1), s.counts.assign(6, 0);
     SrnnArgs a{};
     a.n = s.n, a.seed = 5, a.W = s.buf[0].data(), a.uid = s.uid.data();
     run(OP_INIT, c, a);
@@ -139,14 +151,52 @@ static std::vector<float> soup(int R, int64_t N, int gens, std::vector<int64_t>*
     SrnnArgs a{};
     a.n = s.n, a.n_total = N, a.lo = s.lo, a.seed = 5, a.lr = 0.01f, a.eps = 1e-4f;
     a.attacking_rate = 0.3f, a.learn_from_rate = 0.3f, a.epochs = 2, a.severity = 1;
-    a.flags = 1 | 2 | 4;
-    a.gen_ptr = s.gen.data();
+    a.flags = SRNN_F_SHUFFLE | SRNN_F_REMOVE_DIVERGENT | SRNN_F_REMOVE_ZERO;
+    a.gen_ptr = s.gen.data() + p, a.gen_out = s.gen.data() + (1 - p);
     a.W2 = s.buf[p].data(), a.W = s.buf[1 - p].data(), a.uid = s.uid.data();
-    a.i32e = s.head.data(), a.i32f = s.next_att.data(), a.i32c = s.flags.data();
+    a.heads = s.heads[p].data(), a.nexts = s.nexts[p].data(), a.ballots = s.ballots.data();
     a.action = s.action.data(), a.counterpart = s.counterpart.data(), a.loss = s.loss.data();
     a.respawn = s.respawn.data(), a.uid_out = s.uid.data(), a.counts = s.counts.data(), a.uid_base = s.next_uid.data();
     return a;
   };
+  auto xargs = [&](RankSoup& s, int r, int tp) {  // X2 fields, "this" = parity tp
+    SrnnArgs a = args(s);
+    const int q = 1 - tp;
+    a.world = R, a.rank = r, a.x_cr = cr, a.x_cn = cn, a.x_cq = cq, a.x_blk = blk;
+    a.sendbuf = s.sendbuf.data(), a.recvbuf = s.recvbuf.data(), a.census = s.census.data(), a.err = s.err.data();
+    a.heads = s.heads[tp].data(), a.nexts = s.nexts[tp].data(), a.heads_next = s.heads[q].data();
+    a.nexts_next = s.nexts[q].data(), a.x_dep = s.dep[tp].data(), a.x_dep_next = s.dep[q].data();
+    a.x_rlist = s.rlist[tp].data(), a.x_rlist_next = s.rlist[q].data(), a.x_rcount = s.rcount[tp].data();
+    a.x_rcount_next = s.rcount[q].data(), a.x_rslot = s.rslot[tp].data(), a.x_rslot_next = s.rslot[q].data();
+    a.x_satt = s.satt[tp].data(), a.x_satt_next = s.satt[q].data(), a.x_cno = s.cno[tp].data();
+    a.x_cno_next = s.cno[q].data(), a.x_crq = s.crq[tp].data(), a.x_crq_next = s.crq[q].data();
+    a.x_srep = s.srep.data(), a.x_nsrep = s.nsrep.data(), a.x_part = s.part.data(), a.x_ctl = s.ctl.data();
+    a.x_groups = G;
+    return a;
+  };
+  auto all_to_all = [&]() {  // block d of rank s's sendbuf -> block s of rank d's recvbuf
+    for (int src = 0; src < R; ++src)
+      for (int dst = 0; dst < R; ++dst)
+        std::memcpy(rk[(size_t)dst].recvbuf.data() + (size_t)src * blk, rk[(size_t)src].sendbuf.data() + (size_t)dst * blk,
+                    (size_t)blk);
+  };
+  if (R > 1) {  // prime: this generation's notices / requests (pointers "next" = this parity)
+    for (int r = 0; r < R; ++r) {
+      RankSoup& s = rk[(size_t)r];
+      SrnnArgs a = xargs(s, r, 1 - p);
+      a.W2 = s.buf[p].data(), a.temp = s.bstat[1 - p].data(), a.gen_ptr = nullptr, a.gen = s.gen[(size_t)p];
+      a.flags |= SRNN_F_X2_PRIME;
+      run(OP_X2_PACK, c, a);
+    }
+    all_to_all();
+    for (int r = 0; r < R; ++r) {
+      RankSoup& s = rk[(size_t)r];
+      SrnnArgs a = xargs(s, r, 1 - p);
+      a.temp = s.bstat[1 - p].data(), a.gen_ptr = nullptr, a.gen = s.gen[(size_t)p];
+      a.flags |= SRNN_F_X2_PRIME;
+      run(OP_X2_POST, c, a);
+    }
+  }
   for (int g = 0; g < gens; ++g) {
     if (R == 1) {
       RankSoup& s = rk[0];
@@ -157,47 +207,45 @@ static std::vector<float> soup(int R, int64_t N, int gens, std::vector<int64_t>*
     } else {
       for (int r = 0; r < R; ++r) {
         RankSoup& s = rk[(size_t)r];
-        SrnnArgs a = args(s);
-        a.world = R, a.rank = r, a.cap = cap, a.need = s.need.data(), a.sendcnt = s.sendcnt.data();
-        a.rmap = s.rmap.data(), a.ovf = s.ovf.data(), a.sendbuf = s.sendbuf.data(), a.recvbuf = s.recvbuf.data();
-        run(OP_SOUP_DECIDE, c, a);
-        run(OP_SOUP_PACK, c, a);
+        SrnnArgs a = xargs(s, r, p);
+        a.temp = s.bstat[1 - p].data();
+        run(OP_X2_PACK, c, a);
       }
-      // all-to-all: block d of rank s's sendbuf -> block s of rank d's recvbuf
-      for (int src = 0; src < R; ++src)
-        for (int dst = 0; dst < R; ++dst)
-          std::memcpy(rk[(size_t)dst].recvbuf.data() + (size_t)src * cap * XW,
-                      rk[(size_t)src].sendbuf.data() + (size_t)dst * cap * XW, (size_t)cap * XB);
+      all_to_all();
       for (int r = 0; r < R; ++r) {
         RankSoup& s = rk[(size_t)r];
-        SrnnArgs a = args(s);
-        a.world = R, a.rank = r, a.cap = cap, a.need = s.need.data(), a.sendcnt = s.sendcnt.data();
-        a.rmap = s.rmap.data(), a.ovf = s.ovf.data(), a.sendbuf = s.sendbuf.data(), a.recvbuf = s.recvbuf.data();
-        a.census = s.census.data();
-        run(OP_SOUP_UNPACK, c, a);
-        SrnnArgs u = a;
-        u.flags |= 256;
-        run(OP_UID_ASSIGN, c, u);
-        SrnnArgs e = a;
-        e.flags |= 32;
+        SrnnArgs a = xargs(s, r, p);
+        a.temp = s.bstat[1 - p].data();
+        run(OP_X2_POST, c, a);
+        SrnnArgs e = xargs(s, r, p);
+        e.temp = s.bstat[p].data();
+        e.flags |= SRNN_F_X2 | SRNN_F_RESPAWN_INLINE | SRNN_F_FUSED_CENSUS | SRNN_F_FIX_SEC;
+        SrnnArgs rem = e;
+        rem.flags |= SRNN_F_X2_REMOTE;
+        run(OP_SOUP_EVOLVE, c, rem);
         run(OP_SOUP_EVOLVE, c, e);
-        SrnnArgs k = a;
-        k.W = s.buf[1 - p].data(), k.flags = 8 | 64 | 512, k.ctr = 0x7FFFFFF0;
-        run(OP_CLASSIFY, c, k);
-        CHECK(s.ovf[0] == 0);
+        CHECK(s.err[0] == 0);
       }
     }
     p = 1 - p;
   }
-  if (R > 1) {  // flush: uids of the last generation's newborns (stats all-gather)
+  if (R > 1) {  // flush: finish-only pack -> stats all-gather -> uids of the last newborns
     std::vector<int64_t> all((size_t)(6 * R));
-    for (int r = 0; r < R; ++r)
-      for (int q = 0; q < 6; ++q) all[(size_t)(r * 6 + q)] = (int64_t)rk[(size_t)r].counts[(size_t)q];
     for (int r = 0; r < R; ++r) {
       RankSoup& s = rk[(size_t)r];
-      SrnnArgs a = args(s);
-      a.world = R, a.rank = r, a.stats = all.data(), a.census = s.census.data();
-      run(OP_UID_ASSIGN, c, a);
+      SrnnArgs a = xargs(s, r, p);
+      a.temp = s.bstat[1 - p].data();
+      a.flags |= SRNN_F_X2_FINISH_ONLY;
+      run(OP_X2_PACK, c, a);
+      std::memcpy(all.data() + r * 6, s.sendbuf.data(), 48);
+    }
+    for (int r = 0; r < R; ++r) {
+      RankSoup& s = rk[(size_t)r];
+      SrnnArgs a = xargs(s, r, p);
+      a.temp = s.bstat[1 - p].data(), a.stats = all.data();
+      a.flags |= SRNN_F_X2_FINISH_ONLY;
+      run(OP_X2_POST, c, a);
+      CHECK(s.census[0] + s.census[1] + s.census[2] + s.census[3] + s.census[4] == N);
     }
   }
   std::vector<float> W;
@@ -229,7 +277,8 @@ static void seq_soup(const SrnnCfg& c, int64_t n, int steps) {
   auto args = [&](int v) {
     SrnnArgs a{};
     a.n = a.n_total = n, a.seed = 11, a.lr = 0.01f, a.eps = 1e-4f;
-    a.attacking_rate = 0.3f, a.learn_from_rate = 0.3f, a.epochs = 2, a.severity = 2, a.flags = 1 | 2 | 4;
+    a.attacking_rate = 0.3f, a.learn_from_rate = 0.3f, a.epochs = 2, a.severity = 2;
+    a.flags = SRNN_F_SHUFFLE | SRNN_F_REMOVE_DIVERGENT | SRNN_F_REMOVE_ZERO;
     a.W = W[v].data(), a.gen_ptr = gen[v].data(), a.uid_base = next[v].data(), a.uid_out = uid[v].data();
     a.action = act.data(), a.counterpart = cp.data(), a.loss = loss.data(), a.respawn = rs.data();
     return a;
@@ -258,7 +307,7 @@ static void seq_soup(const SrnnCfg& c, int64_t n, int steps) {
 }
 
 int main() {
-  CHECK(srnn_abi_version() == 14);
+  CHECK(srnn_abi_version() == 15);
   seq_soup(ww22(), 257, 4);
   seq_soup(agg422(), 129, 3);
   ops_smoke(ww22(), 1000);

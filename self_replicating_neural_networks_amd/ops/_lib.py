@@ -20,8 +20,9 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 # SRNN_LIB: load another build of the library (A/B of compiler flags on the GPU box)
 LIB_PATH = os.environ.get("SRNN_LIB") or os.path.join(_HERE, "libsrnn.so")
 CSRC = os.path.normpath(os.path.join(_HERE, "..", "..", "csrc"))
-ABI_VERSION = 14
+ABI_VERSION = 15
 
+# SrnnOp (csrc/srnn_abi.h)
 OP_INIT = 0
 OP_APPLY = 1
 OP_RUN_FIXPOINT = 2
@@ -32,39 +33,39 @@ OP_PERTURB = 6
 OP_SOUP_DECIDE = 7
 OP_RESPAWN_SEQ = 8
 OP_SOUP_EVOLVE = 9
-OP_SCAN = 10
 OP_RESPAWN = 11
 OP_VARY_RUN = 12
-OP_SOUP_PACK = 13
-OP_SOUP_UNPACK = 14
 OP_UID_ASSIGN = 15
 OP_SOUP_GEN = 16
 OP_GEN_FINISH = 17
-OP_SOUP_PERMS = 18
-OP_SOUP_SEQ = 19  # host: sequential (Gauss-Seidel) soup generations
+OP_SOUP_SEQ = 19  # sequential (Gauss-Seidel) soup generations
+OP_X2_PACK = 20   # sharded soup, all-to-all exchange: finish + next decisions + rows (csrc/srnn_shard.hip)
+OP_X2_POST = 21   # sharded soup: uids, census, received notices / requests
 
-FLAG_SHUFFLE = 1
-FLAG_REMOVE_DIVERGENT = 2
-FLAG_REMOVE_ZERO = 4
-FLAG_FIX_SEC = 8
-FLAG_ROW_FLAGS = 16
-FLAG_RESPAWN_INLINE = 32
-FLAG_COUNT_RESPAWNS = 64
-FLAG_FULL_TABLE = 128
-FLAG_STATS_X = 256
-FLAG_GEN_ADVANCE = 512
-FLAG_FUSED_CENSUS = 1024
-FLAG_TWO_PHASE = 2048
-FLAG_SHARDED_DECIDE = 4096
-FLAG_MASKS_BS = 8192
-FLAG_POST_UNPACK = 16384
-FLAG_FINISH_PACK = 32768
-FLAG_ASYNC_FINISH = 65536
-FLAG_PRE_PERMS = 131072
-FLAG_FINISH_BATCH = 262144
-FLAG_GEN_POST = 524288   # sharded: uids + received-row index folded into the generation launch
-FLAG_BORN_TOTAL = 1048576  # batched finish: each generation keeps its newborn count after its block stats
-HELPER_CTL = 1 + 8192  # helper work-queue head + per-SIMD generation-wave counts (csrc/srnn_kernels.h)
+# SrnnFlag bits (csrc/srnn_abi.h: one meaning each)
+FLAG_SHUFFLE = 1 << 0
+FLAG_REMOVE_DIVERGENT = 1 << 1
+FLAG_REMOVE_ZERO = 1 << 2
+FLAG_FIX_SEC = 1 << 3
+FLAG_ROW_FLAGS = 1 << 4
+FLAG_RESPAWN_INLINE = 1 << 5
+FLAG_COUNT_RESPAWNS = 1 << 6
+FLAG_FULL_TABLE = 1 << 7
+FLAG_X2_PRIME = 1 << 8
+FLAG_GEN_ADVANCE = 1 << 9
+FLAG_FUSED_CENSUS = 1 << 10
+FLAG_TWO_PHASE = 1 << 11
+FLAG_MASKS_BS = 1 << 12
+FLAG_GEN_COUNTS = 1 << 13
+FLAG_FINISH_BATCH = 1 << 14
+FLAG_BORN_TOTAL = 1 << 15
+FLAG_X2 = 1 << 16
+FLAG_X2_REMOTE = 1 << 17
+FLAG_X2_FINISH_ONLY = 1 << 18
+
+X2_HDR = 12           # int64 header words of an exchange block
+X2_REMOTE_WAVES = 4096
+NIL = 0xFFFFFFFF      # end of an attack list
 
 
 class SrnnCfg(ctypes.Structure):
@@ -73,30 +74,37 @@ class SrnnCfg(ctypes.Structure):
 
 
 _P = ctypes.c_void_p
+_I64, _I32 = ctypes.c_int64, ctypes.c_int32
 
 
 class SrnnArgs(ctypes.Structure):
     _fields_ = [
-        ("n", ctypes.c_int64), ("n_total", ctypes.c_int64), ("lo", ctypes.c_int64),
-        ("steps", ctypes.c_int32), ("epochs", ctypes.c_int32), ("severity", ctypes.c_int32),
-        ("early_exit", ctypes.c_int32), ("flags", ctypes.c_int32), ("gen", ctypes.c_int32),
+        ("n", _I64), ("n_total", _I64), ("lo", _I64),
+        ("steps", _I32), ("epochs", _I32), ("severity", _I32),
+        ("early_exit", _I32), ("flags", ctypes.c_uint32), ("gen", _I32),
         ("eps", ctypes.c_float), ("lr", ctypes.c_float),
         ("attacking_rate", ctypes.c_float), ("learn_from_rate", ctypes.c_float),
         ("seed", ctypes.c_uint64), ("ctr", ctypes.c_uint32), ("pad0", ctypes.c_uint32),
         ("W", _P), ("W2", _P), ("traj", _P),
         ("idx_f", _P), ("idx_t", _P), ("idx_o", _P), ("uid", _P),
         ("cls", _P), ("nsteps", _P), ("loss", _P), ("counts", _P),
-        ("i32a", _P), ("i32b", _P), ("i32c", _P), ("i32d", _P), ("i32e", _P), ("i32f", _P),
-        ("uid_out", _P), ("uid_base", _P), ("gen_ptr", _P), ("segment", ctypes.c_int64),
-        ("world", ctypes.c_int32), ("rank", ctypes.c_int32), ("cap", ctypes.c_int64),
-        ("sendbuf", _P), ("recvbuf", _P), ("need", _P), ("sendcnt", _P), ("rmap", _P), ("ovf", _P),
-        ("stats", _P), ("census", _P),
+        # soup: decisions and attack lists
+        ("heads", _P), ("nexts", _P), ("heads_next", _P), ("nexts_next", _P),
+        ("dec_at", _P), ("dec_te", _P), ("ballots", _P), ("rowflags", _P), ("done", _P),
+        ("uid_out", _P), ("uid_base", _P), ("gen_ptr", _P), ("gen_out", _P), ("segment", _I64),
+        ("world", _I32), ("rank", _I32),
+        # sharded exchange
+        ("x_cr", _I64), ("x_cn", _I64), ("x_cq", _I64), ("x_blk", _I64),
+        ("sendbuf", _P), ("recvbuf", _P), ("stats", _P), ("census", _P), ("err", _P),
+        ("x_dep", _P), ("x_dep_next", _P), ("x_rlist", _P), ("x_rlist_next", _P),
+        ("x_rcount", _P), ("x_rcount_next", _P), ("x_rslot", _P), ("x_rslot_next", _P),
+        ("x_satt", _P), ("x_satt_next", _P), ("x_cno", _P), ("x_cno_next", _P),
+        ("x_crq", _P), ("x_crq_next", _P), ("x_srep", _P), ("x_nsrep", _P),
+        ("x_part", _P), ("x_ctl", _P), ("x_groups", _I32), ("pad2", _I32),
         ("action", _P), ("counterpart", _P), ("respawn", _P),
-        ("temp", _P), ("temp_bytes", ctypes.c_int64),
-        ("dev", ctypes.c_int32), ("pad1", ctypes.c_int32), ("stream", _P), ("gen_out", _P),
-        ("scratch", _P), ("scratch_bytes", ctypes.c_int64),
-        ("perm_cur", _P), ("perm_next", _P), ("helper_ctl", _P), ("perm_e", ctypes.c_int32),
-        ("helpers", ctypes.c_int32), ("temp2", _P), ("xdone", _P),
+        ("temp", _P), ("temp_bytes", _I64),
+        ("dev", _I32), ("pad1", _I32), ("stream", _P),
+        ("scratch", _P), ("scratch_bytes", _I64),
     ]
 
 
@@ -137,8 +145,6 @@ def lib():
         L.srnn_run.argtypes = [ctypes.c_int, ctypes.POINTER(SrnnCfg), ctypes.POINTER(SrnnArgs)]
         L.srnn_run.restype = ctypes.c_int
         L.srnn_last_error.restype = ctypes.c_char_p
-        L.srnn_scan_temp_bytes.argtypes = [ctypes.c_int64]
-        L.srnn_scan_temp_bytes.restype = ctypes.c_int64
         L.srnn_is_generic.argtypes = [ctypes.POINTER(SrnnCfg), ctypes.c_int]
         L.srnn_is_generic.restype = ctypes.c_int
         L.srnn_generic_scratch_bytes.argtypes = [ctypes.POINTER(SrnnCfg), ctypes.c_int64, ctypes.c_int64]
@@ -207,10 +213,6 @@ def run(op: int, spec, args: SrnnArgs, cfg: SrnnCfg = None, dtype: int = DTYPE_F
     if r != 0:
         msg = L.srnn_last_error().decode(errors="replace")
         raise NativeLibraryError(f"srnn op {op} failed ({r}): {msg} [spec={spec}]")
-
-
-def scan_temp_bytes(n: int) -> int:
-    return int(lib().srnn_scan_temp_bytes(int(n)))
 
 
 def last_error() -> str:

@@ -103,8 +103,9 @@ def run(cfg: ExperimentConfig, resume: bool = False, log=print):
     while eng.time < r.generations:
         k = min(seg or 1, r.generations - eng.time)
         eng.evolve(k)
-        if eng.exchange_overflowed():
-            raise RuntimeError("row exchange overflowed its capacity: raise the rates' headroom")
+        err = eng.exchange_error()  # all-reduced: every rank stops together
+        if err:
+            raise RuntimeError(f"soup row exchange failed: {err}")
         if r.checkpoint_dir and r.checkpoint_every > 0:
             path = write_checkpoint(eng, r.checkpoint_dir)
             if d.rank == 0:

@@ -113,14 +113,20 @@ class Soup(object):
         else:
             if self.engine is None:
                 self._seed_device()
+            shared_counter = self.dist is None or self.dist.world <= 1
+            if shared_counter:
+                # networks / soups created since the last evolve took uids from the process-wide
+                # counter (reference S13): newborns continue after them, never reuse them
+                self.engine.next_uid.clamp_(min=ParticleDecorator.next_uid)
             if self.mode == "native":
                 self.engine.evolve(iterations, record=self.record)
                 self.time += iterations
-                ParticleDecorator.next_uid = max(ParticleDecorator.next_uid, int(self.engine.next_uid[0]))
             else:
                 for _ in range(iterations):
                     self.time += 1
                     self.engine.evolve(1, record=self.record)
+            if shared_counter:
+                ParticleDecorator.next_uid = max(ParticleDecorator.next_uid, int(self.engine.next_uid[0]))
             self._refresh_views()
         return self
 

@@ -1,7 +1,8 @@
 """bench.py's driver contract, end to end on one MI355X: one JSON line from rank 0 with the
 BASELINE.json metric, whole-job value = particles x steps / max-rank time, for N=1 and for N=2
-launched by torch.distributed.run (2 ranks sharing cuda:0 over gloo: RCCL refuses two ranks
-on one device, so this rehearses the multi-rank control flow, not xGMI)."""
+-- launched by torch.distributed.run, and by bench.py itself when no launcher is around
+(2 ranks sharing cuda:0 over gloo: RCCL refuses two ranks on one device, so this rehearses the
+multi-rank control flow, not xGMI)."""
 import json
 import os
 import subprocess
@@ -45,3 +46,16 @@ def test_bench_two_ranks_torchrun_gloo_shared_device():
               "--master-addr", "127.0.0.1", "--master-port", "29633", "bench.py", "--gpus", "2", "--steps", "3",
               "--warmup", "1", "--particles-per-gpu", "20000", "--share-device", "--backend", "gloo"])
     _check(d, 2, 3, 1, 20000)
+
+
+@pytest.mark.gpu
+def test_bench_launches_its_own_ranks():
+    """--gpus 2 without torchrun's env: bench.py starts the ranks itself (child process)"""
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    p = subprocess.run([sys.executable, "bench.py", "--gpus", "2", "--steps", "3", "--warmup", "1",
+                        "--particles-per-gpu", "20000", "--share-device", "--backend", "gloo"],
+                       cwd=ROOT, env=env, capture_output=True, text=True, timeout=150)
+    assert p.returncode == 0, p.stderr[-3000:]
+    lines = [l for l in p.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, p.stdout[-2000:]
+    _check(json.loads(lines[0]), 2, 3, 1, 20000)

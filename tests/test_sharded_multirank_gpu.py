@@ -42,7 +42,7 @@ def _worker(rank, world, port, spec_json, out_dir, dtype, chunks):
         d = Dist(rank, world, 0, None)
         e = SoupEngine(ArchSpec.from_json(spec_json), N_TOTAL, PARAMS, device=dev, seed=21, dist=d,
                        dtype=DTYPES[dtype])
-        assert e.fused and e.post_in_gen
+        assert e.fused and e.x2 and e.overlap
         e.stats = True
         for k in chunks:
             e.evolve(k)
