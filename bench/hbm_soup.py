@@ -1,10 +1,13 @@
 #!/usr/bin/env python
 """BASELINE config 5 at HBM scale on one MI355X: a mixed learn+attack soup with fp16 weight
-tables, population sized to fill the GPU's 288 GB of HBM3E (up to the 2^31 - 2 slots one
-soup addresses), timed per generation, plus an optional streaming checkpoint -> resume round
-trip at that size (io/checkpoint.py format v2) checked bit-exactly.
+tables, population sized to fill the GPU's 288 GB of HBM3E, timed per generation, plus an
+optional streaming checkpoint -> resume round trip at that size (io/checkpoint.py format v2)
+checked bit-exactly.  ``--sharded`` runs the multi-GPU layout (the all-to-all exchange
+protocol of csrc/srnn_shard.hip: int64 slots, O(local) lists) forced at one rank, without the
+per-row diagnostic columns -- the configuration each of 8 ranks runs when the node's soup
+fills every GPU.
 
-  python bench/hbm_soup.py [--n N] [--gens G] [--fill 0.92] [--checkpoint DIR]
+  python bench/hbm_soup.py [--n N] [--gens G] [--fill 0.92] [--sharded] [--checkpoint DIR]
 
 One JSON line: particles, bytes per particle (measured), device memory in use (torch and
 rocm-smi), ms per generation, particle-generations/s, census, checkpoint timings."""
@@ -22,7 +25,8 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 from self_replicating_neural_networks_amd.arch import ArchSpec  # noqa: E402
 from self_replicating_neural_networks_amd.io import checkpoint as C  # noqa: E402
-from self_replicating_neural_networks_amd.soup_engine import MAX_SLOTS, SoupEngine  # noqa: E402
+from self_replicating_neural_networks_amd.parallel.dist import Dist  # noqa: E402
+from self_replicating_neural_networks_amd.soup_engine import MAX_SLOTS_DIRECT, SoupEngine  # noqa: E402
 
 PARAMS = dict(attacking_rate=0.1, learn_from_rate=0.1, learn_from_severity=1, train=10, remove_divergent=True,
               remove_zero=True, epsilon=1e-4)
@@ -72,21 +76,29 @@ def main():
     ap.add_argument("--gens", type=int, default=3)
     ap.add_argument("--fill", type=float, default=0.92)
     ap.add_argument("--checkpoint", default="")
+    ap.add_argument("--sharded", action="store_true", help="all-to-all layout forced at one rank")
     args = ap.parse_args()
+    if args.sharded:
+        import torch.distributed as dist
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29561")
+        dist.init_process_group("gloo", rank=0, world_size=1)
+    d = Dist(0, 1, 0, None, force=True) if args.sharded else None
+    kw = dict(dist=d, diagnostics=not args.sharded)
     dev = torch.device("cuda", 0)
     spec = ArchSpec.weightwise(2, 2)
     dtype = torch.float16
     # measured bytes per particle of the engine (tables, lists, uids, per-row state)
     probe_n = 1 << 20
     base = torch.cuda.memory_allocated(dev)
-    p = SoupEngine(spec, probe_n, PARAMS, device=dev, seed=0, dtype=dtype)
+    p = SoupEngine(spec, probe_n, PARAMS, device=dev, seed=0, dtype=dtype, **kw)
     bpp = (torch.cuda.memory_allocated(dev) - base) / probe_n
     del p
     torch.cuda.empty_cache()
     free, total = torch.cuda.mem_get_info(dev)
-    n = args.n or int(min(MAX_SLOTS, args.fill * free / bpp))
+    n = args.n or int(min(MAX_SLOTS_DIRECT if not args.sharded else 2 ** 32 - 2 ** 26, args.fill * free / bpp))
     t0 = time.perf_counter()
-    eng = SoupEngine(spec, n, PARAMS, device=dev, seed=0, dtype=dtype)
+    eng = SoupEngine(spec, n, PARAMS, device=dev, seed=0, dtype=dtype, **kw)
     eng.stats = True
     torch.cuda.synchronize(dev)
     t_init = time.perf_counter() - t0
@@ -98,7 +110,8 @@ def main():
     torch.cuda.synchronize(dev)
     dt = time.perf_counter() - t0
     res = dict(config=5, name="mixed learn+attack soup, fp16 tables, HBM-filling population (one MI355X)",
-               particles=n, params=PARAMS, dtype="float16", bytes_per_particle=bpp, hbm_total_bytes=total,
+               layout="sharded all-to-all (forced, 1 rank)" if args.sharded else "single rank", particles=n,
+               above_2_31=n > 2 ** 31, params=PARAMS, dtype="float16", bytes_per_particle=bpp, hbm_total_bytes=total,
                device_bytes_torch=mem_torch, device_bytes_peak=torch.cuda.max_memory_allocated(dev),
                vram_used_rocm_smi=smi_vram_used(), init_s=t_init, gens=args.gens,
                ms_per_generation=dt / args.gens * 1e3, particle_generations_per_s=n * args.gens / dt,
@@ -122,7 +135,7 @@ def main():
         del eng
         torch.cuda.empty_cache()
         t0 = time.perf_counter()
-        r = C.load_engine(ck, device=dev)
+        r = C.load_engine(ck, device=dev, dist=d, diagnostics=not args.sharded)
         r.stats = True
         torch.cuda.synchronize(dev)
         t_load = time.perf_counter() - t0

@@ -164,6 +164,8 @@ enum SrnnOp {
 };
 
 int srnn_abi_version();  // 15
+int64_t srnn_args_size();  // sizeof(SrnnArgs): the ctypes mirror checks its layout against it
+int64_t srnn_cfg_size();
 int srnn_has_config(const SrnnCfg* cfg);
 int srnn_run(int op, const SrnnCfg* cfg, const SrnnArgs* args);
 const char* srnn_last_error();

@@ -1762,8 +1762,10 @@ int big_run_s(int op, const SrnnCfg& c, const SrnnArgs& a) {
     case OP_LEARN: hipLaunchKernelGGL((k_big_rows<T, S, SHUF, OP_LEARN>), dim3(g64), dim3(TBROW), 0, st, c, a); break;
     case OP_SOUP_EVOLVE: {
       unsigned g = g64;
-      if ((a.flags & SRNN_F_X2) && (a.flags & SRNN_F_X2_REMOTE))  // bounded grid over the remote list
-        g = g < (unsigned)(X2_REMOTE_WAVES / 4) ? g : (unsigned)(X2_REMOTE_WAVES / 4);
+      if ((a.flags & SRNN_F_X2) && (a.flags & SRNN_F_X2_REMOTE)) {  // bounded grid over the remote list
+        const int64_t rb = (x2_remote_bound(a) + TBROW - 1) / TBROW;
+        g = (unsigned)(rb < X2_REMOTE_WAVES / 4 ? rb : X2_REMOTE_WAVES / 4);
+      }
       hipLaunchKernelGGL((k_big_soup_evolve<T, S, SHUF>), dim3(g), dim3(TBROW), 0, st, c, a);
       break;
     }

@@ -193,6 +193,10 @@ extern "C" {
 
 int srnn_abi_version() { return 15; }
 
+// layout check of the ctypes mirror (ops/_lib.py): sizeof(SrnnArgs) / sizeof(SrnnCfg)
+int64_t srnn_args_size() { return (int64_t)sizeof(SrnnArgs); }
+int64_t srnn_cfg_size() { return (int64_t)sizeof(SrnnCfg); }
+
 const char* srnn_last_error() { return srnn::g_err.c_str(); }
 
 int srnn_has_config(const SrnnCfg* cfg) {

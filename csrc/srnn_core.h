@@ -470,13 +470,6 @@ struct TrainCtx {
   bool shuffle;
   int stride;        // device: threads per block (slot-major, lane fastest: conflict-free b128)
   int aggregator;    // aggregating nets: samples come from the configured aggregator
-  // precomputed nibble permutations (P <= 16 nets in a fused soup generation): the
-  // permutation of epoch counter ctr is pre[(ctr - pre_ctr0) * pre_stride], k < pre_n;
-  // null -> computed here (Philox + Fisher-Yates).  Same values either way.
-  const unsigned long long* pre = nullptr;
-  int64_t pre_stride = 0;
-  uint32_t pre_ctr0 = 0;
-  int32_t pre_n = 0;
 };
 
 struct ApplyCtx {
@@ -524,12 +517,22 @@ struct Weightwise {
     }
   }
 
+  // Frozen SGD samples in the lane's scratch (LDS on the device, slot-major, lane fastest):
+  // P <= 16 keeps (value, coordinates) as float4 per sample (one b128 read per step);
+  // larger nets keep only the value per sample (4 B instead of 16 B of LDS per sample and
+  // lane: WW(4,3) drops from 53 KB to 13 KB per wave) and read the coordinates of the
+  // permuted sample from the constant table.
+  static constexpr int SAMP_F4 = P <= 16 ? P : (P + 3) / 4;  // float4 slots per lane
+
   // One Keras epoch of fit(x, y, batch_size=1, shuffle=True) on the samples of `s`
   // (x_k = point k of s, y_k = s[k]); samples frozen at epoch start. Returns mean loss.
   SRNN_HD static float train_epoch(float* __restrict__ w, const float* __restrict__ s, TrainCtx& c) {
+    float* sv = reinterpret_cast<float*>(c.samp);  // P > 16: values only
 #pragma unroll
-    for (int k = 0; k < P; ++k)
-      c.samp[k * c.stride] = make_float4(s[k], coords.c[k][0], coords.c[k][1], coords.c[k][2]);
+    for (int k = 0; k < P; ++k) {
+      if constexpr (P <= 16) c.samp[k * c.stride] = make_float4(s[k], coords.c[k][0], coords.c[k][1], coords.c[k][2]);
+      else sv[k * c.stride] = s[k];
+    }
     uint64_t pn = 0;
     if constexpr (P <= 16) {
       if (c.shuffle) pn = shuffle16<P>(c.rng, c.uid, c.ctr, P_SHUFFLE);
@@ -545,7 +548,9 @@ struct Weightwise {
       int idx;
       if constexpr (P <= 16) idx = (int)((pn >> (4 * q)) & 15u);
       else idx = c.shuffle ? (int)c.perm[q] : q;
-      float4 smp = c.samp[idx * c.stride];
+      float4 smp;
+      if constexpr (P <= 16) smp = c.samp[idx * c.stride];
+      else smp = make_float4(sv[idx * c.stride], coords.c[idx][0], coords.c[idx][1], coords.c[idx][2]);
       float x[4] = {smp.x, smp.y, smp.z, smp.w};
       float acts[Net::NACT], y[1];
       Net::forward(w, x, acts, y);
@@ -588,40 +593,6 @@ struct Weightwise {
 #pragma unroll
       for (int k = 0; k < P; ++k) ident |= (uint64_t)k << (4 * k);
       float loss = 0.f;
-      if (c.shuffle && c.pre) {
-        // permutations precomputed by the soup generation's helper waves: one 8-byte load
-        // per epoch, issued an epoch ahead (no Philox / Fisher-Yates on this lane)
-        auto pre_at = [&](uint32_t ctr) {
-          int32_t k = (int32_t)(ctr - c.pre_ctr0);
-          k = k < c.pre_n - 1 ? k : c.pre_n - 1;
-          return (uint64_t)c.pre[(int64_t)k * c.pre_stride];
-        };
-        uint64_t pn = pre_at(c.ctr);
-        for (int e = 0; e < E; ++e) {
-          if (SELF && e > 0)
-#pragma unroll
-            for (int k = 0; k < P; ++k) reinterpret_cast<float*>(&c.samp[k * c.stride])[0] = w[k];
-          const uint64_t pn_next = pre_at(c.ctr + 1u);
-          float4 smp[P];
-#pragma unroll
-          for (int q = 0; q < P; ++q) smp[q] = c.samp[(int)((pn >> (4 * q)) & 15u) * c.stride];
-          float acc = 0.f;
-#pragma unroll
-          for (int q = 0; q < P; ++q) {
-            float x[4] = {smp[q].x, smp[q].y, smp[q].z, smp[q].w};
-            float acts[Net::NACT], y[1];
-            Net::forward(w, x, acts, y);
-            float err = y[0] - smp[q].x;
-            acc += err * err;
-            float gy[1] = {2.0f * err};
-            Net::backward_update(w, acts, gy, c.lr);
-          }
-          loss = acc / (float)P;
-          c.ctr += 1;
-          pn = pn_next;
-        }
-        return loss;
-      }
       // one Philox draw per pair of epochs (c.ctr is the same for every lane: uniform branch)
       U4 rr = perm_draw(c.rng, c.uid, c.ctr, P_SHUFFLE);
       uint32_t pair = c.ctr >> 1;

@@ -1447,7 +1447,9 @@ static int generic_launch(int op, const GShape& s, const SrnnArgs& a) {
       case OP_SOUP_EVOLVE:
         if ((a.flags & SRNN_F_X2) && (a.flags & SRNN_F_X2_REMOTE)) {
           // the list length is on the device: a bounded grid-stride launch over the list
-          const int64_t rl = lanes < X2_REMOTE_WAVES * GTB ? lanes : X2_REMOTE_WAVES * GTB;
+          int64_t rl = ((x2_remote_bound(a) + GTB - 1) / GTB) * GTB;
+          rl = rl < lanes ? rl : lanes;
+          rl = rl < X2_REMOTE_WAVES * GTB ? rl : X2_REMOTE_WAVES * GTB;
           hipLaunchKernelGGL((k_generic<GOP_X2_REMOTE>), dim3((unsigned)(rl / GTB)), block, lds, st, s, a, rl);
           break;
         }

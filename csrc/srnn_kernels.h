@@ -64,6 +64,20 @@ SRNN_HD int32_t atomic_add_i32(int32_t* p, int32_t v) {
 #define SAMP_STRIDE 1
 #endif
 
+// float4 sample slots per lane of a net's training scratch (Weightwise::SAMP_F4; the other
+// kinds keep their samples in registers) and the lane's base pointer: float4 slots, or for
+// value-only samples (Weightwise P > 16) float slots, both slot-major with the lane fastest
+template <class Net>
+constexpr int samp_slots() {
+  if constexpr (Net::KIND == 0) return Net::SAMP_F4;
+  else return 1;
+}
+template <class Net>
+SRNN_HD float4* samp_lane(float4* base, int lane) {
+  if constexpr (Net::KIND == 0 && Net::P > 16) return reinterpret_cast<float4*>(reinterpret_cast<float*>(base) + lane);
+  else return base + lane;
+}
+
 SRNN_HD int32_t atomic_or_i32(int32_t* p, int32_t v) {
 #if defined(__HIP_DEVICE_COMPILE__)
   return atomicOr(p, v);
@@ -687,12 +701,12 @@ __global__ __launch_bounds__(TB) void k_op(SrnnCfg c, SrnnArgs a) {
   using I = Item<Net, S>;
   constexpr int P = Net::P;
   constexpr bool NEED_SAMP = (OP == OP_TRAIN || OP == OP_LEARN) && Net::KIND == 0;
-  constexpr int SAMP = NEED_SAMP ? P : 1;  // slot-major [P][TB]: lane fastest
+  constexpr int SAMP = NEED_SAMP ? samp_slots<Net>() : 1;  // slot-major [P][TB]: lane fastest
   constexpr int PERM = (P + 4) & ~3;
   __shared__ float4 s_samp[TB * SAMP];
   __shared__ uint8_t s_perm[TB * PERM];
   const int64_t i = (int64_t)blockIdx.x * TB + threadIdx.x;
-  float4* samp = s_samp + threadIdx.x;  // slot k of this lane at samp[k * TB]
+  float4* samp = samp_lane<Net>(s_samp, threadIdx.x);  // slot k of this lane at samp[k * TB]
   uint8_t* perm = s_perm + threadIdx.x * PERM;
 
   if constexpr (OP == OP_SOUP_DECIDE) {
@@ -747,6 +761,13 @@ inline void bs_publish_host(unsigned long long* bs, int64_t row, bool rs, int8_t
 }
 // X2 local evolve: is row i remote-dependent this generation?
 SRNN_HD bool x2_dep(const SrnnArgs& a, int64_t i) { return (a.x_dep[i >> 5] >> (i & 31)) & 1u; }
+// most entries the remote list of a generation can hold (a slot joins it through a received
+// notice or one of its requests): the remote evolve's grid is sized by this bound, not by n
+// (every wave of that launch takes one ticket on the re-arm counter)
+SRNN_HD int64_t x2_remote_bound(const SrnnArgs& a) {
+  const int64_t b = (int64_t)a.world * (a.x_cn + a.x_cq);
+  return b < a.n ? (b > 1 ? b : 1) : (a.n > 1 ? a.n : 1);
+}
 
 // Soup evolve (OP_SOUP_EVOLVE), one wave per block, lane per slot:
 //  * single rank / all-gather exchange: rows blockIdx * 64 + lane; each wave publishes its
@@ -761,12 +782,12 @@ template <class Net, class S>
 __global__ __launch_bounds__(TB) void k_soup_evolve(SrnnCfg c, SrnnArgs a) {
   using I = Item<Net, S>;
   constexpr int P = Net::P;
-  constexpr int SAMP = Net::KIND == 0 ? P : 1;
+  constexpr int SAMP = samp_slots<Net>();
   constexpr int PERM = (P + 4) & ~3;
   __shared__ float4 s_samp[TB * SAMP];
   __shared__ uint8_t s_perm[TB * PERM];
   const int lane = threadIdx.x;
-  float4* samp = s_samp + lane;
+  float4* samp = samp_lane<Net>(s_samp, lane);
   uint8_t* perm = s_perm + lane * PERM;
   const bool census = (a.flags & SRNN_F_FUSED_CENSUS) != 0;
   auto classify_stored = [&](int64_t i) -> int8_t {
@@ -844,7 +865,7 @@ template <class Net, class S>
 __global__ __launch_bounds__(TB) void k_soup_gen(SrnnCfg c, SrnnArgs a) {
   using I = Item<Net, S>;
   constexpr int P = Net::P;
-  constexpr int SAMP = Net::KIND == 0 ? P : 1;
+  constexpr int SAMP = samp_slots<Net>();
   constexpr int PERM = (P + 4) & ~3;
   __shared__ float4 s_samp[TB * SAMP];
   __shared__ uint8_t s_perm[TB * PERM];
@@ -857,7 +878,7 @@ __global__ __launch_bounds__(TB) void k_soup_gen(SrnnCfg c, SrnnArgs a) {
   bool rs = false;
   int8_t k = -1;
   if (i < a.n) {
-    rs = I::template soup_evolve<true>(c, a, i, s_samp + lane, perm) != 0;
+    rs = I::template soup_evolve<true>(c, a, i, samp_lane<Net>(s_samp, lane), perm) != 0;
     int64_t at, te;
     I::decision(a, i, gen + 1, at, te);
     if (at >= 0) I::link(a.heads_next, a.nexts_next, at, (uint32_t)i);
@@ -1254,7 +1275,7 @@ int gen_finish(const SrnnCfg&, const SrnnArgs& a) {
 template <class Net, class S>
 __global__ __launch_bounds__(TB) void k_soup_seq(SrnnCfg c, SrnnArgs a) {
   using I = Item<Net, S>;
-  constexpr int SAMP = Net::KIND == 0 ? Net::P : 1;
+  constexpr int SAMP = samp_slots<Net>();
   constexpr int PERM = (Net::P + 4) & ~3;
   __shared__ float4 s_samp[TB * SAMP];  // lane 0's slots at s_samp[k * TB] (SAMP_STRIDE)
   __shared__ uint8_t s_perm[PERM];
@@ -1517,6 +1538,7 @@ int launch(const SrnnCfg& c, const SrnnArgs& a) {
   if (OP == OP_SOUP_EVOLVE) {
     if ((a.flags & SRNN_F_X2) && (a.flags & SRNN_F_X2_REMOTE)) {
       // bounded grid over the remote-dependent list (its length is on the device)
+      blocks = (x2_remote_bound(a) + TB - 1) / TB;
       blocks = blocks < X2_REMOTE_WAVES ? blocks : X2_REMOTE_WAVES;
     }
     if ((a.flags & SRNN_F_X2) && (!a.temp || !a.x_dep || !a.x_rlist || !a.x_rcount || !a.x_ctl)) {

@@ -22,11 +22,14 @@
 //
 // Block of the exchange from rank r to rank q (x_blk bytes):
 //   header int64[12]  0..4 census of t-1, 5 newborns of t-1, 6 stats valid, 7 generation t,
-//                     8 reply rows, 9 attack rows, 10 notices (t+1), 11 requests (t+1)
+//                     8 reply rows, 9 attack rows (10, 11 unused)
 //   x_cr rows         replies first (in q's request order), then attack rows (in r's notice
 //                     order); each row = table row + (int64 slot, int64 generation) tag
-//   x_cn notices      (int64 attacker slot, int64 victim slot)
-//   x_cq requests     int64 teacher slot
+//   x_cn notices      (int64 attacker slot, int64 victim slot), -1 after the last one
+//   x_cq requests     int64 teacher slot, -1 after the last one
+// The notice / request areas are appended densely by atomic counters and terminated by the
+// -1 sentinel (no count to publish: no workgroup waits for the others); the sender's post
+// clears its own areas back to -1 once the exchange has left.
 // Capacity overflows set err bit 1 (the generation is invalid; the engine raises on every
 // rank), tag or range mismatches set err bit 4.
 #include "srnn_kernels.h"
@@ -34,7 +37,7 @@
 namespace srnn {
 namespace {
 
-enum : int { H_CENSUS = 0, H_BORN = 5, H_VALID = 6, H_GEN = 7, H_NREP = 8, H_NATT = 9, H_NNOT = 10, H_NREQ = 11 };
+enum : int { H_CENSUS = 0, H_BORN = 5, H_VALID = 6, H_GEN = 7, H_NREP = 8, H_NATT = 9 };
 static_assert(SRNN_X2_HDR == 12, "header words");
 constexpr int XT = 256;  // threads per workgroup
 
@@ -171,15 +174,6 @@ SRNN_HD void write_stats(const SrnnArgs& a, const X2Geom& G, const int64_t* tot,
     h[H_NATT] = a.x_cno ? (a.x_cno[q] < a.x_cn ? a.x_cno[q] : a.x_cn) : 0;
   }
 }
-SRNN_HD void write_meta_counts(const SrnnArgs& a, const X2Geom& G) {
-  for (int q = 0; q < a.world; ++q) {
-    int64_t* h = G.hdr(G.blk(a.sendbuf, a, q));
-    const int64_t nn = a.x_cno_next[q], nr = a.x_crq_next[q];
-    h[H_NNOT] = nn < a.x_cn ? nn : a.x_cn;
-    h[H_NREQ] = nr < a.x_cq ? nr : a.x_cq;
-  }
-}
-
 // stats word w of rank r: the gathered array (flush, all-gather exchange) or the header of
 // r's block in the exchange just received (zeros when not valid)
 SRNN_HD int64_t stat_of(const SrnnArgs& a, const X2Geom& G, int r, int w) {
@@ -188,12 +182,15 @@ SRNN_HD int64_t stat_of(const SrnnArgs& a, const X2Geom& G, int r, int w) {
   return h[H_VALID] ? h[w] : 0;
 }
 
-// received notice k of peer q -> the next generation's list of its victim
+// received notice k of peer q -> the next generation's list of its victim; this rank's own
+// sent notice k to q is cleared back to the sentinel (the exchange has left)
 SRNN_HD void post_notice(const SrnnArgs& a, const X2Geom& G, int q, int64_t k) {
-  const char* b = G.blk(a.recvbuf, a, q);
-  if (k >= G.hdr(b)[H_NNOT]) return;
-  const int64_t* nt = G.notice(b, a, k);
+  int64_t* mine = G.notice(G.blk(a.sendbuf, a, q), a, k);
+  mine[0] = -1;
+  mine[1] = -1;
+  const int64_t* nt = G.notice(G.blk(a.recvbuf, a, q), a, k);
   const int64_t aslot = nt[0], v = nt[1];
+  if (v < 0) return;  // past the last notice
   const int64_t nreq = a.x_crq_next[q] < a.x_cq ? a.x_crq_next[q] : a.x_cq;
   const int64_t pos = nreq + k;  // after the replies to my requests to q
   if (pos >= a.x_cr) {
@@ -209,12 +206,17 @@ SRNN_HD void post_notice(const SrnnArgs& a, const X2Geom& G, int q, int64_t k) {
   Dec::link(a.heads_next, a.nexts_next, v - a.lo, (uint32_t)(a.n + rk));
   mark_remote(a, v - a.lo, SRNN_NIL);
 }
+// received request k of peer q -> a row to reply with next generation; the last valid
+// request's thread (or thread 0 when there is none) stores the count
 SRNN_HD void post_request(const SrnnArgs& a, const X2Geom& G, int q, int64_t k) {
+  *G.request(G.blk(a.sendbuf, a, q), a, k) = -1;
   const char* b = G.blk(a.recvbuf, a, q);
-  const int64_t nr = G.hdr(b)[H_NREQ];
-  if (k == 0) a.x_nsrep[q] = (int32_t)nr;
-  if (k >= nr) return;
   const int64_t te = *G.request(b, a, k);
+  if (te < 0) {
+    if (k == 0) a.x_nsrep[q] = 0;
+    return;
+  }
+  if (k + 1 == a.x_cq || *G.request(b, a, k + 1) < 0) a.x_nsrep[q] = (int32_t)(k + 1);
   if (te < a.lo || te >= a.lo + a.n) {
     err_or(a.err, 4);
     return;
@@ -292,20 +294,6 @@ __global__ __launch_bounds__(XT) void k_x2_pack(SrnnCfg c, SrnnArgs a) {
     // ---- decisions of the next generation (PRIME: of this one) for the local slots
     const int64_t i = ((int64_t)blockIdx.x - a.x_groups) * XT + threadIdx.x;
     if (i < a.n) pack_decide(a, G, i, prime ? gen : gen + 1);
-    // the counters are only touched by (memory-side) atomics: the last workgroup reads them
-    // with returning atomics after every workgroup's ticket
-    __syncthreads();
-    if (threadIdx.x == 0) s_last = atomicAdd(a.x_ctl + 1, 1) == (int32_t)nd - 1;
-    __syncthreads();
-    if (s_last && threadIdx.x == 0) {
-      for (int q = 0; q < a.world; ++q) {
-        int64_t* h = G.hdr(G.blk(a.sendbuf, a, q));
-        const int64_t nn = atomicAdd(a.x_cno_next + q, 0), nr = atomicAdd(a.x_crq_next + q, 0);
-        h[H_NNOT] = nn < a.x_cn ? nn : a.x_cn;
-        h[H_NREQ] = nr < a.x_cq ? nr : a.x_cq;
-      }
-      a.x_ctl[1] = 0;
-    }
     return;
   }
   // ---- rows of this generation's exchange
@@ -417,7 +405,6 @@ void host_pack(const SrnnCfg& c, const SrnnArgs& a) {
   write_stats(a, G, tot, gen);
   if (a.flags & SRNN_F_X2_FINISH_ONLY) return;
   for (int64_t i = 0; i < a.n; ++i) pack_decide(a, G, i, prime ? gen : gen + 1);
-  write_meta_counts(a, G);
   const int64_t rows = (int64_t)a.world * (a.x_cq + a.x_cn);
   for (int64_t idx = 0; idx < rows; ++idx) pack_row(a, G, idx, gen);
 }

@@ -140,7 +140,7 @@ static std::vector<float> soup(int R, int64_t N, int gens, std::vector<int64_t>*
     s.part.assign((size_t)(G * 6), 0), s.ballots.assign(nb + 1, 0ull);
     s.action.assign((size_t)s.n, 0), s.respawn.assign((size_t)s.n, 0), s.counterpart.assign((size_t)s.n, -1);
     s.census.assign(5, 0), s.next_uid.assign(1, N), s.loss.assign((size_t)s.n, 0.f);
-    s.sendbuf.assign((size_t)(R * blk), 0), s.recvbuf.assign((size_t)(R * blk), 0);
+    s.sendbuf.assign((size_t)(R * blk), (char)-1), s.recvbuf.assign((size_t)(R * blk), 0);  // -1: no notices
     s.gen.assign(2, 1), s.counts.assign(6, 0);
     SrnnArgs a{};
     a.n = s.n, a.seed = 5, a.W = s.buf[0].data(), a.uid = s.uid.data();

@@ -182,7 +182,8 @@ def _manifest(path: str, kind: str):
     return m
 
 
-def load_engine(path: str, device="cpu", dist: Optional[Dist] = None, chunk_bytes: int = CHUNK_BYTES):
+def load_engine(path: str, device="cpu", dist: Optional[Dist] = None, chunk_bytes: int = CHUNK_BYTES,
+                diagnostics: bool = True):
     """Rebuild a SoupEngine from a checkpoint (any rank count).  Each rank streams only its
     own rows straight into its device table: host memory O(chunk), not O(shard)."""
     from ..soup_engine import SoupEngine
@@ -192,7 +193,7 @@ def load_engine(path: str, device="cpu", dist: Optional[Dist] = None, chunk_byte
     d = dist or Dist()
     eng = SoupEngine(spec, m["n_total"], m["params"], device=device, seed=m["seed"], lr=m["lr"],
                      shuffle=m["shuffle"], dist=d, dtype=_DTYPES[m.get("dtype", "float32")],
-                     exchange=m.get("exchange", "alltoall"), init=False)
+                     exchange=m.get("exchange", "alltoall"), init=False, diagnostics=diagnostics)
     rows = eng.local_rows()
     rows.zero_()
     _fill_rows(path, eng.lo, eng.hi, spec.P, rows, eng.uid, chunk_bytes)

@@ -170,6 +170,12 @@ def lib():
         v = L.srnn_abi_version()
         if v != ABI_VERSION:
             raise NativeLibraryError(f"libsrnn ABI {v} != expected {ABI_VERSION}: rebuild with `make -C csrc`")
+        L.srnn_args_size.restype = ctypes.c_int64
+        L.srnn_cfg_size.restype = ctypes.c_int64
+        if (L.srnn_args_size(), L.srnn_cfg_size()) != (ctypes.sizeof(SrnnArgs), ctypes.sizeof(SrnnCfg)):
+            raise NativeLibraryError(f"SrnnArgs/SrnnCfg layout mismatch: library {L.srnn_args_size()}/"
+                                     f"{L.srnn_cfg_size()} bytes, ctypes {ctypes.sizeof(SrnnArgs)}/"
+                                     f"{ctypes.sizeof(SrnnCfg)}")
         _lib = L
         return _lib
 

@@ -183,7 +183,12 @@ class Dist:
         return out
 
     def all_to_all(self, out: torch.Tensor, inp: torch.Tensor):
-        """Equal-split all-to-all (RCCL over xGMI for nccl: direct peer links)."""
+        """Equal-split all-to-all (RCCL over xGMI for nccl: direct peer links).  One rank with
+        SRNN_LOOPBACK=1: a device copy instead of the collective (rehearsal timing without
+        RCCL's own latency)."""
+        if self.world == 1 and os.environ.get("SRNN_LOOPBACK") == "1":
+            out.copy_(inp)
+            return out
         if self._use_native(out, inp):
             self.native.all_to_all(out, inp)
         elif self.enabled and inp.is_cuda and dist.get_backend(self.group) == "gloo":

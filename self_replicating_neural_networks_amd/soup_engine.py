@@ -17,13 +17,13 @@ Sharded over R ranks (one process per GPU, RCCL over xGMI), ``exchange="alltoall
 tells the owners of its remote victims (notices) and of its remote teachers (requests);
 int64 slots, O(local) memory and work, so a soup can fill every GPU's HBM.  Per generation:
 
-    C stream: pack_t (finish of t-1 + decisions of t+1 + the rows of exchange t)
-              -> evolve of the local slots of t (no remote attacker / teacher, ~80 %)
-    X stream: all-to-all_t -> post_t (uids of t-1's newborns, census, notices/requests of
-              t+1) -> evolve of the remote-dependent slots of t
+    side stream: evolve of the local slots of t (no remote attacker / teacher, ~84 % at R = 8)
+    main stream: pack_t (finish of t-1 + decisions of t+1 + the rows of exchange t)
+                 -> all-to-all_t -> post_t (uids of t-1's newborns, census, notices/requests
+                 of t+1) -> evolve of the remote-dependent slots of t
     join
 
-so the all-to-all overlaps the local evolve.  ``exchange="allgather"`` instead all-gathers
+so the pack, the all-to-all and the post overlap the local evolve.  ``exchange="allgather"`` instead all-gathers
 every rank's rows each generation (the X01 pattern of SURVEY §2.5: one collective, every
 rank holds the whole table and recomputes every slot's decisions; populations < 2^32).
 Results are bitwise independent of R for both (tests/test_dist_gloo.py).
@@ -90,11 +90,10 @@ def x2_capacities(n_total: int, world: int, attacking_rate: float, learn_from_ra
             if inter[r]:
                 for q in range(R):
                     overlap[r][q] += inter[r] * inter[q] / (s1 - s0)
-    rows = notices = requests = 0.0
+    notices = requests = 0.0
     for r in range(R):
         for q in range(R):
             if q != r:
-                rows = max(rows, ar * overlap[r][q] + lr_ * overlap[q][r])
                 notices = max(notices, ar * overlap[r][q])
                 requests = max(requests, lr_ * overlap[r][q])
     n_max = -(-n_total // R)
@@ -103,37 +102,73 @@ def x2_capacities(n_total: int, world: int, attacking_rate: float, learn_from_ra
     return cq + cn, cn, cq
 
 
+def engine_bytes(spec: ArchSpec, n_total: int, world: int = 1, dtype=torch.float32, exchange: str = "alltoall",
+                 attacking_rate: float = 0.1, learn_from_rate: float = 0.1, segment: int = 0,
+                 diagnostics: bool = True) -> int:
+    """Device bytes one rank of a SoupEngine allocates (the tensors of ``__init__``)."""
+    R = world
+    n = -(-n_total // R)
+    rb = spec.PP * torch.empty((), dtype=dtype).element_size()
+    nb = max(-(-n // 64), 1)
+    b = 2 * n * rb + n * 8 + n * 1 + 2 * n * 4 + nb * 8 + 8 * 4  # tables, uid, respawn, heads, ballots
+    if diagnostics:
+        b += n * (1 + 8 + 4)  # action, counterpart, loss
+    if R > 1 and exchange == "alltoall":
+        cr, cn, cq = x2_capacities(n_total, R, attacking_rate, learn_from_rate, segment)
+        xb = rb + 16
+        blk = -(-(_lib.X2_HDR * 8 + cr * xb + cn * 16 + cq * 8) // 16) * 16
+        nr = max(min(n, R * (cn + cq)), 1)
+        b += 2 * (n + R * cr) * 4            # links of local + received rows
+        b += 2 * max(-(-n // 32), 1) * 4     # remote-dependent bits
+        b += 2 * 2 * nr * 4                  # remote lists
+        b += 2 * R * cr * 8 + 2 * R * cn * 4 + R * cq * 4  # received-row slots, notice / request lists
+        b += 2 * nb * 32                     # block stats of two generations
+        b += 2 * R * blk                     # send + receive buffers
+    elif R > 1:
+        b += 2 * n_total * 4 + n_total * rb + n * 4  # links per global slot, gathered table, row flags
+    else:
+        b += 2 * n * 4 + nb * 32  # links, block stats (+ the batched-finish ring, <= 512 MB)
+        b += min(16 * nb * 32, 512 << 20)
+    return int(b)
+
+
 def plan_population(spec: ArchSpec, dtype=torch.float32, exchange: str = "alltoall", world: int = 1,
                     hbm_bytes: int = 288 * 10 ** 9, fill: float = 0.9, attacking_rate: float = 0.1,
-                    learn_from_rate: float = 0.1, record: bool = False) -> Dict:
-    """Device bytes per particle of a SoupEngine and the largest population that fits
-    ``fill`` of each GPU's HBM (288 GB HBM3E per MI355X).  Per local row: two ping-pong
-    table rows + uid (8 B) + respawn (1 B) + two attack-list heads and links (16 B) + the
-    per-row diagnostics (action / counterpart / loss: 13 B, unless ``record=False`` drops
-    them) ; the all-to-all adds the remote-dependent lists and bits (16.25 B) and the
-    exchange buffers (send + receive: rows, notices, requests at 1.2x the expected load);
-    the all-gather adds the whole gathered table and a link per global slot."""
-    rb = spec.PP * torch.empty((), dtype=dtype).element_size()
-    per_local = 2 * rb + 8 + 1 + 16 + (13 if record else 0) + 1.5  # + ballots / block stats
-    ar, lr_ = max(attacking_rate, 0.0), max(learn_from_rate, 0.0)
-    if exchange == "allgather" or world <= 1:
-        per_slot = 4 + (rb if world > 1 else 0)  # link per global slot + the gathered table
-        per_global = per_slot
-        per_l = per_local
-        limit = MAX_SLOTS_DIRECT
+                    learn_from_rate: float = 0.1, diagnostics: bool = False) -> Dict:
+    """The largest population whose per-rank engine (``engine_bytes``) fits ``fill`` of each
+    GPU's HBM (288 GB HBM3E per MI355X), and what limits it: the HBM, or the uint32 attack-list
+    entries (single-rank / all-gather soups address < 2^32 slots; a sharded all-to-all soup
+    < 2^32 local + received rows per rank)."""
+    kw = dict(world=world, dtype=dtype, exchange=exchange, attacking_rate=attacking_rate,
+              learn_from_rate=learn_from_rate, diagnostics=diagnostics)
+    budget = fill * hbm_bytes
+    lo, hi = 1, 1 << 50
+    while lo < hi:  # largest n_total with engine_bytes <= budget
+        mid = (lo + hi + 1) // 2
+        if engine_bytes(spec, mid, **kw) <= budget:
+            lo = mid
+        else:
+            hi = mid - 1
+    n_fit = lo
+    if world > 1 and exchange == "alltoall":
+        limit = lo
+        # local rows + received rows of a rank stay below 2^32 - 1
+        lo2, hi2 = 1, 1 << 50
+        while lo2 < hi2:
+            mid = (lo2 + hi2 + 1) // 2
+            cr = x2_capacities(mid, world, attacking_rate, learn_from_rate)[0]
+            if -(-mid // world) + world * cr < _lib.NIL:
+                lo2 = mid
+            else:
+                hi2 = mid - 1
+        limit = lo2
     else:
-        xb = rb + 16
-        # exchange rows sent + received, notices (16 B) and requests (8 B) sent + received
-        per_x = 2 * 1.2 * ((ar + lr_) * xb + ar * 16 + lr_ * 8) * (world - 1) / world
-        per_l = per_local + 16.25 + 4 * 1.2 * ar + per_x  # + dep bits, remote list, links of received rows
-        per_global = 0.0
-        limit = world * (MAX_SLOTS_DIRECT - 2 * 1.2 * (ar + lr_) * 0)  # local rows < 2^32 per rank
-    per_particle = per_global + per_l / world  # bytes per GPU per global particle
-    n_fit = int(fill * hbm_bytes / per_particle)
-    n_total = min(n_fit, int(limit))
-    return dict(row_bytes=rb, bytes_per_particle_per_gpu=per_particle, n_total_fit=n_fit, n_total=n_total,
-                limited_by="hbm" if n_fit <= limit else "uint32 list entries", world=world, exchange=exchange,
-                dtype=str(dtype).replace("torch.", ""), bytes_per_gpu=int(n_total * per_particle))
+        limit = MAX_SLOTS_DIRECT
+    n_total = min(n_fit, limit)
+    return dict(n_total=n_total, n_total_fit=n_fit, limited_by="hbm" if n_fit <= limit else "uint32 list entries",
+                bytes_per_gpu=engine_bytes(spec, n_total, **kw),
+                bytes_per_particle_per_gpu=engine_bytes(spec, n_total, **kw) / max(n_total, 1),
+                world=world, exchange=exchange, dtype=str(dtype).replace("torch.", ""))
 
 
 class SoupEngine:
@@ -295,7 +330,10 @@ class SoupEngine:
         self.x_groups = int(min(max(-(-nb // 64), 1), 1024))
         self.nexts = [torch.full((self.n + R * cr,), -1, **i32) for _ in range(2)]
         self.x_dep = [torch.zeros(max(-(-self.n // 32), 1), **i32) for _ in range(2)]
-        self.x_rlist = [torch.zeros(max(2 * self.n, 2), **i32) for _ in range(2)]
+        # a slot is remote-dependent through a received notice or one of its requests: at most
+        # R * (cn + cq) of them per generation
+        nr = max(min(self.n, R * (cn + cq)), 1)
+        self.x_rlist = [torch.zeros(2 * nr, **i32) for _ in range(2)]
         self.x_rcount = [torch.zeros(1, **i32) for _ in range(2)]
         self.x_rslot = [torch.zeros(R * cr, **i64) for _ in range(2)]
         self.x_satt = [torch.zeros(R * cn, **i32) for _ in range(2)]
@@ -306,7 +344,8 @@ class SoupEngine:
         self.x_part = torch.zeros(self.x_groups * 6, **i64)
         self.x_ctl = torch.zeros(8, **i32)
         self.x_bstat = [torch.zeros(nb * 4, **i64) for _ in range(2)]  # u64[4] per 64-row block
-        self.sendbuf = torch.zeros(R * self.x_blk, dtype=torch.uint8, device=dev)
+        # notice / request areas are -1 terminated (csrc/srnn_shard.hip): start all -1
+        self.sendbuf = torch.full((R * self.x_blk,), 255, dtype=torch.uint8, device=dev)
         self.recvbuf = torch.zeros(R * self.x_blk, dtype=torch.uint8, device=dev)
         self.stats_all = torch.zeros(R * 6, **i64)
         self._primed = False
@@ -545,13 +584,15 @@ class SoupEngine:
         xs = self._xs
         # the census of the stored rows inside the evolve (templated and runtime-shape nets),
         # else a classify launch adding to counts; the finish sums both
-        census = self._census_fused() and not record and self._evolve_census
+        # (always on for the sharded exchange, as the census rides on it: shuffle_random nets
+        # classify in a separate launch)
+        census = self.spec.shuffler == "none" and not record and self._evolve_census
         pa = self._x2_base(p)
         pa.W2 = _p(self.table_in)
         pa.temp = _p(self.x_bstat[1 - p])  # the finished generation's block stats
-        po = self._x2_base(p, xs)
+        po = self._x2_base(p)
         po.temp = _p(self.x_bstat[1 - p])
-        ev = self._x2_base(p, xs)
+        ev = self._x2_base(p)
         ev.W2, ev.W = _p(self.table_in), _p(self.rows_out)
         ev.temp = _p(self.x_bstat[p])
         ev.action, ev.counterpart, ev.loss, ev.respawn = (_p(self.action), _p(self.counterpart), _p(self.loss),
@@ -559,33 +600,22 @@ class SoupEngine:
         ev.flags |= _lib.FLAG_X2 | (0 if record else _lib.FLAG_RESPAWN_INLINE)
         if census:
             ev.flags |= _lib.FLAG_FUSED_CENSUS | (_lib.FLAG_FIX_SEC if self.stats_with_sec else 0)
-        rem = self._x2_base(p, xs)
+        rem = self._x2_base(p)
         ctypes.pointer(rem)[0] = ev
         rem.flags = ev.flags | _lib.FLAG_X2_REMOTE
-        loc = self._x2_base(p)
+        loc = self._x2_base(p, xs)
         ctypes.pointer(loc)[0] = ev
-        loc.stream = self._stream()
+        loc.stream = self._stream(xs)
         self._arg_cache[key] = (pa, po, rem, loc, census)
         return self._arg_cache[key]
 
     def _x2_exchange(self, post: _lib.SrnnArgs, remote: Optional[_lib.SrnnArgs] = None):
-        """all-to-all -> post (-> remote evolve), on the comm stream when there is one."""
-        if self._xs is not None:
-            self._xs.wait_stream(torch.cuda.current_stream(self.device))
-            with torch.cuda.stream(self._xs):
-                self.dist.all_to_all(self.recvbuf, self.sendbuf)
-                _lib.run(_lib.OP_X2_POST, self.spec, post, self.cfg)
-                if remote is not None:
-                    _lib.run(_lib.OP_SOUP_EVOLVE, self.spec, remote, self.cfg)
-        else:
-            self.dist.all_to_all(self.recvbuf, self.sendbuf)
-            _lib.run(_lib.OP_X2_POST, self.spec, post, self.cfg)
-            if remote is not None:
-                _lib.run(_lib.OP_SOUP_EVOLVE, self.spec, remote, self.cfg)
-
-    def _x2_join(self):
-        if self._xs is not None:
-            torch.cuda.current_stream(self.device).wait_stream(self._xs)
+        """all-to-all -> post (-> remote evolve) on the current stream (RCCL inside a hipGraph
+        is captured from the origin stream)."""
+        self.dist.all_to_all(self.recvbuf, self.sendbuf)
+        _lib.run(_lib.OP_X2_POST, self.spec, post, self.cfg)
+        if remote is not None:
+            _lib.run(_lib.OP_SOUP_EVOLVE, self.spec, remote, self.cfg)
 
     def _x2_prime(self):
         """First exchange of a (re)started soup: the decisions of THIS generation go out as
@@ -605,12 +635,10 @@ class SoupEngine:
         pa.W2 = _p(self.table_in)
         pa.temp = _p(self.x_bstat[q])
         pa.flags |= _lib.FLAG_X2_PRIME
-        po = self._x2_base(p, self._xs)
+        po = self._x2_base(p)
         ctypes.pointer(po)[0] = pa
-        po.stream = self._stream(self._xs)
         _lib.run(_lib.OP_X2_PACK, self.spec, pa, self.cfg)
         self._x2_exchange(po)
-        self._x2_join()
         self._primed = True
 
     def _x2_generation(self, record: bool = False):
@@ -618,16 +646,25 @@ class SoupEngine:
         if not self._primed:
             self._x2_prime()
         pa, po, rem, loc, census = self._x2_args(record)
+        # the local slots need nothing of this generation's exchange: they start at once on
+        # the side stream, beside pack -> all-to-all -> post -> remote-dependent slots
+        side = self._xs
+        if side is not None:
+            side.wait_stream(torch.cuda.current_stream(self.device))
+            with torch.cuda.stream(side):
+                _lib.run(_lib.OP_SOUP_EVOLVE, spec, loc, cfg)
         _lib.run(_lib.OP_X2_PACK, spec, pa, cfg)
-        self._x2_exchange(po, rem)           # comm stream: all-to-all -> post -> remote slots
-        _lib.run(_lib.OP_SOUP_EVOLVE, spec, loc, cfg)  # compute stream: local slots, meanwhile
-        self._x2_join()
+        self._x2_exchange(po, rem)
+        if side is not None:
+            torch.cuda.current_stream(self.device).wait_stream(side)
+        else:
+            _lib.run(_lib.OP_SOUP_EVOLVE, spec, loc, cfg)
         if record and self.recorder is not None:
             self.recorder.on_evolved(self)
             ra = self._args()
             ra.W, ra.respawn = _p(self.rows_out), _p(self.respawn)
             _lib.run(_lib.OP_RESPAWN, spec, ra, cfg)
-        if (self.stats or record) and not census:
+        if not census:
             # census of the stored rows (classify -> counts, read by the next finish)
             cls, _ = K.classify(self.spec, self.rows_out, self.eps, self.stats_with_sec, uid=None, seed=self.seed,
                                 scratch=self._scratch, ctr=0x7FFFFFF0, counts=self.counts, key_offset=self.lo)

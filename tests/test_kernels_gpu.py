@@ -40,18 +40,24 @@ def test_init_apply_train_classify_vs_oracle(cuda, spec):
     assert _rel(W[:, :spec.P].cpu().numpy(), ow) < (2e-3 if spec.kind == "recurrent" else 1e-4)
     # padding stays zero
     assert torch.all(W[:, spec.P:] == 0)
+    # one step of each op from the SAME inputs (the device's rows): fp32 differences are
+    # rounding only -- fma contraction and summation order.  1e-5 of the row scale for the
+    # feed-forward nets (measured host path vs oracle: <= 4e-6); the recurrent BPTT sums 17
+    # timestep products in another association (host path vs oracle: 1.4e-5) -> 5e-5.
+    tol = 5e-5 if spec.kind == "recurrent" else 1e-5
+    w0 = W[:, :spec.P].cpu().numpy()
     # attack: row i attacked by row i-1
     out = torch.zeros_like(W)
     idx_f = torch.roll(torch.arange(n, device=cuda), 1).contiguous()
     K.apply(spec, W, out, idx_f=idx_f, uid=uid, seed=seed, ctr=3)
-    oo = O.apply(spec, np.roll(ow, 1, axis=0), ow, seed=seed, uids=uid.cpu().numpy(), ctr=3)
-    assert _rel(out[:, :spec.P].cpu().numpy(), oo) < 2e-3
+    oo = O.apply(spec, np.roll(w0, 1, axis=0), w0, seed=seed, uids=uid.cpu().numpy(), ctr=3)
+    assert _rel(out[:, :spec.P].cpu().numpy(), oo) < tol
     # self-train epoch
     W2 = W.clone()
     loss = K.train(spec, W2, epochs=1, lr=0.01, uid=uid, seed=seed, ctr=9)
-    tw, tl = O.train_epoch(spec, ow, ow, 0.01, True, seed, uid.cpu().numpy(), 9)
-    assert _rel(W2[:, :spec.P].cpu().numpy(), tw) < 2e-3
-    assert _rel(loss.cpu().numpy(), tl) < 2e-3
+    tw, tl = O.train_epoch(spec, w0, w0, 0.01, True, seed, uid.cpu().numpy(), 9)
+    assert _rel(W2[:, :spec.P].cpu().numpy(), tw) < tol
+    assert _rel(loss.cpu().numpy(), tl) < tol
     # classification
     cls, counts = K.classify(spec, W, 1e-4, uid=uid, seed=seed)
     ocls = O.classify(spec, ow, 1e-4)
@@ -101,7 +107,8 @@ def test_soup_engine_gpu_vs_oracle(cuda):
     e.evolve(1)
     W1, act, cp, loss, resp = O.soup_generation_sync(spec, W0, uids, 1, 7, params)
     keep = resp == 0
-    assert _rel(e.local_rows()[:, :spec.P].cpu().numpy()[keep], W1[keep]) < 2e-3
+    # a generation = attacks + learn_from + 3 epochs of SGD (~60 dependent steps per particle)
+    assert _rel(e.local_rows()[:, :spec.P].cpu().numpy()[keep], W1[keep]) < 1e-5
     assert (e.action.cpu().numpy() == act).all()
     assert (e.counterpart.cpu().numpy() == cp).all()
     assert (e.respawn.cpu().numpy() == resp).mean() > 0.999
