@@ -40,6 +40,11 @@ enum SrnnFlag : uint32_t {
                                      // received rows, teachers of remote learners come from rlist
   SRNN_F_X2_REMOTE = 1u << 17,       // X2 evolve: the remote-dependent slots of rlist (else: the local slots)
   SRNN_F_X2_FINISH_ONLY = 1u << 18,  // X2 pack: only the finish of the last generation (flush)
+  SRNN_F_X2_BOTH = 1u << 20,         // X2 evolve (with X2_REMOTE): one launch of n/64 waves for the whole
+                                     // generation, the lanes of remote-dependent slots take the remote
+                                     // list's entries -- the single-stream generation
+  SRNN_F_X2_PRIO = 1u << 19,         // X2 pack / post / remote evolve: raised wave issue priority (the
+                                     // exchange chain wins the SIMDs it shares with the local evolve)
 };
 
 // Attack-list entries (uint32, SRNN_NIL ends a list).  Single rank: the attacker's row
@@ -63,7 +68,8 @@ struct SrnnArgs {
   float learn_from_rate;
   uint64_t seed;
   uint32_t ctr;         // op counter for per-particle random streams
-  uint32_t pad0;
+  uint32_t x_emul;      // X2 pack at world 1 only (timing model of R ranks): a Philox-keyed
+                        // fraction x_emul / 2^32 of the local slots is marked remote-dependent
   float* W;             // rows [n][pp] (in/out)
   float* W2;            // second table (source rows / output rows)
   float* traj;          // fixpoint run trajectory [(steps+1)][n][pp] or null
@@ -122,9 +128,13 @@ struct SrnnArgs {
   uint32_t* x_srep;           // [world * x_cq] local rows requested by each peer (this generation)
   int32_t* x_nsrep;           // [world]
   int64_t* x_part;            // [x_groups][6] finish partials (born, census[5]) per workgroup
-  int32_t* x_ctl;             // [8] last-workgroup tickets (re-armed by their last workgroup)
+  int32_t* x_ctl;             // [8] last-workgroup tickets (re-armed by their last workgroup): 0 pack
+                              // finish, 2 post uids, 3 evolve waves
   int32_t x_groups;           // finish / uid workgroups
   int32_t pad2;
+  int32_t* x_hpre;            // [ceil(n/64)] (SRNN_F_X2_BOTH generations) remote-dependent slots before
+                              // each 64-row block within its finish workgroup's range (pack)
+  int32_t* x_hgrp;            // [x_groups] ... before each finish workgroup's range (pack)
   int8_t* action;       // soup: action code per local row (optional)
   int64_t* counterpart; // soup: counterpart slot per local row (optional)
   int8_t* respawn;      // soup: 0 none, 1 divergent_dead, 2 zweo_dead
@@ -163,7 +173,7 @@ enum SrnnOp {
                         // census, received notices linked for the next generation, requests kept
 };
 
-int srnn_abi_version();  // 15
+int srnn_abi_version();  // 17
 int64_t srnn_args_size();  // sizeof(SrnnArgs): the ctypes mirror checks its layout against it
 int64_t srnn_cfg_size();
 int srnn_has_config(const SrnnCfg* cfg);

@@ -765,8 +765,14 @@ SRNN_HD bool x2_dep(const SrnnArgs& a, int64_t i) { return (a.x_dep[i >> 5] >> (
 // notice or one of its requests): the remote evolve's grid is sized by this bound, not by n
 // (every wave of that launch takes one ticket on the re-arm counter)
 SRNN_HD int64_t x2_remote_bound(const SrnnArgs& a) {
+  if (a.x_emul && a.world == 1) return a.n > 1 ? a.n : 1;  // timing model: any local slot
   const int64_t b = (int64_t)a.world * (a.x_cn + a.x_cq);
   return b < a.n ? (b > 1 ? b : 1) : (a.n > 1 ? a.n : 1);
+}
+// workgroups of the remote-list walk (grid-stride over the bound, at most X2_REMOTE_WAVES)
+SRNN_HD int64_t x2_remote_blocks(const SrnnArgs& a) {
+  const int64_t rb = (x2_remote_bound(a) + TB - 1) / TB;
+  return rb < X2_REMOTE_WAVES ? rb : X2_REMOTE_WAVES;
 }
 
 // Soup evolve (OP_SOUP_EVOLVE), one wave per block, lane per slot:
@@ -809,6 +815,48 @@ __global__ __launch_bounds__(TB) void k_soup_evolve(SrnnCfg c, SrnnArgs a) {
     return;
   }
   unsigned long long* bs = reinterpret_cast<unsigned long long*>(a.temp);
+  if (a.flags & SRNN_F_X2_BOTH) {
+    // one launch for the whole generation, n/64 waves: a lane whose own slot is
+    // remote-dependent (x_dep) takes an entry of the remote list instead -- there are exactly as
+    // many such lanes as entries (a slot joins the list when its bit is first set), so every
+    // lane evolves one slot and no wave is added for the remote ones
+    const int64_t i = (int64_t)blockIdx.x * TB + lane;
+    const bool valid = i < a.n;
+    const bool dep = valid && x2_dep(a, i);
+    const int64_t cnt = *(volatile const int32_t*)a.x_rcount;
+    const unsigned long long hm = __ballot(dep);
+    // this wave's first list entry: holes before its block (prefix from pack, x_hpre / x_hgrp)
+    const int64_t nbk = (a.n + TB - 1) / TB, per = (nbk + a.x_groups - 1) / a.x_groups;
+    const int64_t base = hm ? (int64_t)a.x_hpre[blockIdx.x] + a.x_hgrp[blockIdx.x / per] : 0;
+    const int64_t pos = base + (int64_t)__popcll(hm & ((1ull << lane) - 1ull));
+    int64_t j = i;
+    uint32_t tk = SRNN_NIL;
+    bool on = valid && !dep;
+    if (dep && pos < cnt) {
+      j = a.x_rlist[2 * pos];
+      tk = a.x_rlist[2 * pos + 1];
+      on = true;
+    }
+    bool rs = false;
+    int8_t k = -1;
+    if (on) {
+      rs = I::soup_evolve(c, a, j, samp, perm, tk) != 0;
+      if (census) k = classify_stored(j);
+    }
+    const int64_t wd = (int64_t)blockIdx.x * 2 + lane;
+    if (lane < 2 && wd * 32 < a.n) a.x_dep[wd] = 0u;
+    // own slots in the wave's block stats, taken list entries lane by lane
+    bs_publish_wave(bs, blockIdx.x, on && !dep && rs, dep ? (int8_t)-1 : k);
+    if (dep && on) bs_publish_lane(bs, j, rs, k);
+    int32_t prev = 0;
+    if (lane == 0) prev = atomicAdd(a.x_ctl + 3, 1);
+    prev = __shfl(prev, 0);
+    if (prev == (int32_t)gridDim.x - 1 && lane == 0) {  // last wave: the list is re-armed
+      *a.x_rcount = 0;
+      a.x_ctl[3] = 0;
+    }
+    return;
+  }
   if (!(a.flags & SRNN_F_X2_REMOTE)) {
     const int64_t i = (int64_t)blockIdx.x * TB + lane;
     const bool on = i < a.n && !x2_dep(a, i);
@@ -824,6 +872,7 @@ __global__ __launch_bounds__(TB) void k_soup_evolve(SrnnCfg c, SrnnArgs a) {
     bs_publish_wave(bs, blockIdx.x, rs, k);
     return;
   }
+  if (a.flags & SRNN_F_X2_PRIO) __builtin_amdgcn_s_setprio(3);  // the exchange chain's tail
   const int64_t cnt = *(volatile const int32_t*)a.x_rcount;
   for (int64_t base = (int64_t)blockIdx.x * TB; base < cnt; base += (int64_t)gridDim.x * TB) {
     const int64_t q = base + lane;
@@ -1537,9 +1586,13 @@ int launch(const SrnnCfg& c, const SrnnArgs& a) {
   }
   if (OP == OP_SOUP_EVOLVE) {
     if ((a.flags & SRNN_F_X2) && (a.flags & SRNN_F_X2_REMOTE)) {
-      // bounded grid over the remote-dependent list (its length is on the device)
-      blocks = (x2_remote_bound(a) + TB - 1) / TB;
-      blocks = blocks < X2_REMOTE_WAVES ? blocks : X2_REMOTE_WAVES;
+      // bounded grid over the remote-dependent list (its length is on the device), after the
+      // local blocks with SRNN_F_X2_BOTH
+      if (!(a.flags & SRNN_F_X2_BOTH)) blocks = x2_remote_blocks(a);  // (BOTH: n/64 waves)
+    }
+    if ((a.flags & SRNN_F_X2_BOTH) && (!a.x_hpre || !a.x_hgrp || a.x_groups < 1)) {
+      set_error("single-launch X2 evolve needs the hole prefixes of pack (x_hpre, x_hgrp)");
+      return -5;
     }
     if ((a.flags & SRNN_F_X2) && (!a.temp || !a.x_dep || !a.x_rlist || !a.x_rcount || !a.x_ctl)) {
       set_error("X2 evolve needs block stats (temp), x_dep, x_rlist, x_rcount and x_ctl");
@@ -1568,14 +1621,14 @@ template <class Net, class S, class EvolveFn, class ClassifyFn>
 void host_x2_evolve(const SrnnArgs& a, EvolveFn&& evolve, ClassifyFn&& classify) {
   unsigned long long* bs = reinterpret_cast<unsigned long long*>(a.temp);
   const bool census = (a.flags & SRNN_F_FUSED_CENSUS) != 0;
-  if (!(a.flags & SRNN_F_X2_REMOTE)) {
+  if (!(a.flags & SRNN_F_X2_REMOTE) || (a.flags & SRNN_F_X2_BOTH)) {
     host_parallel(a.n, [&](int64_t i) {
       if (x2_dep(a, i)) return;
       const bool rs = evolve(i, SRNN_NIL) != 0;
       bs_publish_host(bs, i, rs, census ? classify(i) : (int8_t)-1);
     });
     for (int64_t w = 0; w < (a.n + 31) / 32; ++w) a.x_dep[w] = 0u;
-    return;
+    if (!(a.flags & SRNN_F_X2_BOTH)) return;
   }
   const int64_t cnt = *a.x_rcount;
   host_parallel(cnt, [&](int64_t q) {

@@ -96,40 +96,65 @@ SRNN_HD void mark_remote(const SrnnArgs& a, int64_t i, uint32_t tk) {
   a.x_rlist_next[2 * (int64_t)c + 1] = tk;
 }
 
-// decisions of local row i for the next generation dgen (pack)
+// timing model of R ranks on one GPU (x_emul, world 1 only): a hashed fraction x_emul / 2^32 of
+// the slots goes through the remote list (same results: their rows are local)
+SRNN_HD bool emul_hit(int64_t g, int32_t dgen, uint32_t x) {
+  uint64_t h = (uint64_t)g * 0x9E3779B97F4A7C15ull ^ ((uint64_t)(uint32_t)dgen * 0xBF58476D1CE4E5B9ull);
+  h ^= h >> 31;
+  h *= 0x94D049BB133111EBull;
+  h ^= h >> 29;
+  return (uint32_t)(h >> 32) < x;
+}
+
+// What pack decides for one local slot: a local attack to link, a notice or request to append
+// for a peer rank, a remote-dependence mark (the teacher's reply row is known only once the
+// request has its position).
+struct PackDec {
+  int64_t g, at, te;
+  int32_t qa, qt;   // owner ranks of victim / teacher (-1: none)
+  bool mark;        // emulated remote dependence (no teacher row)
+};
+SRNN_HD PackDec pack_decision(const SrnnArgs& a, int64_t i, int32_t dgen) {
+  PackDec d;
+  d.g = a.lo + i;
+  Dec::decision(a, d.g, dgen, d.at, d.te);
+  d.qa = d.at >= 0 ? (a.world > 1 ? shard_of(d.at, a.n_total, a.world) : 0) : -1;
+  d.qt = d.te >= 0 ? (a.world > 1 ? shard_of(d.te, a.n_total, a.world) : 0) : -1;
+  if (d.qt == a.rank) d.qt = -1;  // a local teacher needs nothing
+  d.mark = a.x_emul && a.world == 1 && emul_hit(d.g, dgen, a.x_emul);
+  return d;
+}
+// a notice (slot k of peer q's area) and a request (slot k) once their positions are known
+SRNN_HD void put_notice(const SrnnArgs& a, const X2Geom& G, int64_t i, const PackDec& d, int32_t k) {
+  if (k < a.x_cn) {
+    int64_t* nt = G.notice(G.blk(a.sendbuf, a, d.qa), a, k);
+    nt[0] = d.g;
+    nt[1] = d.at;
+    a.x_satt_next[(int64_t)d.qa * a.x_cn + k] = (uint32_t)i;
+  } else {
+    err_or(a.err, 1);
+  }
+}
+SRNN_HD bool put_request(const SrnnArgs& a, const X2Geom& G, const PackDec& d, int32_t k) {
+  if (k < a.x_cq) {
+    *G.request(G.blk(a.sendbuf, a, d.qt), a, k) = d.te;
+    return true;
+  }
+  err_or(a.err, 1);
+  return false;
+}
+
+// decisions of local row i for the next generation dgen (pack; host form: one slot at a time)
 SRNN_HD void pack_decide(const SrnnArgs& a, const X2Geom& G, int64_t i, int32_t dgen) {
-  const int64_t g = a.lo + i;
-  int64_t at, te;
-  Dec::decision(a, g, dgen, at, te);
-  if (at >= 0) {
-    const int32_t q = a.world > 1 ? shard_of(at, a.n_total, a.world) : 0;
-    if (q == a.rank) {
-      Dec::link(a.heads_next, a.nexts_next, at - a.lo, (uint32_t)i);
-    } else {
-      const int32_t k = atomic_add(a.x_cno_next + q, 1);
-      if (k < a.x_cn) {
-        int64_t* nt = G.notice(G.blk(a.sendbuf, a, q), a, k);
-        nt[0] = g;
-        nt[1] = at;
-        a.x_satt_next[(int64_t)q * a.x_cn + k] = (uint32_t)i;
-      } else {
-        err_or(a.err, 1);
-      }
-    }
+  const PackDec d = pack_decision(a, i, dgen);
+  if (d.qa == a.rank) Dec::link(a.heads_next, a.nexts_next, d.at - a.lo, (uint32_t)i);
+  else if (d.qa >= 0) put_notice(a, G, i, d, atomic_add(a.x_cno_next + d.qa, 1));
+  if (d.qt >= 0) {
+    const int32_t k = atomic_add(a.x_crq_next + d.qt, 1);
+    // the reply comes back as row k of q's block in the next exchange
+    if (put_request(a, G, d, k)) mark_remote(a, i, (uint32_t)((int64_t)d.qt * a.x_cr + k));
   }
-  if (te >= 0) {
-    const int32_t q = a.world > 1 ? shard_of(te, a.n_total, a.world) : 0;
-    if (q != a.rank) {
-      const int32_t k = atomic_add(a.x_crq_next + q, 1);
-      if (k < a.x_cq) {
-        *G.request(G.blk(a.sendbuf, a, q), a, k) = te;
-        // the reply comes back as row k of q's block in the next exchange
-        mark_remote(a, i, (uint32_t)((int64_t)q * a.x_cr + k));
-      } else {
-        err_or(a.err, 1);
-      }
-    }
-  }
+  if (d.mark) mark_remote(a, i, SRNN_NIL);
 }
 
 // row copy idx of the exchange (peer q): replies (k < x_cq) then noticed attackers
@@ -184,27 +209,28 @@ SRNN_HD int64_t stat_of(const SrnnArgs& a, const X2Geom& G, int r, int w) {
 
 // received notice k of peer q -> the next generation's list of its victim; this rank's own
 // sent notice k to q is cleared back to the sentinel (the exchange has left)
-SRNN_HD void post_notice(const SrnnArgs& a, const X2Geom& G, int q, int64_t k) {
+// (returns the victim's local row, which becomes remote-dependent; -1: nothing received)
+SRNN_HD int64_t post_notice(const SrnnArgs& a, const X2Geom& G, int q, int64_t k) {
   int64_t* mine = G.notice(G.blk(a.sendbuf, a, q), a, k);
   mine[0] = -1;
   mine[1] = -1;
   const int64_t* nt = G.notice(G.blk(a.recvbuf, a, q), a, k);
   const int64_t aslot = nt[0], v = nt[1];
-  if (v < 0) return;  // past the last notice
+  if (v < 0) return -1;  // past the last notice
   const int64_t nreq = a.x_crq_next[q] < a.x_cq ? a.x_crq_next[q] : a.x_cq;
   const int64_t pos = nreq + k;  // after the replies to my requests to q
   if (pos >= a.x_cr) {
     err_or(a.err, 1);
-    return;
+    return -1;
   }
   if (v < a.lo || v >= a.lo + a.n) {
     err_or(a.err, 4);
-    return;
+    return -1;
   }
   const int64_t rk = (int64_t)q * a.x_cr + pos;
   a.x_rslot_next[rk] = aslot;
   Dec::link(a.heads_next, a.nexts_next, v - a.lo, (uint32_t)(a.n + rk));
-  mark_remote(a, v - a.lo, SRNN_NIL);
+  return v - a.lo;
 }
 // received request k of peer q -> a row to reply with next generation; the last valid
 // request's thread (or thread 0 when there is none) stores the count
@@ -234,6 +260,72 @@ __device__ __forceinline__ int64_t wg_sum(int64_t v, int64_t* s_red) {
   __syncthreads();
   return t;
 }
+// one atomic per WORKGROUP on a shared counter (same-address device atomics serialise: a
+// generation's thousands of notices / requests / remote marks would queue on a few counters):
+// this lane's position among the wanting lanes of the workgroup, -1 when it wants none.  Every
+// thread of the workgroup calls it (two barriers); s: XT / 64 + 1 ints of LDS
+__device__ __forceinline__ int32_t block_reserve(int32_t* ctr, bool want, int32_t* s) {
+  const unsigned long long m = __ballot(want);
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  if (lane == 0) s[wv] = (int32_t)__popcll(m);
+  __syncthreads();
+  int32_t pre = 0, tot = 0;
+#pragma unroll
+  for (int w = 0; w < XT / 64; ++w) {
+    pre += w < wv ? s[w] : 0;
+    tot += s[w];
+  }
+  if (threadIdx.x == 0 && tot) s[XT / 64] = atomicAdd(ctr, tot);
+  __syncthreads();
+  const int32_t base = s[XT / 64];
+  __syncthreads();  // s is reused by the next call
+  return want ? base + pre + (int32_t)__popcll(m & ((1ull << lane) - 1ull)) : -1;
+}
+// mark_remote with the list positions reserved once per workgroup (every thread calls it)
+__device__ __forceinline__ void mark_remote_block(const SrnnArgs& a, int64_t i, uint32_t tk, bool want, int32_t* s) {
+  bool first = false;
+  if (want) {
+    const uint32_t bit = 1u << (i & 31);
+    first = !(atomicOr(a.x_dep_next + (i >> 5), bit) & bit);
+  }
+  const int32_t c = block_reserve(a.x_rcount_next, first, s);
+  if (first) {
+    a.x_rlist_next[2 * (int64_t)c] = (uint32_t)i;
+    a.x_rlist_next[2 * (int64_t)c + 1] = tk;
+  }
+}
+// pack_decide for a whole workgroup: notice / request / list positions reserved per workgroup
+// and peer
+__device__ void pack_decide_block(const SrnnArgs& a, const X2Geom& G, int64_t i, bool on, int32_t dgen, int32_t* s) {
+  PackDec d;
+  d.qa = d.qt = -1;
+  d.mark = false;
+  if (on) d = pack_decision(a, i, dgen);
+  if (d.qa == a.rank) Dec::link(a.heads_next, a.nexts_next, d.at - a.lo, (uint32_t)i);
+  const bool notice = d.qa >= 0 && d.qa != a.rank, request = d.qt >= 0;
+  int32_t kn = -1, kq = -1;
+  if (a.world <= 16) {
+    for (int q = 0; q < a.world; ++q) {
+      if (q == a.rank) continue;
+      const int32_t r1 = block_reserve(a.x_cno_next + q, notice && d.qa == q, s);
+      const int32_t r2 = block_reserve(a.x_crq_next + q, request && d.qt == q, s);
+      kn = r1 >= 0 ? r1 : kn;
+      kq = r2 >= 0 ? r2 : kq;
+    }
+  } else {
+    if (notice) kn = atomicAdd(a.x_cno_next + d.qa, 1);
+    if (request) kq = atomicAdd(a.x_crq_next + d.qt, 1);
+  }
+  if (notice) put_notice(a, G, i, d, kn);
+  bool mark = d.mark;  // (emulated marks exist at world 1 only, where there are no requests)
+  uint32_t tk = SRNN_NIL;
+  if (request && put_request(a, G, d, kq)) {
+    mark = true;
+    tk = (uint32_t)((int64_t)d.qt * a.x_cr + kq);  // the reply: row kq of q's next block
+  }
+  mark_remote_block(a, i, tk, mark, s);
+}
+
 // block range of finish / uid workgroup g (the same split in pack and post)
 SRNN_HD void wg_range(const SrnnArgs& a, int64_t g, int64_t& b0, int64_t& b1) {
   const int64_t nb = (a.n + 63) / 64, per = (nb + a.x_groups - 1) / a.x_groups;
@@ -242,12 +334,14 @@ SRNN_HD void wg_range(const SrnnArgs& a, int64_t g, int64_t& b0, int64_t& b1) {
 }
 
 __global__ __launch_bounds__(XT) void k_x2_pack(SrnnCfg c, SrnnArgs a) {
+  if (a.flags & SRNN_F_X2_PRIO) __builtin_amdgcn_s_setprio(3);
   const X2Geom G = geom(c);
   const int32_t gen = gen_of(a);
   const bool prime = (a.flags & SRNN_F_X2_PRIME) != 0, fin_only = (a.flags & SRNN_F_X2_FINISH_ONLY) != 0;
   const int64_t nd = fin_only ? 0 : (a.n + XT - 1) / XT;
   __shared__ int64_t s_red[XT / 64];
   __shared__ int32_t s_last;
+  __shared__ int32_t s_hw[XT / 64];
   if ((int64_t)blockIdx.x < a.x_groups) {
     // ---- finish of generation t-1: this workgroup's blocks -> partial (born, census)
     int64_t b0, b1;
@@ -264,6 +358,25 @@ __global__ __launch_bounds__(XT) void k_x2_pack(SrnnCfg c, SrnnArgs a) {
       v[5] += (uint32_t)st[3];
     }
     for (int w = 0; w < 6; ++w) v[w] = wg_sum(v[w], s_red);
+    if (a.x_hpre) {
+      // remote-dependent slots (holes) per 64-row block of THIS generation (bits final since
+      // pack / post of the last one): exclusive prefix inside the workgroup's range -> x_hpre,
+      // its total -> x_hgrp (scanned by the last workgroup); the single-launch evolve's waves
+      // map their holes onto the remote list with them
+      const int64_t nw = (a.n + 31) / 32;
+      int32_t carry = 0;
+      for (int64_t c0 = b0; c0 < b1; c0 += XT) {
+        const int64_t b = c0 + threadIdx.x;
+        int32_t h = 0;
+        if (b < b1) h = __popc(a.x_dep[2 * b]) + (2 * b + 1 < nw ? __popc(a.x_dep[2 * b + 1]) : 0);
+        int32_t tot;
+        const int32_t incl = block_incl_scan<XT, int32_t>(h, s_hw, &tot);
+        if (b < b1) a.x_hpre[b] = carry + incl - h;
+        carry += tot;
+        __syncthreads();
+      }
+      if (threadIdx.x == 0) __hip_atomic_store(a.x_hgrp + blockIdx.x, carry, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
     if (threadIdx.x == 0) {
       // partials leave L2 at once (sc1 stores: other XCDs read them), drained before the ticket
       for (int w = 0; w < 6; ++w)
@@ -273,14 +386,29 @@ __global__ __launch_bounds__(XT) void k_x2_pack(SrnnCfg c, SrnnArgs a) {
     }
     __syncthreads();
     if (!s_last) return;
-    if (threadIdx.x == 0) {
-      int64_t tot[6] = {0, 0, 0, 0, 0, 0};  // census[5], born
-      for (int64_t g = 0; g < a.x_groups; ++g) {
-        int64_t p[6];
-        for (int w = 0; w < 6; ++w) p[w] = __hip_atomic_load(a.x_part + g * 6 + w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        tot[5] += p[0];
-        for (int w = 0; w < 5; ++w) tot[w] += p[1 + w];
+    // the last workgroup sums every workgroup's partials: one device-scope load round trip per
+    // thread (a serial walk by one thread costs one round trip per workgroup)
+    int64_t pv[6] = {0, 0, 0, 0, 0, 0};
+    for (int64_t g = threadIdx.x; g < a.x_groups; g += XT)
+      for (int w = 0; w < 6; ++w) pv[w] += __hip_atomic_load(a.x_part + g * 6 + w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    for (int w = 0; w < 6; ++w) pv[w] = wg_sum(pv[w], s_red);
+    if (a.x_hpre) {  // exclusive prefix of the workgroups' hole totals, in place
+      int32_t carry = 0;
+      for (int64_t c0 = 0; c0 < a.x_groups; c0 += XT) {
+        const int64_t g = c0 + threadIdx.x;
+        const int32_t h =
+            g < a.x_groups ? __hip_atomic_load(a.x_hgrp + g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0;
+        int32_t tot;
+        const int32_t incl = block_incl_scan<XT, int32_t>(h, s_hw, &tot);
+        if (g < a.x_groups) a.x_hgrp[g] = carry + incl - h;
+        carry += tot;
+        __syncthreads();
       }
+    }
+    if (threadIdx.x == 0) {
+      int64_t tot[6];  // census[5], born
+      tot[5] = pv[0];
+      for (int w = 0; w < 5; ++w) tot[w] = pv[1 + w];
       if (a.counts) {  // census accumulated by a classify launch (nets without a fused census)
         for (int w = 0; w < 5; ++w) tot[w] += (int64_t)a.counts[w];
         for (int w = 0; w < 6; ++w) a.counts[w] = 0;
@@ -293,7 +421,8 @@ __global__ __launch_bounds__(XT) void k_x2_pack(SrnnCfg c, SrnnArgs a) {
   if ((int64_t)blockIdx.x < a.x_groups + nd) {
     // ---- decisions of the next generation (PRIME: of this one) for the local slots
     const int64_t i = ((int64_t)blockIdx.x - a.x_groups) * XT + threadIdx.x;
-    if (i < a.n) pack_decide(a, G, i, prime ? gen : gen + 1);
+    __shared__ int32_t s_res[XT / 64 + 1];
+    pack_decide_block(a, G, i, i < a.n, prime ? gen : gen + 1, s_res);
     return;
   }
   // ---- rows of this generation's exchange
@@ -302,6 +431,7 @@ __global__ __launch_bounds__(XT) void k_x2_pack(SrnnCfg c, SrnnArgs a) {
 }
 
 __global__ __launch_bounds__(XT) void k_x2_post(SrnnCfg c, SrnnArgs a) {
+  if (a.flags & SRNN_F_X2_PRIO) __builtin_amdgcn_s_setprio(3);
   const X2Geom G = geom(c);
   const bool fin_only = (a.flags & SRNN_F_X2_FINISH_ONLY) != 0;
   __shared__ int64_t s_pre, s_tot, s_base;
@@ -368,7 +498,9 @@ __global__ __launch_bounds__(XT) void k_x2_post(SrnnCfg c, SrnnArgs a) {
   const int64_t nn = ((int64_t)a.world * a.x_cn + XT - 1) / XT;
   if ((int64_t)blockIdx.x < a.x_groups + nn) {
     const int64_t idx = ((int64_t)blockIdx.x - a.x_groups) * XT + threadIdx.x;
-    if (idx < (int64_t)a.world * a.x_cn) post_notice(a, G, (int)(idx / a.x_cn), idx % a.x_cn);
+    const int64_t v = idx < (int64_t)a.world * a.x_cn ? post_notice(a, G, (int)(idx / a.x_cn), idx % a.x_cn) : -1;
+    __shared__ int32_t s_res[XT / 64 + 1];
+    mark_remote_block(a, v, SRNN_NIL, v >= 0, s_res);
     return;
   }
   const int64_t idx = ((int64_t)blockIdx.x - a.x_groups - nn) * XT + threadIdx.x;
@@ -438,7 +570,10 @@ void host_post(const SrnnCfg& c, const SrnnArgs& a) {
   for (int q = 0; q < a.world; ++q) a.x_cno[q] = 0, a.x_crq[q] = 0;
   if (!(a.flags & SRNN_F_X2_PRIME)) Dec::set_gen(a, gen_of(a) + 1);
   for (int q = 0; q < a.world; ++q)
-    for (int64_t k = 0; k < a.x_cn; ++k) post_notice(a, G, q, k);
+    for (int64_t k = 0; k < a.x_cn; ++k) {
+      const int64_t v = post_notice(a, G, q, k);
+      if (v >= 0) mark_remote(a, v, SRNN_NIL);
+    }
   for (int q = 0; q < a.world; ++q)
     for (int64_t k = 0; k < a.x_cq; ++k) post_request(a, G, q, k);
 }

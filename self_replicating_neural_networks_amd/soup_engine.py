@@ -19,11 +19,15 @@ int64 slots, O(local) memory and work, so a soup can fill every GPU's HBM.  Per 
 
     side stream: evolve of the local slots of t (no remote attacker / teacher, ~84 % at R = 8)
     main stream: pack_t (finish of t-1 + decisions of t+1 + the rows of exchange t)
-                 -> all-to-all_t -> post_t (uids of t-1's newborns, census, notices/requests
-                 of t+1) -> evolve of the remote-dependent slots of t
+                 -> all-to-all_t -> evolve of the remote-dependent slots of t
+    post stream: (after the all-to-all) post_t (uids of t-1's newborns, census,
+                 notices/requests of t+1), beside the remote evolve
     join
 
-so the pack, the all-to-all and the post overlap the local evolve.  ``exchange="allgather"`` instead all-gathers
+so the pack, the all-to-all and the post overlap the local evolve, and the chain that sets
+the generation time at R > 1 (pack -> all-to-all -> remote evolve) carries nothing else
+(pack, post and the remote evolve run at raised wave priority; counters are reserved once
+per workgroup).  ``exchange="allgather"`` instead all-gathers
 every rank's rows each generation (the X01 pattern of SURVEY §2.5: one collective, every
 rank holds the whole table and recomputes every slot's decisions; populations < 2^32).
 Results are bitwise independent of R for both (tests/test_dist_gloo.py).
@@ -316,6 +320,18 @@ class SoupEngine:
         bignet = self.spec.kind == "aggregating" and self.spec.P > 64 and not _lib.is_generic(
             self.spec, _lib.OP_SOUP_EVOLVE, self.dtype_code)
         self._evolve_census = not bignet
+        # generation schedule: "serial" -- pack -> all-to-all -> post -> ONE evolve launch of the
+        # local and the remote slots on one stream (no cross-queue dependencies: each costs
+        # ~10 us inside a graph, profiles/r3b); "overlap" -- the local slots on a side stream
+        # beside pack -> all-to-all -> remote evolve, post on a third stream
+        self.schedule = os.environ.get("SRNN_X2_SCHEDULE", "serial")
+        if self.schedule not in ("serial", "overlap"):
+            raise ValueError(f"SRNN_X2_SCHEDULE must be 'serial' or 'overlap', got {self.schedule!r}")
+        # the lane kernels evolve both kinds of slot in one launch (bignet / runtime-shape: two)
+        self._x2_both = not bignet and not _lib.is_generic(self.spec, _lib.OP_SOUP_EVOLVE, self.dtype_code)
+        # single-launch generations: pack leaves, per 64-row block, how many remote-dependent slots
+        # come before it (the launch's lanes on those slots take the remote list's entries)
+        self.x_hpre = self.x_hgrp = None
         p = self.params
         cr, cn, cq = x2_capacities(self.n_total, R, float(p.get("attacking_rate", 0.1)),
                                    float(p.get("learn_from_rate", 0.1)), int(p.get("segment", 0) or 0))
@@ -333,6 +349,13 @@ class SoupEngine:
         # a slot is remote-dependent through a received notice or one of its requests: at most
         # R * (cn + cq) of them per generation
         nr = max(min(self.n, R * (cn + cq)), 1)
+        # timing model of R ranks on one GPU (SRNN_X2_EMULATE_REMOTE=<fraction>, world 1 only):
+        # that fraction of the slots runs through the remote list after the exchange, as the
+        # remote-dependent slots of a multi-rank soup do (same results: the rows are local)
+        fr = float(os.environ.get("SRNN_X2_EMULATE_REMOTE", "0") or 0) if R == 1 else 0.0
+        self.x_emul = int(min(max(fr, 0.0), 1.0) * 0xFFFFFFFF)
+        if self.x_emul:
+            nr = max(self.n, 1)
         self.x_rlist = [torch.zeros(2 * nr, **i32) for _ in range(2)]
         self.x_rcount = [torch.zeros(1, **i32) for _ in range(2)]
         self.x_rslot = [torch.zeros(R * cr, **i64) for _ in range(2)]
@@ -342,6 +365,9 @@ class SoupEngine:
         self.x_srep = torch.zeros(R * cq, **i32)
         self.x_nsrep = torch.zeros(R, **i32)
         self.x_part = torch.zeros(self.x_groups * 6, **i64)
+        if self.schedule == "serial" and self._x2_both:
+            self.x_hpre = torch.zeros(nb, **i32)
+            self.x_hgrp = torch.zeros(self.x_groups, **i32)
         self.x_ctl = torch.zeros(8, **i32)
         self.x_bstat = [torch.zeros(nb * 4, **i64) for _ in range(2)]  # u64[4] per 64-row block
         # notice / request areas are -1 terminated (csrc/srnn_shard.hip): start all -1
@@ -349,8 +375,9 @@ class SoupEngine:
         self.recvbuf = torch.zeros(R * self.x_blk, dtype=torch.uint8, device=dev)
         self.stats_all = torch.zeros(R * 6, **i64)
         self._primed = False
-        self._xs = torch.cuda.Stream(dev) if dev.type == "cuda" else None
-        self.overlap = self._xs is not None
+        self._xs = torch.cuda.Stream(dev) if dev.type == "cuda" else None  # local evolve
+        self._xp = torch.cuda.Stream(dev) if dev.type == "cuda" else None  # post
+        self.overlap = self._xs is not None and self.schedule == "overlap"
 
     # ------------------------------------------------------------------ views
     @property
@@ -556,6 +583,9 @@ class SoupEngine:
         "next" = 1 - p)."""
         a = self._args(stream)
         a.x_cr, a.x_cn, a.x_cq, a.x_blk = self.x_cr, self.x_cn, self.x_cq, self.x_blk
+        a.x_emul = self.x_emul
+        if self.device.type == "cuda" and os.environ.get("SRNN_X2_PRIO", "1") == "1":
+            a.flags |= _lib.FLAG_X2_PRIO  # pack / post / remote evolve win the shared SIMDs
         a.sendbuf, a.recvbuf = _p(self.sendbuf), _p(self.recvbuf)
         a.census = _p(self.census)
         q = 1 - p
@@ -570,6 +600,7 @@ class SoupEngine:
         a.x_crq, a.x_crq_next = _p(self.x_crq[p]), _p(self.x_crq[q])
         a.x_srep, a.x_nsrep = _p(self.x_srep), _p(self.x_nsrep)
         a.x_part, a.x_ctl, a.x_groups = _p(self.x_part), _p(self.x_ctl), self.x_groups
+        a.x_hpre, a.x_hgrp = _p(self.x_hpre), _p(self.x_hgrp)
         a.uid_out, a.uid_base, a.counts = _p(self.uid), _p(self.next_uid), _p(self.counts)
         return a
 
@@ -590,7 +621,7 @@ class SoupEngine:
         pa = self._x2_base(p)
         pa.W2 = _p(self.table_in)
         pa.temp = _p(self.x_bstat[1 - p])  # the finished generation's block stats
-        po = self._x2_base(p)
+        po = self._x2_base(p, self._xp)  # post runs beside the remote evolve
         po.temp = _p(self.x_bstat[1 - p])
         ev = self._x2_base(p)
         ev.W2, ev.W = _p(self.table_in), _p(self.rows_out)
@@ -606,16 +637,35 @@ class SoupEngine:
         loc = self._x2_base(p, xs)
         ctypes.pointer(loc)[0] = ev
         loc.stream = self._stream(xs)
+        if self.schedule == "serial":
+            po = self._x2_base(p)  # everything on the current stream
+            po.temp = _p(self.x_bstat[1 - p])
+            loc = self._x2_base(p)
+            ctypes.pointer(loc)[0] = ev
+            if self._x2_both:
+                rem.flags |= _lib.FLAG_X2_BOTH
+                loc = None
         self._arg_cache[key] = (pa, po, rem, loc, census)
         return self._arg_cache[key]
 
     def _x2_exchange(self, post: _lib.SrnnArgs, remote: Optional[_lib.SrnnArgs] = None):
-        """all-to-all -> post (-> remote evolve) on the current stream (RCCL inside a hipGraph
-        is captured from the origin stream)."""
+        """all-to-all -> remote evolve on the current stream (RCCL inside a hipGraph is
+        captured from the origin stream), post beside the remote evolve on its own stream:
+        the remote-dependent slots of this generation need only the received rows, post
+        prepares the next generation (nothing of this one reads what it writes)."""
         self.dist.all_to_all(self.recvbuf, self.sendbuf)
-        _lib.run(_lib.OP_X2_POST, self.spec, post, self.cfg)
-        if remote is not None:
-            _lib.run(_lib.OP_SOUP_EVOLVE, self.spec, remote, self.cfg)
+        xp = self._xp if remote is not None else None
+        if xp is None:
+            _lib.run(_lib.OP_X2_POST, self.spec, post, self.cfg)
+            if remote is not None:
+                _lib.run(_lib.OP_SOUP_EVOLVE, self.spec, remote, self.cfg)
+            return
+        main = torch.cuda.current_stream(self.device)
+        xp.wait_stream(main)
+        with torch.cuda.stream(xp):
+            _lib.run(_lib.OP_X2_POST, self.spec, post, self.cfg)
+        _lib.run(_lib.OP_SOUP_EVOLVE, self.spec, remote, self.cfg)
+        main.wait_stream(xp)
 
     def _x2_prime(self):
         """First exchange of a (re)started soup: the decisions of THIS generation go out as
@@ -646,6 +696,15 @@ class SoupEngine:
         if not self._primed:
             self._x2_prime()
         pa, po, rem, loc, census = self._x2_args(record)
+        if self.schedule == "serial":
+            _lib.run(_lib.OP_X2_PACK, spec, pa, cfg)
+            self.dist.all_to_all(self.recvbuf, self.sendbuf)
+            _lib.run(_lib.OP_X2_POST, spec, po, cfg)
+            if loc is not None:
+                _lib.run(_lib.OP_SOUP_EVOLVE, spec, loc, cfg)
+            _lib.run(_lib.OP_SOUP_EVOLVE, spec, rem, cfg)  # (with FLAG_X2_BOTH: the local slots too)
+            self._x2_close(record, census)
+            return
         # the local slots need nothing of this generation's exchange: they start at once on
         # the side stream, beside pack -> all-to-all -> post -> remote-dependent slots
         side = self._xs
@@ -659,6 +718,10 @@ class SoupEngine:
             torch.cuda.current_stream(self.device).wait_stream(side)
         else:
             _lib.run(_lib.OP_SOUP_EVOLVE, spec, loc, cfg)
+        self._x2_close(record, census)
+
+    def _x2_close(self, record: bool, census: bool):
+        spec, cfg = self.spec, self.cfg
         if record and self.recorder is not None:
             self.recorder.on_evolved(self)
             ra = self._args()
@@ -827,7 +890,7 @@ class SoupEngine:
         names = ["_bufs", "uid", "next_uid", "_gen_ring", "heads", "nexts", "ballots", "rowflags", "action",
                  "counterpart", "loss", "respawn", "counts", "census", "err", "full", "stats_all", "_blockstat",
                  "_done", "_bs_ring", "x_dep", "x_rlist", "x_rcount", "x_rslot", "x_satt", "x_cno", "x_crq",
-                 "x_srep", "x_nsrep", "x_part", "x_ctl", "x_bstat", "sendbuf", "recvbuf"]
+                 "x_srep", "x_nsrep", "x_part", "x_ctl", "x_bstat", "x_hpre", "x_hgrp", "sendbuf", "recvbuf"]
         out = []
         for k in names:
             v = getattr(self, k, None)

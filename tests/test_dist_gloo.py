@@ -122,3 +122,30 @@ def test_sharded_high_rates_aggregating(tmp_path):
     mp.start_processes(_worker_hi, args=(4, _free_port(), str(tmp_path)), nprocs=4, start_method="spawn", join=True)
     W = np.concatenate([np.load(os.path.join(tmp_path, f"h{r}.npy")) for r in range(4)])
     assert np.array_equal(W, ref.local_rows().numpy(), equal_nan=True)
+
+
+def _worker_emul(rank, world, port, out_dir, frac):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), SRNN_X2_EMULATE_REMOTE=str(frac))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        e = SoupEngine(ArchSpec.weightwise(2, 2), N_TOTAL, PARAMS, device="cpu", seed=21,
+                       dist=Dist(rank, world, 0, None, force=True))
+        assert e.x_emul > 0
+        e.evolve(GENS)
+        assert not e.exchange_overflowed()
+        np.savez(os.path.join(out_dir, "emul.npz"), W=e.local_rows().numpy(), uid=e.uid.numpy())
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("frac", [0.2, 1.0])
+def test_emulated_remote_slots_change_nothing(tmp_path, frac):
+    """the one-rank timing model of R ranks (SRNN_X2_EMULATE_REMOTE) sends a fraction of the
+    slots through the remote list: the soup is bitwise the single-rank one"""
+    ref = SoupEngine(ArchSpec.weightwise(2, 2), N_TOTAL, PARAMS, device="cpu", seed=21)
+    ref.evolve(GENS)
+    mp.start_processes(_worker_emul, args=(1, _free_port(), str(tmp_path), frac), nprocs=1, start_method="spawn",
+                       join=True)
+    got = np.load(os.path.join(tmp_path, "emul.npz"))
+    assert np.array_equal(got["W"], ref.local_rows().numpy(), equal_nan=True)
+    assert np.array_equal(got["uid"], ref.uid.numpy())

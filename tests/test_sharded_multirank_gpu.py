@@ -33,8 +33,9 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, spec_json, out_dir, dtype, chunks):
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), SRNN_SHARE_DEVICE="1")
+def _worker(rank, world, port, spec_json, out_dir, dtype, chunks, schedule):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), SRNN_SHARE_DEVICE="1",
+                      SRNN_X2_SCHEDULE=schedule)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         dev = torch.device("cuda", 0)
@@ -42,7 +43,7 @@ def _worker(rank, world, port, spec_json, out_dir, dtype, chunks):
         d = Dist(rank, world, 0, None)
         e = SoupEngine(ArchSpec.from_json(spec_json), N_TOTAL, PARAMS, device=dev, seed=21, dist=d,
                        dtype=DTYPES[dtype])
-        assert e.fused and e.x2 and e.overlap
+        assert e.fused and e.x2 and e.overlap == (schedule == "overlap") and e.schedule == schedule
         e.stats = True
         for k in chunks:
             e.evolve(k)
@@ -56,16 +57,18 @@ def _worker(rank, world, port, spec_json, out_dir, dtype, chunks):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,dtype,chunks", [(2, "float32", (2, 4)), (3, "float32", (6,)),
-                                                (2, "bfloat16", (3, 3))])
-def test_multirank_device_soup_equals_single_rank(cuda, tmp_path, world, dtype, chunks):
+@pytest.mark.parametrize("world,dtype,chunks,schedule", [
+    (2, "float32", (2, 4), "serial"), (3, "float32", (6,), "serial"), (2, "bfloat16", (3, 3), "serial"),
+    (2, "float32", (2, 4), "overlap"), (3, "float32", (6,), "overlap")])
+def test_multirank_device_soup_equals_single_rank(cuda, tmp_path, world, dtype, chunks, schedule):
+    """both generation schedules: one stream, or the local slots beside the exchange"""
     spec = ArchSpec.weightwise(2, 2)
     ref = SoupEngine(spec, N_TOTAL, PARAMS, device=cuda, seed=21, dtype=DTYPES[dtype])
     ref.stats = True
     ref.evolve(sum(chunks))
     ref_counts = ref.count()
     torch.cuda.synchronize()
-    mp.start_processes(_worker, args=(world, _free_port(), spec.to_json(), str(tmp_path), dtype, chunks),
+    mp.start_processes(_worker, args=(world, _free_port(), spec.to_json(), str(tmp_path), dtype, chunks, schedule),
                        nprocs=world, start_method="spawn", join=True)
     parts = [np.load(os.path.join(tmp_path, f"r{r}.npz")) for r in range(world)]
     W = np.concatenate([p["W"] for p in parts])
