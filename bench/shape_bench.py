@@ -44,7 +44,7 @@ def timeit(fn, reps=5, warmup=1):
 def sgd_macs(spec):
     """MACs of one SGD step (forward + input gradients + weight updates) of one particle."""
     if spec.kind == "weightwise":
-        shapes = spec.layer_shapes()
+        shapes = spec.layer_shapes
         fwd = sum(r * c for r, c in shapes)
         bwd = sum(r * c for r, c in shapes[1:])
         return fwd + bwd + fwd, spec.P  # per step, steps per epoch
@@ -63,6 +63,7 @@ def engine_of(spec, op):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--n", type=int, default=100_000)
+    ap.add_argument("--big-n", type=int, default=16_384, help="population of the shapes with P > 100")
     ap.add_argument("--epochs", type=int, default=20)
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--only", default="")
@@ -76,7 +77,7 @@ def main():
         name = f"{spec.kind}({spec.width},{spec.depth})"
         if args.only and args.only != name and name != "weightwise(2,2)":
             continue
-        n = args.n
+        n = args.n if spec.P <= 100 else args.big_n
         uid = torch.arange(n, dtype=torch.int64, device=dev)
         W = torch.zeros(n, spec.PP, device=dev)
         K.init_rows(spec, W, uid, 1)
@@ -102,7 +103,7 @@ def main():
         t_gen = r.get("soup_gen_graph_us", r["soup_gen_us"])
         if base is None:
             base = (t_gen, gen_flops)
-        r["time_ratio_vs_ww22"] = round(t_gen / base[0], 2)
+        r["time_ratio_vs_ww22"] = round(t_gen / base[0] * args.n / n, 2)  # per particle
         r["flop_ratio_vs_ww22"] = round(gen_flops / base[1], 2)
         print(json.dumps(r), flush=True)
         del eng, W, W0

@@ -13,6 +13,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <math.h>
+#include <type_traits>
 
 #define SRNN_HD __host__ __device__ __forceinline__
 
@@ -556,8 +557,10 @@ struct Weightwise {
       Net::forward(w, x, acts, y);
       float e = y[0] - smp.x;
       loss += e * e;
-      float gy[1] = {2.0f * e};
-      Net::backward_update(w, acts, gy, c.lr);
+      // dL/dy = 2e; the folded step -lr * 2e is formed as -(2 lr) * e: the same real product,
+      // rounded once, with one multiply less on the per-sample chain
+      float gy[1] = {e};
+      Net::backward_update(w, acts, gy, 2.0f * c.lr);
     }
     c.ctr += 1;
     return loss / (float)P;
@@ -597,10 +600,9 @@ struct Weightwise {
       U4 rr = perm_draw(c.rng, c.uid, c.ctr, P_SHUFFLE);
       uint32_t pair = c.ctr >> 1;
       uint64_t pn = c.shuffle ? perm_from_bits<P>(perm_bits(rr, c.ctr)) : ident;
-      for (int e = 0; e < E; ++e) {
-        if (SELF && e > 0)
-#pragma unroll
-          for (int k = 0; k < P; ++k) reinterpret_cast<float*>(&c.samp[k * c.stride])[0] = w[k];
+      const float lr2 = 2.0f * c.lr;  // folded step -(2 lr) * err (train_epoch)
+      // one epoch; only the last one's mean loss is returned, so only it accumulates the loss
+      auto epoch = [&](auto with_loss) {
         uint64_t pn_next = ident;
         if (c.shuffle) {
           const uint32_t nx = c.ctr + 1u;
@@ -620,13 +622,20 @@ struct Weightwise {
           float acts[Net::NACT], y[1];
           Net::forward(w, x, acts, y);
           float err = y[0] - smp[q].x;
-          acc += err * err;
-          float gy[1] = {2.0f * err};
-          Net::backward_update(w, acts, gy, c.lr);
+          if constexpr (decltype(with_loss)::value) acc += err * err;
+          float gy[1] = {err};
+          Net::backward_update(w, acts, gy, lr2);
         }
-        loss = acc / (float)P;
+        if constexpr (decltype(with_loss)::value) loss = acc / (float)P;
         c.ctr += 1;
         pn = pn_next;
+      };
+      for (int e = 0; e < E; ++e) {
+        if (SELF && e > 0)
+#pragma unroll
+          for (int k = 0; k < P; ++k) reinterpret_cast<float*>(&c.samp[k * c.stride])[0] = w[k];
+        if (e + 1 < E) epoch(std::false_type{});
+        else epoch(std::true_type{});
       }
       return loss;
     }

@@ -469,8 +469,8 @@ SRNN_HD float g_train_epoch(const GCtx& x, SV w, const SV& smp, TrainCtx& c) {
       g_forward(s, w, v1, acts, v2);
       float e = v2[0] - v1[0];
       loss += e * e;
-      v2[0] = 2.0f * e;
-      g_backward(s, w, acts, v2, c.lr, v3, v4);
+      v2[0] = e;  // the folded step -(2 lr) * e (Weightwise::train_epoch)
+      g_backward(s, w, acts, v2, 2.0f * c.lr, v3, v4);
     }
     c.ctr += 1;
     return loss / (float)s.P;

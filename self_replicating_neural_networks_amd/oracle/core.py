@@ -329,7 +329,8 @@ def train_epoch(spec: ArchSpec, w, s, lr=0.01, shuffle=True, seed=0, uids=None, 
             out, acts = _mlp_forward(mats, xs)
             e = out[:, 0] - ys
             loss += e * e
-            _mlp_backward_update(mats, acts, (np.float32(2.0) * e)[:, None], lr)
+            # dL/dy = 2e, folded step -(2 lr) * e (csrc Weightwise::train_epoch)
+            _mlp_backward_update(mats, acts, e[:, None], 2 * lr)
         return _flat(spec, mats), loss / np.float32(spec.P)
     if spec.kind in ("aggregating", "fft"):
         g = aggregate(spec, s, spec.aggregator) if spec.kind == "aggregating" else fft_reduce(spec, s)

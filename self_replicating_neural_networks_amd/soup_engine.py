@@ -814,9 +814,9 @@ class SoupEngine:
         left = int(iterations)
         while left > 0:
             # the largest captured multi-generation graph that fits what is left
-            ch = next((c for c in self._chunks if c[2] <= left), None)
+            ch = next((c for c in self._chunks if c[2] <= left and c[1] == self._p), None)
             if (ch is not None and not (record and self.recorder is not None)
-                    and self._p == ch[1] and self.trajectory is None and self.metrics is None):
+                    and self.trajectory is None and self.metrics is None):
                 # G generations in one graph launch (no inter-graph gaps)
                 self._join_side()
                 ch[0].replay()
@@ -963,24 +963,39 @@ class SoupEngine:
             return False
         # graphs[k] was captured with parity p0 ^ k; index them by parity
         self._graphs = graphs if p0 == 0 else graphs[::-1]
+        self._chunks = []
         self._capture_chunk(s, p0, pend0)
+        if self._chunks:
+            # one more (eager) generation, then the same chunks from the other parity: an
+            # evolve replays multi-generation graphs whatever parity it starts at (an odd
+            # warmup would otherwise leave every later generation on single-generation graphs)
+            with torch.cuda.stream(s):
+                self.time += 1
+                self._generation()
+                self._join_side()
+            torch.cuda.current_stream(self.device).wait_stream(s)
+            torch.cuda.synchronize(self.device)
+            self._capture_chunk(s, self._p, self._pending)
         return True
 
     @staticmethod
     def _chunk_sizes():
         """Generations per multi-generation graph (SRNN_GRAPH_CHUNKS, even sizes): an evolve
         of K generations replays the largest that fit, so a short timed region pays few
-        launches and few finish launches (16 + 4 for K = 20 instead of 8 + 8 + 4 singles)."""
-        v = os.environ.get("SRNN_GRAPH_CHUNKS") or os.environ.get("SRNN_GRAPH_CHUNK") or "16,8,4,2"
+        launches and few finish launches (one 20-generation graph for K = 20, 20 + 20 + 8 + 2
+        for K = 50)."""
+        v = os.environ.get("SRNN_GRAPH_CHUNKS") or os.environ.get("SRNN_GRAPH_CHUNK") or "20,16,8,4,2"
         return sorted({int(x) for x in v.split(",") if int(x) >= 2 and int(x) % 2 == 0}, reverse=True)
 
     def _capture_chunk(self, s, p0, pend0):
-        self._chunks = []
+        """Multi-generation graphs starting (and ending) at parity p0, added to _chunks
+        (largest first)."""
         for G in self._chunk_sizes():
             ch = self._capture_chunk_g(s, p0, pend0, G)
             if ch is None:
                 break
             self._chunks.append(ch)
+        self._chunks.sort(key=lambda c: -c[2])
         self._chunk = self._chunks[0] if self._chunks else None
 
     def _flags_state(self):
