@@ -13,7 +13,6 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <math.h>
-#include <type_traits>
 
 #define SRNN_HD __host__ __device__ __forceinline__
 
@@ -601,8 +600,10 @@ struct Weightwise {
       uint32_t pair = c.ctr >> 1;
       uint64_t pn = c.shuffle ? perm_from_bits<P>(perm_bits(rr, c.ctr)) : ident;
       const float lr2 = 2.0f * c.lr;  // folded step -(2 lr) * err (train_epoch)
-      // one epoch; only the last one's mean loss is returned, so only it accumulates the loss
-      auto epoch = [&](auto with_loss) {
+      for (int e = 0; e < E; ++e) {
+        if (SELF && e > 0)
+#pragma unroll
+          for (int k = 0; k < P; ++k) reinterpret_cast<float*>(&c.samp[k * c.stride])[0] = w[k];
         uint64_t pn_next = ident;
         if (c.shuffle) {
           const uint32_t nx = c.ctr + 1u;
@@ -622,20 +623,13 @@ struct Weightwise {
           float acts[Net::NACT], y[1];
           Net::forward(w, x, acts, y);
           float err = y[0] - smp[q].x;
-          if constexpr (decltype(with_loss)::value) acc += err * err;
+          acc += err * err;
           float gy[1] = {err};
           Net::backward_update(w, acts, gy, lr2);
         }
-        if constexpr (decltype(with_loss)::value) loss = acc / (float)P;
+        loss = acc / (float)P;
         c.ctr += 1;
         pn = pn_next;
-      };
-      for (int e = 0; e < E; ++e) {
-        if (SELF && e > 0)
-#pragma unroll
-          for (int k = 0; k < P; ++k) reinterpret_cast<float*>(&c.samp[k * c.stride])[0] = w[k];
-        if (e + 1 < E) epoch(std::false_type{});
-        else epoch(std::true_type{});
       }
       return loss;
     }

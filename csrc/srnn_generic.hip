@@ -1397,6 +1397,227 @@ static bool generic_op_supported(int op) {
   }
 }
 
+// ==================================================================================
+// Wide Weightwise nets, U lanes per particle (SGD: train / learn_from).  The lane-per-particle
+// path streams every weight, activation and sample through element-major scratch in HBM
+// (WW(16, 2): 0.27 TFLOP/s, profiles/r3d).  Here a wave holds G = 64 / U particles, U = the
+// next power of two >= width: lane u of a particle computes unit u of every layer, the weights
+// (hidden W x W layers with a padded row stride: the backward pass reads rows), the frozen
+// samples, the permutation and the activations live in LDS, and the coordinate table is shared
+// by the block.  Every dot product keeps the lane path's order (x[0]*k then fma over the inputs;
+// the output unit's chain on one lane), every weight gets the same single fma, so results are
+// bitwise those of g_train_epochs (tests/test_generic_gpu.py).
+// ==================================================================================
+struct WWave {
+  int U, G, PW, GS;         // lanes per particle, particles per wave, padded weights, floats per particle
+  int poff[GMAXL], pst[GMAXL];  // padded layer offsets and row strides
+  int o_sv, o_perm, o_acts, o_sa, o_sb, o_misc;
+};
+static bool ww_wave_geom(const GShape& s, WWave& g) {
+  if (s.kind != 0 || s.P <= 16 || s.W < 3 || s.W > 64) return false;
+  g.U = 4;
+  while (g.U < s.W) g.U *= 2;
+  g.G = 64 / g.U;
+  int o = 0;
+  for (int l = 0; l < s.NL; ++l) {
+    g.pst[l] = s.cols[l] + ((l > 0 && l < s.D) ? 1 : 0);  // hidden layers: odd row stride
+    g.poff[l] = o;
+    o += s.rows[l] * g.pst[l];
+  }
+  g.PW = o;
+  g.o_sv = o;
+  g.o_perm = g.o_sv + s.P;
+  g.o_acts = g.o_perm + s.P;
+  g.o_sa = g.o_acts + s.IN + s.D * s.W;
+  g.o_sb = g.o_sa + s.W;
+  g.o_misc = g.o_sb + s.W;
+  g.GS = g.o_misc + 4;
+  return true;
+}
+static size_t ww_wave_lds(const GShape& s, const WWave& g) { return ((size_t)3 * s.P + (size_t)g.G * g.GS) * 4; }
+
+// padded LDS index of flat weight k
+__device__ __forceinline__ int ww_pidx(const GShape& s, const WWave& g, int k) {
+  int l = 0;
+  while (l + 1 < s.NL && s.off[l + 1] <= k) ++l;
+  const int q = k - s.off[l], i = q / s.cols[l], j = q - i * s.cols[l];
+  return g.poff[l] + i * g.pst[l] + j;
+}
+
+template <int OP>
+__global__ __launch_bounds__(64) void k_ww_wave(GShape s, WWave g, SrnnArgs a) {
+  extern __shared__ float sm[];
+  float* coords = sm;  // [P][3], whole block
+  make_coords_dev(s, coords);
+  const int lane = threadIdx.x, u = lane % g.U, grp = lane / g.U;
+  float* pw = sm + 3 * s.P + grp * g.GS;  // this particle's region
+  float* sv = pw + g.o_sv;
+  int* perm = reinterpret_cast<int*>(pw + g.o_perm);
+  float* acts = pw + g.o_acts;
+  float* misc = pw + g.o_misc;
+  const int W = s.W, D = s.D;
+  const float lr2 = 2.0f * a.lr;  // the folded step -(2 lr) * e (Weightwise::train_epoch)
+  const bool shuffle = (a.flags & SRNN_F_SHUFFLE) != 0;
+  const Rng rng = GItem::rng(a);
+  for (int64_t base = (int64_t)blockIdx.x * g.G; base < a.n; base += (int64_t)gridDim.x * g.G) {
+    const int64_t i = base + grp;
+    const bool active = i < a.n;
+    if (active) {
+      const char* row = GItem::rowp(s, a.W, i);
+      for (int k = u; k < s.P; k += g.U) pw[ww_pidx(s, g, k)] = g_dec(row, k, s.dtype);
+      if (OP == OP_LEARN) {
+        const char* t = GItem::rowp(s, a.W2, a.idx_t ? a.idx_t[i] : i);
+        for (int k = u; k < s.P; k += g.U) sv[k] = g_dec(t, k, s.dtype);
+      }
+    }
+    __syncthreads();
+    const uint64_t uid = active ? GItem::uid_of(a, i) : 0;
+    uint32_t ctr = a.ctr;
+    float loss = 0.f;
+    for (int e = 0; e < a.epochs; ++e) {
+      if (OP == OP_TRAIN)  // samples = the weights at the epoch start
+        for (int k = u; k < s.P; k += g.U) sv[k] = pw[ww_pidx(s, g, k)];
+      __syncthreads();
+      if (shuffle) {
+        // g_fisher_yates (same draws: one Philox block per 4 swaps, stream (uid, ctr * 64 +
+        // block)); the swap chain on lane 0 of the particle
+        for (int k = u; k < s.P; k += g.U) perm[k] = k;
+        __syncthreads();
+        if (u == 0 && active) {
+          U4 r{0, 0, 0, 0};
+          int used = 4;
+          uint32_t blk = 0;
+          for (int t = s.P - 1; t > 0; --t) {
+            if (used == 4) {
+              r = rng.draw(uid, ctr * 64u + blk, P_SHUFFLE);
+              ++blk;
+              used = 0;
+            }
+            const uint32_t x = used == 0 ? r.x : used == 1 ? r.y : used == 2 ? r.z : r.w;
+            ++used;
+            int j = (int)(u01(x) * (float)(t + 1));
+            if (j > t) j = t;
+            const int pt = perm[t];
+            perm[t] = perm[j];
+            perm[j] = pt;
+          }
+        }
+        __syncthreads();
+      }
+      float acc = 0.f;
+      for (int q = 0; q < s.P; ++q) {
+        const int idx = shuffle ? perm[q] : q;
+        const float x0 = sv[idx];
+        const float x1 = coords[3 * idx], x2 = coords[3 * idx + 1], x3 = coords[3 * idx + 2];
+        if (u < 4) acts[u] = u == 0 ? x0 : u == 1 ? x1 : u == 2 ? x2 : x3;
+        // layer 0: h1[u] = x0*K0[0][u] then fma over the 3 coordinates
+        if (u < W) {
+          const float* K = pw + g.poff[0];
+          float h = x0 * K[u];
+          h = fmaf(x1, K[g.pst[0] + u], h);
+          h = fmaf(x2, K[2 * g.pst[0] + u], h);
+          h = fmaf(x3, K[3 * g.pst[0] + u], h);
+          acts[4 + u] = h;
+        }
+        __syncthreads();
+        for (int l = 1; l < D; ++l) {  // hidden layers: column u
+          if (u < W) {
+            const float* K = pw + g.poff[l];
+            const float* x = acts + 4 + (l - 1) * W;
+            float h = x[0] * K[u];
+            for (int r = 1; r < W; ++r) h = fmaf(x[r], K[r * g.pst[l] + u], h);
+            acts[4 + l * W + u] = h;
+          }
+          __syncthreads();
+        }
+        // output unit (one chain, lane 0) -> error, loss, the step so = -(2 lr) * e
+        if (u == 0) {
+          const float* K = pw + g.poff[D];
+          const float* x = acts + 4 + (D - 1) * W;
+          float y = x[0] * K[0];
+          for (int r = 1; r < W; ++r) y = fmaf(x[r], K[r], y);
+          const float err = y - x0;
+          acc += err * err;
+          misc[0] = -lr2 * err;
+        }
+        __syncthreads();
+        // last layer (W x 1): si[u] = K[u] * so (pre-update), K[u] += h_D[u] * so
+        float* si = pw + g.o_sa;
+        float* sn = pw + g.o_sb;
+        if (u < W) {
+          float* K = pw + g.poff[D];
+          const float so = misc[0];
+          si[u] = K[u] * so;
+          K[u] = fmaf(acts[4 + (D - 1) * W + u], so, K[u]);
+        }
+        __syncthreads();
+        for (int l = D - 1; l >= 1; --l) {  // hidden layers: row u (si from the pre-update row)
+          if (u < W) {
+            float* K = pw + g.poff[l] + u * g.pst[l];
+            float sacc = K[0] * si[0];
+            for (int c = 1; c < W; ++c) sacc = fmaf(K[c], si[c], sacc);
+            const float xr = acts[4 + (l - 1) * W + u];
+            for (int c = 0; c < W; ++c) K[c] = fmaf(xr, si[c], K[c]);
+            sn[u] = sacc;
+          }
+          __syncthreads();
+          float* t = si;
+          si = sn;
+          sn = t;
+        }
+        // layer 0 (4 x W): column u, no input gradient
+        if (u < W) {
+          float* K = pw + g.poff[0];
+          const float so = si[u];
+          K[u] = fmaf(x0, so, K[u]);
+          K[g.pst[0] + u] = fmaf(x1, so, K[g.pst[0] + u]);
+          K[2 * g.pst[0] + u] = fmaf(x2, so, K[2 * g.pst[0] + u]);
+          K[3 * g.pst[0] + u] = fmaf(x3, so, K[3 * g.pst[0] + u]);
+        }
+        __syncthreads();
+      }
+      loss = acc / (float)s.P;
+      ctr += 1;
+    }
+    if (active) {
+      char* row = GItem::rowp(s, a.W, i);
+      for (int k = u; k < s.PP; k += g.U) {
+        const float v = k < s.P ? pw[ww_pidx(s, g, k)] : 0.f;
+        if (s.dtype == 0) reinterpret_cast<float*>(row)[k] = v;
+        else reinterpret_cast<uint16_t*>(row)[k] = s.dtype == 1 ? StBF16::enc(v) : StF16::enc(v);
+      }
+      if (a.loss && u == 0) a.loss[i] = loss;
+    }
+    __syncthreads();
+  }
+}
+
+static int g_ww_wave = -1;  // SRNN_WW_WAVE=0: lane path for every width (A/B tests)
+extern "C" void srnn_set_ww_wave(int on) { g_ww_wave = on ? 1 : 0; }
+static bool ww_serves(int op, const GShape& s, const SrnnArgs& a, WWave& g) {
+  if (g_ww_wave < 0) {
+    const char* e = std::getenv("SRNN_WW_WAVE");
+    g_ww_wave = (e && e[0] == '0') ? 0 : 1;
+  }
+  if (!g_ww_wave || !a.dev || (op != OP_TRAIN && op != OP_LEARN)) return false;
+  return ww_wave_geom(s, g) && ww_wave_lds(s, g) <= 64 * 1024;
+}
+static int ww_launch(int op, const GShape& s, const WWave& g, const SrnnArgs& a) {
+  if (a.n <= 0) return 0;
+  int64_t blocks = (a.n + g.G - 1) / g.G;
+  blocks = blocks < 65536 ? blocks : 65536;
+  const size_t lds = ww_wave_lds(s, g);
+  hipStream_t st = (hipStream_t)a.stream;
+  if (op == OP_TRAIN) hipLaunchKernelGGL((k_ww_wave<OP_TRAIN>), dim3((unsigned)blocks), dim3(64), lds, st, s, g, a);
+  else hipLaunchKernelGGL((k_ww_wave<OP_LEARN>), dim3((unsigned)blocks), dim3(64), lds, st, s, g, a);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) {
+    set_error(hipGetErrorString(e));
+    return -3;
+  }
+  return 0;
+}
+
 // lanes of a device launch and the scratch bytes they need
 static int64_t generic_lanes(const GShape& s, const SrnnArgs& a, int64_t items) {
   const int64_t per = g_lane_bytes(s);
@@ -1421,6 +1642,8 @@ static int generic_launch(int op, const GShape& s, const SrnnArgs& a) {
     hipLaunchKernelGGL(k_g_respawn_seq, dim3(1), dim3(GTBR), 0, st, s, a);
   } else if (rw_serves(op, s, a)) {
     return rw_launch(op, s, a);
+  } else if (WWave g; ww_serves(op, s, a, g)) {
+    return ww_launch(op, s, g, a);
   } else {
     if (a.n <= 0) return 0;
     const int64_t lanes = generic_lanes(s, a, a.n);

@@ -155,6 +155,8 @@ def lib():
         L.srnn_set_force_generic.restype = None
         L.srnn_set_rnn_wave.argtypes = [ctypes.c_int]
         L.srnn_set_rnn_wave.restype = None
+        L.srnn_set_ww_wave.argtypes = [ctypes.c_int]
+        L.srnn_set_ww_wave.restype = None
         vp, i64, cp = ctypes.c_void_p, ctypes.c_int64, ctypes.c_char_p
         for name, args in (("srnn_comm_available", [cp]), ("srnn_comm_unique_id", [cp, vp, ctypes.c_int]),
                            ("srnn_comm_init", [cp, vp, ctypes.c_int, ctypes.c_int, ctypes.c_int,
@@ -207,6 +209,12 @@ def set_force_generic(on: bool) -> None:
 def set_rnn_wave(on: bool) -> None:
     """Wide Recurrent nets wave per particle (default) or lane per particle (A/B tests)."""
     lib().srnn_set_rnn_wave(1 if on else 0)
+
+
+def set_ww_wave(on: bool) -> None:
+    """Runtime-shape Weightwise training on lanes-per-particle waves (default) or lane per
+    particle (A/B tests)."""
+    lib().srnn_set_ww_wave(1 if on else 0)
 
 
 def generic_scratch_bytes(spec, n: int, dtype: int = DTYPE_FP32, max_lanes: int = 65536) -> int:

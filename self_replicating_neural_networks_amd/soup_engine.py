@@ -930,11 +930,14 @@ class SoupEngine:
             return False
         s = torch.cuda.Stream(self.device)
         s.wait_stream(torch.cuda.current_stream(self.device))
+        # max(warmup, 1) eager generations in all: the last one runs between the capture of the
+        # multi-generation graphs of the two parities (below)
         with torch.cuda.stream(s):
-            for _ in range(max(warmup, 1)):
+            for _ in range(max(warmup, 1) - 1):
                 self.time += 1
                 self._generation()
             self._join_side()
+            self._prepare_capture()
         torch.cuda.current_stream(self.device).wait_stream(s)
         torch.cuda.synchronize(self.device)
         graphs = []
@@ -960,23 +963,37 @@ class SoupEngine:
             ok = self._agree(self._validate_graphs(graphs if p0 == 0 else graphs[::-1]))
         if not ok:
             self._graphs = None
+            self.time += 1  # the last warmup generation, eagerly
+            self._generation()
+            self._join_side()
             return False
         # graphs[k] was captured with parity p0 ^ k; index them by parity
         self._graphs = graphs if p0 == 0 else graphs[::-1]
         self._chunks = []
         self._capture_chunk(s, p0, pend0)
+        # the last warmup generation (eager), then the same chunks from the other parity: an
+        # evolve replays multi-generation graphs whatever parity it starts at (an odd
+        # warmup would otherwise leave every later generation on single-generation graphs)
+        with torch.cuda.stream(s):
+            self.time += 1
+            self._generation()
+            self._join_side()
+        torch.cuda.current_stream(self.device).wait_stream(s)
+        torch.cuda.synchronize(self.device)
         if self._chunks:
-            # one more (eager) generation, then the same chunks from the other parity: an
-            # evolve replays multi-generation graphs whatever parity it starts at (an odd
-            # warmup would otherwise leave every later generation on single-generation graphs)
-            with torch.cuda.stream(s):
-                self.time += 1
-                self._generation()
-                self._join_side()
-            torch.cuda.current_stream(self.device).wait_stream(s)
-            torch.cuda.synchronize(self.device)
             self._capture_chunk(s, self._p, self._pending)
         return True
+
+    def _prepare_capture(self):
+        """The one-time work a first generation does before its graph-captured steady state:
+        this generation's attack lists (fused single rank) or the first exchange (sharded)."""
+        if self.x2:
+            if not self._primed:
+                self._x2_prime()
+        elif self.fused and not self._lists_ready and not self.dist.enabled:
+            a, _, _ = self._gen_args()
+            _lib.run(_lib.OP_SOUP_DECIDE, self.spec, a, self.cfg)
+            self._lists_ready = True
 
     @staticmethod
     def _chunk_sizes():

@@ -294,8 +294,9 @@ def test_fused_generation_equals_unfused(cuda, spec):
 
 
 def test_multi_generation_graph_equals_eager(cuda):
-    """capture() also records graphs of 16, 8, 4 and 2 consecutive generations (one launch
-    each): 21 generations through them (16 + 4 + a single-generation graph) == eager."""
+    """capture() also records graphs of 20, 16, 8, 4 and 2 consecutive generations for both
+    start parities (one launch each): 21 and then 23 generations through them (20 + a
+    single-generation graph, then 20 + 2 + 1 from the other parity) == eager."""
     spec = ArchSpec.weightwise(2, 2)
     params = dict(attacking_rate=0.1, learn_from_rate=0.1, train=4, remove_divergent=True, remove_zero=True,
                   epsilon=1e-4)
@@ -303,11 +304,14 @@ def test_multi_generation_graph_equals_eager(cuda):
     b = SoupEngine(spec, 30000, params, device=cuda, seed=21)
     a.stats = b.stats = True
     assert a.capture(warmup=1)
-    assert a._chunk is not None and [c[2] for c in a._chunks] == [16, 8, 4, 2]
+    assert a._chunk is not None and [c[2] for c in a._chunks] == [20, 20, 16, 16, 8, 8, 4, 4, 2, 2]
+    assert sorted({c[1] for c in a._chunks}) == [0, 1]
     b.evolve(1)
     a.evolve(21)
     b.evolve(21)
-    assert a.time == b.time == 22
+    a.evolve(23)
+    b.evolve(23)
+    assert a.time == b.time == 45
     assert torch.equal(a.local_rows(), b.local_rows())
     assert torch.equal(a.uid, b.uid)
     assert a.last_census() == b.last_census()

@@ -1,0 +1,64 @@
+"""Runtime-shape Weightwise SGD on lanes-per-particle waves (csrc/srnn_generic.hip k_ww_wave:
+U = next power of two >= width lanes per particle, weights / samples / activations in LDS):
+bitwise equal to the lane-per-particle runtime-shape path on the same device (same operation
+order, same Philox shuffles), for self-training and learn_from, fp32 and 16-bit tables, and close
+to the numpy oracle."""
+import numpy as np
+import pytest
+import torch
+
+from self_replicating_neural_networks_amd.arch import ArchSpec
+from self_replicating_neural_networks_amd.ops import _lib
+from self_replicating_neural_networks_amd.ops import kernels as K
+from self_replicating_neural_networks_amd.oracle import core as O
+
+pytestmark = pytest.mark.gpu
+
+
+def _train_learn(spec, dev, dtype, n=700, shuffle=True):
+    uid = torch.arange(n, dtype=torch.int64, device=dev) + 3
+    W = torch.zeros(n, spec.PP, device=dev)
+    K.init_rows(spec, W, uid, 9)
+    W = W.to(dtype)
+    T = W.clone()
+    tl = K.train(spec, T, epochs=3, uid=uid, seed=9, ctr=17, shuffle=shuffle)
+    L = W.clone()
+    idx = torch.roll(torch.arange(n, device=dev), 5).contiguous()
+    ll = K.learn_from(spec, L, W, idx_t=idx, epochs=2, uid=uid, seed=9, ctr=4, shuffle=shuffle)
+    torch.cuda.synchronize()
+    return dict(train=T, train_loss=tl, learn=L, learn_loss=ll), W
+
+
+@pytest.mark.parametrize("w,d", [(3, 3), (10, 3), (16, 2), (5, 4), (32, 2)])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16], ids=["f32", "bf16"])
+def test_ww_wave_equals_lane_path(cuda, w, d, dtype):
+    spec = ArchSpec.weightwise(w, d)
+    assert _lib.is_generic(spec, _lib.OP_TRAIN, K.dtype_code(dtype))
+    outs = []
+    for wave in (True, False):
+        _lib.set_ww_wave(wave)
+        try:
+            outs.append(_train_learn(spec, cuda, dtype)[0])
+        finally:
+            _lib.set_ww_wave(True)
+    a, b = outs
+    bits = lambda t: t.contiguous().view(torch.uint8)
+    bad = [k for k in a if not torch.equal(bits(a[k]), bits(b[k]))]
+    assert not bad, bad
+
+
+def test_ww_wave_close_to_oracle(cuda):
+    spec = ArchSpec.weightwise(10, 3)
+    out, W0 = _train_learn(spec, cuda, torch.float32, n=64)
+    uid = np.arange(64, dtype=np.int64) + 3
+    ow = W0[:, :spec.P].cpu().numpy()
+    ref = ow.copy()
+    ctr = 17
+    for _ in range(3):
+        ref, _loss = O.train_epoch(spec, ref, ref.copy(), shuffle=True, seed=9, uids=uid, ctr=ctr)
+        ctr += 1
+    got = out["train"][:, :spec.P].cpu().numpy()
+    ok = np.all(np.isfinite(got), 1) & np.all(np.isfinite(ref), 1)
+    assert ok.sum() > 32
+    err = np.max(np.abs(got[ok] - ref[ok]) / (np.max(np.abs(ref[ok]), 1, keepdims=True) + 1e-6))
+    assert err < 1e-4
