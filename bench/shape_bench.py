@@ -56,7 +56,12 @@ def sgd_macs(spec):
 
 def engine_of(spec, op):
     if _lib.is_generic(spec, op):
-        return "runtime-shape"
+        if op in (_lib.OP_TRAIN, _lib.OP_LEARN):
+            if spec.kind == "weightwise" and spec.P > 16 and 3 <= spec.width <= 64:
+                return "runtime-shape, lanes-per-particle waves (k_ww_wave)"
+            if spec.kind == "recurrent" and spec.width >= 8:
+                return "runtime-shape, wave per particle (k_rnn_wave)"
+        return "runtime-shape, lane per particle"
     return "wave" if K.is_wave_per_particle(spec) else "lane"
 
 
@@ -67,6 +72,8 @@ def main():
     ap.add_argument("--epochs", type=int, default=20)
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--only", default="")
+    ap.add_argument("--soup-max-p", type=int, default=400,
+                    help="time soup generations only up to this P (larger nets' soups run the lane path)")
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     specs = [ArchSpec.weightwise(2, 2), ArchSpec.weightwise(3, 3), ArchSpec.weightwise(4, 3),
@@ -93,6 +100,10 @@ def main():
         r["train_us"] = round(t, 1)
         r["sgd_steps_per_s"] = n * args.epochs * steps / (t * 1e-6)
         r["train_tflops"] = n * args.epochs * steps * macs * 2 / (t * 1e-6) / 1e12
+        print(json.dumps({"arch": name, "train_us": r["train_us"], "note": "train done"}), flush=True)
+        if spec.P > args.soup_max_p:
+            print(json.dumps(r), flush=True)
+            continue
         eng = SoupEngine(spec, n, dict(PARAMS, train=args.epochs), device=dev, seed=5)
         eng.evolve(1)
         r["soup_gen_us"] = round(timeit(lambda: eng.evolve(1), args.reps), 1)
