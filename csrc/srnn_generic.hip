@@ -957,6 +957,8 @@ __global__ __launch_bounds__(GTBR) void k_g_respawn_seq(GShape s, SrnnArgs a) {
       g_store(s, GItem::rowp(s, a.W, r), w);
     }
   }
+  // the ballots are consumed (the lanes-per-particle soup kernel ORs its respawns into them)
+  for (int64_t b = b0; b < b1; ++b) a.ballots[b] = 0ull;
   __syncthreads();
   if (threadIdx.x == 0) {
     a.uid_base[0] = base + total;
@@ -1413,7 +1415,7 @@ struct WWave {
   int poff[GMAXL], pst[GMAXL];  // padded layer offsets and row strides
   int o_sv, o_perm, o_acts, o_sa, o_sb, o_misc;
 };
-static bool ww_wave_geom(const GShape& s, WWave& g) {
+static bool ww_wave_geom(const GShape& s, WWave& g, bool soup = false) {
   if (s.kind != 0 || s.P <= 16 || s.W < 3 || s.W > 64) return false;
   g.U = 4;
   while (g.U < s.W) g.U *= 2;
@@ -1431,7 +1433,7 @@ static bool ww_wave_geom(const GShape& s, WWave& g) {
   g.o_sa = g.o_acts + s.IN + s.D * s.W;
   g.o_sb = g.o_sa + s.W;
   g.o_misc = g.o_sb + s.W;
-  g.GS = g.o_misc + 4;
+  g.GS = g.o_misc + 4 + (soup ? s.P + 2 * g.U * s.W : 0);  // soups: apply output + per-lane vectors
   return true;
 }
 static size_t ww_wave_lds(const GShape& s, const WWave& g) { return ((size_t)3 * s.P + (size_t)g.G * g.GS) * 4; }
@@ -1444,149 +1446,344 @@ __device__ __forceinline__ int ww_pidx(const GShape& s, const WWave& g, int k) {
   return g.poff[l] + i * g.pst[l] + j;
 }
 
+// per-particle LDS regions of a WWave group
+struct WWGroup {
+  float* w;      // padded weights
+  float* sv;     // frozen samples / teacher or attacker row (flat)
+  int* perm;
+  float* acts;   // [x (4)][h_1 (W)] ... [h_D (W)]
+  float* sa;
+  float* sb;
+  float* misc;   // [0] the step so, [1..3] per-particle scalars
+  float* ob;     // (soups) apply output, flat
+  float* hb;     // (soups) per-lane forward vectors, 2 W per lane of the group
+};
+__device__ __forceinline__ WWGroup ww_group(const GShape& s, const WWave& g, float* sm, int grp) {
+  float* pw = sm + 3 * s.P + grp * g.GS;
+  WWGroup r;
+  r.w = pw;
+  r.sv = pw + g.o_sv;
+  r.perm = reinterpret_cast<int*>(pw + g.o_perm);
+  r.acts = pw + g.o_acts;
+  r.sa = pw + g.o_sa;
+  r.sb = pw + g.o_sb;
+  r.misc = pw + g.o_misc;
+  r.ob = pw + g.o_misc + 4;
+  r.hb = r.ob + s.P;
+  return r;
+}
+
+// E SGD epochs of one particle per group (g_train_epochs): SELF -- the samples are the weights
+// at each epoch start, else the row already in sv.  Every lane of the wave calls it (barriers);
+// only `live` groups draw shuffles and update their weights (a soup's non-learners sit out the
+// learn_from epochs of the wave).  Returns the last epoch's mean loss (lane u == 0).
+__device__ float ww_epochs(const GShape& s, const WWave& g, const WWGroup& R, const float* coords, int u, bool live,
+                           int E, bool self, uint64_t uid, uint32_t& ctr, float lr, bool shuffle, const Rng& rng) {
+  const int W = s.W, D = s.D;
+  const float lr2 = 2.0f * lr;  // the folded step -(2 lr) * e (Weightwise::train_epoch)
+  float loss = 0.f;
+  for (int e = 0; e < E; ++e) {
+    if (self)  // samples = the weights at the epoch start
+      for (int k = u; k < s.P; k += g.U) R.sv[k] = R.w[ww_pidx(s, g, k)];
+    __syncthreads();
+    if (shuffle) {
+      // g_fisher_yates (same draws: one Philox block per 4 swaps, stream (uid, ctr * 64 +
+      // block)); the swap chain on lane 0 of the particle
+      for (int k = u; k < s.P; k += g.U) R.perm[k] = k;
+      __syncthreads();
+      if (u == 0 && live) {
+        U4 r{0, 0, 0, 0};
+        int used = 4;
+        uint32_t blk = 0;
+        for (int t = s.P - 1; t > 0; --t) {
+          if (used == 4) {
+            r = rng.draw(uid, ctr * 64u + blk, P_SHUFFLE);
+            ++blk;
+            used = 0;
+          }
+          const uint32_t x = used == 0 ? r.x : used == 1 ? r.y : used == 2 ? r.z : r.w;
+          ++used;
+          int j = (int)(u01(x) * (float)(t + 1));
+          if (j > t) j = t;
+          const int pt = R.perm[t];
+          R.perm[t] = R.perm[j];
+          R.perm[j] = pt;
+        }
+      }
+      __syncthreads();
+    }
+    float acc = 0.f;
+    for (int q = 0; q < s.P; ++q) {
+      const int idx = shuffle ? R.perm[q] : q;
+      const float x0 = R.sv[idx];
+      const float x1 = coords[3 * idx], x2 = coords[3 * idx + 1], x3 = coords[3 * idx + 2];
+      // layer 0: h1[u] = x0*K0[0][u] then fma over the 3 coordinates
+      if (u < W) {
+        const float* K = R.w + g.poff[0];
+        float h = x0 * K[u];
+        h = fmaf(x1, K[g.pst[0] + u], h);
+        h = fmaf(x2, K[2 * g.pst[0] + u], h);
+        h = fmaf(x3, K[3 * g.pst[0] + u], h);
+        R.acts[4 + u] = h;
+      }
+      __syncthreads();
+      for (int l = 1; l < D; ++l) {  // hidden layers: column u
+        if (u < W) {
+          const float* K = R.w + g.poff[l];
+          const float* x = R.acts + 4 + (l - 1) * W;
+          float h = x[0] * K[u];
+          for (int r = 1; r < W; ++r) h = fmaf(x[r], K[r * g.pst[l] + u], h);
+          R.acts[4 + l * W + u] = h;
+        }
+        __syncthreads();
+      }
+      // output unit (one chain, lane 0) -> error, loss, the step so = -(2 lr) * e
+      if (u == 0) {
+        const float* K = R.w + g.poff[D];
+        const float* x = R.acts + 4 + (D - 1) * W;
+        float y = x[0] * K[0];
+        for (int r = 1; r < W; ++r) y = fmaf(x[r], K[r], y);
+        const float err = y - x0;
+        acc += err * err;
+        R.misc[0] = -lr2 * err;
+      }
+      __syncthreads();
+      // last layer (W x 1): si[u] = K[u] * so (pre-update), K[u] += h_D[u] * so
+      float* si = R.sa;
+      float* sn = R.sb;
+      if (u < W) {
+        float* K = R.w + g.poff[D];
+        const float so = R.misc[0];
+        si[u] = K[u] * so;
+        if (live) K[u] = fmaf(R.acts[4 + (D - 1) * W + u], so, K[u]);
+      }
+      __syncthreads();
+      for (int l = D - 1; l >= 1; --l) {  // hidden layers: row u (si from the pre-update row)
+        if (u < W) {
+          float* K = R.w + g.poff[l] + u * g.pst[l];
+          float sacc = K[0] * si[0];
+          for (int c = 1; c < W; ++c) sacc = fmaf(K[c], si[c], sacc);
+          const float xr = R.acts[4 + (l - 1) * W + u];
+          if (live)
+            for (int c = 0; c < W; ++c) K[c] = fmaf(xr, si[c], K[c]);
+          sn[u] = sacc;
+        }
+        __syncthreads();
+        float* t = si;
+        si = sn;
+        sn = t;
+      }
+      // layer 0 (4 x W): column u, no input gradient
+      if (u < W && live) {
+        float* K = R.w + g.poff[0];
+        const float so = si[u];
+        K[u] = fmaf(x0, so, K[u]);
+        K[g.pst[0] + u] = fmaf(x1, so, K[g.pst[0] + u]);
+        K[2 * g.pst[0] + u] = fmaf(x2, so, K[2 * g.pst[0] + u]);
+        K[3 * g.pst[0] + u] = fmaf(x3, so, K[3 * g.pst[0] + u]);
+      }
+      __syncthreads();
+    }
+    loss = acc / (float)s.P;
+    ctr += 1;
+  }
+  return loss;
+}
+
+__device__ void ww_load(const GShape& s, const WWave& g, float* pw, const char* row, int u) {
+  for (int k = u; k < s.P; k += g.U) pw[ww_pidx(s, g, k)] = g_dec(row, k, s.dtype);
+}
+__device__ void ww_store(const GShape& s, const WWave& g, const float* pw, char* row, int u) {
+  for (int k = u; k < s.PP; k += g.U) {
+    const float v = k < s.P ? pw[ww_pidx(s, g, k)] : 0.f;
+    if (s.dtype == 0) reinterpret_cast<float*>(row)[k] = v;
+    else reinterpret_cast<uint16_t*>(row)[k] = s.dtype == 1 ? StBF16::enc(v) : StF16::enc(v);
+  }
+}
+
 template <int OP>
 __global__ __launch_bounds__(64) void k_ww_wave(GShape s, WWave g, SrnnArgs a) {
   extern __shared__ float sm[];
   float* coords = sm;  // [P][3], whole block
   make_coords_dev(s, coords);
   const int lane = threadIdx.x, u = lane % g.U, grp = lane / g.U;
-  float* pw = sm + 3 * s.P + grp * g.GS;  // this particle's region
-  float* sv = pw + g.o_sv;
-  int* perm = reinterpret_cast<int*>(pw + g.o_perm);
-  float* acts = pw + g.o_acts;
-  float* misc = pw + g.o_misc;
-  const int W = s.W, D = s.D;
-  const float lr2 = 2.0f * a.lr;  // the folded step -(2 lr) * e (Weightwise::train_epoch)
+  const WWGroup R = ww_group(s, g, sm, grp);
   const bool shuffle = (a.flags & SRNN_F_SHUFFLE) != 0;
   const Rng rng = GItem::rng(a);
   for (int64_t base = (int64_t)blockIdx.x * g.G; base < a.n; base += (int64_t)gridDim.x * g.G) {
     const int64_t i = base + grp;
     const bool active = i < a.n;
     if (active) {
-      const char* row = GItem::rowp(s, a.W, i);
-      for (int k = u; k < s.P; k += g.U) pw[ww_pidx(s, g, k)] = g_dec(row, k, s.dtype);
+      ww_load(s, g, R.w, GItem::rowp(s, a.W, i), u);
       if (OP == OP_LEARN) {
         const char* t = GItem::rowp(s, a.W2, a.idx_t ? a.idx_t[i] : i);
-        for (int k = u; k < s.P; k += g.U) sv[k] = g_dec(t, k, s.dtype);
+        for (int k = u; k < s.P; k += g.U) R.sv[k] = g_dec(t, k, s.dtype);
       }
     }
     __syncthreads();
-    const uint64_t uid = active ? GItem::uid_of(a, i) : 0;
     uint32_t ctr = a.ctr;
-    float loss = 0.f;
-    for (int e = 0; e < a.epochs; ++e) {
-      if (OP == OP_TRAIN)  // samples = the weights at the epoch start
-        for (int k = u; k < s.P; k += g.U) sv[k] = pw[ww_pidx(s, g, k)];
-      __syncthreads();
-      if (shuffle) {
-        // g_fisher_yates (same draws: one Philox block per 4 swaps, stream (uid, ctr * 64 +
-        // block)); the swap chain on lane 0 of the particle
-        for (int k = u; k < s.P; k += g.U) perm[k] = k;
-        __syncthreads();
-        if (u == 0 && active) {
-          U4 r{0, 0, 0, 0};
-          int used = 4;
-          uint32_t blk = 0;
-          for (int t = s.P - 1; t > 0; --t) {
-            if (used == 4) {
-              r = rng.draw(uid, ctr * 64u + blk, P_SHUFFLE);
-              ++blk;
-              used = 0;
-            }
-            const uint32_t x = used == 0 ? r.x : used == 1 ? r.y : used == 2 ? r.z : r.w;
-            ++used;
-            int j = (int)(u01(x) * (float)(t + 1));
-            if (j > t) j = t;
-            const int pt = perm[t];
-            perm[t] = perm[j];
-            perm[j] = pt;
-          }
-        }
-        __syncthreads();
-      }
-      float acc = 0.f;
-      for (int q = 0; q < s.P; ++q) {
-        const int idx = shuffle ? perm[q] : q;
-        const float x0 = sv[idx];
-        const float x1 = coords[3 * idx], x2 = coords[3 * idx + 1], x3 = coords[3 * idx + 2];
-        if (u < 4) acts[u] = u == 0 ? x0 : u == 1 ? x1 : u == 2 ? x2 : x3;
-        // layer 0: h1[u] = x0*K0[0][u] then fma over the 3 coordinates
-        if (u < W) {
-          const float* K = pw + g.poff[0];
-          float h = x0 * K[u];
-          h = fmaf(x1, K[g.pst[0] + u], h);
-          h = fmaf(x2, K[2 * g.pst[0] + u], h);
-          h = fmaf(x3, K[3 * g.pst[0] + u], h);
-          acts[4 + u] = h;
-        }
-        __syncthreads();
-        for (int l = 1; l < D; ++l) {  // hidden layers: column u
-          if (u < W) {
-            const float* K = pw + g.poff[l];
-            const float* x = acts + 4 + (l - 1) * W;
-            float h = x[0] * K[u];
-            for (int r = 1; r < W; ++r) h = fmaf(x[r], K[r * g.pst[l] + u], h);
-            acts[4 + l * W + u] = h;
-          }
-          __syncthreads();
-        }
-        // output unit (one chain, lane 0) -> error, loss, the step so = -(2 lr) * e
-        if (u == 0) {
-          const float* K = pw + g.poff[D];
-          const float* x = acts + 4 + (D - 1) * W;
-          float y = x[0] * K[0];
-          for (int r = 1; r < W; ++r) y = fmaf(x[r], K[r], y);
-          const float err = y - x0;
-          acc += err * err;
-          misc[0] = -lr2 * err;
-        }
-        __syncthreads();
-        // last layer (W x 1): si[u] = K[u] * so (pre-update), K[u] += h_D[u] * so
-        float* si = pw + g.o_sa;
-        float* sn = pw + g.o_sb;
-        if (u < W) {
-          float* K = pw + g.poff[D];
-          const float so = misc[0];
-          si[u] = K[u] * so;
-          K[u] = fmaf(acts[4 + (D - 1) * W + u], so, K[u]);
-        }
-        __syncthreads();
-        for (int l = D - 1; l >= 1; --l) {  // hidden layers: row u (si from the pre-update row)
-          if (u < W) {
-            float* K = pw + g.poff[l] + u * g.pst[l];
-            float sacc = K[0] * si[0];
-            for (int c = 1; c < W; ++c) sacc = fmaf(K[c], si[c], sacc);
-            const float xr = acts[4 + (l - 1) * W + u];
-            for (int c = 0; c < W; ++c) K[c] = fmaf(xr, si[c], K[c]);
-            sn[u] = sacc;
-          }
-          __syncthreads();
-          float* t = si;
-          si = sn;
-          sn = t;
-        }
-        // layer 0 (4 x W): column u, no input gradient
-        if (u < W) {
-          float* K = pw + g.poff[0];
-          const float so = si[u];
-          K[u] = fmaf(x0, so, K[u]);
-          K[g.pst[0] + u] = fmaf(x1, so, K[g.pst[0] + u]);
-          K[2 * g.pst[0] + u] = fmaf(x2, so, K[2 * g.pst[0] + u]);
-          K[3 * g.pst[0] + u] = fmaf(x3, so, K[3 * g.pst[0] + u]);
-        }
-        __syncthreads();
-      }
-      loss = acc / (float)s.P;
-      ctr += 1;
-    }
+    const float loss = ww_epochs(s, g, R, coords, u, active, a.epochs, OP == OP_TRAIN,
+                                 active ? GItem::uid_of(a, i) : 0, ctr, a.lr, shuffle, rng);
     if (active) {
-      char* row = GItem::rowp(s, a.W, i);
-      for (int k = u; k < s.PP; k += g.U) {
-        const float v = k < s.P ? pw[ww_pidx(s, g, k)] : 0.f;
-        if (s.dtype == 0) reinterpret_cast<float*>(row)[k] = v;
-        else reinterpret_cast<uint16_t*>(row)[k] = s.dtype == 1 ? StBF16::enc(v) : StF16::enc(v);
-      }
+      ww_store(s, g, R.w, GItem::rowp(s, a.W, i), u);
       if (a.loss && u == 0) a.loss[i] = loss;
+    }
+    __syncthreads();
+  }
+}
+
+// Soup generation of the single-rank / all-gather runtime-shape engine (GItem::soup_evolve):
+// attacks received in ascending attacker-slot order (the attacker net evaluated at the
+// victim's P weight points, lanes over the points), learn_from, self-train, respawn with
+// inline re-init; respawn flags per row (SRNN_F_ROW_FLAGS) or OR-ed into the 64-row ballots
+// (zeroed by their consumer, k_g_respawn_seq).
+__global__ __launch_bounds__(64) void k_ww_wave_soup(GShape s, WWave g, SrnnArgs a) {
+  extern __shared__ float sm[];
+  float* coords = sm;
+  make_coords_dev(s, coords);
+  const int lane = threadIdx.x, u = lane % g.U, grp = lane / g.U;
+  const WWGroup R = ww_group(s, g, sm, grp);
+  const bool shuffle = (a.flags & SRNN_F_SHUFFLE) != 0;
+  const Rng rng = GItem::rng(a);
+  const int64_t rb = g_rb(s);
+  const int32_t gen = a.gen_ptr ? a.gen_ptr[0] : a.gen;
+  const int W = s.W, D = s.D;
+  int* ictl = reinterpret_cast<int*>(R.misc);  // [1] attacker entry, [2] its state
+  for (int64_t base = (int64_t)blockIdx.x * g.G; base < a.n; base += (int64_t)gridDim.x * g.G) {
+    const int64_t j = base + grp;
+    const bool active = j < a.n;
+    const int64_t gs = a.lo + j;
+    if (active) ww_load(s, g, R.w, GItem::rowp(s, a.W2, j), u);
+    // 1. attacks: lane 0 of the group walks the list for the next attacker (ascending slot)
+    uint32_t head = SRNN_NIL;
+    if (active) head = a.heads[j];
+    uint64_t last = 0;
+    bool first = true;
+    for (;;) {
+      if (u == 0) {
+        uint32_t be = SRNN_NIL;
+        if (active && head != SRNN_NIL) {
+          uint64_t best = ~0ull;
+          for (uint32_t e = head; e != SRNN_NIL; e = a.nexts[e]) {
+            const uint64_t sl = ent_slot(a, e);
+            if ((first || sl > last) && sl < best) best = sl, be = e;
+          }
+          if (be != SRNN_NIL) last = best, first = false;
+        }
+        ictl[1] = (int)be;
+      }
+      __syncthreads();
+      const uint32_t be = (uint32_t)ictl[1];
+      const bool more = be != SRNN_NIL;
+      if (__ballot(more) == 0ull) break;  // every group of the wave is done
+      if (more) {
+        const char* r = ent_row(a, be, rb);
+        for (int k = u; k < s.P; k += g.U) R.sv[k] = g_dec(r, k, s.dtype);  // the attacker's weights
+      }
+      __syncthreads();
+      if (more) {  // out[k] = f_attacker(w[k], coords k) for the points of this lane
+        float* h = R.hb + u * 2 * W;
+        float* h2 = h + W;
+        for (int k = u; k < s.P; k += g.U) {
+          const float x0 = R.w[ww_pidx(s, g, k)], x1 = coords[3 * k], x2 = coords[3 * k + 1], x3 = coords[3 * k + 2];
+          const float* K = R.sv;  // flat: layer l at s.off[l], row-major (rows x cols)
+          for (int c = 0; c < W; ++c) {
+            float acc = x0 * K[c];
+            acc = fmaf(x1, K[W + c], acc);
+            acc = fmaf(x2, K[2 * W + c], acc);
+            acc = fmaf(x3, K[3 * W + c], acc);
+            h[c] = acc;
+          }
+          for (int l = 1; l < D; ++l) {
+            const float* Kl = R.sv + s.off[l];
+            for (int c = 0; c < W; ++c) {
+              float acc = h[0] * Kl[c];
+              for (int r = 1; r < W; ++r) acc = fmaf(h[r], Kl[r * W + c], acc);
+              h2[c] = acc;
+            }
+            for (int c = 0; c < W; ++c) h[c] = h2[c];
+          }
+          const float* KD = R.sv + s.off[D];
+          float y = h[0] * KD[0];
+          for (int r = 1; r < W; ++r) y = fmaf(h[r], KD[r], y);
+          R.ob[k] = g_q(y, s.dtype);
+        }
+      }
+      __syncthreads();
+      if (more)
+        for (int k = u; k < s.P; k += g.U) R.w[ww_pidx(s, g, k)] = R.ob[k];
+      __syncthreads();
+    }
+    if (active && u == 0 && head != SRNN_NIL) a.heads[j] = SRNN_NIL;  // consumed
+    // 2. decisions of this slot, learn_from the teacher's generation-start row
+    int64_t my_at = -1, te = -1;
+    if (active) Item<Weightwise<1, 1>, StF32>::decision(a, gs, gen, my_at, te);
+    int8_t act = my_at >= 0 ? A_ATTACKING : A_NONE;
+    int64_t cp = my_at >= 0 ? my_at : -1;
+    const bool learn = active && te >= 0;
+    if (learn) {
+      const char* r = teacher_row(a, te, SRNN_NIL, rb);
+      for (int k = u; k < s.P; k += g.U) R.sv[k] = g_dec(r, k, s.dtype);
+    }
+    __syncthreads();
+    uint32_t ctr = (uint32_t)gen * 1024u + 512u;
+    float loss = 0.f;
+    // the groups of a wave learn together (a group without a teacher runs the epochs on its own
+    // samples with its lanes masked out of every write: live = false keeps its state)
+    if (__ballot(learn) != 0ull && a.severity > 0) {
+      const float l2 = ww_epochs(s, g, R, coords, u, learn, a.severity, false, (uint64_t)gs, ctr, a.lr, shuffle, rng);
+      if (learn) loss = l2;
+    }
+    if (learn) act = A_LEARN_FROM, cp = te;
+    if (a.epochs > 0) {
+      uint32_t c2 = (uint32_t)gen * 1024u + 512u + (learn ? (uint32_t)a.severity : 0u);
+      loss = ww_epochs(s, g, R, coords, u, active, a.epochs, true, (uint64_t)gs, c2, a.lr, shuffle, rng);
+      act = A_TRAIN_SELF;
+      cp = -1;
+    }
+    // 3. respawn (the zero test on the old particle; at most one of the two)
+    bool bad = false, nz = false;
+    for (int k = u; k < s.P; k += g.U) {
+      float& v = R.w[ww_pidx(s, g, k)];
+      v = g_q(v, s.dtype);
+      bad |= !finitef(v);
+      nz |= !((-a.eps <= v) && (v <= a.eps));
+    }
+    const unsigned long long gm = (g.U == 64 ? ~0ull : ((1ull << g.U) - 1ull)) << (grp * g.U);
+    const bool div = (__ballot(bad) & gm) != 0ull, zero = (__ballot(nz) & gm) == 0ull;
+    int8_t rs = 0;
+    if ((a.flags & SRNN_F_REMOVE_DIVERGENT) && div) rs = 1;
+    else if ((a.flags & SRNN_F_REMOVE_ZERO) && zero) rs = 2;
+    __syncthreads();
+    if (active && rs && (a.flags & SRNN_F_RESPAWN_INLINE)) {  // g_init: glorot per layer
+      const uint64_t key = respawn_key(gen, gs);
+      for (int l = 0; l < s.NL; ++l) {
+        const int n = s.rows[l] * s.cols[l];
+        const float lim = sqrtf(6.0f / (float)(s.rows[l] + s.cols[l]));
+        for (int b = u; b < (n + 3) / 4; b += g.U) {
+          const U4 q4 = rng.draw(key, (uint32_t)s.off[l] * 1024u + (uint32_t)b, P_INIT);
+          const uint32_t xs[4] = {q4.x, q4.y, q4.z, q4.w};
+          for (int q = 0; q < 4; ++q) {
+            const int k = b * 4 + q;
+            if (k < n) R.w[ww_pidx(s, g, s.off[l] + k)] = -lim + 2.0f * lim * u01(xs[q]);
+          }
+        }
+      }
+    }
+    __syncthreads();
+    if (active) {
+      ww_store(s, g, R.w, GItem::rowp(s, a.W, j), u);
+      if (u == 0) {
+        if (a.action) a.action[j] = act;
+        if (a.counterpart) a.counterpart[j] = cp;
+        if (a.loss) a.loss[j] = loss;
+        if (a.respawn) a.respawn[j] = rs;
+        if (a.flags & SRNN_F_ROW_FLAGS) {
+          if (a.rowflags) a.rowflags[j] = rs ? 1 : 0;
+        } else if (a.ballots && rs) {
+          atomicOr(a.ballots + (j >> 6), 1ull << (j & 63));
+        }
+      }
     }
     __syncthreads();
   }
@@ -1599,7 +1796,12 @@ static bool ww_serves(int op, const GShape& s, const SrnnArgs& a, WWave& g) {
     const char* e = std::getenv("SRNN_WW_WAVE");
     g_ww_wave = (e && e[0] == '0') ? 0 : 1;
   }
-  if (!g_ww_wave || !a.dev || (op != OP_TRAIN && op != OP_LEARN)) return false;
+  if (!g_ww_wave || !a.dev) return false;
+  if (op == OP_SOUP_EVOLVE) {  // single rank / all-gather generations (the sharded X2 modes: lane path)
+    if (a.flags & SRNN_F_X2) return false;
+    return ww_wave_geom(s, g, true) && ww_wave_lds(s, g) <= 64 * 1024;
+  }
+  if (op != OP_TRAIN && op != OP_LEARN) return false;
   return ww_wave_geom(s, g) && ww_wave_lds(s, g) <= 64 * 1024;
 }
 static int ww_launch(int op, const GShape& s, const WWave& g, const SrnnArgs& a) {
@@ -1609,7 +1811,8 @@ static int ww_launch(int op, const GShape& s, const WWave& g, const SrnnArgs& a)
   const size_t lds = ww_wave_lds(s, g);
   hipStream_t st = (hipStream_t)a.stream;
   if (op == OP_TRAIN) hipLaunchKernelGGL((k_ww_wave<OP_TRAIN>), dim3((unsigned)blocks), dim3(64), lds, st, s, g, a);
-  else hipLaunchKernelGGL((k_ww_wave<OP_LEARN>), dim3((unsigned)blocks), dim3(64), lds, st, s, g, a);
+  else if (op == OP_LEARN) hipLaunchKernelGGL((k_ww_wave<OP_LEARN>), dim3((unsigned)blocks), dim3(64), lds, st, s, g, a);
+  else hipLaunchKernelGGL(k_ww_wave_soup, dim3((unsigned)blocks), dim3(64), lds, st, s, g, a);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) {
     set_error(hipGetErrorString(e));

@@ -62,3 +62,46 @@ def test_ww_wave_close_to_oracle(cuda):
     assert ok.sum() > 32
     err = np.max(np.abs(got[ok] - ref[ok]) / (np.max(np.abs(ref[ok]), 1, keepdims=True) + 1e-6))
     assert err < 1e-4
+
+
+SOUP = dict(attacking_rate=0.3, learn_from_rate=0.3, train=2, learn_from_severity=1, remove_divergent=True,
+            remove_zero=True, epsilon=1e-4)
+
+
+def _soup(spec, dev, dtype, graphs):
+    from self_replicating_neural_networks_amd.soup_engine import SoupEngine
+
+    e = SoupEngine(spec, 333, SOUP, device=dev, seed=13, dtype=dtype)
+    e.stats = True
+    if graphs:
+        assert e.capture(warmup=1)
+        e.evolve(3)
+    else:
+        e.evolve(4)
+    torch.cuda.synchronize()
+    return (e.local_rows().clone(), e.uid.clone(), e.loss.clone(), e.action.clone(), e.counterpart.clone(),
+            e.respawn.clone(), e.last_census(), int(e.next_uid))
+
+
+@pytest.mark.parametrize("w,d", [(3, 3), (10, 3), (16, 2)])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.float16], ids=["f32", "f16"])
+def test_ww_wave_soup_equals_lane_path(cuda, w, d, dtype):
+    """soup generations (attacks in ascending attacker order, learn_from, self-train, respawn
+    with inline re-init) on lanes-per-particle waves == the lane path, bitwise; graphs == eager"""
+    spec = ArchSpec.weightwise(w, d)
+    outs = []
+    for wave in (True, False):
+        _lib.set_ww_wave(wave)
+        try:
+            outs.append(_soup(spec, cuda, dtype, graphs=False))
+        finally:
+            _lib.set_ww_wave(True)
+    a, b = outs
+    bits = lambda t: t.contiguous().view(torch.uint8) if t.is_floating_point() else t
+    for k, (x, y) in enumerate(zip(a[:6], b[:6])):
+        assert torch.equal(bits(x), bits(y)), k
+    assert a[6:] == b[6:]
+    assert int((a[3] == 3).sum()) > 0  # self-training happened
+    g = _soup(spec, cuda, dtype, graphs=True)
+    for k, (x, y) in enumerate(zip(g[:6], a[:6])):
+        assert torch.equal(bits(x), bits(y)), k
