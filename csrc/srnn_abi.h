@@ -43,6 +43,8 @@ enum SrnnFlag : uint32_t {
   SRNN_F_X2_BOTH = 1u << 20,         // X2 evolve (with X2_REMOTE): one launch of n/64 waves for the whole
                                      // generation, the lanes of remote-dependent slots take the remote
                                      // list's entries -- the single-stream generation
+  SRNN_F_X2_POST_FUSED = 1u << 21,   // X2 evolve with X2_BOTH: its first workgroups run the post of this
+                                     // generation's exchange (block stats of the last one in temp2)
   SRNN_F_X2_PRIO = 1u << 19,         // X2 pack / post / remote evolve: raised wave issue priority (the
                                      // exchange chain wins the SIMDs it shares with the local evolve)
 };
@@ -135,6 +137,7 @@ struct SrnnArgs {
   int32_t* x_hpre;            // [ceil(n/64)] (SRNN_F_X2_BOTH generations) remote-dependent slots before
                               // each 64-row block within its finish workgroup's range (pack)
   int32_t* x_hgrp;            // [x_groups] ... before each finish workgroup's range (pack)
+  void* temp2;                // SRNN_F_X2_POST_FUSED: the previous generation's block stats (post's temp)
   int8_t* action;       // soup: action code per local row (optional)
   int64_t* counterpart; // soup: counterpart slot per local row (optional)
   int8_t* respawn;      // soup: 0 none, 1 divergent_dead, 2 zweo_dead
@@ -173,7 +176,7 @@ enum SrnnOp {
                         // census, received notices linked for the next generation, requests kept
 };
 
-int srnn_abi_version();  // 17
+int srnn_abi_version();  // 18
 int64_t srnn_args_size();  // sizeof(SrnnArgs): the ctypes mirror checks its layout against it
 int64_t srnn_cfg_size();
 int srnn_has_config(const SrnnCfg* cfg);

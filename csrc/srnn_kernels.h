@@ -16,6 +16,8 @@
 #include <climits>
 #include <cstdlib>
 
+extern "C" int srnn_x2_run(int op, const SrnnCfg* c, const SrnnArgs* a);  // srnn_shard.hip
+
 namespace srnn {
 
 void set_error(const char* msg);
@@ -728,6 +730,34 @@ __global__ __launch_bounds__(TB) void k_op(SrnnCfg c, SrnnArgs a) {
   }
 }
 
+// Inclusive scan over an NT-thread block: wave shuffles (no barrier) + one LDS pass over
+// the NT/64 wave totals (one barrier) instead of a log2(NT)-round Hillis-Steele scan with
+// two barriers per round.  *total receives the block sum.
+template <int NT, class T = int32_t>
+__device__ __forceinline__ T block_incl_scan(T v, T* s_wave, T* total) {
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  T x = v;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const T y = __shfl_up(x, off);
+    if (lane >= off) x += y;
+  }
+  if (lane == 63) s_wave[wv] = x;
+  __syncthreads();
+  T pre = 0, tot = 0;
+#pragma unroll
+  for (int w = 0; w < NT / 64; ++w) {
+    const T sw = s_wave[w];
+    pre += (w < wv) ? sw : 0;
+    tot += sw;
+  }
+  *total = tot;
+  return x + pre;
+}
+
+// the sharded exchange protocol's steps (pack / post roles), used by the single-launch X2 evolve
+#include "srnn_shard.h"
+
 // ----------------------------------------------------------------------------------
 // X2 block stats (u64[4] per 64-row block of a generation: respawn ballot; class counts
 // c0 | c1 << 32, c2 | c3 << 32, c4) are accumulated with atomics: the local and the remote
@@ -816,18 +846,28 @@ __global__ __launch_bounds__(TB) void k_soup_evolve(SrnnCfg c, SrnnArgs a) {
   }
   unsigned long long* bs = reinterpret_cast<unsigned long long*>(a.temp);
   if (a.flags & SRNN_F_X2_BOTH) {
+    // SRNN_F_X2_POST_FUSED: the first workgroups are the post of this generation's exchange
+    // (uids of the last generation's newborns, census, the next generation's notices and
+    // requests); nothing the evolve reads is written by it
+    const int64_t npb = (a.flags & SRNN_F_X2_POST_FUSED) ? x2::post_blocks<TB>(a) : 0;
+    if ((int64_t)blockIdx.x < npb) {
+      if (a.flags & SRNN_F_X2_PRIO) __builtin_amdgcn_s_setprio(3);
+      x2::post_block<TB>(x2::geom(c), a, reinterpret_cast<unsigned long long*>(a.temp2), blockIdx.x);
+      return;
+    }
+    const int64_t eb = (int64_t)blockIdx.x - npb;  // this wave's 64-row block
     // one launch for the whole generation, n/64 waves: a lane whose own slot is
     // remote-dependent (x_dep) takes an entry of the remote list instead -- there are exactly as
     // many such lanes as entries (a slot joins the list when its bit is first set), so every
     // lane evolves one slot and no wave is added for the remote ones
-    const int64_t i = (int64_t)blockIdx.x * TB + lane;
+    const int64_t i = eb * TB + lane;
     const bool valid = i < a.n;
     const bool dep = valid && x2_dep(a, i);
     const int64_t cnt = *(volatile const int32_t*)a.x_rcount;
     const unsigned long long hm = __ballot(dep);
     // this wave's first list entry: holes before its block (prefix from pack, x_hpre / x_hgrp)
     const int64_t nbk = (a.n + TB - 1) / TB, per = (nbk + a.x_groups - 1) / a.x_groups;
-    const int64_t base = hm ? (int64_t)a.x_hpre[blockIdx.x] + a.x_hgrp[blockIdx.x / per] : 0;
+    const int64_t base = hm ? (int64_t)a.x_hpre[eb] + a.x_hgrp[eb / per] : 0;
     const int64_t pos = base + (int64_t)__popcll(hm & ((1ull << lane) - 1ull));
     int64_t j = i;
     uint32_t tk = SRNN_NIL;
@@ -843,15 +883,15 @@ __global__ __launch_bounds__(TB) void k_soup_evolve(SrnnCfg c, SrnnArgs a) {
       rs = I::soup_evolve(c, a, j, samp, perm, tk) != 0;
       if (census) k = classify_stored(j);
     }
-    const int64_t wd = (int64_t)blockIdx.x * 2 + lane;
+    const int64_t wd = eb * 2 + lane;
     if (lane < 2 && wd * 32 < a.n) a.x_dep[wd] = 0u;
     // own slots in the wave's block stats, taken list entries lane by lane
-    bs_publish_wave(bs, blockIdx.x, on && !dep && rs, dep ? (int8_t)-1 : k);
+    bs_publish_wave(bs, eb, on && !dep && rs, dep ? (int8_t)-1 : k);
     if (dep && on) bs_publish_lane(bs, j, rs, k);
     int32_t prev = 0;
     if (lane == 0) prev = atomicAdd(a.x_ctl + 3, 1);
     prev = __shfl(prev, 0);
-    if (prev == (int32_t)gridDim.x - 1 && lane == 0) {  // last wave: the list is re-armed
+    if (prev == (int32_t)((int64_t)gridDim.x - npb) - 1 && lane == 0) {  // last wave: the list is re-armed
       *a.x_rcount = 0;
       a.x_ctl[3] = 0;
     }
@@ -1033,30 +1073,6 @@ __global__ __launch_bounds__(TB) void k_soup_gen(SrnnCfg c, SrnnArgs a) {
   }
 }
 
-// Inclusive scan over an NT-thread block: wave shuffles (no barrier) + one LDS pass over
-// the NT/64 wave totals (one barrier) instead of a log2(NT)-round Hillis-Steele scan with
-// two barriers per round.  *total receives the block sum.
-template <int NT, class T = int32_t>
-__device__ __forceinline__ T block_incl_scan(T v, T* s_wave, T* total) {
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  T x = v;
-#pragma unroll
-  for (int off = 1; off < 64; off <<= 1) {
-    const T y = __shfl_up(x, off);
-    if (lane >= off) x += y;
-  }
-  if (lane == 63) s_wave[wv] = x;
-  __syncthreads();
-  T pre = 0, tot = 0;
-#pragma unroll
-  for (int w = 0; w < NT / 64; ++w) {
-    const T sw = s_wave[w];
-    pre += (w < wv) ? sw : 0;
-    tot += sw;
-  }
-  *total = tot;
-  return x + pre;
-}
 
 // Second phase of the two-phase fused single-rank generation: one SRNN_FINISH_NT-thread
 // workgroup reduces the per-wave census counts, scans the respawn ballots in slot order,
@@ -1589,6 +1605,11 @@ int launch(const SrnnCfg& c, const SrnnArgs& a) {
       // bounded grid over the remote-dependent list (its length is on the device), after the
       // local blocks with SRNN_F_X2_BOTH
       if (!(a.flags & SRNN_F_X2_BOTH)) blocks = x2_remote_blocks(a);  // (BOTH: n/64 waves)
+      else if (a.flags & SRNN_F_X2_POST_FUSED) blocks += x2::post_blocks<TB>(a);  // + post's workgroups
+    }
+    if ((a.flags & SRNN_F_X2_POST_FUSED) && (!(a.flags & SRNN_F_X2_BOTH) || !a.temp2 || !a.recvbuf)) {
+      set_error("X2 evolve with the fused post needs X2_BOTH, temp2 (the last generation's block stats), recvbuf");
+      return -5;
     }
     if ((a.flags & SRNN_F_X2_BOTH) && (!a.x_hpre || !a.x_hgrp || a.x_groups < 1)) {
       set_error("single-launch X2 evolve needs the hole prefixes of pack (x_hpre, x_hgrp)");
@@ -1672,6 +1693,13 @@ int host_run(const SrnnCfg& c, const SrnnArgs& a) {
         return I::classify_w(w, a.eps, (a.flags & SRNN_F_FIX_SEC) != 0,
                              I::actx(a, c, (uint64_t)(a.lo + i), 0x7FFFFFF0u, perm));
       };
+      if (a.flags & SRNN_F_X2_POST_FUSED) {  // the post of this exchange first (host order)
+        SrnnArgs pa = a;
+        pa.temp = a.temp2;
+        pa.flags &= ~(uint32_t)(SRNN_F_X2_POST_FUSED | SRNN_F_X2_BOTH | SRNN_F_X2_REMOTE);
+        const int r = srnn_x2_run(OP_X2_POST, &c, &pa);
+        if (r) return r;
+      }
       host_x2_evolve<Net, S>(a, evolve, classify);
       return 0;
     }

@@ -20,7 +20,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 # SRNN_LIB: load another build of the library (A/B of compiler flags on the GPU box)
 LIB_PATH = os.environ.get("SRNN_LIB") or os.path.join(_HERE, "libsrnn.so")
 CSRC = os.path.normpath(os.path.join(_HERE, "..", "..", "csrc"))
-ABI_VERSION = 17
+ABI_VERSION = 18
 
 # SrnnOp (csrc/srnn_abi.h)
 OP_INIT = 0
@@ -64,6 +64,7 @@ FLAG_X2_REMOTE = 1 << 17
 FLAG_X2_FINISH_ONLY = 1 << 18
 FLAG_X2_PRIO = 1 << 19
 FLAG_X2_BOTH = 1 << 20
+FLAG_X2_POST_FUSED = 1 << 21
 
 X2_HDR = 12           # int64 header words of an exchange block
 X2_REMOTE_WAVES = 4096
@@ -102,7 +103,7 @@ class SrnnArgs(ctypes.Structure):
         ("x_rcount", _P), ("x_rcount_next", _P), ("x_rslot", _P), ("x_rslot_next", _P),
         ("x_satt", _P), ("x_satt_next", _P), ("x_cno", _P), ("x_cno_next", _P),
         ("x_crq", _P), ("x_crq_next", _P), ("x_srep", _P), ("x_nsrep", _P),
-        ("x_part", _P), ("x_ctl", _P), ("x_groups", _I32), ("pad2", _I32), ("x_hpre", _P), ("x_hgrp", _P),
+        ("x_part", _P), ("x_ctl", _P), ("x_groups", _I32), ("pad2", _I32), ("x_hpre", _P), ("x_hgrp", _P), ("temp2", _P),
         ("action", _P), ("counterpart", _P), ("respawn", _P),
         ("temp", _P), ("temp_bytes", _I64),
         ("dev", _I32), ("pad1", _I32), ("stream", _P),

@@ -320,8 +320,8 @@ class SoupEngine:
         bignet = self.spec.kind == "aggregating" and self.spec.P > 64 and not _lib.is_generic(
             self.spec, _lib.OP_SOUP_EVOLVE, self.dtype_code)
         self._evolve_census = not bignet
-        # generation schedule: "serial" -- pack -> all-to-all -> post -> ONE evolve launch of the
-        # local and the remote slots on one stream (no cross-queue dependencies: each costs
+        # generation schedule: "serial" -- pack -> all-to-all -> ONE launch: post's workgroups +
+        # the evolve of the local and the remote slots, on one stream (no cross-queue dependencies: each costs
         # ~10 us inside a graph, profiles/r3b); "overlap" -- the local slots on a side stream
         # beside pack -> all-to-all -> remote evolve, post on a third stream
         self.schedule = os.environ.get("SRNN_X2_SCHEDULE", "serial")
@@ -643,8 +643,11 @@ class SoupEngine:
             loc = self._x2_base(p)
             ctypes.pointer(loc)[0] = ev
             if self._x2_both:
-                rem.flags |= _lib.FLAG_X2_BOTH
+                # ONE launch: post's workgroups first, then n/64 waves evolving every slot
+                rem.flags |= _lib.FLAG_X2_BOTH | _lib.FLAG_X2_POST_FUSED
+                rem.temp2 = _p(self.x_bstat[1 - p])
                 loc = None
+                po = None
         self._arg_cache[key] = (pa, po, rem, loc, census)
         return self._arg_cache[key]
 
@@ -699,7 +702,8 @@ class SoupEngine:
         if self.schedule == "serial":
             _lib.run(_lib.OP_X2_PACK, spec, pa, cfg)
             self.dist.all_to_all(self.recvbuf, self.sendbuf)
-            _lib.run(_lib.OP_X2_POST, spec, po, cfg)
+            if po is not None:  # (else fused into the evolve launch)
+                _lib.run(_lib.OP_X2_POST, spec, po, cfg)
             if loc is not None:
                 _lib.run(_lib.OP_SOUP_EVOLVE, spec, loc, cfg)
             _lib.run(_lib.OP_SOUP_EVOLVE, spec, rem, cfg)  # (with FLAG_X2_BOTH: the local slots too)
