@@ -1632,7 +1632,7 @@ __global__ __launch_bounds__(64) void k_ww_wave(GShape s, WWave g, SrnnArgs a) {
   }
 }
 
-// Soup generation of the single-rank / all-gather runtime-shape engine (GItem::soup_evolve):
+// Soup generation of the single-rank runtime-shape engine (GItem::soup_evolve):
 // attacks received in ascending attacker-slot order (the attacker net evaluated at the
 // victim's P weight points, lanes over the points), learn_from, self-train, respawn with
 // inline re-init; respawn flags per row (SRNN_F_ROW_FLAGS) or OR-ed into the 64-row ballots
@@ -1797,8 +1797,8 @@ static bool ww_serves(int op, const GShape& s, const SrnnArgs& a, WWave& g) {
     g_ww_wave = (e && e[0] == '0') ? 0 : 1;
   }
   if (!g_ww_wave || !a.dev) return false;
-  if (op == OP_SOUP_EVOLVE) {  // single rank / all-gather generations (the sharded X2 modes: lane path)
-    if (a.flags & SRNN_F_X2) return false;
+  if (op == OP_SOUP_EVOLVE) {  // single-rank generations (sharded exchanges: the lane path)
+    if (a.flags & (SRNN_F_X2 | SRNN_F_FULL_TABLE)) return false;
     return ww_wave_geom(s, g, true) && ww_wave_lds(s, g) <= 64 * 1024;
   }
   if (op != OP_TRAIN && op != OP_LEARN) return false;
