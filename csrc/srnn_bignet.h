@@ -1338,7 +1338,7 @@ struct ChunkPerm {
     uint32_t blk = 0;
     for (int i = T::P - 1; i > 0; --i) {
       if (used == 4) {
-        r = rng.draw(id, step * 64u + blk, P_AGGSHUF);
+        r = rng.draw(id, step, P_AGGSHUF + (blk << 8));
         ++blk;
         used = 0;
       }

@@ -302,8 +302,9 @@ SRNN_HD void fisher_yates(uint8_t* perm, int n, const Rng& rng, uint64_t id, uin
   uint32_t blk = 0;
   for (int i = n - 1; i > 0; --i) {
     if (used == 4) {
-      // fold the block counter into the high bits of step to give each block its own counter
-      r = rng.draw(id, step * 64u + blk, purpose);
+      // every 4-draw block its own counter: the block index in the purpose word's high bits
+      // (step * 64 + blk would run into the next step's blocks for n > 257)
+      r = rng.draw(id, step, purpose + (blk << 8));
       ++blk;
       used = 0;
     }

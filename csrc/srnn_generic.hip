@@ -264,7 +264,7 @@ SRNN_HD void g_fisher_yates(SV perm, int n, const Rng& rng, uint64_t id, uint32_
   uint32_t blk = 0;
   for (int i = n - 1; i > 0; --i) {
     if (used == 4) {
-      r = rng.draw(id, step * 64u + blk, purpose);
+      r = rng.draw(id, step, purpose + (blk << 8));  // (fisher_yates of srnn_core.h)
       ++blk;
       used = 0;
     }
@@ -1487,8 +1487,8 @@ __device__ float ww_epochs(const GShape& s, const WWave& g, const WWGroup& R, co
       for (int k = u; k < s.P; k += g.U) R.sv[k] = R.w[ww_pidx(s, g, k)];
     __syncthreads();
     if (shuffle) {
-      // g_fisher_yates (same draws: one Philox block per 4 swaps, stream (uid, ctr * 64 +
-      // block)); the swap chain on lane 0 of the particle
+      // g_fisher_yates (same draws: one Philox block per 4 swaps, stream (uid, ctr, purpose +
+      // block << 8)); the swap chain on lane 0 of the particle
       for (int k = u; k < s.P; k += g.U) R.perm[k] = k;
       __syncthreads();
       if (u == 0 && live) {
@@ -1497,7 +1497,7 @@ __device__ float ww_epochs(const GShape& s, const WWave& g, const WWGroup& R, co
         uint32_t blk = 0;
         for (int t = s.P - 1; t > 0; --t) {
           if (used == 4) {
-            r = rng.draw(uid, ctr * 64u + blk, P_SHUFFLE);
+            r = rng.draw(uid, ctr, P_SHUFFLE + (blk << 8));
             ++blk;
             used = 0;
           }

@@ -63,7 +63,8 @@ def fisher_yates(n_items, seed, ids, step, purpose):
     used, blk = 4, 0
     for i in range(n_items - 1, 0, -1):
         if used == 4:
-            words = draw(seed, ids, np.uint64((int(step) * 64 + blk) & M32), purpose)
+            # block index in the purpose word's high bits (csrc fisher_yates)
+            words = draw(seed, ids, np.uint64(int(step) & M32), (int(purpose) + (blk << 8)) & M32)
             blk += 1
             used = 0
         x = words[used]
