@@ -537,7 +537,7 @@ struct Item {
   // (SRNN_F_X2).  Returns the respawn code (also in respawn[j]).
   template <bool SINGLE = false>
   SRNN_HD static int8_t soup_evolve(const SrnnCfg& c, const SrnnArgs& a, int64_t j, float4* samp, uint8_t* perm,
-                                    uint32_t tk = SRNN_NIL) {
+                                    uint32_t tk = SRNN_NIL, float* wout = nullptr) {
     const int64_t g = a.lo + j;
     float w[P], f[P], o[P];
     load(rowp(a.W2, j), w);
@@ -607,6 +607,10 @@ struct Item {
     else if ((a.flags & SRNN_F_REMOVE_ZERO) && is_zero<P>(w, a.eps)) rs = 2;
     if (rs && (a.flags & SRNN_F_RESPAWN_INLINE)) Net::init(w, rng(a), respawn_key(gen, g));  // newborn
     store(rowp(a.W, j), w);
+    if (wout) {  // the stored row as a reload would see it (the census classifies it from registers)
+      copy(wout, w);
+      q(wout);
+    }
     if (a.action) a.action[j] = act;
     if (a.counterpart) a.counterpart[j] = cp;
     if (a.loss) a.loss[j] = loss;
@@ -826,11 +830,14 @@ __global__ __launch_bounds__(TB) void k_soup_evolve(SrnnCfg c, SrnnArgs a) {
   float4* samp = samp_lane<Net>(s_samp, lane);
   uint8_t* perm = s_perm + lane * PERM;
   const bool census = (a.flags & SRNN_F_FUSED_CENSUS) != 0;
+  auto classify_w_ = [&](const float* w, int64_t i) -> int8_t {  // census class of stored row i
+    return I::classify_w(w, a.eps, (a.flags & SRNN_F_FIX_SEC) != 0,
+                         I::actx(a, c, (uint64_t)(a.lo + i), 0x7FFFFFF0u, perm));
+  };
   auto classify_stored = [&](int64_t i) -> int8_t {
     float w[P];
     I::load(I::rowp(a.W, i), w);
-    return I::classify_w(w, a.eps, (a.flags & SRNN_F_FIX_SEC) != 0,
-                         I::actx(a, c, (uint64_t)(a.lo + i), 0x7FFFFFF0u, perm));
+    return classify_w_(w, i);
   };
   if (!(a.flags & SRNN_F_X2)) {
     const int64_t i = (int64_t)blockIdx.x * TB + lane;
@@ -880,8 +887,9 @@ __global__ __launch_bounds__(TB) void k_soup_evolve(SrnnCfg c, SrnnArgs a) {
     bool rs = false;
     int8_t k = -1;
     if (on) {
-      rs = I::soup_evolve(c, a, j, samp, perm, tk) != 0;
-      if (census) k = classify_stored(j);
+      float w[P];
+      rs = I::soup_evolve(c, a, j, samp, perm, tk, w) != 0;
+      if (census) k = classify_w_(w, j);
     }
     const int64_t wd = eb * 2 + lane;
     if (lane < 2 && wd * 32 < a.n) a.x_dep[wd] = 0u;
@@ -903,8 +911,9 @@ __global__ __launch_bounds__(TB) void k_soup_evolve(SrnnCfg c, SrnnArgs a) {
     bool rs = false;
     int8_t k = -1;
     if (on) {
-      rs = I::soup_evolve(c, a, i, samp, perm) != 0;
-      if (census) k = classify_stored(i);
+      float w[P];
+      rs = I::soup_evolve(c, a, i, samp, perm, SRNN_NIL, w) != 0;
+      if (census) k = classify_w_(w, i);
     }
     // this wave's two dependency words are consumed (every lane read its bit above)
     const int64_t wd = (int64_t)blockIdx.x * 2 + lane;
@@ -967,16 +976,14 @@ __global__ __launch_bounds__(TB) void k_soup_gen(SrnnCfg c, SrnnArgs a) {
   bool rs = false;
   int8_t k = -1;
   if (i < a.n) {
-    rs = I::template soup_evolve<true>(c, a, i, samp_lane<Net>(s_samp, lane), perm) != 0;
+    float w[P];  // the stored row (no reload of what this lane just wrote)
+    rs = I::template soup_evolve<true>(c, a, i, samp_lane<Net>(s_samp, lane), perm, SRNN_NIL, w) != 0;
     int64_t at, te;
     I::decision(a, i, gen + 1, at, te);
     if (at >= 0) I::link(a.heads_next, a.nexts_next, at, (uint32_t)i);
-    if (census) {
-      float w[P];
-      I::load(I::rowp(a.W, i), w);
+    if (census)
       k = I::classify_w(w, a.eps, (a.flags & SRNN_F_FIX_SEC) != 0,
                         I::actx(a, c, (uint64_t)(a.lo + i), 0x7FFFFFF0u, perm));
-    }
   }
   if ((a.flags & SRNN_F_GEN_COUNTS) && gb == 0 && threadIdx.x == 0) {
     // this launch advances the generation counter (the other ring slot: no block of this
