@@ -172,6 +172,7 @@ def main(argv=None):
                        "collectives": ("native RCCL communicator (" + d.native.library + ")") if d.native
                        else (f"torch.distributed ({backend})" if d.enabled else None),
                        "overlap": getattr(eng, "overlap", False),
+                       "sharded_schedule": getattr(eng, "schedule", None) if getattr(eng, "x2", False) else None,
                        "census_every_step": eng.stats, "final_census": census},
         }), flush=True)
     eng.release_graphs()  # graph executables reference the RCCL communicator
