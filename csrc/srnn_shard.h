@@ -8,6 +8,7 @@ namespace x2 {
 enum : int { H_CENSUS = 0, H_BORN = 5, H_VALID = 6, H_GEN = 7, H_NREP = 8, H_NATT = 9 };
 static_assert(SRNN_X2_HDR == 12, "header words");
 constexpr int XT = 256;  // threads per workgroup of pack / post
+constexpr int X2_LDS_PEERS = 256;  // ranks whose notice / request positions are reserved in LDS
 
 struct X2Geom {
   int64_t rb, xb;
@@ -274,15 +275,24 @@ __device__ __forceinline__ void pack_decide_block(const SrnnArgs& a, const X2Geo
   if (d.qa == a.rank) Dec::link(a.heads_next, a.nexts_next, d.at - a.lo, (uint32_t)i);
   const bool notice = d.qa >= 0 && d.qa != a.rank, request = d.qt >= 0;
   int32_t kn = -1, kq = -1;
-  if (a.world <= 16) {
-    for (int q = 0; q < a.world; ++q) {
-      if (q == a.rank) continue;
-      const int32_t r1 = block_reserve(a.x_cno_next + q, notice && d.qa == q, s);
-      const int32_t r2 = block_reserve(a.x_crq_next + q, request && d.qt == q, s);
-      kn = r1 >= 0 ? r1 : kn;
-      kq = r2 >= 0 ? r2 : kq;
+  if (a.world > 1 && a.world <= X2_LDS_PEERS) {
+    // per-peer positions: LDS atomics inside the workgroup, then ONE device atomic per peer and
+    // counter (three barriers whatever the rank count)
+    __shared__ int32_t s_cn[X2_LDS_PEERS], s_cq[X2_LDS_PEERS];
+    for (int q = threadIdx.x; q < a.world; q += XT) s_cn[q] = 0, s_cq[q] = 0;
+    __syncthreads();
+    const int32_t ln = notice ? atomicAdd(&s_cn[d.qa], 1) : -1;
+    const int32_t lq = request ? atomicAdd(&s_cq[d.qt], 1) : -1;
+    __syncthreads();
+    for (int q = threadIdx.x; q < a.world; q += XT) {
+      const int32_t cn = s_cn[q], cq = s_cq[q];
+      s_cn[q] = cn ? atomicAdd(a.x_cno_next + q, cn) : 0;
+      s_cq[q] = cq ? atomicAdd(a.x_crq_next + q, cq) : 0;
     }
-  } else {
+    __syncthreads();
+    if (notice) kn = s_cn[d.qa] + ln;
+    if (request) kq = s_cq[d.qt] + lq;
+  } else if (a.world > 1) {
     if (notice) kn = atomicAdd(a.x_cno_next + d.qa, 1);
     if (request) kq = atomicAdd(a.x_crq_next + d.qt, 1);
   }
