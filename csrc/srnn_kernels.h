@@ -1295,8 +1295,9 @@ __global__ __launch_bounds__(NT) void k_gen_finish_par(SrnnArgs a, int32_t nb, i
       for (int q = 0; q < 5; ++q) a.census[(int64_t)g * 6 + q] = census ? (int64_t)s_cs[q] : 0;
       a.census[(int64_t)g * 6 + 5] = total_born;
     }
-    // every workgroup read next_uid before its ticket: the last one may overwrite it
-    __threadfence();
+    // every workgroup read next_uid (and the newborn totals) before its ticket -- the loads
+    // completed, their values are in use -- so the last one may overwrite them; the other
+    // workgroups' uid / census stores need no release: only later launches read them
     const int32_t prev = atomicAdd(a.done, 1);
     if (prev == m - 1) {
       a.uid_base[0] = base + total_all;
