@@ -89,6 +89,54 @@ def test_mixed_self_fixpoints_curve(tmp_path):
     assert np.all(rnn < 0.25)                 # published 0 .. 0.1
 
 
+def _numpy_ww_self_attacks(n, attacks=4, eps=1e-4, seed=0):
+    """Independent float32 NumPy re-derivation of the Keras WeightwiseNeuralNetwork(2, 2)
+    self-attack loop of mixed-self-fixpoints.py:81-86 at trains=0 (network.py:213-273
+    apply_to_weights with normalize_id, network.py:140-157 is_fixpoint; glorot_uniform
+    kernels, linear, no bias).  Shares no code with the engine."""
+    rng = np.random.default_rng(seed)
+    shapes = [(4, 2), (2, 2), (2, 1)]
+    W = [rng.uniform(-np.sqrt(6 / sum(s)), np.sqrt(6 / sum(s)), (n,) + s).astype(np.float32)
+         for s in shapes]
+
+    def nid(v, m):
+        return v / m if m > 1 else float(v)
+    pts = [(L, c, k, nid(L, 2), nid(c, s[0] - 1), nid(k, s[1] - 1))
+           for L, s in enumerate(shapes) for c in range(s[0]) for k in range(s[1])]
+
+    def apply(net, src):
+        out = [w.copy() for w in src]
+        for L, c, k, nl, nc, nk in pts:
+            h = np.stack([src[L][:, c, k]] + [np.full(n, v, np.float32) for v in (nl, nc, nk)], 1)[:, None]
+            for w in net:
+                h = h @ w
+            out[L][:, c, k] = h[:, 0, 0]
+        return out
+
+    active = np.ones(n, bool)
+    with np.errstate(all="ignore"):
+        for _ in range(attacks):
+            W = [np.where(active[:, None, None], b, a) for a, b in zip(W, apply(W, W))]
+            nxt = apply(W, W)
+            fin = np.all([np.isfinite(w.reshape(n, -1)).all(1) for w in W], 0)
+            fix = np.all([(np.abs(a - b) < eps).reshape(n, -1).all(1) & np.isfinite(b.reshape(n, -1)).all(1)
+                          for a, b in zip(W, nxt)], 0)
+            active &= ~(fix | ~fin)
+    return fix.mean()
+
+
+def test_mixed_self_fixpoints_ww_zero_trains_independent(tmp_path):
+    """The published Weightwise point at trains=0 is 4/20 = 0.2; the engine gives ~0.43.
+    An engine-independent NumPy derivation of the same loop also gives ~0.43, so the
+    published point is a 20-trial draw ~2 standard errors low, not a semantic gap."""
+    p_np = _numpy_ww_self_attacks(8000)
+    r = E.mixed_self_fixpoints(trials=4000, device="cpu", seed=9, root=str(tmp_path),
+                               trains=[0], specs=(E.WW,))
+    p_eng = r["data"][0]["ys"][0]
+    assert 0.38 < p_np < 0.48
+    assert within(p_eng, 4000, p_np, 8000)
+
+
 def test_network_trajectorys_records(tmp_path):
     r = E.network_trajectorys(trials=20, device="cpu", seed=7, root=str(tmp_path))
     assert sum(r["counters"].values()) == 20
