@@ -1151,34 +1151,57 @@ __device__ __forceinline__ float rw_dot(const float* x, const float* k, int ks, 
   return acc;
 }
 
+// Layer geometry of a SimpleRNN stack from (width, depth) alone (make_gshape's kind-2 tables
+// in closed form): compile-time when the kernel is instantiated for one width / depth, so the
+// layer and dot-product loops unroll and the ~420 SALU instructions per timestep of table
+// lookups and loop control of the runtime-shape form (profiles/r2h_long_recurrent_wave.md)
+// go away; WT = DT = 0 is the runtime-shape instantiation (same formulas, runtime W / D).
+template <int WT, int DT>
+struct RD {
+  int w_, d_;
+  __device__ explicit RD(const GShape& s) : w_(WT ? WT : s.W), d_(DT ? DT : s.D) {}
+  __device__ __forceinline__ int W() const { return WT ? WT : w_; }
+  __device__ __forceinline__ int D() const { return DT ? DT : d_; }
+  __device__ __forceinline__ int NL() const { return D() + 1; }
+  __device__ __forceinline__ int in_(int L) const { return L == 0 ? 1 : W(); }
+  __device__ __forceinline__ int un(int L) const { return L == D() ? 1 : W(); }
+  __device__ __forceinline__ int koff(int L) const { return L == 0 ? 0 : W() + W() * W() + (L - 1) * 2 * W() * W(); }
+  __device__ __forceinline__ int roff(int L) const { return koff(L) + in_(L) * un(L); }
+  __device__ __forceinline__ int P() const { return koff(D()) + W() + 1; }
+  __device__ __forceinline__ int HS() const { return D() * W() + 1; }
+};
+
 // forward over the sequence: y_t = h_D[t][0]; states to hs (global, [P][HS]) and/or the
 // outputs to out (LDS, [P]) when given
+template <int WT, int DT>
 __device__ void rw_forward(const GShape& s, const RWave& r, const float* wts, const float* seq, float* hs,
                            float* out) {
+  const RD<WT, DT> d(s);
   const int lane = threadIdx.x;
   float* hc = r.h0;  // time t
   float* hp = r.h1;  // time t - 1
-  for (int q = lane; q < s.HS; q += 64) hc[q] = 0.f, hp[q] = 0.f;
+  for (int q = lane; q < d.HS(); q += 64) hc[q] = 0.f, hp[q] = 0.f;
   rw_sync();
-  for (int t = 0; t < s.P; ++t) {
+  for (int t = 0; t < d.P(); ++t) {
     const float x0 = seq[t];
-    for (int L = 0; L < s.NL; ++L) {
-      const int I = s.in_[L], U = s.un[L];
+#pragma unroll
+    for (int L = 0; L < (DT ? DT + 1 : d.NL()); ++L) {
+      const int I = d.in_(L), U = d.un(L);
       float hn = 0.f;
       if (lane < U) {
-        const float* K = wts + s.koff[L];
-        const float* R = wts + s.roff[L];
+        const float* K = wts + d.koff(L);
+        const float* R = wts + d.roff(L);
         // layer L-1 at time t (this timestep), or the scalar input
-        const float xk = L == 0 ? x0 * K[lane] : rw_dot(hc + (L - 1) * s.W, K + lane, U, I, true, 0.f);
-        const float hr = rw_dot(hp + L * s.W, R + lane, U, U, true, 0.f);
+        const float xk = L == 0 ? x0 * K[lane] : rw_dot(hc + (L - 1) * d.W(), K + lane, U, I, true, 0.f);
+        const float hr = rw_dot(hp + L * d.W(), R + lane, U, U, true, 0.f);
         hn = xk + hr;
       }
-      if (lane < U) hc[L * s.W + lane] = hn;
+      if (lane < U) hc[L * d.W() + lane] = hn;
       rw_sync();
     }
     if (hs)
-      for (int q = lane; q < s.HS; q += 64) hs[(int64_t)t * s.HS + q] = hc[q];
-    if (out && lane == 0) out[t] = hc[s.D * s.W];
+      for (int q = lane; q < d.HS(); q += 64) hs[(int64_t)t * d.HS() + q] = hc[q];
+    if (out && lane == 0) out[t] = hc[d.D() * d.W()];
     float* tmp = hc;  // h(t) becomes h(t - 1); the old buffer is overwritten layer by layer
     hc = hp;
     hp = tmp;
@@ -1188,58 +1211,62 @@ __device__ void rw_forward(const GShape& s, const RWave& r, const float* wts, co
 
 // one self-train / learn epoch (g_train_epoch, recurrent branch): forward with states, BPTT,
 // one SGD step; returns the loss (mean over timesteps)
+template <int WT, int DT>
 __device__ float rw_train_epoch(const GShape& s, const RWave& r, float* hs, float lr) {
+  const RD<WT, DT> d(s);
   const int lane = threadIdx.x;
-  rw_forward(s, r, r.w, r.seq, hs, nullptr);
+  rw_forward<WT, DT>(s, r, r.w, r.seq, hs, nullptr);
   // the states are read back by other lanes of this wave: the stores are at L2 after the
   // wait, and the reads below are memory-side (L2) loads -- never a stale L1 line left by the
   // previous particle's pass over the same region
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   float* gw = r.aux;
-  for (int k = lane; k < s.P; k += 64) gw[k] = 0.f;
-  for (int q = lane; q < s.HS; q += 64) r.carry[q] = 0.f;
+  const int P = d.P(), HS = d.HS(), Wd = d.W();
+  for (int k = lane; k < P; k += 64) gw[k] = 0.f;
+  for (int q = lane; q < HS; q += 64) r.carry[q] = 0.f;
   rw_sync();
   float loss = 0.f;
-  for (int t = s.P - 1; t >= 0; --t) {
-    for (int q = lane; q < s.HS; q += 64) {
-      r.hst[q] = __hip_atomic_load(hs + (int64_t)t * s.HS + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      r.hsp[q] = t > 0 ? __hip_atomic_load(hs + (int64_t)(t - 1) * s.HS + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+  for (int t = P - 1; t >= 0; --t) {
+    for (int q = lane; q < HS; q += 64) {
+      r.hst[q] = __hip_atomic_load(hs + (int64_t)t * HS + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      r.hsp[q] = t > 0 ? __hip_atomic_load(hs + (int64_t)(t - 1) * HS + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
                        : 0.f;
     }
     rw_sync();
-    const float e = r.hst[s.D * s.W] - r.seq[t];
+    const float e = r.hst[d.D() * Wd] - r.seq[t];
     loss += e * e;
-    if (lane == 0) r.dtop[0] = 2.0f * e / (float)s.P;
+    if (lane == 0) r.dtop[0] = 2.0f * e / (float)P;
     rw_sync();
-    for (int L = s.D; L >= 0; --L) {
-      const int U = s.un[L], I = s.in_[L];
+#pragma unroll
+    for (int L = (DT ? DT : d.D()); L >= 0; --L) {
+      const int U = d.un(L), I = d.in_(L);
       float dhj = 0.f;
-      if (lane < U) dhj = r.dtop[lane] + r.carry[L * s.W + lane];
+      if (lane < U) dhj = r.dtop[lane] + r.carry[L * Wd + lane];
       if (lane < U) r.dh[lane] = dhj;
       rw_sync();
       if (lane < U) {  // kernel / recurrent-kernel gradients of column j = lane
         for (int i = 0; i < I; ++i) {
-          const float xi = L == 0 ? r.seq[t] : r.hst[(L - 1) * s.W + i];
-          float* gk = gw + s.koff[L] + i * U + lane;
+          const float xi = L == 0 ? r.seq[t] : r.hst[(L - 1) * Wd + i];
+          float* gk = gw + d.koff(L) + i * U + lane;
           *gk = fmaf(xi, dhj, *gk);
         }
         for (int i = 0; i < U; ++i) {
-          float* gr = gw + s.roff[L] + i * U + lane;
-          *gr = fmaf(r.hsp[L * s.W + i], dhj, *gr);
+          float* gr = gw + d.roff(L) + i * U + lane;
+          *gr = fmaf(r.hsp[L * Wd + i], dhj, *gr);
         }
       }
       float dxi = 0.f, cri = 0.f;
-      if (L > 0 && lane < I) dxi = rw_dot(r.dh, r.w + s.koff[L] + lane * U, 1, U, false, 0.f);
-      if (lane < U) cri = rw_dot(r.dh, r.w + s.roff[L] + lane * U, 1, U, false, 0.f);
+      if (L > 0 && lane < I) dxi = rw_dot(r.dh, r.w + d.koff(L) + lane * U, 1, U, false, 0.f);
+      if (lane < U) cri = rw_dot(r.dh, r.w + d.roff(L) + lane * U, 1, U, false, 0.f);
       rw_sync();
-      if (lane < U) r.carry[L * s.W + lane] = cri;
+      if (lane < U) r.carry[L * Wd + lane] = cri;
       if (L > 0 && lane < I) r.dtop[lane] = dxi;
       rw_sync();
     }
   }
-  for (int k = lane; k < s.P; k += 64) r.w[k] = fmaf(gw[k], -lr, r.w[k]);
+  for (int k = lane; k < P; k += 64) r.w[k] = fmaf(gw[k], -lr, r.w[k]);
   rw_sync();
-  return loss / (float)s.P;
+  return loss / (float)P;
 }
 
 __device__ __forceinline__ bool rw_all(bool b) { return __ballot(!b) == 0ull; }
@@ -1274,16 +1301,17 @@ __device__ void rw_quant(const GShape& s, float* v) {
 }
 
 // classification (g_classify_w): f1 = apply(w, w), f2 = apply(w, f1); uses aux and seq
+template <int WT, int DT>
 __device__ int8_t rw_classify(const GShape& s, const RWave& r, float eps, bool with_sec) {
   if (rw_diverged(s, r.w)) return C_DIVERGENT;
   float* f1 = r.aux;
-  rw_forward(s, r, r.w, r.w, nullptr, f1);
+  rw_forward<WT, DT>(s, r, r.w, r.w, nullptr, f1);
   rw_quant(s, f1);
   rw_sync();
   if (!rw_diverged(s, f1) && rw_within(s, f1, r.w, eps)) return rw_zero(s, r.w, eps) ? C_FIX_ZERO : C_FIX_OTHER;
   if (with_sec) {
     float* f2 = r.seq;
-    rw_forward(s, r, r.w, f1, nullptr, f2);
+    rw_forward<WT, DT>(s, r, r.w, f1, nullptr, f2);
     rw_quant(s, f2);
     rw_sync();
     if (!rw_diverged(s, f2) && rw_within(s, f2, r.w, eps)) return C_FIX_SEC;
@@ -1291,7 +1319,7 @@ __device__ int8_t rw_classify(const GShape& s, const RWave& r, float eps, bool w
   return C_OTHER;
 }
 
-template <int OP>
+template <int OP, int WT, int DT>
 __global__ __launch_bounds__(64) void k_rnn_wave(GShape s, SrnnArgs a) {
   extern __shared__ float sm[];
   const RWave r = rw_layout(s, sm);
@@ -1303,7 +1331,7 @@ __global__ __launch_bounds__(64) void k_rnn_wave(GShape s, SrnnArgs a) {
       rw_load(s, GItem::rowp(s, a.W, fi), r.w);
       rw_load(s, GItem::rowp(s, a.W, ti), r.seq);
       rw_sync();
-      rw_forward(s, r, r.w, r.seq, nullptr, r.aux);
+      rw_forward<WT, DT>(s, r, r.w, r.seq, nullptr, r.aux);
       rw_quant(s, r.aux);
       rw_sync();
       rw_store(s, GItem::rowp(s, a.W2, oi), r.aux);
@@ -1317,7 +1345,7 @@ __global__ __launch_bounds__(64) void k_rnn_wave(GShape s, SrnnArgs a) {
           for (int k = lane; k < s.P; k += 64) r.seq[k] = r.w[k];
           rw_sync();
         }
-        loss = rw_train_epoch(s, r, hs, a.lr);
+        loss = rw_train_epoch<WT, DT>(s, r, hs, a.lr);
       }
       rw_store(s, GItem::rowp(s, a.W, i), r.w);
       if (a.loss && lane == 0) a.loss[i] = loss;
@@ -1327,7 +1355,7 @@ __global__ __launch_bounds__(64) void k_rnn_wave(GShape s, SrnnArgs a) {
       int st = 0;
       for (; st < a.steps; ++st) {
         if (a.early_exit && rw_diverged(s, r.w)) break;
-        rw_forward(s, r, r.w, r.w, nullptr, r.aux);
+        rw_forward<WT, DT>(s, r, r.w, r.w, nullptr, r.aux);
         rw_quant(s, r.aux);
         rw_sync();
         if (a.early_exit && !rw_diverged(s, r.aux) && rw_within(s, r.aux, r.w, a.eps)) break;
@@ -1337,7 +1365,7 @@ __global__ __launch_bounds__(64) void k_rnn_wave(GShape s, SrnnArgs a) {
       rw_store(s, GItem::rowp(s, a.W, i), r.w);
       if (a.nsteps && lane == 0) a.nsteps[i] = st;
       if (a.cls) {
-        const int8_t k = rw_classify(s, r, a.eps, (a.flags & SRNN_F_FIX_SEC) != 0);
+        const int8_t k = rw_classify<WT, DT>(s, r, a.eps, (a.flags & SRNN_F_FIX_SEC) != 0);
         if (lane == 0) a.cls[i] = k;
       }
     }
@@ -1349,6 +1377,23 @@ __global__ __launch_bounds__(64) void k_rnn_wave(GShape s, SrnnArgs a) {
 // apply / train / learn / run_fixpoint (no trajectory) wave per particle
 static int g_rnn_wave = -1;  // SRNN_RNN_WAVE=0: lane path for every width (A/B tests)
 extern "C" void srnn_set_rnn_wave(int on) { g_rnn_wave = on ? 1 : 0; }
+// width / depth-specialised instantiations (RNN(8|16|32, 2), RNN(8|16, 3); RNN(32, 3) fully
+// unrolled spills past 256 VGPRs and stays runtime-shape); 0: the runtime-shape kernel
+// for every shape (A/B tests, SRNN_RNN_SPEC=0)
+static int g_rnn_spec = [] {
+  const char* e = std::getenv("SRNN_RNN_SPEC");
+  return (e && e[0] == '0') ? 0 : 1;
+}();
+extern "C" void srnn_set_rnn_spec(int on) { g_rnn_spec = on ? 1 : 0; }
+template <int WT, int DT>
+static void rw_launch_shape(int op, dim3 grid, size_t lds, hipStream_t st, const GShape& s, const SrnnArgs& a) {
+  switch (op) {
+    case OP_APPLY: hipLaunchKernelGGL((k_rnn_wave<OP_APPLY, WT, DT>), grid, dim3(64), lds, st, s, a); break;
+    case OP_TRAIN: hipLaunchKernelGGL((k_rnn_wave<OP_TRAIN, WT, DT>), grid, dim3(64), lds, st, s, a); break;
+    case OP_LEARN: hipLaunchKernelGGL((k_rnn_wave<OP_LEARN, WT, DT>), grid, dim3(64), lds, st, s, a); break;
+    default: hipLaunchKernelGGL((k_rnn_wave<OP_RUN_FIXPOINT, WT, DT>), grid, dim3(64), lds, st, s, a); break;
+  }
+}
 static bool rw_serves(int op, const GShape& s, const SrnnArgs& a) {
   if (g_rnn_wave < 0) {
     const char* e = std::getenv("SRNN_RNN_WAVE");
@@ -1356,6 +1401,14 @@ static bool rw_serves(int op, const GShape& s, const SrnnArgs& a) {
   }
   if (!g_rnn_wave) return false;
   if (s.kind != 2 || s.W < RW_MIN_WIDTH || s.W > 64 || rw_lds_bytes(s) > 60 * 1024 || !a.dev) return false;
+  // RD's closed form of the layer tables must be make_gshape's
+  for (int l = 0; l < s.NL; ++l) {
+    const int kl = l == 0 ? 0 : s.W + s.W * s.W + (l - 1) * 2 * s.W * s.W;
+    if (s.koff[l] != kl || s.roff[l] != kl + s.in_[l] * s.un[l] || s.un[l] != (l == s.D ? 1 : s.W) ||
+        s.in_[l] != (l == 0 ? 1 : s.W))
+      return false;
+  }
+  if (s.P != s.koff[s.D] + s.W + 1 || s.HS != s.D * s.W + 1) return false;
   if (op == OP_RUN_FIXPOINT) return a.traj == nullptr;
   return op == OP_APPLY || op == OP_TRAIN || op == OP_LEARN;
 }
@@ -1372,15 +1425,18 @@ static int rw_launch(int op, const GShape& s, const SrnnArgs& a) {
   }
   const size_t lds = rw_lds_bytes(s);
   hipStream_t st = (hipStream_t)a.stream;
-  switch (op) {
-    case OP_APPLY: hipLaunchKernelGGL((k_rnn_wave<OP_APPLY>), dim3((unsigned)blocks), dim3(64), lds, st, s, a); break;
-    case OP_TRAIN: hipLaunchKernelGGL((k_rnn_wave<OP_TRAIN>), dim3((unsigned)blocks), dim3(64), lds, st, s, a); break;
-    case OP_LEARN: hipLaunchKernelGGL((k_rnn_wave<OP_LEARN>), dim3((unsigned)blocks), dim3(64), lds, st, s, a); break;
-    case OP_RUN_FIXPOINT:
-      hipLaunchKernelGGL((k_rnn_wave<OP_RUN_FIXPOINT>), dim3((unsigned)blocks), dim3(64), lds, st, s, a);
-      break;
-    default: set_error("recurrent wave path: op"); return -1;
+  if (op != OP_APPLY && op != OP_TRAIN && op != OP_LEARN && op != OP_RUN_FIXPOINT) {
+    set_error("recurrent wave path: op");
+    return -1;
   }
+  const int w = g_rnn_spec ? s.W : 0, d = g_rnn_spec ? s.D : 0;
+  const dim3 grid((unsigned)blocks);
+  if (w == 8 && d == 2) rw_launch_shape<8, 2>(op, grid, lds, st, s, a);
+  else if (w == 16 && d == 2) rw_launch_shape<16, 2>(op, grid, lds, st, s, a);
+  else if (w == 32 && d == 2) rw_launch_shape<32, 2>(op, grid, lds, st, s, a);
+  else if (w == 8 && d == 3) rw_launch_shape<8, 3>(op, grid, lds, st, s, a);
+  else if (w == 16 && d == 3) rw_launch_shape<16, 3>(op, grid, lds, st, s, a);
+  else rw_launch_shape<0, 0>(op, grid, lds, st, s, a);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) {
     set_error(hipGetErrorString(e));

@@ -54,3 +54,23 @@ def test_rnn_wave_equals_lane_path(cuda, w, d):
     h = _ops(spec, "cpu")
     ok = torch.isfinite(h["apply"]).all(1) & torch.isfinite(a["apply"].cpu()).all(1)
     assert torch.allclose(a["apply"].cpu()[ok], h["apply"][ok], rtol=1e-3, atol=1e-5)
+
+
+@pytest.mark.parametrize("w,d", [(8, 2), (16, 2), (32, 2), (8, 3), (16, 3)])
+def test_rnn_wave_specialised_equals_runtime_shape(cuda, w, d):
+    """The width / depth-specialised wave kernels (compile-time layer tables, unrolled loops)
+    are bitwise the runtime-shape wave kernel."""
+    spec = ArchSpec.recurrent(w, d)
+    outs = []
+    for on in (True, False):
+        _lib.set_rnn_spec(on)
+        try:
+            outs.append(_ops(spec, cuda, n=200))
+        finally:
+            _lib.set_rnn_spec(True)
+    a, b = outs
+    for k in a:
+        x, y = a[k], b[k]
+        if x.dtype == torch.float32:
+            x, y = x.view(torch.int32), y.view(torch.int32)
+        assert torch.equal(x, y), k
