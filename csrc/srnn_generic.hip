@@ -1222,6 +1222,18 @@ __device__ float rw_train_epoch(const GShape& s, const RWave& r, float* hs, floa
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   float* gw = r.aux;
   const int P = d.P(), HS = d.HS(), Wd = d.W();
+  // specialised widths up to 16: lane j's gradient column of every layer in registers (<= 98
+  // floats at RNN(16, 3)) instead of an LDS read-modify-write per multiply-add; the same fma
+  // sequence per element, so the result is the LDS form's
+  constexpr bool REG = WT > 0 && WT <= 16;
+  constexpr int RL = REG ? DT + 1 : 1, RW = REG ? WT : 1;
+  float ak[RL][RW], ar[RL][RW];
+  if constexpr (REG) {
+#pragma unroll
+    for (int L = 0; L < RL; ++L)
+#pragma unroll
+      for (int i = 0; i < RW; ++i) ak[L][i] = 0.f, ar[L][i] = 0.f;
+  }
   for (int k = lane; k < P; k += 64) gw[k] = 0.f;
   for (int q = lane; q < HS; q += 64) r.carry[q] = 0.f;
   rw_sync();
@@ -1245,14 +1257,21 @@ __device__ float rw_train_epoch(const GShape& s, const RWave& r, float* hs, floa
       if (lane < U) r.dh[lane] = dhj;
       rw_sync();
       if (lane < U) {  // kernel / recurrent-kernel gradients of column j = lane
-        for (int i = 0; i < I; ++i) {
-          const float xi = L == 0 ? r.seq[t] : r.hst[(L - 1) * Wd + i];
-          float* gk = gw + d.koff(L) + i * U + lane;
-          *gk = fmaf(xi, dhj, *gk);
-        }
-        for (int i = 0; i < U; ++i) {
-          float* gr = gw + d.roff(L) + i * U + lane;
-          *gr = fmaf(r.hsp[L * Wd + i], dhj, *gr);
+        if constexpr (REG) {
+#pragma unroll
+          for (int i = 0; i < I; ++i) ak[L][i] = fmaf(L == 0 ? r.seq[t] : r.hst[(L - 1) * Wd + i], dhj, ak[L][i]);
+#pragma unroll
+          for (int i = 0; i < U; ++i) ar[L][i] = fmaf(r.hsp[L * Wd + i], dhj, ar[L][i]);
+        } else {
+          for (int i = 0; i < I; ++i) {
+            const float xi = L == 0 ? r.seq[t] : r.hst[(L - 1) * Wd + i];
+            float* gk = gw + d.koff(L) + i * U + lane;
+            *gk = fmaf(xi, dhj, *gk);
+          }
+          for (int i = 0; i < U; ++i) {
+            float* gr = gw + d.roff(L) + i * U + lane;
+            *gr = fmaf(r.hsp[L * Wd + i], dhj, *gr);
+          }
         }
       }
       float dxi = 0.f, cri = 0.f;
@@ -1263,6 +1282,19 @@ __device__ float rw_train_epoch(const GShape& s, const RWave& r, float* hs, floa
       if (L > 0 && lane < I) r.dtop[lane] = dxi;
       rw_sync();
     }
+  }
+  if constexpr (REG) {
+#pragma unroll
+    for (int L = 0; L < RL; ++L) {
+      const int U = d.un(L), I = d.in_(L);
+      if (lane < U) {
+#pragma unroll
+        for (int i = 0; i < I; ++i) gw[d.koff(L) + i * U + lane] = ak[L][i];
+#pragma unroll
+        for (int i = 0; i < U; ++i) gw[d.roff(L) + i * U + lane] = ar[L][i];
+      }
+    }
+    rw_sync();
   }
   for (int k = lane; k < P; k += 64) r.w[k] = fmaf(gw[k], -lr, r.w[k]);
   rw_sync();
