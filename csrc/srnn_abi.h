@@ -183,6 +183,8 @@ int srnn_has_config(const SrnnCfg* cfg);
 int srnn_run(int op, const SrnnCfg* cfg, const SrnnArgs* args);
 const char* srnn_last_error();
 int srnn_is_generic(const SrnnCfg* cfg, int op);
+int srnn_supports(const SrnnCfg* cfg, int op, int dev);  // 1: op has a host (0) / device (1) path
+int srnn_generic_op_supported(int op, int dev);
 void srnn_set_force_generic(int on);  // 1: this op of this config runs on the generic engine
 int64_t srnn_generic_scratch_bytes(const SrnnCfg* cfg, int64_t n, int64_t max_lanes);
 }

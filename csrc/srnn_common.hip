@@ -213,6 +213,15 @@ int srnn_is_generic(const SrnnCfg* cfg, int op) {
   return route(op, cfg, &probe) == 1 ? 1 : 0;
 }
 
+// 1 when `op` of this configuration has an implementation on the host (dev 0) / device (dev 1)
+int srnn_supports(const SrnnCfg* cfg, int op, int dev) {
+  SrnnArgs probe{};
+  probe.dev = dev;
+  const int r = route(op, cfg, &probe);
+  if (r == 0) return 1;
+  return r == 1 && srnn_generic_op_supported(op, dev) ? 1 : 0;
+}
+
 int srnn_run(int op, const SrnnCfg* cfg, const SrnnArgs* a) {
   srnn::set_error("");
   const Hooks& h = hooks();

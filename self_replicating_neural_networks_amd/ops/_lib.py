@@ -150,6 +150,8 @@ def lib():
         L.srnn_last_error.restype = ctypes.c_char_p
         L.srnn_is_generic.argtypes = [ctypes.POINTER(SrnnCfg), ctypes.c_int]
         L.srnn_is_generic.restype = ctypes.c_int
+        L.srnn_supports.argtypes = [ctypes.POINTER(SrnnCfg), ctypes.c_int, ctypes.c_int]
+        L.srnn_supports.restype = ctypes.c_int
         L.srnn_generic_scratch_bytes.argtypes = [ctypes.POINTER(SrnnCfg), ctypes.c_int64, ctypes.c_int64]
         L.srnn_generic_scratch_bytes.restype = ctypes.c_int64
         L.srnn_set_force_generic.argtypes = [ctypes.c_int]
@@ -202,6 +204,12 @@ def is_generic(spec, op: int, dtype: int = DTYPE_FP32) -> bool:
     """True when ``op`` of this architecture runs on the runtime-shape engine
     (csrc/srnn_generic.hip) on the GPU instead of a shape-specialised kernel."""
     return bool(lib().srnn_is_generic(ctypes.byref(make_cfg(spec, dtype)), int(op)))
+
+
+def supports(spec, op: int, device: bool, dtype: int = DTYPE_FP32) -> bool:
+    """True when ``op`` of this architecture has a native implementation on the device
+    (``device=True``) or on the host."""
+    return bool(lib().srnn_supports(ctypes.byref(make_cfg(spec, dtype)), int(op), 1 if device else 0))
 
 
 def set_force_generic(on: bool) -> None:

@@ -44,6 +44,11 @@ class SequentialSoupEngine:
         self.params.update(params or {})
         self.seed, self.lr, self.shuffle = int(seed), float(lr), bool(shuffle)
         self.dtype_code = K.dtype_code(dtype)
+        if not _lib.supports(spec, _lib.OP_SOUP_SEQ, self.device.type != "cpu", self.dtype_code):
+            raise NotImplementedError(
+                f"no native sequential soup loop for {spec} on {self.device.type}: the device loop exists for "
+                "the instantiated lane-per-particle shapes only; use device='cpu' (any shape) or the "
+                "synchronous SoupEngine")
         self.W = torch.zeros((self.n, spec.PP), dtype=dtype)
         self.uid = torch.arange(self.n, dtype=torch.int64)
         if weights is not None:

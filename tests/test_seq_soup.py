@@ -134,3 +134,16 @@ def test_sequential_soup_runtime_shape_north_star_net():
     scale = np.max(np.abs(W1[ok]), 1, keepdims=True) + 1e-6
     assert np.max(np.abs(e.W[:, :spec.P].numpy()[ok] - W1[ok]) / scale) < 5e-3
     assert int(e.next_uid[0]) == 24 + int((rs > 0).sum())
+
+
+def test_unsupported_device_shape_fails_at_construction():
+    """The one-lane device loop (k_soup_seq) exists for the lane-per-particle templates only; a
+    runtime-shape net (the Aggregating(4,10,3) north-star net) asked for on the device is
+    refused when the engine is built, not at its first evolve (the host loop runs any shape)."""
+    import pytest
+    from self_replicating_neural_networks_amd.ops import _lib
+    spec = ArchSpec.aggregating(4, 10, 3)
+    assert _lib.supports(spec, _lib.OP_SOUP_SEQ, False) and not _lib.supports(spec, _lib.OP_SOUP_SEQ, True)
+    assert _lib.supports(ArchSpec.weightwise(2, 2), _lib.OP_SOUP_SEQ, True)
+    with pytest.raises(NotImplementedError, match="device='cpu'"):
+        SequentialSoupEngine(spec, 8, device="cuda")
