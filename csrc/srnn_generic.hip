@@ -1487,6 +1487,10 @@ static bool generic_op_supported(int op) {
   }
 }
 
+extern "C" int srnn_generic_op_supported(int op, int dev) {
+  return generic_op_supported(op) || (op == OP_SOUP_SEQ && !dev) ? 1 : 0;  // sequential: host loop
+}
+
 // ==================================================================================
 // Wide Weightwise nets, U lanes per particle (SGD: train / learn_from).  The lane-per-particle
 // path streams every weight, activation and sample through element-major scratch in HBM
