@@ -60,7 +60,8 @@ def engine_of(spec, op):
             if spec.kind == "weightwise" and spec.P > 16 and 3 <= spec.width <= 64:
                 return "runtime-shape, lanes-per-particle waves (k_ww_wave)"
             if spec.kind == "recurrent" and spec.width >= 8:
-                return "runtime-shape, wave per particle (k_rnn_wave)"
+                spec_wd = (spec.width, spec.depth) in ((8, 2), (16, 2), (32, 2), (8, 3), (16, 3))
+                return ("width/depth-specialised" if spec_wd else "runtime-shape") + ", wave per particle (k_rnn_wave)"
         return "runtime-shape, lane per particle"
     return "wave" if K.is_wave_per_particle(spec) else "lane"
 
