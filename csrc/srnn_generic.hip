@@ -1225,7 +1225,7 @@ __device__ float rw_train_epoch(const GShape& s, const RWave& r, float* hs, floa
   // specialised widths up to 16: lane j's gradient column of every layer in registers (<= 98
   // floats at RNN(16, 3)) instead of an LDS read-modify-write per multiply-add; the same fma
   // sequence per element, so the result is the LDS form's
-  constexpr bool REG = WT > 0 && WT <= 16;
+  constexpr bool REG = WT > 0 && (WT <= 16 || DT == 2);
   constexpr int RL = REG ? DT + 1 : 1, RW = REG ? WT : 1;
   float ak[RL][RW], ar[RL][RW];
   if constexpr (REG) {
