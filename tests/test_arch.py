@@ -59,3 +59,19 @@ def test_flatten_roundtrip():
 def test_only_linear_supported():
     with pytest.raises(NotImplementedError):
         ArchSpec("weightwise", 2, 2, activation="sigmoid")
+
+
+@pytest.mark.parametrize("w,d", [(2, 2), (8, 2), (16, 2), (32, 2), (8, 3), (16, 3), (12, 3), (5, 4)])
+def test_recurrent_closed_form_tables(w, d):
+    """csrc/srnn_generic.hip struct RD (the specialised Recurrent wave kernels) derives the
+    SimpleRNN tables from (width, depth) alone: kernel of layer L at W + W^2 + (L-1) 2W^2
+    (0 for L = 0), its recurrent kernel right after it, P = koff(D) + W + 1."""
+    spec = ArchSpec.recurrent(w, d)
+    offs, shapes = spec.offsets, spec.layer_shapes
+    for L in range(d + 1):
+        koff = 0 if L == 0 else w + w * w + (L - 1) * 2 * w * w
+        i_n, u_n = (1 if L == 0 else w), (1 if L == d else w)
+        assert offs[2 * L] == koff and shapes[2 * L] == (i_n, u_n)
+        assert offs[2 * L + 1] == koff + i_n * u_n and shapes[2 * L + 1] == (u_n, u_n)
+    koff_d = w + w * w + (d - 1) * 2 * w * w
+    assert spec.P == koff_d + w + 1
