@@ -62,6 +62,9 @@ def engine_of(spec, op):
             if spec.kind == "recurrent" and spec.width >= 8:
                 spec_wd = (spec.width, spec.depth) in ((8, 2), (16, 2), (32, 2), (8, 3), (16, 3))
                 return ("width/depth-specialised" if spec_wd else "runtime-shape") + ", wave per particle (k_rnn_wave)"
+        if (op == _lib.OP_SOUP_EVOLVE and spec.kind == "recurrent" and spec.width >= 8
+                and os.environ.get("SRNN_RNN_SOUP", "1") != "0"):
+            return "runtime-shape, wave per particle (k_rnn_wave_soup)"
         return "runtime-shape, lane per particle"
     return "wave" if K.is_wave_per_particle(spec) else "lane"
 

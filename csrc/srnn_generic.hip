@@ -1405,6 +1405,112 @@ __global__ __launch_bounds__(64) void k_rnn_wave(GShape s, SrnnArgs a) {
   }
 }
 
+// per-workgroup device scratch of the wave soup: BPTT states (P x HS floats, padded to a
+// double) + the orthogonal-init matrix of an inline respawn (W x W doubles)
+SRNN_HD int64_t rw_soup_scratch_bytes(const GShape& s) {
+  const int64_t hsf = ((int64_t)s.P * s.HS + 1) & ~(int64_t)1;
+  return hsf * 4 + (int64_t)s.W * s.W * 8;
+}
+
+// Soup generation of the single-rank runtime-shape engine for wide Recurrent nets, one wave per
+// particle, in GItem::soup_evolve's order: attacks received in ascending attacker-slot order
+// (attacker net over the victim's weight sequence, quantised), decision, learn_from the
+// teacher's generation-start row, self-train, respawn (inline re-init on lane 0 with the lane
+// path's g_init); respawn flags per row (SRNN_F_ROW_FLAGS) or OR-ed into the 64-row ballots
+// (zeroed by their consumer, k_g_respawn_seq)
+template <int WT, int DT>
+__global__ __launch_bounds__(64) void k_rnn_wave_soup(GShape s, SrnnArgs a) {
+  extern __shared__ float sm[];
+  const RWave r = rw_layout(s, sm);
+  const int lane = threadIdx.x;
+  char* scr = reinterpret_cast<char*>(a.scratch) + (int64_t)blockIdx.x * rw_soup_scratch_bytes(s);
+  float* hs = reinterpret_cast<float*>(scr);
+  double* orth = reinterpret_cast<double*>(scr + (((int64_t)s.P * s.HS + 1) & ~(int64_t)1) * 4);
+  const int64_t rb = g_rb(s);
+  const int32_t gen = a.gen_ptr ? a.gen_ptr[0] : a.gen;
+  __shared__ uint32_t s_be;
+  for (int64_t j = blockIdx.x; j < a.n; j += gridDim.x) {
+    const int64_t gs = a.lo + j;
+    rw_load(s, GItem::rowp(s, a.W2, j), r.w);
+    const uint32_t head = a.heads[j];
+    uint64_t last = 0;
+    bool first = true;
+    for (;;) {  // 1. attacks
+      if (lane == 0) {
+        uint32_t be = SRNN_NIL;
+        if (head != SRNN_NIL) {
+          uint64_t best = ~0ull;
+          for (uint32_t e = head; e != SRNN_NIL; e = a.nexts[e]) {
+            const uint64_t sl = ent_slot(a, e);
+            if ((first || sl > last) && sl < best) best = sl, be = e;
+          }
+          if (be != SRNN_NIL) last = best, first = false;
+        }
+        s_be = be;
+      }
+      rw_sync();
+      const uint32_t be = s_be;
+      if (be == SRNN_NIL) break;
+      rw_load(s, ent_row(a, be, rb), r.seq);  // the attacker's weights
+      rw_sync();
+      rw_forward<WT, DT>(s, r, r.seq, r.w, nullptr, r.aux);
+      rw_quant(s, r.aux);
+      rw_sync();
+      for (int k = lane; k < s.P; k += 64) r.w[k] = r.aux[k];
+      rw_sync();
+    }
+    if (lane == 0 && head != SRNN_NIL) a.heads[j] = SRNN_NIL;  // consumed
+    // 2. decision, learn_from, self-train
+    int64_t my_at = -1, te = -1;
+    Item<Weightwise<1, 1>, StF32>::decision(a, gs, gen, my_at, te);
+    int8_t act = my_at >= 0 ? A_ATTACKING : A_NONE;
+    int64_t cp = my_at >= 0 ? my_at : -1;
+    float loss = 0.f;
+    if (te >= 0) {
+      rw_load(s, teacher_row(a, te, SRNN_NIL, rb), r.seq);
+      rw_sync();
+      for (int e = 0; e < a.severity; ++e) loss = rw_train_epoch<WT, DT>(s, r, hs, a.lr);
+      act = A_LEARN_FROM;
+      cp = te;
+    }
+    if (a.epochs > 0) {
+      for (int e = 0; e < a.epochs; ++e) {
+        for (int k = lane; k < s.P; k += 64) r.seq[k] = r.w[k];
+        rw_sync();
+        loss = rw_train_epoch<WT, DT>(s, r, hs, a.lr);
+      }
+      act = A_TRAIN_SELF;
+      cp = -1;
+    }
+    // 3. respawn
+    rw_quant(s, r.w);
+    rw_sync();
+    int8_t rs = 0;
+    if ((a.flags & SRNN_F_REMOVE_DIVERGENT) && rw_diverged(s, r.w)) rs = 1;
+    else if ((a.flags & SRNN_F_REMOVE_ZERO) && rw_zero(s, r.w, a.eps)) rs = 2;
+    if (rs && (a.flags & SRNN_F_RESPAWN_INLINE)) {
+      if (lane == 0) {
+        const GCtx x{&s, nullptr, 1, nullptr, orth};
+        g_init(x, SV{r.w, 1}, GItem::rng(a), respawn_key(gen, gs));
+      }
+      rw_sync();
+    }
+    rw_store(s, GItem::rowp(s, a.W, j), r.w);
+    if (lane == 0) {
+      if (a.action) a.action[j] = act;
+      if (a.counterpart) a.counterpart[j] = cp;
+      if (a.loss) a.loss[j] = loss;
+      if (a.respawn) a.respawn[j] = rs;
+      if (a.flags & SRNN_F_ROW_FLAGS) {
+        if (a.rowflags) a.rowflags[j] = rs ? 1 : 0;
+      } else if (a.ballots && rs) {
+        atomicOr(a.ballots + (j >> 6), 1ull << (j & 63));
+      }
+    }
+    rw_sync();
+  }
+}
+
 // recurrent nets at least RW_MIN_WIDTH wide whose three P-vectors fit a workgroup's LDS run
 // apply / train / learn / run_fixpoint (no trajectory) wave per particle
 static int g_rnn_wave = -1;  // SRNN_RNN_WAVE=0: lane path for every width (A/B tests)
@@ -1417,12 +1523,19 @@ static int g_rnn_spec = [] {
   return (e && e[0] == '0') ? 0 : 1;
 }();
 extern "C" void srnn_set_rnn_spec(int on) { g_rnn_spec = on ? 1 : 0; }
+// wave-per-particle soup generations of wide Recurrent nets (SRNN_RNN_SOUP=0: the lane path)
+static int g_rnn_soup = [] {
+  const char* e = std::getenv("SRNN_RNN_SOUP");
+  return (e && e[0] == '0') ? 0 : 1;
+}();
+extern "C" void srnn_set_rnn_soup(int on) { g_rnn_soup = on ? 1 : 0; }
 template <int WT, int DT>
 static void rw_launch_shape(int op, dim3 grid, size_t lds, hipStream_t st, const GShape& s, const SrnnArgs& a) {
   switch (op) {
     case OP_APPLY: hipLaunchKernelGGL((k_rnn_wave<OP_APPLY, WT, DT>), grid, dim3(64), lds, st, s, a); break;
     case OP_TRAIN: hipLaunchKernelGGL((k_rnn_wave<OP_TRAIN, WT, DT>), grid, dim3(64), lds, st, s, a); break;
     case OP_LEARN: hipLaunchKernelGGL((k_rnn_wave<OP_LEARN, WT, DT>), grid, dim3(64), lds, st, s, a); break;
+    case OP_SOUP_EVOLVE: hipLaunchKernelGGL((k_rnn_wave_soup<WT, DT>), grid, dim3(64), lds, st, s, a); break;
     default: hipLaunchKernelGGL((k_rnn_wave<OP_RUN_FIXPOINT, WT, DT>), grid, dim3(64), lds, st, s, a); break;
   }
 }
@@ -1441,14 +1554,16 @@ static bool rw_serves(int op, const GShape& s, const SrnnArgs& a) {
       return false;
   }
   if (s.P != s.koff[s.D] + s.W + 1 || s.HS != s.D * s.W + 1) return false;
+  if (op == OP_SOUP_EVOLVE)  // single-rank generations (sharded exchanges: the lane path)
+    return g_rnn_soup && !(a.flags & (SRNN_F_X2 | SRNN_F_FULL_TABLE)) && a.heads && a.nexts;
   if (op == OP_RUN_FIXPOINT) return a.traj == nullptr;
   return op == OP_APPLY || op == OP_TRAIN || op == OP_LEARN;
 }
 static int rw_launch(int op, const GShape& s, const SrnnArgs& a) {
   if (a.n <= 0) return 0;
-  const int64_t per = (int64_t)s.P * s.HS * (int64_t)sizeof(float);
+  const int64_t per = op == OP_SOUP_EVOLVE ? rw_soup_scratch_bytes(s) : (int64_t)s.P * s.HS * (int64_t)sizeof(float);
   int64_t blocks = a.scratch ? a.scratch_bytes / per : 0;
-  if (op != OP_TRAIN && op != OP_LEARN) blocks = 4096;  // no BPTT states
+  if (op != OP_TRAIN && op != OP_LEARN && op != OP_SOUP_EVOLVE) blocks = 4096;  // no BPTT states
   blocks = blocks < a.n ? blocks : a.n;
   blocks = blocks < 8192 ? blocks : 8192;
   if (blocks <= 0) {
@@ -1457,7 +1572,7 @@ static int rw_launch(int op, const GShape& s, const SrnnArgs& a) {
   }
   const size_t lds = rw_lds_bytes(s);
   hipStream_t st = (hipStream_t)a.stream;
-  if (op != OP_APPLY && op != OP_TRAIN && op != OP_LEARN && op != OP_RUN_FIXPOINT) {
+  if (op != OP_APPLY && op != OP_TRAIN && op != OP_LEARN && op != OP_RUN_FIXPOINT && op != OP_SOUP_EVOLVE) {
     set_error("recurrent wave path: op");
     return -1;
   }

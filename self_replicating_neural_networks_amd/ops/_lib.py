@@ -162,6 +162,8 @@ def lib():
         L.srnn_set_ww_wave.restype = None
         L.srnn_set_rnn_spec.argtypes = [ctypes.c_int]
         L.srnn_set_rnn_spec.restype = None
+        L.srnn_set_rnn_soup.argtypes = [ctypes.c_int]
+        L.srnn_set_rnn_soup.restype = None
         vp, i64, cp = ctypes.c_void_p, ctypes.c_int64, ctypes.c_char_p
         for name, args in (("srnn_comm_available", [cp]), ("srnn_comm_unique_id", [cp, vp, ctypes.c_int]),
                            ("srnn_comm_init", [cp, vp, ctypes.c_int, ctypes.c_int, ctypes.c_int,
@@ -226,6 +228,12 @@ def set_rnn_spec(on: bool) -> None:
     """Width / depth-specialised Recurrent wave kernels for RNN(8|16|32, 2) and RNN(8|16, 3) (default) or the
     runtime-shape wave kernel for every width (A/B tests)."""
     lib().srnn_set_rnn_spec(1 if on else 0)
+
+
+def set_rnn_soup(on: bool) -> None:
+    """Single-rank soup generations of wide Recurrent nets wave per particle (default) or on the
+    lane path (A/B tests)."""
+    lib().srnn_set_rnn_soup(1 if on else 0)
 
 
 def set_ww_wave(on: bool) -> None:

@@ -74,3 +74,46 @@ def test_rnn_wave_specialised_equals_runtime_shape(cuda, w, d):
         if x.dtype == torch.float32:
             x, y = x.view(torch.int32), y.view(torch.int32)
         assert torch.equal(x, y), k
+
+
+SOUP = dict(attacking_rate=0.2, learn_from_rate=0.2, train=2, learn_from_severity=2, remove_divergent=True,
+            remove_zero=True, epsilon=1e-4)
+
+
+def _soup(spec, dev, dtype, graphs):
+    from self_replicating_neural_networks_amd.soup_engine import SoupEngine
+
+    e = SoupEngine(spec, 150, SOUP, device=dev, seed=13, dtype=dtype)
+    e.stats = True
+    if graphs:
+        assert e.capture(warmup=1)
+        e.evolve(2)
+    else:
+        e.evolve(3)
+    torch.cuda.synchronize()
+    return (e.local_rows().clone(), e.uid.clone(), e.loss.clone(), e.action.clone(), e.counterpart.clone(),
+            e.respawn.clone(), e.last_census(), int(e.next_uid))
+
+
+@pytest.mark.parametrize("w,d", [(8, 2), (12, 3)])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.float16], ids=["f32", "f16"])
+def test_rnn_wave_soup_equals_lane_path(cuda, w, d, dtype):
+    """Recurrent soup generations wave per particle (k_rnn_wave_soup: attacks, learn_from,
+    self-train, respawn with inline re-init) == the lane path, bitwise; graphs == eager"""
+    spec = ArchSpec.recurrent(w, d)
+    outs = []
+    for wave in (True, False):
+        _lib.set_rnn_soup(wave)
+        try:
+            outs.append(_soup(spec, cuda, dtype, graphs=False))
+        finally:
+            _lib.set_rnn_soup(True)
+    a, b = outs
+    bits = lambda t: t.contiguous().view(torch.uint8) if t.is_floating_point() else t
+    for k, (x, y) in enumerate(zip(a[:6], b[:6])):
+        assert torch.equal(bits(x), bits(y)), k
+    assert a[6:] == b[6:]
+    assert int((a[3] == 3).sum()) > 0  # self-training happened
+    g = _soup(spec, cuda, dtype, graphs=True)
+    for k, (x, y) in enumerate(zip(g[:6], a[:6])):
+        assert torch.equal(bits(x), bits(y)), k
