@@ -7,17 +7,19 @@ particle: attacks (rate 0.1), learn_from (rate 0.1, severity 1), 20 self-train e
 divergent/zero respawn, plus the per-generation fixpoint census (``Soup.count``,
 code/soup.py:89-103) all-reduced over ranks.  The soup configuration is the reference's
 active soup demo (code/soup.py:127-138: WeightwiseNeuralNetwork(2, 2), train=20,
-remove_divergent, remove_zero, epsilon=1e-4) with 100k particles per GPU (weak
-scaling: the population is sharded, every rank owns 100k particles; at N=1 this is the
-100k-particle soup).  Random-init weights, fp32 (the reference's dtype; bf16 would make
-the 1e-4 fixpoint test meaningless).
+remove_divergent, remove_zero, epsilon=1e-4).  Random-init weights, fp32 (the reference's
+dtype; bf16 would make the 1e-4 fixpoint test meaningless).
 
-Multi-GPU (N>1): one process per GPU, every rank owns 100k particles of ONE global soup
-(partners uniform over all N x 100k slots).  Per generation each rank ships the rows other
-ranks need (attackers of their victims, teachers their learners requested one generation
-ahead) in ONE all-to-all on the soup's own RCCL communicator over xGMI, on a comm stream,
-while the slots that need no remote row evolve on the compute stream (soup_engine.py).
-Single GPU: the fused generation kernel, 16/8/4/2 generations per hipGraph.
+Scaling (``--scaling``): ``strong`` (default) is the metric as BASELINE.json writes it -- ONE
+100k-particle soup at any GPU count (100k / N particles per rank); ``weak`` keeps
+``--particles-per-gpu`` per rank (an N x 100k soup).
+
+Multi-GPU (N>1): one process per GPU, each rank owns a contiguous shard of ONE global soup
+(partners uniform over all slots).  Per generation (soup_engine.py, serial schedule) each
+rank packs the rows other ranks need (attackers of their victims, teachers their learners
+requested one generation ahead), ONE all-to-all on the soup's own RCCL communicator over
+xGMI moves them, and ONE launch runs the exchange's post and the evolve of every local slot.
+Single GPU: the fused generation kernel, 20/16/8/4/2 generations per hipGraph.
 
 value = particles x generations / second over the whole job (max time over ranks).
 
@@ -41,7 +43,14 @@ def parse_args(argv=None):
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--particles-per-gpu", type=int, default=100_000)
+    ap.add_argument("--scaling", choices=["strong", "weak"], default="strong",
+                    help="strong: one --particles soup at any GPU count (the BASELINE metric); "
+                         "weak: --particles-per-gpu on every rank")
+    ap.add_argument("--particles", type=int, default=100_000, help="soup size (strong scaling)")
+    ap.add_argument("--particles-per-gpu", type=int, default=100_000, help="per-rank soup size (weak scaling)")
+    ap.add_argument("--order", choices=["sequential", "synchronous"], default="synchronous",
+                    help="sequential: the reference's in-place, index-ordered generation (level-scheduled, "
+                         "single rank); synchronous: every read from the generation-start table (shardable)")
     ap.add_argument("--train", type=int, default=20)
     ap.add_argument("--attacking-rate", type=float, default=0.1)
     ap.add_argument("--learn-from-rate", type=float, default=0.1)
@@ -84,6 +93,7 @@ def model_string(args) -> str:
     else:
         parts.append("no learn_from")
     parts.append("remove divergent/zero")
+    parts.append("reference (sequential) order" if args.order == "sequential" else "synchronous order")
     return "Soup of WeightwiseNeuralNetwork(width=2, depth=2), " + ", ".join(parts)
 
 
@@ -101,6 +111,7 @@ def main(argv=None):
     import torch
     import torch.distributed as dist
     from self_replicating_neural_networks_amd.arch import ArchSpec
+    from self_replicating_neural_networks_amd.config import ExecConfig
     from self_replicating_neural_networks_amd.parallel.dist import from_env
     from self_replicating_neural_networks_amd.soup_engine import SoupEngine
 
@@ -125,8 +136,15 @@ def main(argv=None):
     params = dict(attacking_rate=args.attacking_rate, learn_from_rate=args.learn_from_rate,
                   learn_from_severity=args.severity, train=args.train,
                   remove_divergent=True, remove_zero=True, epsilon=1e-4)
-    n_total = args.particles_per_gpu * d.world
-    eng = SoupEngine(spec, n_total, params, device=dev, seed=args.seed, dist=d)
+    n_total = args.particles if args.scaling == "strong" else args.particles_per_gpu * d.world
+    execution = ExecConfig().resolved()
+    execution.apply_library()
+    if args.order == "sequential" and d.enabled:
+        print("bench.py: the reference-order generation is single-rank (--order synchronous shards)",
+              file=sys.stderr)
+        sys.exit(2)
+    eng = SoupEngine(spec, n_total, params, device=dev, seed=args.seed, dist=d, execution=execution,
+                     order=args.order)
     eng.stats = not args.no_stats
     graphed = False
     if on_gpu and not args.no_graph:
@@ -151,6 +169,16 @@ def main(argv=None):
         raise SystemExit(f"soup row exchange failed ({err}): the measured generations are invalid")
     census = eng.count()
     value = n_total * args.steps / dt
+    # what RCCL itself reports about the soup's communicator on every rank (ncclCommCount /
+    # ncclCommUserRank): the line shows that the collective really spanned N ranks
+    comm = None
+    if d.native is not None:
+        mine = torch.tensor([d.native.nranks, d.native.comm_rank], dtype=torch.int64, device=dev)
+        allr = torch.zeros(2 * d.world, dtype=torch.int64, device=dev)
+        d.all_gather_into(allr, mine)
+        allr = allr.view(d.world, 2).cpu().tolist()
+        comm = {"library": d.native.library, "rccl_nranks": [r[0] for r in allr],
+                "rccl_user_ranks": [r[1] for r in allr]}
     if d.rank == 0:
         print(json.dumps({
             "metric": "self-application steps/sec (whole node) for 100k-particle soup",
@@ -161,19 +189,21 @@ def main(argv=None):
             "warmup": args.warmup,
             "ms_per_step": dt / args.steps * 1e3,
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": args.scaling,
             "vs_baseline": None,
             "dtype": "fp32",
             "data": "synthetic (random-init particles, Philox seed %d)" % args.seed,
             "config": {"model": model_string(args),
-                       "global_batch": n_total, "particles_per_gpu": args.particles_per_gpu, "seq_len": None,
+                       "global_batch": n_total, "particles_per_gpu": n_total / d.world, "seq_len": None,
                        "parallelism": f"population-dp{d.world}", "device": args.device, "hip_graph": graphed,
                        "multi_generation_graph": eng._chunk is not None,
-                       "collectives": ("native RCCL communicator (" + d.native.library + ")") if d.native
+                       "collectives": comm if comm is not None
                        else (f"torch.distributed ({backend})" if d.enabled else None),
+                       "world_size": d.world, "execution": execution.in_force(),
                        "overlap": getattr(eng, "overlap", False),
                        "sharded_schedule": getattr(eng, "schedule", None) if getattr(eng, "x2", False) else None,
-                       "census_every_step": eng.stats, "final_census": census},
+                       "census_every_step": eng.stats, "final_census": census, "order": args.order,
+                       "ordered_levels": eng.ordered_levels() if args.order == "sequential" else None},
         }), flush=True)
     eng.release_graphs()  # graph executables reference the RCCL communicator
     d.close()

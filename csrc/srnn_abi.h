@@ -149,6 +149,13 @@ struct SrnnArgs {
   void* stream;         // hipStream_t for dev == 1
   void* scratch;        // generic (runtime-shape) engine: per-lane vectors, element-major; null ->
   int64_t scratch_bytes;  // the library's own cached device buffer (not inside a graph capture)
+  // ---- ordered (reference-order) generation, OP_SOUP_ORDERED (srnn_ordered.h)
+  float* W3;            // [n][pp] attack outputs A(k) of this generation
+  int32_t* o_src;       // [n][4] source versions of each turn's reads + its level
+  int32_t* o_list;      // [(o_levels + 1) * n] work lists of levels 0..o_levels-1 and the tail
+  int32_t* o_ctl;       // [19] list lengths, max level, error bits (zeroed by the plan kernel)
+  int32_t o_levels;     // parallel level launches per generation (1..16); deeper turns: the tail
+  int32_t pad3;
 };
 
 #define SRNN_X2_HDR 12  // int64 header words of an X2 exchange block (see srnn_shard.hip)
@@ -174,9 +181,11 @@ enum SrnnOp {
                         // (links, notices, requests) + the rows of this generation's exchange
   OP_X2_POST = 21,      // after the all-to-all: uids of the previous generation's newborns, global
                         // census, received notices linked for the next generation, requests kept
+  OP_SOUP_ORDERED = 22, // one reference-order (sequential, in-place) generation, level-scheduled:
+                        // bitwise OP_SOUP_SEQ, every particle of a level in parallel (srnn_ordered.h)
 };
 
-int srnn_abi_version();  // 18
+int srnn_abi_version();  // 19
 int64_t srnn_args_size();  // sizeof(SrnnArgs): the ctypes mirror checks its layout against it
 int64_t srnn_cfg_size();
 int srnn_has_config(const SrnnCfg* cfg);
@@ -186,5 +195,21 @@ int srnn_is_generic(const SrnnCfg* cfg, int op);
 int srnn_supports(const SrnnCfg* cfg, int op, int dev);  // 1: op has a host (0) / device (1) path
 int srnn_generic_op_supported(int op, int dev);
 void srnn_set_force_generic(int on);  // 1: this op of this config runs on the generic engine
+// Execution knobs (config.py ExecConfig): which kernel family serves an op.  A value set here
+// is used unless the knob's environment variable is set (the variable overrides: A/B runs);
+// -1 = unset (built-in default).  srnn_get_knob returns the value in force.
+enum SrnnKnob {
+  SRNN_KNOB_FORCE_GENERIC = 0,  // SRNN_FORCE_GENERIC: every op on the runtime-shape engine (default 0)
+  SRNN_KNOB_RNN_WAVE = 1,       // SRNN_RNN_WAVE: wide Recurrent nets wave per particle (default 1)
+  SRNN_KNOB_RNN_SPEC = 2,       // SRNN_RNN_SPEC: width/depth-specialised Recurrent wave kernels (default 1)
+  SRNN_KNOB_RNN_SOUP = 3,       // SRNN_RNN_SOUP: wide Recurrent soup generations wave per particle (default 1)
+  SRNN_KNOB_WW_WAVE = 4,        // SRNN_WW_WAVE: wide Weightwise training lanes-per-particle waves (default 1)
+  SRNN_KNOB_BIG_WAVE = 5,       // SRNN_BIG_WAVE: P = 280 nets on the wave kernels instead of row kernels (default 0)
+  SRNN_KNOB_FIX_GROUP = 6,      // SRNN_FIX_GROUP: 16-lane run_fixpoint (1), lane (0), by population size (-1)
+  SRNN_KNOB_SOUP_LANES = 7,     // SRNN_SOUP_LANES: lanes per particle of WW(2,2) soup generations (0 = by size)
+  SRNN_KNOB_COUNT = 8
+};
+void srnn_set_knob(int knob, int value);
+int srnn_get_knob(int knob);
 int64_t srnn_generic_scratch_bytes(const SrnnCfg* cfg, int64_t n, int64_t max_lanes);
 }

@@ -1807,8 +1807,7 @@ int big_run(int op, const SrnnCfg& c, const SrnnArgs& a) {
   }
   // lane-per-particle row kernels (default) or the wave-per-particle ones (SRNN_BIG_WAVE=1,
   // fp32 tables without shuffle only)
-  const char* wave_env = std::getenv("SRNN_BIG_WAVE");
-  const bool row_kernels = !(wave_env && wave_env[0] == '1');
+  const bool row_kernels = knob(SRNN_KNOB_BIG_WAVE, 0) != 1;
   const bool wave_op = !row_kernels && (op == OP_APPLY || op == OP_CLASSIFY || op == OP_TRAIN || op == OP_LEARN);
   if (op != OP_RUN_FIXPOINT && !(wave_op && c.dtype == 0 && c.shuffler == 0)) {
     if (a.n <= 0 && op != OP_SOUP_DECIDE) return 0;

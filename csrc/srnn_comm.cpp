@@ -38,6 +38,8 @@ struct Rccl {
   ncclResult_t (*all_reduce)(const void*, void*, size_t, ncclDataType_t, ncclRedOp_t, ncclComm_t,
                              hipStream_t) = nullptr;
   const char* (*error_string)(ncclResult_t) = nullptr;
+  ncclResult_t (*comm_count)(const ncclComm_t, int*) = nullptr;      // optional: introspection
+  ncclResult_t (*comm_user_rank)(const ncclComm_t, int*) = nullptr;
   std::string path;
 };
 
@@ -69,6 +71,8 @@ bool load(const char* hint) {
               sym(h, "ncclAllGather", r.all_gather) && sym(h, "ncclAllReduce", r.all_reduce) &&
               sym(h, "ncclGetErrorString", r.error_string);
     if (!ok) continue;
+    sym(h, "ncclCommCount", r.comm_count);
+    sym(h, "ncclCommUserRank", r.comm_user_rank);
     r.path = c;
     g_rccl = r;
     return true;
@@ -136,6 +140,19 @@ int srnn_comm_async_error(void* comm) {
   int r = check(g_rccl.async_error((ncclComm_t)comm, &a), "ncclCommGetAsyncError");
   if (r) return r;
   return check(a, "async");
+}
+
+// ranks of the communicator and this process's rank in it, as RCCL reports them
+// (ncclCommCount / ncclCommUserRank): the bench prints them so a run shows that RCCL saw N ranks
+int srnn_comm_count(void* comm) {
+  if (!comm || !g_rccl.comm_count) return -1;
+  int n = -1;
+  return check(g_rccl.comm_count((ncclComm_t)comm, &n), "ncclCommCount") ? -1 : n;
+}
+int srnn_comm_user_rank(void* comm) {
+  if (!comm || !g_rccl.comm_user_rank) return -1;
+  int r = -1;
+  return check(g_rccl.comm_user_rank((ncclComm_t)comm, &r), "ncclCommUserRank") ? -1 : r;
 }
 
 // equal-split all-to-all of `bytes_per_peer` bytes per destination (4-byte granules)

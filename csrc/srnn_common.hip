@@ -76,6 +76,7 @@ const char* op_name(int op) {
     case OP_SOUP_SEQ: return "srnn:soup_seq";
     case OP_X2_PACK: return "srnn:x2_pack";
     case OP_X2_POST: return "srnn:x2_post";
+    case OP_SOUP_ORDERED: return "srnn:soup_ordered";
     default: return "srnn:op";
   }
 }
@@ -105,16 +106,24 @@ static int dispatch_special(int op, const SrnnCfg* c, const SrnnArgs* a) {
   }
 }
 
-// SRNN_FORCE_GENERIC=1 (or srnn_set_force_generic) routes every op to the runtime-shape
-// engine: the A/B switch of tests/test_generic.py
-static int g_force_generic = -1;
-static bool force_generic() {
-  if (g_force_generic < 0) {
-    const char* e = std::getenv("SRNN_FORCE_GENERIC");
-    g_force_generic = (e && e[0] == '1') ? 1 : 0;
-  }
-  return g_force_generic == 1;
+// ---- execution knobs (srnn_abi.h SrnnKnob; config.py ExecConfig): environment variable if
+// set (read on every query: A/B tests flip it between calls), else the value set through the
+// API, else the built-in default
+namespace {
+const char* const g_knob_env[SRNN_KNOB_COUNT] = {"SRNN_FORCE_GENERIC", "SRNN_RNN_WAVE", "SRNN_RNN_SPEC",
+                                                 "SRNN_RNN_SOUP",      "SRNN_WW_WAVE",  "SRNN_BIG_WAVE",
+                                                 "SRNN_FIX_GROUP",     "SRNN_SOUP_LANES"};
+int g_knob[SRNN_KNOB_COUNT] = {-1, -1, -1, -1, -1, -1, -1, -1};
+}  // namespace
+namespace srnn {
+int knob(int id, int dflt) {
+  if (id < 0 || id >= SRNN_KNOB_COUNT) return dflt;
+  const char* e = std::getenv(g_knob_env[id]);
+  if (e && *e) return std::atoi(e);
+  return g_knob[id] >= 0 ? g_knob[id] : dflt;
 }
+}  // namespace srnn
+static bool force_generic() { return srnn::knob(SRNN_KNOB_FORCE_GENERIC, 0) == 1; }
 
 // which engine serves (op, cfg, host/device): 0 specialised, 1 generic, -1 none
 static int route(int op, const SrnnCfg* c, const SrnnArgs* a) {
@@ -191,7 +200,7 @@ static int with_scratch(int op, const SrnnCfg* c, const SrnnArgs* a) {
 
 extern "C" {
 
-int srnn_abi_version() { return 18; }
+int srnn_abi_version() { return 19; }
 
 // layout check of the ctypes mirror (ops/_lib.py): sizeof(SrnnArgs) / sizeof(SrnnCfg)
 int64_t srnn_args_size() { return (int64_t)sizeof(SrnnArgs); }
@@ -205,7 +214,11 @@ int srnn_has_config(const SrnnCfg* cfg) {
   return route(0, cfg, &probe) >= 0 ? 1 : 0;
 }
 
-void srnn_set_force_generic(int on) { g_force_generic = on ? 1 : 0; }
+void srnn_set_force_generic(int on) { srnn_set_knob(SRNN_KNOB_FORCE_GENERIC, on ? 1 : 0); }
+void srnn_set_knob(int id, int value) {
+  if (id >= 0 && id < SRNN_KNOB_COUNT) g_knob[id] = value < 0 ? -1 : value;
+}
+int srnn_get_knob(int id) { return srnn::knob(id, -1); }
 
 int srnn_is_generic(const SrnnCfg* cfg, int op) {
   SrnnArgs probe{};

@@ -1513,22 +1513,14 @@ __global__ __launch_bounds__(64) void k_rnn_wave_soup(GShape s, SrnnArgs a) {
 
 // recurrent nets at least RW_MIN_WIDTH wide whose three P-vectors fit a workgroup's LDS run
 // apply / train / learn / run_fixpoint (no trajectory) wave per particle
-static int g_rnn_wave = -1;  // SRNN_RNN_WAVE=0: lane path for every width (A/B tests)
-extern "C" void srnn_set_rnn_wave(int on) { g_rnn_wave = on ? 1 : 0; }
+// knob SRNN_KNOB_RNN_WAVE = 0: lane path for every width (A/B tests)
+extern "C" void srnn_set_rnn_wave(int on) { srnn_set_knob(SRNN_KNOB_RNN_WAVE, on ? 1 : 0); }
 // width / depth-specialised instantiations (RNN(8|16|32, 2), RNN(8|16, 3); RNN(32, 3) fully
 // unrolled spills past 256 VGPRs and stays runtime-shape); 0: the runtime-shape kernel
 // for every shape (A/B tests, SRNN_RNN_SPEC=0)
-static int g_rnn_spec = [] {
-  const char* e = std::getenv("SRNN_RNN_SPEC");
-  return (e && e[0] == '0') ? 0 : 1;
-}();
-extern "C" void srnn_set_rnn_spec(int on) { g_rnn_spec = on ? 1 : 0; }
-// wave-per-particle soup generations of wide Recurrent nets (SRNN_RNN_SOUP=0: the lane path)
-static int g_rnn_soup = [] {
-  const char* e = std::getenv("SRNN_RNN_SOUP");
-  return (e && e[0] == '0') ? 0 : 1;
-}();
-extern "C" void srnn_set_rnn_soup(int on) { g_rnn_soup = on ? 1 : 0; }
+extern "C" void srnn_set_rnn_spec(int on) { srnn_set_knob(SRNN_KNOB_RNN_SPEC, on ? 1 : 0); }
+// wave-per-particle soup generations of wide Recurrent nets (knob SRNN_KNOB_RNN_SOUP = 0: the lane path)
+extern "C" void srnn_set_rnn_soup(int on) { srnn_set_knob(SRNN_KNOB_RNN_SOUP, on ? 1 : 0); }
 template <int WT, int DT>
 static void rw_launch_shape(int op, dim3 grid, size_t lds, hipStream_t st, const GShape& s, const SrnnArgs& a) {
   switch (op) {
@@ -1540,11 +1532,7 @@ static void rw_launch_shape(int op, dim3 grid, size_t lds, hipStream_t st, const
   }
 }
 static bool rw_serves(int op, const GShape& s, const SrnnArgs& a) {
-  if (g_rnn_wave < 0) {
-    const char* e = std::getenv("SRNN_RNN_WAVE");
-    g_rnn_wave = (e && e[0] == '0') ? 0 : 1;
-  }
-  if (!g_rnn_wave) return false;
+  if (knob(SRNN_KNOB_RNN_WAVE, 1) == 0) return false;
   if (s.kind != 2 || s.W < RW_MIN_WIDTH || s.W > 64 || rw_lds_bytes(s) > 60 * 1024 || !a.dev) return false;
   // RD's closed form of the layer tables must be make_gshape's
   for (int l = 0; l < s.NL; ++l) {
@@ -1555,7 +1543,7 @@ static bool rw_serves(int op, const GShape& s, const SrnnArgs& a) {
   }
   if (s.P != s.koff[s.D] + s.W + 1 || s.HS != s.D * s.W + 1) return false;
   if (op == OP_SOUP_EVOLVE)  // single-rank generations (sharded exchanges: the lane path)
-    return g_rnn_soup && !(a.flags & (SRNN_F_X2 | SRNN_F_FULL_TABLE)) && a.heads && a.nexts;
+    return knob(SRNN_KNOB_RNN_SOUP, 1) != 0 && !(a.flags & (SRNN_F_X2 | SRNN_F_FULL_TABLE)) && a.heads && a.nexts;
   if (op == OP_RUN_FIXPOINT) return a.traj == nullptr;
   return op == OP_APPLY || op == OP_TRAIN || op == OP_LEARN;
 }
@@ -1576,7 +1564,8 @@ static int rw_launch(int op, const GShape& s, const SrnnArgs& a) {
     set_error("recurrent wave path: op");
     return -1;
   }
-  const int w = g_rnn_spec ? s.W : 0, d = g_rnn_spec ? s.D : 0;
+  const bool spec = knob(SRNN_KNOB_RNN_SPEC, 1) != 0;
+  const int w = spec ? s.W : 0, d = spec ? s.D : 0;
   const dim3 grid((unsigned)blocks);
   if (w == 8 && d == 2) rw_launch_shape<8, 2>(op, grid, lds, st, s, a);
   else if (w == 16 && d == 2) rw_launch_shape<16, 2>(op, grid, lds, st, s, a);
@@ -1996,14 +1985,10 @@ __global__ __launch_bounds__(64) void k_ww_wave_soup(GShape s, WWave g, SrnnArgs
   }
 }
 
-static int g_ww_wave = -1;  // SRNN_WW_WAVE=0: lane path for every width (A/B tests)
-extern "C" void srnn_set_ww_wave(int on) { g_ww_wave = on ? 1 : 0; }
+// knob SRNN_KNOB_WW_WAVE = 0: lane path for every width (A/B tests)
+extern "C" void srnn_set_ww_wave(int on) { srnn_set_knob(SRNN_KNOB_WW_WAVE, on ? 1 : 0); }
 static bool ww_serves(int op, const GShape& s, const SrnnArgs& a, WWave& g) {
-  if (g_ww_wave < 0) {
-    const char* e = std::getenv("SRNN_WW_WAVE");
-    g_ww_wave = (e && e[0] == '0') ? 0 : 1;
-  }
-  if (!g_ww_wave || !a.dev) return false;
+  if (knob(SRNN_KNOB_WW_WAVE, 1) == 0 || !a.dev) return false;
   if (op == OP_SOUP_EVOLVE) {  // single-rank generations (sharded exchanges: the lane path)
     if (a.flags & (SRNN_F_X2 | SRNN_F_FULL_TABLE)) return false;
     return ww_wave_geom(s, g, true) && ww_wave_lds(s, g) <= 64 * 1024;

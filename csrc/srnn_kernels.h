@@ -21,6 +21,7 @@ extern "C" int srnn_x2_run(int op, const SrnnCfg* c, const SrnnArgs* a);  // srn
 namespace srnn {
 
 void set_error(const char* msg);
+int knob(int id, int dflt);  // srnn_common.hip: execution knob in force (SrnnKnob)
 
 constexpr int TB = 64;  // threads per block: one wave; lane-private LDS scratch per thread
 // waves of the X2 remote evolve (grid-stride over the remote-dependent list, whose length is
@@ -1594,9 +1595,9 @@ int launch(const SrnnCfg& c, const SrnnArgs& a) {
   }
   hipStream_t st = (hipStream_t)a.stream;
   if constexpr (OP == OP_RUN_FIXPOINT && Net::KIND == 0 && Net::P <= 16) {
-    // small populations: 16 lanes per particle (SRNN_FIX_GROUP=0/1 forces either form)
-    const char* env = std::getenv("SRNN_FIX_GROUP");
-    const bool group = env ? env[0] == '1' : a.n <= FIX_GROUP_MAX_N;
+    // small populations: 16 lanes per particle (knob SRNN_KNOB_FIX_GROUP 0/1 forces either form)
+    const int kg = knob(SRNN_KNOB_FIX_GROUP, -1);
+    const bool group = kg >= 0 ? kg == 1 : a.n <= FIX_GROUP_MAX_N;
     if (group) {
       hipLaunchKernelGGL((k_fix_group<Net, S>), dim3((unsigned)((a.n * 16 + TBG - 1) / TBG)), dim3(TBG), 0, st, c,
                          a);
@@ -1819,6 +1820,9 @@ int respawn_seq(const SrnnCfg& c, const SrnnArgs& a) {
   return 0;
 }
 
+// reference-order generations scheduled by dependency level (OP_SOUP_ORDERED)
+#include "srnn_ordered.h"
+
 template <class Net, int OP, class S>
 int run_one(const SrnnCfg& c, const SrnnArgs& a) {
   return a.dev ? launch<Net, OP, S>(c, a) : host_run<Net, OP, S>(c, a);
@@ -1842,6 +1846,7 @@ int run_net_op(int op, const SrnnCfg& c, const SrnnArgs& a) {
     case OP_SOUP_GEN: return soup_gen<Net, S>(c, a);
     case OP_GEN_FINISH: return gen_finish<Net, S>(c, a);
     case OP_SOUP_SEQ: return soup_seq<Net, S>(c, a);
+    case OP_SOUP_ORDERED: return soup_ordered<Net, S>(c, a);
     default: set_error("unknown op"); return -1;
   }
 }

@@ -1,0 +1,481 @@
+// srnn_ordered.h — the reference's sequential, in-place soup generation on the GPU
+// (OP_SOUP_ORDERED), bitwise equal to the serial loop (Item::soup_seq_one / OP_SOUP_SEQ).
+// Included by srnn_kernels.h inside namespace srnn.
+//
+// Reference Soup.evolve (code/soup.py:51-87) visits particles in index order and updates
+// the table IN PLACE: particle k sees every change made by particles < k in the same
+// generation.  Read literally that is a serial loop; but the decisions of a
+// generation are a pure function of (seed, slot, generation), so its whole dependency
+// structure is known before any weight is touched:
+//
+//   turn k reads   its own row at turn start   = the last write to row k before k
+//                  the victim's row (attack)   = the last write to row at_k before k
+//                  the teacher's row (learn)   = the last write to row te_k before k
+//                                                (or k's own / just-attacked row)
+//   turn k writes  A(k) = f_k(victim)          (the attack output, row at_k)
+//                  E(k) = k's row at turn end  (after learn / train / respawn)
+//
+// Writes to a row r happen at "times" j (A(j) for each attacker j of r) and r + 1/2 (E(r)).
+// Keeping every written version (A(j) in table W3 row j, E(j) in W row j, the generation
+// start in W2) removes the write-after-read hazards, so only read-after-write edges remain:
+// turn k depends on the turns that produced the versions it reads.  That DAG is shallow
+// (longest path ~ log n: 5-6 levels at 100k particles, 86 % of the turns at level 0), so a
+// generation runs as
+//
+//   k_ord_plan    per turn: decisions, the source version of each of its reads (src codes)
+//   k_ord_levels  per turn: level = 1 + max level of its producers (memoised DFS over the
+//                 src codes), appended to its level's work list (one atomic per wave+level)
+//   k_ord_level   x C launches: the turns of level L, one lane per turn
+//   k_ord_tail    one wave: the turns of levels >= C in rounds (fence + barrier per round)
+//   k_ord_close   per row: its final version (a row attacked after its own turn ends the
+//                 generation as that attack's output), census class, the next generation's
+//                 decisions linked, block stats for the finish (newborn uids in slot order)
+//
+// Every turn runs the serial loop's per-particle code with the same Philox streams (attack
+// keyed (k, gen*1024+1), SGD (k, gen*1024+512), newborn init respawn_key(gen, k)), so a
+// generation equals OP_SOUP_SEQ bitwise (tests/test_ordered_soup.py, host and device).  No
+// workgroup waits for another: levels are separated by kernel boundaries, the tail's rounds
+// by one wave's own barrier.
+#pragma once
+
+namespace ord {
+
+// src codes: >= 0 a version written this generation (2j: A(j) in W3, 2j+1: E(j) in W);
+// -(r+1): the generation-start row r (W2); SELF / ATK: the turn's own current row / its own
+// attack output (learn_from of itself / of its victim); NONE: no such read
+constexpr int32_t SRC_SELF = INT32_MIN;
+constexpr int32_t SRC_ATK = INT32_MIN + 1;
+constexpr int32_t SRC_NONE = INT32_MIN + 2;
+constexpr int MAXD = 64;        // DFS stack of the level computation (error bit 1 past it)
+constexpr int MAX_LEVELS = 16;  // parallel level launches per generation (the rest: the tail)
+// o_ctl words: [0, C) list lengths of levels 0..C-1, [C] tail length, [C+1] max level,
+// [C+2] error bits (1: dependency chain deeper than MAXD)
+constexpr int CTL_WORDS = MAX_LEVELS + 3;
+
+SRNN_HD int32_t code_A(int64_t j) { return (int32_t)(2 * j); }
+SRNN_HD int32_t code_E(int64_t j) { return (int32_t)(2 * j + 1); }
+SRNN_HD int32_t code_G(int64_t r) { return (int32_t)(-(r + 1)); }
+SRNN_HD int64_t producer(int32_t c) { return c >= 0 ? (int64_t)(c >> 1) : -1; }
+
+// the last attacker j < k of row r this generation (-1: none); the list is unordered
+SRNN_HD int64_t last_attacker_before(const SrnnArgs& a, int64_t r, int64_t k) {
+  int64_t best = -1;
+  for (uint32_t e = a.heads[r]; e != SRNN_NIL; e = a.nexts[e]) {
+    const int64_t j = (int64_t)e;
+    if (j < k && j > best) best = j;
+  }
+  return best;
+}
+// the version of row r that turn k reads (before any write of its own): the latest of
+// A(j) (time j, j an attacker of r) and E(r) (time r + 1/2) strictly before time k
+SRNN_HD int32_t latest(const SrnnArgs& a, int64_t r, int64_t k) {
+  const int64_t ja = last_attacker_before(a, r, k);
+  if (r < k && ja <= r) return code_E(r);
+  return ja >= 0 ? code_A(ja) : code_G(r);
+}
+
+template <class Net, class S>
+struct Ord {
+  using I = Item<Net, S>;
+  static constexpr int P = Net::P;
+
+  SRNN_HD static void read_version(const SrnnArgs& a, int32_t code, float* w) {
+    if (code >= 0) {
+      const int64_t j = code >> 1;
+      I::load((code & 1) ? I::rowp(a.W, j) : I::rowp(a.W3, j), w);
+    } else {
+      I::load(I::rowp(a.W2, (int64_t)(-(int64_t)code - 1)), w);
+    }
+  }
+
+  // src codes of turn k (generation gen) -> o_src[k] = {own, victim, teacher, level = -1}
+  SRNN_HD static void plan(const SrnnArgs& a, int64_t k, int32_t gen) {
+    int64_t at, te;
+    I::decision(a, k, gen, at, te);
+    int32_t* s = a.o_src + 4 * k;
+    s[0] = latest(a, k, k);
+    s[1] = (at >= 0 && at != k) ? latest(a, at, k) : SRC_NONE;
+    if (te < 0) s[2] = SRC_NONE;
+    else if (te == k) s[2] = SRC_SELF;
+    else if (te == at) s[2] = SRC_ATK;
+    else s[2] = latest(a, te, k);
+    s[3] = -1;
+  }
+
+  // turn k: the serial loop's particle step (soup_seq_one) reading the versions of its plan
+  SRNN_HD static void turn(const SrnnCfg& c, const SrnnArgs& a, int64_t k, int32_t gen, float4* samp, uint8_t* perm) {
+    const int32_t* s = a.o_src + 4 * k;
+    int64_t at, te;
+    I::decision(a, k, gen, at, te);
+    float w[P], f[P], o[P];
+    read_version(a, s[0], w);
+    int8_t act = A_NONE;
+    int64_t cp = -1;
+    if (at >= 0) {  // 1. attack: the victim's row becomes f_k(victim) (A(k))
+      if (at == k) I::copy(f, w);
+      else read_version(a, s[1], f);
+      Net::apply(w, f, o, I::actx(a, c, (uint64_t)k, (uint32_t)gen * 1024u + 1u, perm));
+      I::q(o);
+      I::store(I::rowp(a.W3, k), o);
+      if (at == k) I::copy(w, o);
+      act = A_ATTACKING;
+      cp = at;
+    }
+    TrainCtx tc;
+    tc.lr = a.lr;
+    tc.rng = I::rng(a);
+    tc.uid = (uint64_t)k;
+    tc.ctr = (uint32_t)gen * 1024u + 512u;
+    tc.samp = samp;
+    tc.perm = perm;
+    tc.shuffle = (a.flags & SRNN_F_SHUFFLE) != 0;
+    tc.stride = SAMP_STRIDE;
+    tc.aggregator = c.aggregator;
+    float loss = 0.f;
+    if (te >= 0) {  // 2. learn_from the teacher's current row
+      if (s[2] == SRC_SELF) I::copy(f, w);
+      else if (s[2] == SRC_ATK) I::copy(f, o);
+      else read_version(a, s[2], f);
+      if constexpr (Net::KIND == 0) {
+        if (a.severity > 0) loss = Net::template train_epochs<false>(w, f, a.severity, tc);
+      } else {
+        for (int e = 0; e < a.severity; ++e) loss = Net::train_epoch(w, f, tc);
+      }
+      act = A_LEARN_FROM;
+      cp = te;
+    }
+    if (a.epochs > 0) {  // 3. self-train
+      if constexpr (Net::KIND == 0) {
+        loss = Net::template train_epochs<true>(w, f, a.epochs, tc);
+      } else {
+        for (int e = 0; e < a.epochs; ++e) {
+          I::copy(f, w);
+          loss = Net::train_epoch(w, f, tc);
+        }
+      }
+      act = A_TRAIN_SELF;
+      cp = -1;
+    }
+    I::q(w);  // 4. respawn (the stored state decides; the zero test on the old particle)
+    int8_t rs = 0;
+    if ((a.flags & SRNN_F_REMOVE_DIVERGENT) && is_diverged<P>(w)) rs = 1;
+    else if ((a.flags & SRNN_F_REMOVE_ZERO) && is_zero<P>(w, a.eps)) rs = 2;
+    if (a.traj) I::store(I::rowp(a.traj, k), w);  // recording: the state before any respawn
+    if (rs) Net::init(w, I::rng(a), respawn_key(gen, k));
+    I::store(I::rowp(a.W, k), w);  // E(k)
+    if (a.action) a.action[k] = act;
+    if (a.counterpart) a.counterpart[k] = cp;
+    if (a.loss) a.loss[k] = loss;
+    if (a.respawn) a.respawn[k] = rs;
+  }
+
+  // row r after the generation: the last attack after its own turn, else E(r) (in W);
+  // consumes r's attack list.  w receives the final row as a reload would see it.
+  SRNN_HD static void close_row(const SrnnArgs& a, int64_t r, float* w) {
+    const int64_t ja = last_attacker_before(a, r, a.n);
+    a.heads[r] = SRNN_NIL;  // consumed: NIL for the generation after next
+    if (ja > r) {
+      I::load(I::rowp(a.W3, ja), w);
+      I::store(I::rowp(a.W, r), w);
+    } else {
+      I::load(I::rowp(a.W, r), w);
+    }
+  }
+};
+
+__device__ __forceinline__ int32_t ld_level(const int32_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+}  // namespace ord
+
+template <class Net, class S>
+__global__ __launch_bounds__(TB) void k_ord_plan(SrnnCfg, SrnnArgs a) {
+  const int64_t k = (int64_t)blockIdx.x * TB + threadIdx.x;
+  if (blockIdx.x == 0 && threadIdx.x < ord::CTL_WORDS) a.o_ctl[threadIdx.x] = 0;  // read from the next launch on
+  if (k < a.n) ord::Ord<Net, S>::plan(a, k, Item<Net, S>::gen_of(a));
+}
+
+// level of every turn (memoised DFS: a producer's level another lane already stored is
+// reused, a missing one is computed here -- both give the same value) + the level lists
+template <class Net, class S>
+__global__ __launch_bounds__(TB) void k_ord_levels(SrnnCfg, SrnnArgs a) {
+  const int64_t k = (int64_t)blockIdx.x * TB + threadIdx.x;
+  const int lane = threadIdx.x;
+  const int C = a.o_levels;
+  const bool valid = k < a.n;
+  int32_t lv = 0;
+  if (valid) {
+    int32_t* src = a.o_src;
+    int32_t stk[ord::MAXD];
+    int sp = 0;
+    stk[sp++] = (int32_t)k;
+    bool bad = false;
+    while (sp > 0) {
+      const int64_t j = stk[sp - 1];
+      if (ord::ld_level(src + 4 * j + 3) >= 0) {
+        --sp;
+        continue;
+      }
+      int32_t best = -1;
+      bool pushed = false;
+#pragma unroll
+      for (int q = 0; q < 3; ++q) {
+        const int64_t p = ord::producer(src[4 * j + q]);
+        if (p < 0 || pushed) continue;
+        const int32_t lp = ord::ld_level(src + 4 * p + 3);
+        if (lp < 0) {
+          if (sp == ord::MAXD) {
+            bad = true;
+            break;
+          }
+          stk[sp++] = (int32_t)p;
+          pushed = true;
+        } else {
+          best = lp > best ? lp : best;
+        }
+      }
+      if (bad) break;
+      if (!pushed) {
+        __hip_atomic_store(src + 4 * j + 3, best + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        --sp;
+      }
+    }
+    if (bad) {
+      atomicOr(a.o_ctl + C + 2, 1);
+      lv = 0;
+    } else {
+      lv = ord::ld_level(src + 4 * k + 3);
+    }
+  }
+  // append to the list of min(level, C): one atomic per (wave, list)
+  const int32_t L = lv < C ? lv : C;
+  unsigned long long rem = __ballot(valid);
+  while (rem) {
+    const int leader = __ffsll((long long)rem) - 1;
+    const int32_t Ll = __shfl(L, leader);
+    const unsigned long long m = __ballot(valid && L == Ll);
+    int32_t base = 0;
+    if (lane == leader) base = atomicAdd(a.o_ctl + Ll, (int32_t)__popcll(m));
+    base = __shfl(base, leader);
+    if (valid && L == Ll) a.o_list[(int64_t)Ll * a.n + base + __popcll(m & ((1ull << lane) - 1ull))] = (int32_t)k;
+    rem &= ~m;
+  }
+  int32_t mx = valid ? lv : 0;
+  for (int off = 32; off > 0; off >>= 1) {
+    const int32_t y = __shfl_xor(mx, off);
+    mx = y > mx ? y : mx;
+  }
+  if (lane == 0 && mx >= C) atomicMax(a.o_ctl + C + 1, mx);
+}
+
+// the turns of level L (grid-stride over its list)
+template <class Net, class S>
+__global__ __launch_bounds__(TB) void k_ord_level(SrnnCfg c, SrnnArgs a, int32_t L) {
+  using I = Item<Net, S>;
+  constexpr int SAMP = samp_slots<Net>();
+  constexpr int PERM = (Net::P + 4) & ~3;
+  __shared__ float4 s_samp[TB * SAMP];
+  __shared__ uint8_t s_perm[TB * PERM];
+  const int lane = threadIdx.x;
+  const int32_t gen = I::gen_of(a);
+  const int64_t cnt = *(volatile const int32_t*)(a.o_ctl + L);
+  const int32_t* list = a.o_list + (int64_t)L * a.n;
+  for (int64_t base = (int64_t)blockIdx.x * TB; base < cnt; base += (int64_t)gridDim.x * TB) {
+    const int64_t q = base + lane;
+    if (q < cnt)
+      ord::Ord<Net, S>::turn(c, a, list[q], gen, samp_lane<Net>(s_samp, lane), s_perm + lane * PERM);
+  }
+}
+
+// levels >= C: one wave, level by level; the versions a round writes are released before the
+// barrier and the wave's L1 is invalidated after it (rows share cache lines with rows
+// written by earlier rounds)
+template <class Net, class S>
+__global__ __launch_bounds__(TB) void k_ord_tail(SrnnCfg c, SrnnArgs a) {
+  using I = Item<Net, S>;
+  constexpr int SAMP = samp_slots<Net>();
+  constexpr int PERM = (Net::P + 4) & ~3;
+  __shared__ float4 s_samp[TB * SAMP];
+  __shared__ uint8_t s_perm[TB * PERM];
+  const int lane = threadIdx.x;
+  const int C = a.o_levels;
+  const int64_t cnt = *(volatile const int32_t*)(a.o_ctl + C);
+  if (cnt == 0) return;
+  const int32_t maxl = *(volatile const int32_t*)(a.o_ctl + C + 1);
+  const int32_t gen = I::gen_of(a);
+  const int32_t* list = a.o_list + (int64_t)C * a.n;
+  for (int32_t lv = C; lv <= maxl; ++lv) {
+    for (int64_t q = lane; q < cnt; q += TB) {
+      const int64_t k = list[q];
+      if (ord::ld_level(a.o_src + 4 * k + 3) == lv)
+        ord::Ord<Net, S>::turn(c, a, k, gen, samp_lane<Net>(s_samp, lane), s_perm + lane * PERM);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    __syncthreads();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  }
+}
+
+// final rows, census, next decisions, block stats (the fused generation's two-phase form:
+// k_gen_finish / the batched finish number the newborns afterwards)
+template <class Net, class S>
+__global__ __launch_bounds__(TB) void k_ord_close(SrnnCfg c, SrnnArgs a) {
+  using I = Item<Net, S>;
+  constexpr int PERM = (Net::P + 4) & ~3;
+  __shared__ uint8_t s_perm[TB * PERM];
+  const int64_t gb = blockIdx.x;
+  const int64_t r = gb * TB + threadIdx.x;
+  const int lane = threadIdx.x;
+  uint8_t* perm = s_perm + lane * PERM;
+  const int32_t gen = I::gen_of(a);
+  const bool census = (a.flags & SRNN_F_FUSED_CENSUS) != 0;
+  bool rs = false;
+  int8_t k = -1;
+  if (r < a.n) {
+    float w[Net::P];
+    ord::Ord<Net, S>::close_row(a, r, w);
+    rs = a.respawn[r] != 0;
+    int64_t at, te;
+    I::decision(a, r, gen + 1, at, te);
+    if (at >= 0) I::link(a.heads_next, a.nexts_next, at, (uint32_t)r);
+    if (census)
+      k = I::classify_w(w, a.eps, (a.flags & SRNN_F_FIX_SEC) != 0, I::actx(a, c, (uint64_t)r, 0x7FFFFFF0u, perm));
+  }
+  if ((a.flags & SRNN_F_GEN_COUNTS) && gb == 0 && lane == 0) I::set_gen(a, gen + 1);
+  const unsigned long long m = __ballot(rs);
+  uint32_t cnt[5];
+#pragma unroll
+  for (int q = 0; q < 5; ++q) cnt[q] = (uint32_t)__popcll(__ballot(k == q));
+  if (lane == 0) {
+    unsigned long long* bs = reinterpret_cast<unsigned long long*>(a.temp);
+    unsigned long long* mine = bs + gb * 4;
+    mine[0] = m;
+    mine[1] = (unsigned long long)cnt[0] | ((unsigned long long)cnt[1] << 32);
+    mine[2] = (unsigned long long)cnt[2] | ((unsigned long long)cnt[3] << 32);
+    mine[3] = (unsigned long long)cnt[4];
+    if ((a.flags & SRNN_F_BORN_TOTAL) && m) atomicAdd(bs + ((a.n + TB - 1) / TB) * 4, (unsigned long long)__popcll(m));
+  }
+}
+
+// OP_SOUP_ORDERED: one sequential (reference-order) generation of a single-rank table.
+// W2: generation-start rows, W: the generation's rows (E versions, then the final table),
+// W3: attack outputs, o_src [n][4], o_list [(C+1) n], o_ctl [CTL_WORDS], o_levels = C;
+// heads / nexts: this generation's attack lists (consumed), heads_next / nexts_next: the
+// next generation's (linked here).  Device: the block stats of the two-phase fused
+// generation in temp (SRNN_F_TWO_PHASE); host: the finish inline (uids, census, counter).
+template <class Net, class S>
+int soup_ordered(const SrnnCfg& c, const SrnnArgs& a) {
+  using I = Item<Net, S>;
+  using O = ord::Ord<Net, S>;
+  if (a.world > 1 || a.lo != 0 || a.n_total != a.n || a.n >= (int64_t)(1 << 30)) {
+    set_error("ordered soup generation: one unsharded table of < 2^30 rows");
+    return -5;
+  }
+  if (!a.W || !a.W2 || !a.W3 || !a.o_src || !a.o_list || !a.o_ctl || !a.heads || !a.nexts || !a.heads_next ||
+      !a.nexts_next || !a.respawn || a.o_levels < 1 || a.o_levels > ord::MAX_LEVELS) {
+    set_error("ordered soup generation needs W, W2, W3, o_src, o_list, o_ctl, both attack lists, respawn and "
+              "1 <= o_levels <= 16");
+    return -5;
+  }
+  const int32_t C = a.o_levels;
+  if (!a.dev) {
+    const int32_t gen = I::gen_of(a);
+    for (int w = 0; w < ord::CTL_WORDS; ++w) a.o_ctl[w] = 0;
+    host_parallel(a.n, [&](int64_t k) { O::plan(a, k, gen); });
+    // levels in index order (every producer precedes its consumer)
+    std::vector<std::vector<int64_t>> lists((size_t)C + 1);
+    int32_t maxl = 0;
+    for (int64_t k = 0; k < a.n; ++k) {
+      int32_t* s = a.o_src + 4 * k;
+      int32_t lv = 0;
+      for (int q = 0; q < 3; ++q) {
+        const int64_t p = ord::producer(s[q]);
+        if (p >= 0) lv = std::max(lv, a.o_src[4 * p + 3] + 1);
+      }
+      s[3] = lv;
+      maxl = std::max(maxl, lv);
+      lists[(size_t)std::min(lv, C)].push_back(k);
+    }
+    for (int32_t L = 0; L <= C; ++L) a.o_ctl[L] = (int32_t)lists[(size_t)L].size();
+    a.o_ctl[C + 1] = maxl;
+    auto run_turn = [&](int64_t k) {
+      float4 samp[Net::P + 1];
+      uint8_t perm[Net::P + 4];
+      O::turn(c, a, k, gen, samp, perm);
+    };
+    for (int32_t L = 0; L < C; ++L) {
+      const auto& li = lists[(size_t)L];
+      host_parallel((int64_t)li.size(), [&](int64_t q) { run_turn(li[(size_t)q]); });
+    }
+    for (int32_t L = C; L <= maxl; ++L) {  // the tail, level by level
+      std::vector<int64_t> li;
+      for (int64_t k : lists[(size_t)C])
+        if (a.o_src[4 * k + 3] == L) li.push_back(k);
+      host_parallel((int64_t)li.size(), [&](int64_t q) { run_turn(li[(size_t)q]); });
+    }
+    std::vector<int8_t> ks((size_t)a.n, (int8_t)-1);
+    const bool census = (a.flags & SRNN_F_FUSED_CENSUS) != 0;
+    host_parallel(a.n, [&](int64_t r) {
+      float w[Net::P];
+      uint8_t perm[Net::P + 4];
+      O::close_row(a, r, w);
+      if (census)
+        ks[(size_t)r] = I::classify_w(w, a.eps, (a.flags & SRNN_F_FIX_SEC) != 0,
+                                      I::actx(a, c, (uint64_t)r, 0x7FFFFFF0u, perm));
+    });
+    for (int64_t r = 0; r < a.n; ++r) {
+      int64_t at, te;
+      I::decision(a, r, gen + 1, at, te);
+      if (at >= 0) {
+        a.nexts_next[r] = a.heads_next[at];
+        a.heads_next[at] = (uint32_t)r;
+      }
+    }
+    uint64_t cs[5] = {0, 0, 0, 0, 0};
+    for (int64_t r = 0; r < a.n; ++r)
+      if (ks[(size_t)r] >= 0) cs[ks[(size_t)r]]++;
+    int64_t u = a.uid_base ? a.uid_base[0] : 0, total = 0;
+    for (int64_t r = 0; r < a.n; ++r)
+      if (a.respawn[r]) {
+        if (a.uid_out) a.uid_out[r] = u;
+        ++u;
+        ++total;
+      }
+    if (a.uid_base) a.uid_base[0] = u;
+    I::set_gen(a, gen + 1);
+    if (a.counts) {
+      for (int q = 0; q < 5; ++q) a.counts[q] = census ? cs[q] : 0;
+      a.counts[5] = (uint64_t)total;
+    }
+    return 0;
+  }
+  if (!(a.flags & SRNN_F_TWO_PHASE) || !a.temp) {
+    set_error("device ordered soup generation: two-phase block stats (temp) needed");
+    return -5;
+  }
+  const int64_t nb = (a.n + TB - 1) / TB;
+  if (nb <= 0) return 0;
+  hipStream_t st = (hipStream_t)a.stream;
+  hipLaunchKernelGGL((k_ord_plan<Net, S>), dim3((unsigned)nb), dim3(TB), 0, st, c, a);
+  hipLaunchKernelGGL((k_ord_levels<Net, S>), dim3((unsigned)nb), dim3(TB), 0, st, c, a);
+  for (int32_t L = 0; L < C; ++L) {
+    // level L holds ~n / 7^L turns at the reference's rates: a grid that covers it in one
+    // pass, grid-stride beyond (any count is processed)
+    int64_t blocks = L == 0 ? nb : std::max<int64_t>(64, nb >> (2 * L));
+    blocks = std::min(blocks, nb);
+    hipLaunchKernelGGL((k_ord_level<Net, S>), dim3((unsigned)blocks), dim3(TB), 0, st, c, a, L);
+  }
+  hipLaunchKernelGGL((k_ord_tail<Net, S>), dim3(1), dim3(TB), 0, st, c, a);
+  hipLaunchKernelGGL((k_ord_close<Net, S>), dim3((unsigned)nb), dim3(TB), 0, st, c, a);
+  if (!(a.flags & SRNN_F_GEN_COUNTS)) {
+    constexpr int FNT = SRNN_FINISH_NT;
+    hipLaunchKernelGGL((k_gen_finish<Net, S, FNT>), dim3(1), dim3(FNT), 0, st, a, (int32_t)nb);
+  }
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) {
+    set_error(hipGetErrorString(e));
+    return -3;
+  }
+  return 0;
+}

@@ -49,9 +49,6 @@ __global__ __launch_bounds__(XT) void k_x2_pack(SrnnCfg c, SrnnArgs a) {
   __shared__ int32_t s_last;
   __shared__ int32_t s_hw[XT / 64];
   if ((int64_t)blockIdx.x < a.x_groups) {
-#ifdef SRNN_EXP_NOFINISH
-    return;  // timing experiment only (wrong results)
-#endif
     // ---- finish of generation t-1: this workgroup's blocks -> partial (born, census)
     int64_t b0, b1;
     wg_range(a, blockIdx.x, b0, b1);
@@ -130,9 +127,6 @@ __global__ __launch_bounds__(XT) void k_x2_pack(SrnnCfg c, SrnnArgs a) {
   if ((int64_t)blockIdx.x < a.x_groups + nd) {
     // ---- decisions of the next generation (PRIME: of this one) for the local slots
     const int64_t i = ((int64_t)blockIdx.x - a.x_groups) * XT + threadIdx.x;
-#ifdef SRNN_EXP_NODECIDE
-    return;  // timing experiment only (wrong results)
-#endif
     __shared__ int32_t s_res[XT / 64 + 1];
     pack_decide_block(a, G, i, i < a.n, prime ? gen : gen + 1, s_res);
     return;

@@ -11,7 +11,8 @@ from __future__ import annotations
 
 import dataclasses
 import json
-from typing import Any, Dict, Optional
+import os
+from typing import Any, Dict, Optional, Tuple
 
 from .arch import ArchSpec
 
@@ -61,6 +62,112 @@ class RecorderConfig:
         return self
 
 
+def _env_bool(name: str, default: bool) -> bool:
+    v = os.environ.get(name)
+    return default if v is None or v == "" else v not in ("0", "false", "False", "no")
+
+
+@dataclasses.dataclass(frozen=True)
+class ExecConfig:
+    """Execution knobs: which schedule / kernel family runs, never what is computed (every
+    choice gives bitwise the same soup).  Each field has an environment variable that, when
+    set, overrides it (A/B runs on the GPU box); ``resolved()`` applies those overrides and
+    is what the engines use and what bench.py prints.
+
+    Engine-level (``SoupEngine``): ``finish_mode``, ``finish_par``, ``graph_chunks``,
+    ``x2_schedule``, ``x2_prio``, ``x2_emulate_remote``, ``sharded_graph``; process-level
+    (``Dist``): ``native_comm``, ``loopback``; library-level (libsrnn knobs, process wide,
+    ``apply_library()``): ``force_generic`` ... ``soup_lanes`` (None: the library's default)."""
+    finish_mode: str = "batch"              # SRNN_FINISH_MODE: batch | serial (single-rank generation finish)
+    finish_par: bool = True                 # SRNN_FINISH_PAR: one finish workgroup per batched generation
+    graph_chunks: Tuple[int, ...] = (20, 16, 8, 4, 2)  # SRNN_GRAPH_CHUNKS: generations per multi-generation graph
+    x2_schedule: str = "serial"             # SRNN_X2_SCHEDULE: serial | overlap (sharded generation)
+    x2_prio: bool = True                    # SRNN_X2_PRIO: raised wave priority of the exchange chain
+    x2_emulate_remote: float = 0.0          # SRNN_X2_EMULATE_REMOTE: one-rank timing model of R ranks
+    sharded_graph: bool = True              # SRNN_SHARDED_GRAPH: capture sharded generations (RCCL inside)
+    native_comm: bool = True                # SRNN_NATIVE_COMM: the soup's own RCCL communicator
+    loopback: bool = False                  # SRNN_LOOPBACK: one-rank all-to-all as a device copy
+    force_generic: Optional[bool] = None    # SRNN_FORCE_GENERIC
+    ww_wave: Optional[bool] = None          # SRNN_WW_WAVE
+    rnn_wave: Optional[bool] = None         # SRNN_RNN_WAVE
+    rnn_spec: Optional[bool] = None         # SRNN_RNN_SPEC
+    rnn_soup: Optional[bool] = None         # SRNN_RNN_SOUP
+    big_wave: Optional[bool] = None         # SRNN_BIG_WAVE
+    fix_group: Optional[bool] = None        # SRNN_FIX_GROUP (None: by population size)
+    soup_lanes: Optional[int] = None        # SRNN_SOUP_LANES (None / 0: by population size)
+    order_levels: int = 4                   # SRNN_ORDER_LEVELS: parallel level launches of a reference-order
+                                            # generation (deeper levels run in its one-wave tail)
+
+    _ENV = dict(finish_mode="SRNN_FINISH_MODE", finish_par="SRNN_FINISH_PAR", graph_chunks="SRNN_GRAPH_CHUNKS",
+                x2_schedule="SRNN_X2_SCHEDULE", x2_prio="SRNN_X2_PRIO", x2_emulate_remote="SRNN_X2_EMULATE_REMOTE",
+                sharded_graph="SRNN_SHARDED_GRAPH", native_comm="SRNN_NATIVE_COMM", loopback="SRNN_LOOPBACK",
+                force_generic="SRNN_FORCE_GENERIC", ww_wave="SRNN_WW_WAVE", rnn_wave="SRNN_RNN_WAVE",
+                rnn_spec="SRNN_RNN_SPEC", rnn_soup="SRNN_RNN_SOUP", big_wave="SRNN_BIG_WAVE",
+                fix_group="SRNN_FIX_GROUP", soup_lanes="SRNN_SOUP_LANES", order_levels="SRNN_ORDER_LEVELS")
+    LIBRARY_KNOBS = ("force_generic", "ww_wave", "rnn_wave", "rnn_spec", "rnn_soup", "big_wave", "fix_group",
+                     "soup_lanes")
+
+    def validate(self):
+        if self.finish_mode not in ("batch", "serial"):
+            raise ValueError("finish_mode must be batch or serial")
+        if self.x2_schedule not in ("serial", "overlap"):
+            raise ValueError("x2_schedule must be serial or overlap")
+        if any(int(g) < 2 or int(g) % 2 for g in self.graph_chunks):
+            raise ValueError("graph_chunks must be even sizes >= 2")
+        if not 0.0 <= self.x2_emulate_remote <= 1.0:
+            raise ValueError("x2_emulate_remote is a fraction in [0, 1]")
+        if not 1 <= int(self.order_levels) <= 16:
+            raise ValueError("order_levels must be in 1..16")
+        return self
+
+    def resolved(self) -> "ExecConfig":
+        """This config with every knob whose environment variable is set overridden by it."""
+        kw = {}
+        for f in dataclasses.fields(self):
+            env = self._ENV.get(f.name)
+            v = os.environ.get(env) if env else None
+            if v is None or v == "":
+                continue
+            cur = getattr(self, f.name)
+            if f.name == "graph_chunks":
+                kw[f.name] = tuple(sorted({int(x) for x in v.split(",") if int(x) >= 2 and int(x) % 2 == 0},
+                                          reverse=True))
+            elif f.name in ("finish_mode", "x2_schedule"):
+                kw[f.name] = v
+            elif f.name == "x2_emulate_remote":
+                kw[f.name] = float(v)
+            elif f.name in ("soup_lanes", "order_levels"):
+                kw[f.name] = int(v)
+            else:
+                kw[f.name] = _env_bool(env, bool(cur))
+        return dataclasses.replace(self, **kw).validate() if kw else self.validate()
+
+    def apply_library(self) -> None:
+        """Push the library-level knobs that are set (not None) into libsrnn (process wide;
+        their environment variables still override inside the library)."""
+        from .ops import _lib
+        for name in self.LIBRARY_KNOBS:
+            v = getattr(self, name)
+            if v is not None:
+                _lib.set_knob(name, int(v))
+
+    def as_dict(self) -> Dict[str, Any]:
+        d = {f.name: getattr(self, f.name) for f in dataclasses.fields(self)}
+        d["graph_chunks"] = list(self.graph_chunks)
+        return d
+
+    def in_force(self) -> Dict[str, Any]:
+        """The resolved knobs plus the library knobs' values in force (env included; -1 =
+        the library's built-in default): what a benchmark line records."""
+        d = self.resolved().as_dict()
+        try:
+            from .ops import _lib
+            d["library"] = {k: _lib.get_knob(k) for k in self.LIBRARY_KNOBS}
+        except Exception:  # noqa: BLE001 -- no library: nothing to report
+            pass
+        return d
+
+
 @dataclasses.dataclass(frozen=True)
 class RunConfig:
     """How a soup runs: population, precision, parallelism, I/O."""
@@ -81,6 +188,7 @@ class RunConfig:
     checkpoint_every: int = 0
     collective_timeout_s: float = 600.0    # process-group timeout (failure detection)
     recorder: RecorderConfig = RecorderConfig()
+    execution: ExecConfig = ExecConfig()   # schedules / kernel families (env vars override)
 
     def validate(self):
         if self.n_total < 1 or self.generations < 0:
@@ -95,6 +203,7 @@ class RunConfig:
             # the census is fused into the generation kernel: on (every generation) or off
             raise ValueError("census_every must be 0 (final census only) or 1 (every generation)")
         self.recorder.validate()
+        self.execution.validate()
         return self
 
     def torch_dtype(self):
@@ -115,8 +224,9 @@ class ExperimentConfig:
         return self
 
     def to_dict(self) -> Dict[str, Any]:
-        return dict(arch=json.loads(self.arch.to_json()), soup=dataclasses.asdict(self.soup),
-                    run=dataclasses.asdict(self.run))
+        run = dataclasses.asdict(self.run)
+        run["execution"] = self.run.execution.as_dict()
+        return dict(arch=json.loads(self.arch.to_json()), soup=dataclasses.asdict(self.soup), run=run)
 
     def to_json(self) -> str:
         return json.dumps(self.to_dict(), indent=1, sort_keys=True)
@@ -126,8 +236,13 @@ class ExperimentConfig:
         run = dict(d.get("run", {}))
         run.pop("reference_compat", None)  # accepted from round-1 config files; quirks live in the compat API
         rec = RecorderConfig(**run.pop("recorder", {}))
+        ex = dict(run.pop("execution", {}))
+        if "graph_chunks" in ex:
+            ex["graph_chunks"] = tuple(ex["graph_chunks"])
+        ex = ExecConfig(**ex)
         return ExperimentConfig(arch=ArchSpec.from_json(json.dumps(d["arch"])) if "arch" in d else ArchSpec.weightwise(2, 2),
-                                soup=SoupConfig(**d.get("soup", {})), run=RunConfig(recorder=rec, **run)).validate()
+                                soup=SoupConfig(**d.get("soup", {})),
+                                run=RunConfig(recorder=rec, execution=ex, **run)).validate()
 
     @staticmethod
     def from_json(s: str) -> "ExperimentConfig":

@@ -20,7 +20,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 # SRNN_LIB: load another build of the library (A/B of compiler flags on the GPU box)
 LIB_PATH = os.environ.get("SRNN_LIB") or os.path.join(_HERE, "libsrnn.so")
 CSRC = os.path.normpath(os.path.join(_HERE, "..", "..", "csrc"))
-ABI_VERSION = 18
+ABI_VERSION = 19
 
 # SrnnOp (csrc/srnn_abi.h)
 OP_INIT = 0
@@ -41,6 +41,8 @@ OP_GEN_FINISH = 17
 OP_SOUP_SEQ = 19  # sequential (Gauss-Seidel) soup generations
 OP_X2_PACK = 20   # sharded soup, all-to-all exchange: finish + next decisions + rows (csrc/srnn_shard.hip)
 OP_X2_POST = 21   # sharded soup: uids, census, received notices / requests
+OP_SOUP_ORDERED = 22  # reference-order (sequential) generation, level-scheduled (csrc/srnn_ordered.h)
+ORD_CTL_WORDS = 19    # o_ctl words of an ordered generation
 
 # SrnnFlag bits (csrc/srnn_abi.h: one meaning each)
 FLAG_SHUFFLE = 1 << 0
@@ -108,6 +110,8 @@ class SrnnArgs(ctypes.Structure):
         ("temp", _P), ("temp_bytes", _I64),
         ("dev", _I32), ("pad1", _I32), ("stream", _P),
         ("scratch", _P), ("scratch_bytes", _I64),
+        # ordered (reference-order) generation
+        ("W3", _P), ("o_src", _P), ("o_list", _P), ("o_ctl", _P), ("o_levels", _I32), ("pad3", _I32),
     ]
 
 
@@ -171,10 +175,13 @@ def lib():
                            ("srnn_comm_destroy", [vp, ctypes.c_int]), ("srnn_comm_async_error", [vp]),
                            ("srnn_comm_all_to_all", [vp, vp, vp, i64, vp]),
                            ("srnn_comm_all_gather", [vp, vp, vp, i64, vp]),
-                           ("srnn_comm_all_reduce_i64", [vp, vp, vp, i64, vp])):
+                           ("srnn_comm_all_reduce_i64", [vp, vp, vp, i64, vp]),
+                           ("srnn_comm_count", [vp]), ("srnn_comm_user_rank", [vp]),
+                           ("srnn_set_knob", [ctypes.c_int, ctypes.c_int]), ("srnn_get_knob", [ctypes.c_int])):
             f = getattr(L, name)
             f.argtypes = args
             f.restype = ctypes.c_int
+        L.srnn_set_knob.restype = None
         L.srnn_comm_library.restype = ctypes.c_char_p
         L.srnn_storage_encode.argtypes = [vp, vp, i64, ctypes.c_int, vp]
         L.srnn_storage_encode.restype = ctypes.c_int
@@ -212,6 +219,25 @@ def supports(spec, op: int, device: bool, dtype: int = DTYPE_FP32) -> bool:
     """True when ``op`` of this architecture has a native implementation on the device
     (``device=True``) or on the host."""
     return bool(lib().srnn_supports(ctypes.byref(make_cfg(spec, dtype)), int(op), 1 if device else 0))
+
+
+# execution knobs (csrc/srnn_abi.h SrnnKnob; config.py ExecConfig): the environment variable
+# of a knob, when set, overrides what is set here
+KNOBS = {"force_generic": 0, "rnn_wave": 1, "rnn_spec": 2, "rnn_soup": 3, "ww_wave": 4, "big_wave": 5,
+         "fix_group": 6, "soup_lanes": 7}
+KNOB_ENV = {"force_generic": "SRNN_FORCE_GENERIC", "rnn_wave": "SRNN_RNN_WAVE", "rnn_spec": "SRNN_RNN_SPEC",
+            "rnn_soup": "SRNN_RNN_SOUP", "ww_wave": "SRNN_WW_WAVE", "big_wave": "SRNN_BIG_WAVE",
+            "fix_group": "SRNN_FIX_GROUP", "soup_lanes": "SRNN_SOUP_LANES"}
+
+
+def set_knob(name: str, value: int) -> None:
+    """Set a library execution knob (-1: back to the built-in default)."""
+    lib().srnn_set_knob(KNOBS[name], int(value))
+
+
+def get_knob(name: str) -> int:
+    """The knob's value in force (environment override included); -1 = built-in default."""
+    return int(lib().srnn_get_knob(KNOBS[name]))
 
 
 def set_force_generic(on: bool) -> None:

@@ -3,11 +3,19 @@
 The reference is single-process; here a population of ``n_total`` particles
 is sharded contiguously over the ranks of a ``torch.distributed`` group.  On ROCm the
 ``"nccl"`` backend is RCCL, whose collectives run over the xGMI links of an MI355X node;
-CPU tests use ``"gloo"``.  Only three collective shapes are needed:
+CPU tests use ``"gloo"``.  The collective shapes:
 
-* all-gather of weight rows (cross-shard attacks / learn_from partners),
-* all-reduce of int64 class histograms (fixpoint-fraction statistics),
-* all-gather of per-rank respawn counts (globally sequential uids).
+* all-to-all of fixed-size exchange blocks (``all_to_all``): the row path of a sharded soup
+  (``SoupEngine(exchange="alltoall")``, the default): each rank ships only the rows its
+  peers' attacks and learn_from requests need, plus notices / requests / stats headers;
+* all-gather of weight rows (``all_gather_rows``): the optional ``exchange="allgather"``
+  soup (every rank holds the whole table) and the trajectory / uid gathers;
+* all-reduce of int64 class histograms (fixpoint-fraction statistics) and all-gather of
+  per-rank stats (globally sequential uids).
+
+The device collectives go through the soup's own RCCL communicator (``NativeComm``,
+csrc/srnn_comm.cpp) so they can be captured in hipGraphs; torch.distributed carries the
+rendezvous and the CPU (gloo) rehearsals.
 """
 from __future__ import annotations
 
@@ -58,6 +66,16 @@ class NativeComm:
         self.comm = h
         self.library = self.L.srnn_comm_library().decode()
 
+    @property
+    def nranks(self) -> int:
+        """Ranks of the communicator as RCCL reports them (ncclCommCount; -1 if unavailable)."""
+        return int(self.L.srnn_comm_count(self.comm)) if self.comm else -1
+
+    @property
+    def comm_rank(self) -> int:
+        """This process's rank in the communicator (ncclCommUserRank; -1 if unavailable)."""
+        return int(self.L.srnn_comm_user_rank(self.comm)) if self.comm else -1
+
     def _stream(self):
         return self._ct.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
 
@@ -106,7 +124,13 @@ class Dist:
     # multi-GPU generation -- and its hipGraph capture with RCCL -- on a one-GPU box
     force: bool = False
     native: Optional[NativeComm] = None   # own RCCL communicator (device collectives)
+    # ExecConfig (native_comm, loopback); None: the defaults, environment variables override
+    execution: Optional[object] = None
     _pad_bufs: dict = dataclasses.field(default_factory=dict, repr=False)
+
+    def _exec(self):
+        from ..config import ExecConfig
+        return (self.execution or ExecConfig()).resolved()
 
     def enable_native_comm(self, device) -> bool:
         """Create the soup's own RCCL communicator on ``device`` (collective over all
@@ -114,7 +138,7 @@ class Dist:
         if self.native is not None:
             return True
         device = torch.device(device)
-        if (not self.enabled or device.type != "cuda" or os.environ.get("SRNN_NATIVE_COMM", "1") != "1"
+        if (not self.enabled or device.type != "cuda" or not self._exec().native_comm
                 or dist.get_backend(self.group) != "nccl"):
             return False
         try:
@@ -184,9 +208,9 @@ class Dist:
 
     def all_to_all(self, out: torch.Tensor, inp: torch.Tensor):
         """Equal-split all-to-all (RCCL over xGMI for nccl: direct peer links).  One rank with
-        SRNN_LOOPBACK=1: a device copy instead of the collective (rehearsal timing without
+        ExecConfig.loopback: a device copy instead of the collective (rehearsal timing without
         RCCL's own latency)."""
-        if self.world == 1 and os.environ.get("SRNN_LOOPBACK") == "1":
+        if self.world == 1 and self._exec().loopback:
             out.copy_(inp)
             return out
         if self._use_native(out, inp):

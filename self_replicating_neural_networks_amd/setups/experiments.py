@@ -21,7 +21,9 @@ from ..arch import ArchSpec
 from ..experiment import Experiment, FixpointExperiment, SoupExperiment
 from ..models import network as N
 from ..oracle.core import CLASS_NAMES
+from ..ops import _lib
 from ..population import Population, counts_dict
+from ..seq_soup import SequentialSoupEngine
 from ..soup import Soup
 from ..soup_engine import SoupEngine
 from ..utils import rng as _rng
@@ -160,9 +162,20 @@ def known_fixpoint_variation(depth=10, trials=100, max_steps=100, epsilon=1e-4, 
 
 
 # ------------------------------------------------------------------------------ soups
-def _soup_census(spec, trials, soup_size, soup_life, params, device, seed, with_sec=False):
-    """``trials`` independent soups as sub-soups (segments) of one engine."""
-    eng = SoupEngine(spec, trials * soup_size, dict(params, segment=soup_size), device=device, seed=seed)
+def _soup_census(spec, trials, soup_size, soup_life, params, device, seed, with_sec=False, order="sequential"):
+    """``trials`` independent soups as sub-soups (segments) of one engine, in the reference's
+    order by default (``order="sequential"``: each sub-soup evolves particle by particle, in
+    place -- code/soup.py:51-87 -- on the level-scheduled device generation, or on the host
+    loop for shapes without one); ``order="synchronous"`` runs the Jacobi generation."""
+    params = dict(params, segment=soup_size)
+    if order == "sequential":
+        dev_side = torch.device(device).type != "cpu"
+        if _lib.supports(spec, _lib.OP_SOUP_ORDERED, dev_side):
+            eng = SoupEngine(spec, trials * soup_size, params, device=device, seed=seed, order="sequential")
+        else:
+            eng = SequentialSoupEngine(spec, trials * soup_size, params, seed=seed)
+    else:
+        eng = SoupEngine(spec, trials * soup_size, params, device=device, seed=seed)
     eng.evolve(soup_life)
     return eng.count(with_sec=with_sec)
 

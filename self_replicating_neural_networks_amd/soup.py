@@ -8,14 +8,20 @@
 * ``mode="native"`` — the sequential algorithm on a weight table in one native call per
   ``evolve`` (``seq_soup.SequentialSoupEngine``, any size; slot-keyed Philox streams instead
   of the process-wide ``prng``; trajectory states recorded like the other modes).
-* ``mode="device"`` — the population lives in a device weight table and every
-  generation is one fused kernel pipeline (``SoupEngine``), optionally sharded over the
-  ranks of a process group.  Within a generation all reads come from the
-  generation-start weights (synchronous update); population-level statistics match the
-  sequential mode and the published curves (tests/test_soup_statistics.py: learn_from
-  severities, Mann-Whitney U device vs sequential; trajectory-soup census 13/7).
+* ``mode="ordered"`` — the sequential algorithm on a device weight table
+  (``SoupEngine(order="sequential")``): every generation's dependency DAG is scheduled by
+  level, bitwise the serial loop of ``native`` (csrc/srnn_ordered.h), any size, single rank,
+  the lane-template shapes.
+* ``mode="device"`` — the SYNCHRONOUS (Jacobi) generation (``SoupEngine``): every read of a
+  generation comes from the generation-start weights, so a particle attacked after its own
+  turn is trained before the census instead of ending the generation untrained; optionally
+  sharded over the ranks of a process group.  Its statistics differ measurably from the
+  reference order at large sizes (tests/test_ordered_soup.py); choose it explicitly.
 
-``mode="auto"`` picks sequential for ``size <= 100`` and device otherwise.
+``mode="auto"`` keeps the reference order: ``sequential`` for ``size <= 100``, ``ordered``
+above (``native`` for shapes without a device ordered generation).  A soup sharded over a
+process group (``dist``) has no reference-order generation: ``auto`` refuses it, pass
+``mode="device"`` to ask for the synchronous one.
 """
 from __future__ import annotations
 
@@ -49,11 +55,14 @@ class Soup(object):
         self.params.update(kwargs)
         self.time = 0
         if mode == "auto":
-            mode = "sequential" if size <= 100 and dist is None else "device"
-        if mode not in ("sequential", "native", "device"):
-            raise ValueError("mode must be 'sequential', 'native', 'device' or 'auto'")
-        if mode == "native" and dist is not None:
-            raise ValueError("native sequential soups are single-process (their order is serial)")
+            if dist is not None:
+                raise ValueError("Soup(mode='auto') keeps the reference's sequential order, which has no sharded "
+                                 "form; pass mode='device' for the synchronous (Jacobi) sharded soup")
+            mode = "sequential" if size <= 100 else "ordered"
+        if mode not in ("sequential", "native", "ordered", "device"):
+            raise ValueError("mode must be 'sequential', 'native', 'ordered', 'device' or 'auto'")
+        if mode in ("native", "ordered") and dist is not None:
+            raise ValueError("sequential-order soups are single-process (their order is serial)")
         self.mode = mode
         self.device = device
         self.seed_value = seed
@@ -131,7 +140,7 @@ class Soup(object):
         return self
 
     def count(self):
-        if self.mode in ("device", "native"):
+        if self.mode in ("device", "native", "ordered"):
             if self.engine is None:
                 self._seed_device()
             return self.engine.count()
@@ -224,7 +233,15 @@ class Soup(object):
         if device is None:
             device = "cuda" if torch.cuda.is_available() else "cpu"
         seed = self.seed_value if self.seed_value is not None else _rng.get_seed() ^ ParticleDecorator.next_uid
-        self.engine = SoupEngine(spec, self.size, params, device=device, seed=seed, lr=lr, dist=self.dist)
+        if self.mode == "ordered":
+            from .ops import _lib
+            if not _lib.supports(spec, _lib.OP_SOUP_ORDERED, torch.device(device).type != "cpu"):
+                # no level-scheduled generation for this shape: the same order on the host loop
+                self.mode = "native"
+                return self._seed_device()
+            self.engine = SoupEngine(spec, self.size, params, device=device, seed=seed, lr=lr, order="sequential")
+        else:
+            self.engine = SoupEngine(spec, self.size, params, device=device, seed=seed, lr=lr, dist=self.dist)
         # global uids continue the process-wide particle counter (reference S13)
         base = ParticleDecorator.next_uid
         self.engine.uid.add_(base)
@@ -268,10 +285,15 @@ class StateRecorder:
                 self.states_of(uid).append({"class": self.class_name, "weights": w.copy(), "time": time,
                                             "action": "init", "counterpart": None})
 
-    def on_evolved(self, eng):
-        uid_slots = eng.uid.clone()
-        self._snap = (eng.rows_out[:, : eng.spec.P].clone(), eng.action.clone(), eng.counterpart.clone(),
+    def on_evolved(self, eng, rows=None, old_uid=None, ordered: bool = False):
+        """Snapshot of a generation's per-particle records.  ``rows``: the pre-respawn states
+        (default: the engine's output table before its respawn pass); ``ordered``: a
+        reference-order generation, whose counterparts are read as of each particle's turn."""
+        uid_slots = (old_uid if old_uid is not None else eng.uid).clone()
+        rows = eng.rows_out if rows is None else rows
+        self._snap = (rows[:, : eng.spec.P].clone(), eng.action.clone(), eng.counterpart.clone(),
                       eng.loss.clone(), eng.respawn.clone(), uid_slots)
+        self._ordered = ordered
 
     def on_sequential_generation(self, eng, time, old_uid):
         """After one generation of a ``SequentialSoupEngine`` (its counterparts are uids)."""
@@ -282,6 +304,8 @@ class StateRecorder:
         """``uid_of_slot`` maps counterpart slots to uids (None: counterparts are uids)."""
         W, act, cp, loss, resp, old_uid = (t.cpu().numpy() for t in self._snap)
         new_uid = eng.uid.cpu().numpy()
+        ordered = getattr(self, "_ordered", False)
+        self._ordered = False
         train = int(eng.params.get("train", 0))
         newW = eng.local_rows()[:, : eng.spec.P].cpu().numpy()
         for j in range(W.shape[0]):
@@ -289,8 +313,15 @@ class StateRecorder:
             a = ACTION_NAMES[int(act[j])]
             if a is not None:
                 d["action"] = a
-                d["counterpart"] = (None if a == "train_self" else
-                                    int(cp[j]) if uid_of_slot is None else int(uid_of_slot[int(cp[j])]))
+                if a == "train_self":
+                    d["counterpart"] = None
+                elif uid_of_slot is None:
+                    d["counterpart"] = int(cp[j])
+                elif ordered and int(cp[j]) < j and resp[int(cp[j])]:
+                    # the counterpart's turn came first and replaced it: the newborn (reference S11/S12)
+                    d["counterpart"] = int(new_uid[int(cp[j])])
+                else:
+                    d["counterpart"] = int(uid_of_slot[int(cp[j])])
             if a == "train_self":
                 d["fitted"] = train
                 d["loss"] = float(loss[j])

@@ -15,22 +15,23 @@ newborns with globally sequential uids (reference S13).
 Sharded over R ranks (one process per GPU, RCCL over xGMI), ``exchange="alltoall"``
 (csrc/srnn_shard.hip): every rank decides only its OWN slots, one generation ahead, and
 tells the owners of its remote victims (notices) and of its remote teachers (requests);
-int64 slots, O(local) memory and work, so a soup can fill every GPU's HBM.  Per generation:
+int64 slots, O(local) memory and work, so a soup can fill every GPU's HBM.  The shipped
+schedule (``ExecConfig.x2_schedule = "serial"``) runs a generation on ONE stream:
 
-    side stream: evolve of the local slots of t (no remote attacker / teacher, ~84 % at R = 8)
-    main stream: pack_t (finish of t-1 + decisions of t+1 + the rows of exchange t)
-                 -> all-to-all_t -> evolve of the remote-dependent slots of t
-    post stream: (after the all-to-all) post_t (uids of t-1's newborns, census,
-                 notices/requests of t+1), beside the remote evolve
-    join
+    pack_t        finish of t-1 (census partials, newborn counts) + decisions of t+1
+                  (links, notices, requests) + the rows of exchange t
+    all-to-all_t  one RCCL all-to-all of fixed-size blocks on the soup's own communicator
+    evolve_t      ONE launch: post_t's workgroups first (uids of t-1's newborns, global
+                  census, received notices / requests of t+1), then n/64 evolve waves in
+                  which the lanes of remote-dependent slots take the remote list's entries
 
-so the pack, the all-to-all and the post overlap the local evolve, and the chain that sets
-the generation time at R > 1 (pack -> all-to-all -> remote evolve) carries nothing else
-(pack, post and the remote evolve run at raised wave priority; counters are reserved once
-per workgroup).  ``exchange="allgather"`` instead all-gathers
-every rank's rows each generation (the X01 pattern of SURVEY §2.5: one collective, every
-rank holds the whole table and recomputes every slot's decisions; populations < 2^32).
-Results are bitwise independent of R for both (tests/test_dist_gloo.py).
+Each cross-queue dependency inside a hipGraph costs ~10 us (profiles/r3b), which is why the
+alternative ``"overlap"`` schedule (local slots on a side stream beside pack ->
+all-to-all -> remote evolve, post on a third stream) measured slower and is opt-in.
+``exchange="allgather"`` instead all-gathers every rank's rows each generation (the X01
+pattern of SURVEY §2.5: one collective, every rank holds the whole table and recomputes
+every slot's decisions; populations < 2^32).  Results are bitwise independent of R for
+both (tests/test_dist_gloo.py).
 
 ``dtype`` selects the storage of the weight tables and exchange rows (fp32, bf16, fp16;
 arithmetic is fp32 -- SURVEY §7.7).
@@ -50,6 +51,7 @@ from typing import Dict, Optional
 import torch
 
 from .arch import ArchSpec
+from .config import ExecConfig
 from .ops import _lib
 from .ops import kernels as K
 from .parallel.dist import Dist
@@ -106,6 +108,12 @@ def x2_capacities(n_total: int, world: int, attacking_rate: float, learn_from_ra
     return cq + cn, cn, cq
 
 
+def _finish_batch(nb: int, chunks) -> int:
+    """Generations whose block stats share one batched-finish ring (single rank): the largest
+    graph chunk, fewer when one generation's stats (32 B per 64-row block) pass 512 MB."""
+    return max(1, min(max(list(chunks) or [1]), (512 << 20) // (nb * 32)))
+
+
 def engine_bytes(spec: ArchSpec, n_total: int, world: int = 1, dtype=torch.float32, exchange: str = "alltoall",
                  attacking_rate: float = 0.1, learn_from_rate: float = 0.1, segment: int = 0,
                  diagnostics: bool = True) -> int:
@@ -131,20 +139,23 @@ def engine_bytes(spec: ArchSpec, n_total: int, world: int = 1, dtype=torch.float
     elif R > 1:
         b += 2 * n_total * 4 + n_total * rb + n * 4  # links per global slot, gathered table, row flags
     else:
-        b += 2 * n * 4 + nb * 32  # links, block stats (+ the batched-finish ring, <= 512 MB)
-        b += min(16 * nb * 32, 512 << 20)
+        b += 2 * n * 4 + nb * 32  # links, block stats
+        # the batched-finish ring, sized as SoupEngine._init_single_or_allgather sizes it
+        b += _finish_batch(nb, ExecConfig().resolved().graph_chunks) * (nb * 8 + 2) * 4
     return int(b)
 
 
 def plan_population(spec: ArchSpec, dtype=torch.float32, exchange: str = "alltoall", world: int = 1,
                     hbm_bytes: int = 288 * 10 ** 9, fill: float = 0.9, attacking_rate: float = 0.1,
-                    learn_from_rate: float = 0.1, diagnostics: bool = False) -> Dict:
+                    learn_from_rate: float = 0.1, diagnostics: bool = False, segment: int = 0) -> Dict:
     """The largest population whose per-rank engine (``engine_bytes``) fits ``fill`` of each
     GPU's HBM (288 GB HBM3E per MI355X), and what limits it: the HBM, or the uint32 attack-list
     entries (single-rank / all-gather soups address < 2^32 slots; a sharded all-to-all soup
-    < 2^32 local + received rows per rank)."""
+    < 2^32 local + received rows per rank).  HBM-filling soups run without the per-row
+    diagnostics columns (``diagnostics=False``, 13 B per row); the returned ``engine_kwargs``
+    are what the planned ``SoupEngine`` must be built with for the plan to hold."""
     kw = dict(world=world, dtype=dtype, exchange=exchange, attacking_rate=attacking_rate,
-              learn_from_rate=learn_from_rate, diagnostics=diagnostics)
+              learn_from_rate=learn_from_rate, diagnostics=diagnostics, segment=segment)
     budget = fill * hbm_bytes
     lo, hi = 1, 1 << 50
     while lo < hi:  # largest n_total with engine_bytes <= budget
@@ -155,12 +166,12 @@ def plan_population(spec: ArchSpec, dtype=torch.float32, exchange: str = "alltoa
             hi = mid - 1
     n_fit = lo
     if world > 1 and exchange == "alltoall":
-        limit = lo
-        # local rows + received rows of a rank stay below 2^32 - 1
+        # local rows + received rows of a rank stay below 2^32 - 1 (capacities as _init_x2
+        # computes them, segment included)
         lo2, hi2 = 1, 1 << 50
         while lo2 < hi2:
             mid = (lo2 + hi2 + 1) // 2
-            cr = x2_capacities(mid, world, attacking_rate, learn_from_rate)[0]
+            cr = x2_capacities(mid, world, attacking_rate, learn_from_rate, segment)[0]
             if -(-mid // world) + world * cr < _lib.NIL:
                 lo2 = mid
             else:
@@ -172,7 +183,8 @@ def plan_population(spec: ArchSpec, dtype=torch.float32, exchange: str = "alltoa
     return dict(n_total=n_total, n_total_fit=n_fit, limited_by="hbm" if n_fit <= limit else "uint32 list entries",
                 bytes_per_gpu=engine_bytes(spec, n_total, **kw),
                 bytes_per_particle_per_gpu=engine_bytes(spec, n_total, **kw) / max(n_total, 1),
-                world=world, exchange=exchange, dtype=str(dtype).replace("torch.", ""))
+                world=world, exchange=exchange, dtype=str(dtype).replace("torch.", ""),
+                engine_kwargs=dict(dtype=dtype, exchange=exchange, diagnostics=diagnostics))
 
 
 class SoupEngine:
@@ -181,12 +193,22 @@ class SoupEngine:
     def __init__(self, spec: ArchSpec, n_total: int, params: Dict, device="cpu", seed: int = 0,
                  lr: float = 0.01, shuffle: bool = True, dist: Optional[Dist] = None, weights=None,
                  dtype: torch.dtype = torch.float32, exchange: str = "alltoall", local_weights=None,
-                 init: bool = True, diagnostics: bool = True):
+                 init: bool = True, diagnostics: bool = True, execution: Optional[ExecConfig] = None,
+                 order: str = "synchronous"):
         """``weights``: the whole population's initial rows [n_total, >= P] (every rank
         takes its slice); ``local_weights``: only this rank's rows [hi - lo, >= P];
         ``init=False``: leave the rows for the caller to fill (the streaming checkpoint
         loader writes them straight into the device table); ``diagnostics=False``: no
-        per-row action / counterpart / loss columns (HBM-filling soups)."""
+        per-row action / counterpart / loss columns (HBM-filling soups); ``execution``: schedules
+        and kernel families (config.ExecConfig; its environment variables override it);
+        ``order``: ``"sequential"`` -- the reference's in-place, index-ordered generation
+        (code/soup.py:51-87) scheduled by dependency level on the device (OP_SOUP_ORDERED,
+        bitwise the serial loop; single rank, lane-template shapes) -- or ``"synchronous"``
+        (Jacobi: every read from the generation-start table; any shape, sharded)."""
+        if order not in ("synchronous", "sequential"):
+            raise ValueError(f"order must be 'synchronous' or 'sequential', got {order!r}")
+        self.order = order
+        self.execution = (execution or ExecConfig()).resolved()
         self.spec = spec
         self.n_total = int(n_total)
         self.params = dict(attacking_rate=0.1, learn_from_rate=0.1, train=0, learn_from_severity=1)
@@ -268,6 +290,8 @@ class SoupEngine:
             self.nexts = [torch.full((n_links,), -1, **i32) for _ in range(2)]
             self._init_single_or_allgather(nb)
         self.cfg = _lib.make_cfg(spec, self.dtype_code)
+        if order == "sequential":
+            self._init_ordered()
         # initial particles: uids 0..n_total-1, keyed init (identical for any rank count)
         local = self.local_rows()
         if weights is not None or local_weights is not None:
@@ -295,13 +319,13 @@ class SoupEngine:
         # newborn uids): "batch" -- the generation kernel advances the counter itself, the
         # block stats of up to G generations go to a ring and ONE launch finishes them all
         # (per graph chunk / evolve call); "serial" -- a finish launch after every generation
-        fm = os.environ.get("SRNN_FINISH_MODE", "batch")
+        fm = self.execution.finish_mode
         if self.device.type != "cuda" or self.dist.enabled or not self.fused:
             fm = "serial"
         self.finish_mode = fm
         # the ring holds 32 B per 64-row block per pending generation: at HBM-filling sizes
         # (2e9 rows = 1 GB per generation) fewer generations share one finish launch
-        self._batch = max(1, min(max(self._chunk_sizes() or [1]), (512 << 20) // (nb * 32)))
+        self._batch = _finish_batch(nb, self._chunk_sizes())
         # (+ 8 bytes per generation: its newborn count, accumulated by the generation waves)
         self._bs_ring = torch.zeros((self._batch, nb * 8 + 2), **i32) if fm == "batch" else None
         self._pending_fin = 0  # batch mode: generations whose finish is still due
@@ -309,6 +333,36 @@ class SoupEngine:
             self.full = torch.zeros((self.n_total, self.spec.PP), dtype=self.dtype, device=dev)
             self.stats_all = torch.zeros(self.dist.world * 6, dtype=torch.int64, device=dev)
             self.rowflags = torch.zeros(max(self.n, 1), **i32)
+
+    def _init_ordered(self):
+        """Buffers of the reference-order generation (csrc/srnn_ordered.h): attack outputs,
+        per-turn source versions + level, level work lists, control words."""
+        if self.dist.enabled:
+            raise NotImplementedError("reference-order (sequential) generations are single-rank: its levels would "
+                                      "need one exchange each; shard with order='synchronous'")
+        dev_side = self.device.type != "cpu"
+        if self.generic or not _lib.supports(self.spec, _lib.OP_SOUP_ORDERED, dev_side, self.dtype_code):
+            raise NotImplementedError(
+                f"no level-scheduled reference-order generation for {self.spec}: it exists for the "
+                "lane-per-particle template shapes; SequentialSoupEngine runs the same order for any shape on the "
+                "host, SoupEngine(order='synchronous') any shape on the device")
+        if self.n >= 1 << 30:
+            raise ValueError("reference-order generations address < 2^30 slots")
+        dev = self.device
+        C = int(self.execution.order_levels)
+        self.order_levels = C
+        self._abuf = torch.zeros((self.n, self.spec.PP), dtype=self.dtype, device=dev)
+        self._osrc = torch.zeros(4 * max(self.n, 1), dtype=torch.int32, device=dev)
+        self._olist = torch.zeros((C + 1) * max(self.n, 1), dtype=torch.int32, device=dev)
+        self._octl = torch.zeros(_lib.ORD_CTL_WORDS, dtype=torch.int32, device=dev)
+        self._rec_rows = None  # recording: every particle's state before any respawn
+
+    def ordered_levels(self) -> Dict[str, int]:
+        """Dependency levels of the last reference-order generation: turns per parallel level,
+        the tail's turns, the deepest level, error bits (1: a chain deeper than the DFS stack)."""
+        c = self._octl.cpu().tolist()
+        C = self.order_levels
+        return dict(levels=c[:C], tail=c[C], max_level=c[C + 1], error=c[C + 2])
 
     def _init_x2(self, n_links):
         dev, R = self.device, self.dist.world
@@ -324,9 +378,7 @@ class SoupEngine:
         # the evolve of the local and the remote slots, on one stream (no cross-queue dependencies: each costs
         # ~10 us inside a graph, profiles/r3b); "overlap" -- the local slots on a side stream
         # beside pack -> all-to-all -> remote evolve, post on a third stream
-        self.schedule = os.environ.get("SRNN_X2_SCHEDULE", "serial")
-        if self.schedule not in ("serial", "overlap"):
-            raise ValueError(f"SRNN_X2_SCHEDULE must be 'serial' or 'overlap', got {self.schedule!r}")
+        self.schedule = self.execution.x2_schedule
         # the lane kernels evolve both kinds of slot in one launch (bignet / runtime-shape: two)
         self._x2_both = not bignet and not _lib.is_generic(self.spec, _lib.OP_SOUP_EVOLVE, self.dtype_code)
         # single-launch generations: pack leaves, per 64-row block, how many remote-dependent slots
@@ -352,7 +404,7 @@ class SoupEngine:
         # timing model of R ranks on one GPU (SRNN_X2_EMULATE_REMOTE=<fraction>, world 1 only):
         # that fraction of the slots runs through the remote list after the exchange, as the
         # remote-dependent slots of a multi-rank soup do (same results: the rows are local)
-        fr = float(os.environ.get("SRNN_X2_EMULATE_REMOTE", "0") or 0) if R == 1 else 0.0
+        fr = self.execution.x2_emulate_remote if R == 1 else 0.0
         self.x_emul = int(min(max(fr, 0.0), 1.0) * 0xFFFFFFFF)
         if self.x_emul:
             nr = max(self.n, 1)
@@ -490,6 +542,9 @@ class SoupEngine:
                 fa.flags |= _lib.FLAG_TWO_PHASE
             if self._census_fused():
                 fa.flags |= _lib.FLAG_FUSED_CENSUS | (_lib.FLAG_FIX_SEC if self.stats_with_sec else 0)
+            if self.order == "sequential":
+                fa.W3, fa.o_src, fa.o_list, fa.o_ctl = _p(self._abuf), _p(self._osrc), _p(self._olist), _p(self._octl)
+                fa.o_levels = self.order_levels
             ca = fa
         self._arg_cache[key] = (a, ca, a.flags)
         return self._arg_cache[key]
@@ -501,6 +556,8 @@ class SoupEngine:
         a, ca, flags = self._gen_args()
         a.flags = flags
         if not self.dist.enabled:
+            if self.order == "sequential":
+                return self._ordered_generation(a, ca, record)
             if self.fused and not (record and self.recorder is not None):
                 # ONE launch: evolve + next generation's attack lists + census + uids
                 if not self._lists_ready:
@@ -555,6 +612,37 @@ class SoupEngine:
         self._pending = True
         self._flush()
 
+    def _ordered_generation(self, a, ca, record: bool):
+        """One reference-order generation (OP_SOUP_ORDERED: plan -> levels -> level launches ->
+        tail -> close; the newborns' uids by the finish, batched like the fused generation's).
+        Recording keeps every particle's pre-respawn row and counterparts as slots; the
+        recorder maps them to uids as of each turn (a counterpart slot < k that respawned at
+        its own turn is already the newborn)."""
+        spec, cfg = self.spec, self.cfg
+        if not self._lists_ready:
+            _lib.run(_lib.OP_SOUP_DECIDE, spec, a, cfg)
+        rec = record and self.recorder is not None
+        if rec:
+            if self._rec_rows is None:
+                self._rec_rows = torch.zeros_like(self._abuf)
+            ca.traj = _p(self._rec_rows)
+            uid0 = self.uid.clone()
+        try:
+            _lib.run(_lib.OP_SOUP_ORDERED, spec, ca, cfg)
+        finally:
+            ca.traj = None
+        self._lists_ready = True
+        self._p = 1 - self._p
+        if self.finish_mode == "batch":
+            self._fin_flags = ca.flags
+            self._pending_fin += 1
+            if self._pending_fin == self._batch or rec:
+                self._finish_pending()
+        elif self.stats and not (ca.flags & _lib.FLAG_FUSED_CENSUS):
+            self.classify_local(self.stats_with_sec, zero=False)
+        if rec:
+            self.recorder.on_evolved(self, rows=self._rec_rows, old_uid=uid0, ordered=True)
+
     def _finish_pending(self):
         """Batch mode: ONE finish launch for the generations whose block stats wait in the
         ring (in generation order: census of each, newborn uids, next_uid)."""
@@ -567,7 +655,7 @@ class SoupEngine:
         a.flags = (self._fin_flags & (_lib.FLAG_FUSED_CENSUS | _lib.FLAG_BORN_TOTAL)) | _lib.FLAG_FINISH_BATCH
         a.temp, a.temp_bytes = _p(self._bs_ring), self._bs_ring.stride(0) * 4
         a.uid_out, a.uid_base, a.counts = _p(self.uid), _p(self.next_uid), _p(self.counts)
-        if os.environ.get("SRNN_FINISH_PAR", "1") == "1":
+        if self.execution.finish_par:
             a.done = _p(self._done)  # done counter: one finish workgroup per generation
         _lib.run(_lib.OP_GEN_FINISH, self.spec, a, self.cfg)
         self._pending_fin = 0
@@ -584,7 +672,7 @@ class SoupEngine:
         a = self._args(stream)
         a.x_cr, a.x_cn, a.x_cq, a.x_blk = self.x_cr, self.x_cn, self.x_cq, self.x_blk
         a.x_emul = self.x_emul
-        if self.device.type == "cuda" and os.environ.get("SRNN_X2_PRIO", "1") == "1":
+        if self.device.type == "cuda" and self.execution.x2_prio:
             a.flags |= _lib.FLAG_X2_PRIO  # pack / post / remote evolve win the shared SIMDs
         a.sendbuf, a.recvbuf = _p(self.sendbuf), _p(self.recvbuf)
         a.census = _p(self.census)
@@ -772,9 +860,14 @@ class SoupEngine:
             _lib.run(_lib.OP_UID_ASSIGN, self.spec, a, self.cfg)
         self._pending = False
 
+    def local_exchange_error(self) -> int:
+        """This rank's exchange error bits (X2_ERRORS), read without communicating."""
+        return int(self.err.item()) if self.dist.enabled else 0
+
     def exchange_error(self) -> Optional[str]:
         """Description of any exchange error of this soup on ANY rank (the flags are
-        all-reduced so every rank stops together), or None."""
+        all-gathered so every rank stops together), or None.  COLLECTIVE: every rank must
+        call it (``local_exchange_error`` reads this rank's bits alone)."""
         if not self.dist.enabled:
             return None
         out = torch.zeros(self.dist.world, dtype=torch.int64, device=self.device)
@@ -787,6 +880,7 @@ class SoupEngine:
         return "; ".join(msg for bit, msg in X2_ERRORS.items() if v & bit) or f"error bits {v}"
 
     def exchange_overflowed(self) -> bool:
+        """Collective, like ``exchange_error``: every rank must call it."""
         return self.exchange_error() is not None
 
     def classify_local(self, with_sec: bool = True, zero: bool = True):
@@ -930,7 +1024,7 @@ class SoupEngine:
             # torch's process-group collectives are not captured: their watchdog thread
             # queries events recorded by the capturing stream
             return False
-        if self.dist.world > 1 and os.environ.get("SRNN_SHARDED_GRAPH", "1") != "1":
+        if self.dist.world > 1 and not self.execution.sharded_graph:
             return False
         s = torch.cuda.Stream(self.device)
         s.wait_stream(torch.cuda.current_stream(self.device))
@@ -947,6 +1041,7 @@ class SoupEngine:
         graphs = []
         p0 = self._p
         pend0 = self._pending
+        flags0 = self._flags_state()
         ok = True
         try:
             for _ in range(2):
@@ -962,6 +1057,7 @@ class SoupEngine:
             ok = False
         self._p = p0
         self._pending = pend0
+        self._set_flags_state(flags0)  # a capture that failed midway may have advanced them
         ok = self._agree(ok)
         if ok and validate:
             ok = self._agree(self._validate_graphs(graphs if p0 == 0 else graphs[::-1]))
@@ -999,14 +1095,12 @@ class SoupEngine:
             _lib.run(_lib.OP_SOUP_DECIDE, self.spec, a, self.cfg)
             self._lists_ready = True
 
-    @staticmethod
-    def _chunk_sizes():
-        """Generations per multi-generation graph (SRNN_GRAPH_CHUNKS, even sizes): an evolve
-        of K generations replays the largest that fit, so a short timed region pays few
+    def _chunk_sizes(self):
+        """Generations per multi-generation graph (ExecConfig.graph_chunks, even sizes): an
+        evolve of K generations replays the largest that fit, so a short timed region pays few
         launches and few finish launches (one 20-generation graph for K = 20, 20 + 20 + 8 + 2
         for K = 50)."""
-        v = os.environ.get("SRNN_GRAPH_CHUNKS") or os.environ.get("SRNN_GRAPH_CHUNK") or "20,16,8,4,2"
-        return sorted({int(x) for x in v.split(",") if int(x) >= 2 and int(x) % 2 == 0}, reverse=True)
+        return sorted({int(x) for x in self.execution.graph_chunks}, reverse=True)
 
     def _capture_chunk(self, s, p0, pend0):
         """Multi-generation graphs starting (and ending) at parity p0, added to _chunks

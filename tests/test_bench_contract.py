@@ -16,18 +16,43 @@ def _env(**kw):
     return env
 
 
-def test_bench_self_launch_cpu_two_ranks():
-    p = subprocess.run([sys.executable, "bench.py", "--gpus", "2", "--device", "cpu", "--steps", "2", "--warmup", "1",
-                        "--particles-per-gpu", "1500", "--train", "2"],
-                       cwd=ROOT, env=_env(), capture_output=True, text=True, timeout=300)
+def _bench(*args, timeout=300):
+    p = subprocess.run([sys.executable, "bench.py", "--device", "cpu", "--steps", "2", "--warmup", "1", "--train", "2",
+                        *args], cwd=ROOT, env=_env(), capture_output=True, text=True, timeout=timeout)
     assert p.returncode == 0, p.stderr[-3000:]
     lines = [l for l in p.stdout.splitlines() if l.startswith("{")]
     assert len(lines) == 1, p.stdout[-2000:]
-    d = json.loads(lines[0])
+    return json.loads(lines[0])
+
+
+def test_bench_self_launch_cpu_two_ranks_weak():
+    d = _bench("--gpus", "2", "--scaling", "weak", "--particles-per-gpu", "1500")
     assert d["n_gpus"] == 2 and d["config"]["global_batch"] == 3000 and d["config"]["device"] == "cpu"
-    assert d["config"]["parallelism"] == "population-dp2"
+    assert d["scaling"] == "weak" and d["config"]["particles_per_gpu"] == 1500
+    assert d["config"]["parallelism"] == "population-dp2" and d["config"]["world_size"] == 2
     assert "train=2" in d["config"]["model"]  # the config string follows the actual parameters
     assert sum(d["config"]["final_census"].values()) == 3000
+
+
+def test_bench_strong_scaling_default_one_and_two_ranks():
+    """strong scaling (the default) keeps ONE soup of --particles at any rank count; the
+    execution knobs in force are part of the line"""
+    one = _bench("--particles", "2000")
+    two = _bench("--gpus", "2", "--particles", "2000")
+    for d, n in ((one, 1), (two, 2)):
+        assert d["scaling"] == "strong" and d["n_gpus"] == n
+        assert d["config"]["global_batch"] == 2000 and d["config"]["particles_per_gpu"] == 2000 / n
+        assert sum(d["config"]["final_census"].values()) == 2000
+        ex = d["config"]["execution"]
+        assert ex["x2_schedule"] == "serial" and ex["finish_mode"] == "batch" and ex["graph_chunks"][0] == 20
+        assert set(ex["library"]) >= {"ww_wave", "rnn_wave", "soup_lanes"}
+    # the same soup, bitwise: rank count does not change the census
+    assert one["config"]["final_census"] == two["config"]["final_census"]
+
+
+def test_bench_weak_scaling_one_rank():
+    d = _bench("--scaling", "weak", "--particles-per-gpu", "1200")
+    assert d["scaling"] == "weak" and d["config"]["global_batch"] == 1200
 
 
 def test_bench_world_size_mismatch_exits_nonzero():

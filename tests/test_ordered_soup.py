@@ -1,0 +1,167 @@
+"""Reference-order soups on the level-scheduled generation (SoupEngine(order="sequential"),
+OP_SOUP_ORDERED, csrc/srnn_ordered.h) against the serial loop (SequentialSoupEngine,
+OP_SOUP_SEQ): the reference's in-place, index-ordered Soup.evolve (code/soup.py:51-87,
+SURVEY S11) computed level by level must be BITWISE the serial loop -- rows, uids, actions,
+counterparts, losses, respawns -- on the host and on the device."""
+import numpy as np
+import pytest
+import torch
+
+from self_replicating_neural_networks_amd.arch import ArchSpec
+from self_replicating_neural_networks_amd.config import ExecConfig
+from self_replicating_neural_networks_amd.models import network as N
+from self_replicating_neural_networks_amd.ops import _lib
+from self_replicating_neural_networks_amd.seq_soup import SequentialSoupEngine
+from self_replicating_neural_networks_amd.soup import Soup
+from self_replicating_neural_networks_amd.soup_engine import SoupEngine
+
+SPECS = [ArchSpec.weightwise(2, 2), ArchSpec.aggregating(4, 2, 2), ArchSpec.recurrent(2, 2)]
+IDS = ["ww", "agg", "rnn"]
+HOT = dict(attacking_rate=0.3, learn_from_rate=0.3, train=2, learn_from_severity=2, remove_divergent=True,
+           remove_zero=True, epsilon=1e-4)
+
+
+def _same(ordered: SoupEngine, seq: SequentialSoupEngine, P: int):
+    W = ordered.local_rows()[:, :P].cpu()
+    assert torch.equal(W.view(torch.int32) if W.dtype == torch.float32 else W.view(torch.int16),
+                       seq.W[:, :P].view(torch.int32) if seq.W.dtype == torch.float32 else seq.W[:, :P].view(torch.int16))
+    assert torch.equal(ordered.uid.cpu(), seq.uid.cpu())
+    assert int(ordered.next_uid[0]) == int(seq.next_uid[0])
+    assert torch.equal(ordered.action.cpu(), seq.action.cpu())
+    assert torch.equal(ordered.counterpart.cpu(), seq.counterpart.cpu())
+    assert torch.equal(ordered.respawn.cpu(), seq.respawn.cpu())
+    assert torch.equal(ordered.loss.cpu().view(torch.int32), seq.loss.cpu().view(torch.int32))
+
+
+@pytest.mark.parametrize("spec", SPECS, ids=IDS)
+@pytest.mark.parametrize("levels", [4, 1])
+def test_host_ordered_generation_is_the_serial_loop(spec, levels):
+    """host path of OP_SOUP_ORDERED == OP_SOUP_SEQ bitwise, generation by generation (levels=1
+    sends every turn past level 0 through the tail)"""
+    n, seed = 300, 5
+    o = SoupEngine(spec, n, HOT, device="cpu", seed=seed, order="sequential",
+                   execution=ExecConfig(order_levels=levels))
+    s = SequentialSoupEngine(spec, n, HOT, seed=seed)
+    _same(o, s, spec.P)
+    deep = 0
+    for _ in range(4):
+        o.evolve(1)
+        s.evolve(1)
+        _same(o, s, spec.P)
+        deep = max(deep, o.ordered_levels()["max_level"])
+    assert deep >= 2  # the test exercised real dependency chains
+    assert o.ordered_levels()["error"] == 0
+
+
+def test_host_ordered_sub_soups_and_multi_generation_evolve():
+    spec = ArchSpec.weightwise(2, 2)
+    p = dict(HOT, segment=10)
+    o = SoupEngine(spec, 500, p, device="cpu", seed=9, order="sequential")
+    s = SequentialSoupEngine(spec, 500, p, seed=9)
+    o.evolve(5)
+    s.evolve(5)
+    _same(o, s, spec.P)
+
+
+def test_ordered_differs_from_synchronous():
+    """same decisions and keys: the in-place order is a different computation from Jacobi"""
+    spec = ArchSpec.weightwise(2, 2)
+    o = SoupEngine(spec, 200, HOT, device="cpu", seed=3, order="sequential").evolve(1)
+    j = SoupEngine(spec, 200, HOT, device="cpu", seed=3).evolve(1)
+    assert not torch.equal(o.local_rows(), j.local_rows())
+
+
+def test_level_profile_of_the_bench_soup():
+    """the headline soup's dependency DAG (attack 0.1, learn 0.1): most turns at level 0, a
+    shallow tail (the reason a level-scheduled generation is fast)"""
+    spec = ArchSpec.weightwise(2, 2)
+    p = dict(attacking_rate=0.1, learn_from_rate=0.1, train=0, remove_divergent=True, remove_zero=True, epsilon=1e-4)
+    o = SoupEngine(spec, 20000, p, device="cpu", seed=1, order="sequential").evolve(1)
+    lv = o.ordered_levels()
+    assert lv["levels"][0] > 0.8 * 20000 and lv["max_level"] <= 8 and lv["error"] == 0
+    assert sum(lv["levels"]) + lv["tail"] == 20000
+
+
+def test_ordered_order_validation():
+    spec = ArchSpec.weightwise(2, 2)
+    with pytest.raises(ValueError):
+        SoupEngine(spec, 10, HOT, device="cpu", order="gauss")
+    with pytest.raises(NotImplementedError, match="SequentialSoupEngine"):
+        SoupEngine(ArchSpec.aggregating(4, 10, 3), 10, HOT, device="cpu", order="sequential")
+
+
+def _ww_trainer():
+    return N.TrainingNeuralNetworkDecorator(N.WeightwiseNeuralNetwork(2, 2)).with_params(epsilon=1e-4)
+
+
+def test_soup_auto_mode_keeps_the_reference_order():
+    small = Soup(50, _ww_trainer)
+    big = Soup(500, _ww_trainer)
+    assert small.mode == "sequential" and big.mode == "ordered"
+    with pytest.raises(ValueError, match="mode='device'"):
+        Soup(500, _ww_trainer, dist=object())
+    big.with_params(train=1, remove_divergent=True, remove_zero=True)
+    big.seed()
+    big.evolve(2)
+    assert isinstance(big.engine, SoupEngine) and big.engine.order == "sequential"
+    assert sum(big.count().values()) == 500
+
+
+def test_ordered_soup_records_reference_states():
+    """recording keeps each particle's pre-respawn state and its counterparts as of its turn"""
+    s = Soup(150, _ww_trainer, mode="ordered", seed=4).with_params(
+        attacking_rate=0.3, learn_from_rate=0.2, train=1, remove_divergent=True, remove_zero=True)
+    s.seed()
+    s.evolve(3)
+    n_states = sum(len(p.get_states()) for p in s.historical_particles.values())
+    assert n_states >= 150 * 3
+    acts = {st.get("action") for p in s.historical_particles.values() for st in p.get_states()}
+    assert {"init", "train_self"} <= acts
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("spec", SPECS, ids=IDS)
+def test_device_ordered_generation_is_the_serial_loop(spec):
+    """device OP_SOUP_ORDERED (plan / levels / level launches / tail / close) == the host serial
+    loop bitwise, eager and captured in hipGraphs"""
+    n, seed = 3000, 7
+    for graphs in (False, True):
+        o = SoupEngine(spec, n, HOT, device="cuda", seed=seed, order="sequential")
+        s = SequentialSoupEngine(spec, n, HOT, seed=seed)
+        if graphs:
+            assert o.capture(warmup=1)
+            s.evolve(1)  # capture runs one warmup generation eagerly
+        _same(o, s, spec.P)
+        for _ in range(3):
+            o.evolve(2)
+            s.evolve(2)
+            _same(o, s, spec.P)
+        assert o.ordered_levels()["error"] == 0
+        o.release_graphs()
+
+
+@pytest.mark.gpu
+def test_device_ordered_tail_and_bf16_tables():
+    spec = ArchSpec.weightwise(2, 2)
+    o = SoupEngine(spec, 2000, HOT, device="cuda", seed=2, order="sequential", dtype=torch.bfloat16,
+                   execution=ExecConfig(order_levels=1))
+    s = SequentialSoupEngine(spec, 2000, HOT, seed=2, dtype=torch.bfloat16)
+    for _ in range(3):
+        o.evolve(1)
+        s.evolve(1)
+        _same(o, s, spec.P)
+    assert o.ordered_levels()["tail"] > 0
+
+
+@pytest.mark.gpu
+def test_device_ordered_headline_soup_matches_host_ordered():
+    """100k particles at the bench's parameters: device == host level-scheduled generation"""
+    spec = ArchSpec.weightwise(2, 2)
+    p = dict(attacking_rate=0.1, learn_from_rate=0.1, train=20, remove_divergent=True, remove_zero=True, epsilon=1e-4)
+    o = SoupEngine(spec, 100_000, p, device="cuda", seed=0, order="sequential")
+    h = SoupEngine(spec, 100_000, p, device="cpu", seed=0, order="sequential")
+    o.evolve(2)
+    h.evolve(2)
+    assert torch.equal(o.local_rows().cpu().view(torch.int32), h.local_rows().view(torch.int32))
+    assert torch.equal(o.uid.cpu(), h.uid)
+    assert o.count() == h.count()
