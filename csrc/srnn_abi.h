@@ -156,6 +156,10 @@ struct SrnnArgs {
   int32_t* o_ctl;       // [19] list lengths, max level, error bits (zeroed by the plan kernel)
   int32_t o_levels;     // parallel level launches per generation (1..16); deeper turns: the tail
   int32_t pad3;
+  // ---- precomputed SGD epoch permutations of a soup generation (nibble Weightwise nets, shuffle
+  // on): [severity + epochs][n] uint64, epoch e of local row j at ptab[e * n + j] (counter
+  // gen * 1024 + 512 + e); filled by the generation's own k_perm_table launch.  null: inline
+  uint64_t* ptab;
 };
 
 #define SRNN_X2_HDR 12  // int64 header words of an X2 exchange block (see srnn_shard.hip)
@@ -185,7 +189,7 @@ enum SrnnOp {
                         // bitwise OP_SOUP_SEQ, every particle of a level in parallel (srnn_ordered.h)
 };
 
-int srnn_abi_version();  // 19
+int srnn_abi_version();  // 20
 int64_t srnn_args_size();  // sizeof(SrnnArgs): the ctypes mirror checks its layout against it
 int64_t srnn_cfg_size();
 int srnn_has_config(const SrnnCfg* cfg);

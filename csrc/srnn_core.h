@@ -471,6 +471,12 @@ struct TrainCtx {
   bool shuffle;
   int stride;        // device: threads per block (slot-major, lane fastest: conflict-free b128)
   int aggregator;    // aggregating nets: samples come from the configured aggregator
+  // precomputed epoch permutations (nibble nets, shuffle on): epoch with counter ctr uses
+  // ptab[(ctr - pbase) * pstride] (ptab already points at this particle's column), so the
+  // SGD chain carries no Philox / Fisher-Yates work (k_perm_table computes them beforehand)
+  const uint64_t* ptab = nullptr;
+  int64_t pstride = 0;
+  uint32_t pbase = 0;
 };
 
 struct ApplyCtx {
@@ -574,8 +580,63 @@ struct Weightwise {
   // permuted order, and the next epoch's permutation (Philox + Fisher-Yates, independent
   // of the weights) is computed inside the current epoch's block for the scheduler to
   // interleave with the dependent SGD chain.
+  // train_epochs with the epoch permutations read from a precomputed table (TrainCtx::ptab):
+  // the same permutations, samples and SGD chain -- the next epoch's permutation is a load
+  // issued a whole epoch ahead instead of a Philox draw + Fisher-Yates on the chain's SIMD --
+  // and the loss accumulated in the last epoch only (earlier epochs' losses are discarded)
+  template <bool SELF>
+  SRNN_HD static float train_epochs_tab(float* __restrict__ w, const float* __restrict__ t, int E, TrainCtx& c) {
+    static_assert(P <= 16, "nibble permutations");
+#pragma unroll
+    for (int k = 0; k < P; ++k)
+      c.samp[k * c.stride] = make_float4(SELF ? w[k] : t[k], coords.c[k][0], coords.c[k][1], coords.c[k][2]);
+    const uint64_t* pt = c.ptab + (int64_t)(c.ctr - c.pbase) * c.pstride;
+    uint64_t pn = pt[0];
+    const float lr2 = 2.0f * c.lr;  // folded step -(2 lr) * err (train_epoch)
+    float loss = 0.f;
+    for (int e = 0; e < E; ++e) {
+      if (SELF && e > 0)
+#pragma unroll
+        for (int k = 0; k < P; ++k) reinterpret_cast<float*>(&c.samp[k * c.stride])[0] = w[k];
+      const bool last = e + 1 == E;
+      const uint64_t pn_next = last ? 0ull : pt[(int64_t)(e + 1) * c.pstride];
+      float4 smp[P];
+#pragma unroll
+      for (int q = 0; q < P; ++q) smp[q] = c.samp[(int)((pn >> (4 * q)) & 15u) * c.stride];
+      if (!last) {
+#pragma unroll
+        for (int q = 0; q < P; ++q) {
+          float x[4] = {smp[q].x, smp[q].y, smp[q].z, smp[q].w};
+          float acts[Net::NACT], y[1];
+          Net::forward(w, x, acts, y);
+          float gy[1] = {y[0] - smp[q].x};
+          Net::backward_update(w, acts, gy, lr2);
+        }
+      } else {
+        float acc = 0.f;
+#pragma unroll
+        for (int q = 0; q < P; ++q) {
+          float x[4] = {smp[q].x, smp[q].y, smp[q].z, smp[q].w};
+          float acts[Net::NACT], y[1];
+          Net::forward(w, x, acts, y);
+          float err = y[0] - smp[q].x;
+          acc += err * err;
+          float gy[1] = {err};
+          Net::backward_update(w, acts, gy, lr2);
+        }
+        loss = acc / (float)P;
+      }
+      c.ctr += 1;
+      pn = pn_next;
+    }
+    return loss;
+  }
+
   template <bool SELF>
   SRNN_HD static float train_epochs(float* __restrict__ w, const float* __restrict__ t, int E, TrainCtx& c) {
+    if constexpr (P <= 16) {
+      if (c.ptab && c.shuffle && E > 0) return train_epochs_tab<SELF>(w, t, E, c);
+    }
     if constexpr (P > 16) {
       float s[P], loss = 0.f;
 #pragma unroll

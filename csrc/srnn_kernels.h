@@ -15,6 +15,7 @@
 #include <algorithm>
 #include <climits>
 #include <cstdlib>
+#include <type_traits>
 
 extern "C" int srnn_x2_run(int op, const SrnnCfg* c, const SrnnArgs* a);  // srnn_shard.hip
 
@@ -574,6 +575,11 @@ struct Item {
     tc.shuffle = (a.flags & SRNN_F_SHUFFLE) != 0;
     tc.stride = SAMP_STRIDE;
     tc.aggregator = c.aggregator;
+    if (a.ptab && a.dev) {  // this generation's permutations, precomputed (k_perm_table)
+      tc.ptab = a.ptab + j;
+      tc.pstride = a.n;
+      tc.pbase = tc.ctr;
+    }
     float loss = 0.f;
     // 2. learn_from a teacher (its generation-start weights)
     if (te >= 0) {
@@ -732,6 +738,40 @@ __global__ __launch_bounds__(TB) void k_op(SrnnCfg c, SrnnArgs a) {
     else if constexpr (OP == OP_PERTURB) I::perturb(c, a, i, samp, perm);
     else if constexpr (OP == OP_RESPAWN) I::respawn(a, i);
     else if constexpr (OP == OP_VARY_RUN) I::vary_run(c, a, i, samp, perm);
+  }
+}
+
+// Epoch permutations of a soup generation ahead of it (SrnnArgs::ptab): thread (row, pair)
+// draws the Philox block of epochs 2p, 2p + 1 (counters gen*1024 + 512 + e, keyed by the
+// row's global slot) and stores both nibble permutations -- exactly what train_epochs would
+// compute inline, moved off the latency-bound SGD chains into one fully parallel launch.
+constexpr int TBP = 256;
+template <class Net>
+__global__ __launch_bounds__(TBP) void k_perm_table(SrnnArgs a, int32_t E) {
+  constexpr int P = Net::P;
+  const int64_t npair = (E + 1) / 2;
+  const int64_t t = (int64_t)blockIdx.x * TBP + threadIdx.x;
+  if (t >= a.n * npair) return;
+  const int64_t row = t % a.n, p = t / a.n;
+  const int32_t gen = a.gen_ptr ? a.gen_ptr[0] : a.gen;
+  const uint32_t c0 = (uint32_t)gen * 1024u + 512u + 2u * (uint32_t)p;  // even: one draw, two epochs
+  const Rng rng{(uint32_t)a.seed, (uint32_t)(a.seed >> 32)};
+  const U4 r = perm_draw(rng, (uint64_t)(a.lo + row), c0, P_SHUFFLE);
+  a.ptab[2 * p * a.n + row] = perm_from_bits<P>(perm_bits(r, c0));
+  if (2 * p + 1 < E) a.ptab[(2 * p + 1) * a.n + row] = perm_from_bits<P>(perm_bits(r, c0 + 1u));
+}
+// launch the permutation table of this generation when the caller gave one (nibble nets)
+template <class Net>
+int perm_table(const SrnnArgs& a) {
+  if constexpr (Net::KIND != 0 || Net::P > 16) {
+    return 0;
+  } else {
+    const int32_t E = (a.severity > 0 ? a.severity : 0) + (a.epochs > 0 ? a.epochs : 0);
+    if (!a.ptab || !a.dev || !(a.flags & SRNN_F_SHUFFLE) || E <= 0 || a.n <= 0) return 0;
+    const int64_t threads = a.n * ((E + 1) / 2);
+    hipLaunchKernelGGL((k_perm_table<Net>), dim3((unsigned)((threads + TBP - 1) / TBP)), dim3(TBP), 0,
+                       (hipStream_t)a.stream, a, E);
+    return 0;
   }
 }
 
@@ -1339,6 +1379,10 @@ int gen_finish(const SrnnCfg&, const SrnnArgs& a) {
   return 0;
 }
 
+// reference-order generations scheduled by dependency level (OP_SOUP_ORDERED), and the
+// two-lanes-per-particle WW(2,2) generations (srnn_pair.h, included from srnn_ordered.h)
+#include "srnn_ordered.h"
+
 // OP_SOUP_SEQ: `steps` sequential soup generations starting at generation *gen_ptr (or
 // a.gen) on a host table, one particle after another (the reference order is serial by
 // definition: a single CPU core runs it ~100x faster than per-particle device launches and
@@ -1451,7 +1495,15 @@ int soup_gen(const SrnnCfg& c, const SrnnArgs& a) {
     set_error("fused soup generation needs block stats (temp), the next lists and a done counter");
     return -5;
   }
-  hipLaunchKernelGGL((k_soup_gen<Net, S>), dim3((unsigned)blocks), dim3(TB), 0, (hipStream_t)a.stream, c, a);
+  perm_table<Net>(a);
+  bool pairs = false;
+  if constexpr (std::is_same_v<Net, Weightwise<2, 2>>) pairs = (a.flags & SRNN_F_TWO_PHASE) && use_pairs(a.n);
+  if (pairs) {  // below ~0.6 waves per SIMD: two lanes per particle (srnn_pair.h)
+    if constexpr (std::is_same_v<Net, Weightwise<2, 2>>)
+      hipLaunchKernelGGL((k_soup_gen2<S>), dim3((unsigned)blocks), dim3(pair::TBW), 0, (hipStream_t)a.stream, c, a);
+  } else {
+    hipLaunchKernelGGL((k_soup_gen<Net, S>), dim3((unsigned)blocks), dim3(TB), 0, (hipStream_t)a.stream, c, a);
+  }
   if ((a.flags & SRNN_F_TWO_PHASE) && !(a.flags & SRNN_F_GEN_COUNTS)) {
     constexpr int FNT = SRNN_FINISH_NT;
     hipLaunchKernelGGL((k_gen_finish<Net, S, FNT>), dim3(1), dim3(FNT), 0, (hipStream_t)a.stream, a, (int32_t)blocks);
@@ -1627,6 +1679,35 @@ int launch(const SrnnCfg& c, const SrnnArgs& a) {
     if ((a.flags & SRNN_F_X2) && (!a.temp || !a.x_dep || !a.x_rlist || !a.x_rcount || !a.x_ctl)) {
       set_error("X2 evolve needs block stats (temp), x_dep, x_rlist, x_rcount and x_ctl");
       return -5;
+    }
+    // the generation's permutation table: computed right before a launch that evolves every slot
+    // of the generation (single rank / all-gather, or the single-launch X2 evolve); a launch that
+    // evolves only part of them (the overlap schedule's local / remote halves) computes inline
+    const bool whole = !(a.flags & SRNN_F_X2) || ((a.flags & SRNN_F_X2_REMOTE) && (a.flags & SRNN_F_X2_BOTH));
+    if (a.ptab && !whole) {
+      SrnnArgs b = a;
+      b.ptab = nullptr;
+      hipLaunchKernelGGL((k_soup_evolve<Net, S>), dim3((unsigned)blocks), dim3(TB), 0, st, c, b);
+      hipError_t e = hipGetLastError();
+      if (e != hipSuccess) {
+        set_error(hipGetErrorString(e));
+        return -3;
+      }
+      return 0;
+    }
+    perm_table<Net>(a);
+    if constexpr (std::is_same_v<Net, Weightwise<2, 2>>) {
+      const uint32_t both = SRNN_F_X2 | SRNN_F_X2_REMOTE | SRNN_F_X2_BOTH;
+      if ((a.flags & both) == both && use_pairs(a.n)) {  // the sharded generation on lane pairs
+        const int64_t pb = (a.flags & SRNN_F_X2_POST_FUSED) ? x2::post_blocks<pair::TBW>(a) : 0;
+        hipLaunchKernelGGL((k_soup_evolve2<S>), dim3((unsigned)(pb + (a.n + 63) / 64)), dim3(pair::TBW), 0, st, c, a);
+        hipError_t e = hipGetLastError();
+        if (e != hipSuccess) {
+          set_error(hipGetErrorString(e));
+          return -3;
+        }
+        return 0;
+      }
     }
     hipLaunchKernelGGL((k_soup_evolve<Net, S>), dim3((unsigned)blocks), dim3(TB), 0, st, c, a);
   } else if (OP == OP_CLASSIFY && a.counts) {
@@ -1819,9 +1900,6 @@ int respawn_seq(const SrnnCfg& c, const SrnnArgs& a) {
     for (int q = 0; q < 5; ++q) a.counts[q] = 0;
   return 0;
 }
-
-// reference-order generations scheduled by dependency level (OP_SOUP_ORDERED)
-#include "srnn_ordered.h"
 
 template <class Net, int OP, class S>
 int run_one(const SrnnCfg& c, const SrnnArgs& a) {

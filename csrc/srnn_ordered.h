@@ -131,6 +131,11 @@ struct Ord {
     tc.shuffle = (a.flags & SRNN_F_SHUFFLE) != 0;
     tc.stride = SAMP_STRIDE;
     tc.aggregator = c.aggregator;
+    if (a.ptab && a.dev) {  // this generation's permutations, precomputed (k_perm_table)
+      tc.ptab = a.ptab + k;
+      tc.pstride = a.n;
+      tc.pbase = tc.ctr;
+    }
     float loss = 0.f;
     if (te >= 0) {  // 2. learn_from the teacher's current row
       if (s[2] == SRC_SELF) I::copy(f, w);
@@ -358,6 +363,8 @@ __global__ __launch_bounds__(TB) void k_ord_close(SrnnCfg c, SrnnArgs a) {
   }
 }
 
+#include "srnn_pair.h"
+
 // OP_SOUP_ORDERED: one sequential (reference-order) generation of a single-rank table.
 // W2: generation-start rows, W: the generation's rows (E versions, then the final table),
 // W3: attack outputs, o_src [n][4], o_list [(C+1) n], o_ctl [CTL_WORDS], o_levels = C;
@@ -457,16 +464,32 @@ int soup_ordered(const SrnnCfg& c, const SrnnArgs& a) {
   const int64_t nb = (a.n + TB - 1) / TB;
   if (nb <= 0) return 0;
   hipStream_t st = (hipStream_t)a.stream;
+  perm_table<Net>(a);
   hipLaunchKernelGGL((k_ord_plan<Net, S>), dim3((unsigned)nb), dim3(TB), 0, st, c, a);
   hipLaunchKernelGGL((k_ord_levels<Net, S>), dim3((unsigned)nb), dim3(TB), 0, st, c, a);
+  constexpr bool ww22 = std::is_same_v<Net, Weightwise<2, 2>>;
   for (int32_t L = 0; L < C; ++L) {
     // level L holds ~n / 7^L turns at the reference's rates: a grid that covers it in one
-    // pass, grid-stride beyond (any count is processed)
+    // pass, grid-stride beyond (any count is processed); the small levels of WW(2,2) run on
+    // lane pairs (latency-bound: srnn_pair.h)
     int64_t blocks = L == 0 ? nb : std::max<int64_t>(64, nb >> (2 * L));
     blocks = std::min(blocks, nb);
-    hipLaunchKernelGGL((k_ord_level<Net, S>), dim3((unsigned)blocks), dim3(TB), 0, st, c, a, L);
+    bool pairs = false;
+    if constexpr (ww22) pairs = L > 0 && use_pairs(a.n >> (2 * L + 1));
+    if (pairs) {
+      if constexpr (ww22)
+        hipLaunchKernelGGL((k_ord_level2<S>), dim3((unsigned)blocks), dim3(pair::TBW), 0, st, c, a, L);
+    } else {
+      hipLaunchKernelGGL((k_ord_level<Net, S>), dim3((unsigned)blocks), dim3(TB), 0, st, c, a, L);
+    }
   }
-  hipLaunchKernelGGL((k_ord_tail<Net, S>), dim3(1), dim3(TB), 0, st, c, a);
+  bool tail_pairs = false;
+  if constexpr (ww22) tail_pairs = use_pairs(0);
+  if (tail_pairs) {
+    if constexpr (ww22) hipLaunchKernelGGL((k_ord_tail2<S>), dim3(1), dim3(pair::TBW), 0, st, c, a);
+  } else {
+    hipLaunchKernelGGL((k_ord_tail<Net, S>), dim3(1), dim3(TB), 0, st, c, a);
+  }
   hipLaunchKernelGGL((k_ord_close<Net, S>), dim3((unsigned)nb), dim3(TB), 0, st, c, a);
   if (!(a.flags & SRNN_F_GEN_COUNTS)) {
     constexpr int FNT = SRNN_FINISH_NT;

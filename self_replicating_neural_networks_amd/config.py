@@ -97,13 +97,16 @@ class ExecConfig:
     soup_lanes: Optional[int] = None        # SRNN_SOUP_LANES (None / 0: by population size)
     order_levels: int = 4                   # SRNN_ORDER_LEVELS: parallel level launches of a reference-order
                                             # generation (deeper levels run in its one-wave tail)
+    perm_table: bool = True                 # SRNN_PERM_TABLE: a generation's SGD permutations precomputed by
+                                            # one launch ahead of it (nibble Weightwise nets on the device)
 
     _ENV = dict(finish_mode="SRNN_FINISH_MODE", finish_par="SRNN_FINISH_PAR", graph_chunks="SRNN_GRAPH_CHUNKS",
                 x2_schedule="SRNN_X2_SCHEDULE", x2_prio="SRNN_X2_PRIO", x2_emulate_remote="SRNN_X2_EMULATE_REMOTE",
                 sharded_graph="SRNN_SHARDED_GRAPH", native_comm="SRNN_NATIVE_COMM", loopback="SRNN_LOOPBACK",
                 force_generic="SRNN_FORCE_GENERIC", ww_wave="SRNN_WW_WAVE", rnn_wave="SRNN_RNN_WAVE",
                 rnn_spec="SRNN_RNN_SPEC", rnn_soup="SRNN_RNN_SOUP", big_wave="SRNN_BIG_WAVE",
-                fix_group="SRNN_FIX_GROUP", soup_lanes="SRNN_SOUP_LANES", order_levels="SRNN_ORDER_LEVELS")
+                fix_group="SRNN_FIX_GROUP", soup_lanes="SRNN_SOUP_LANES", order_levels="SRNN_ORDER_LEVELS",
+                perm_table="SRNN_PERM_TABLE")
     LIBRARY_KNOBS = ("force_generic", "ww_wave", "rnn_wave", "rnn_spec", "rnn_soup", "big_wave", "fix_group",
                      "soup_lanes")
 

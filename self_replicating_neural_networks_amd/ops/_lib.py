@@ -20,7 +20,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 # SRNN_LIB: load another build of the library (A/B of compiler flags on the GPU box)
 LIB_PATH = os.environ.get("SRNN_LIB") or os.path.join(_HERE, "libsrnn.so")
 CSRC = os.path.normpath(os.path.join(_HERE, "..", "..", "csrc"))
-ABI_VERSION = 19
+ABI_VERSION = 20
 
 # SrnnOp (csrc/srnn_abi.h)
 OP_INIT = 0
@@ -112,6 +112,8 @@ class SrnnArgs(ctypes.Structure):
         ("scratch", _P), ("scratch_bytes", _I64),
         # ordered (reference-order) generation
         ("W3", _P), ("o_src", _P), ("o_list", _P), ("o_ctl", _P), ("o_levels", _I32), ("pad3", _I32),
+        # precomputed SGD epoch permutations of a soup generation
+        ("ptab", _P),
     ]
 
 

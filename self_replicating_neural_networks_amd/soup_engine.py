@@ -334,6 +334,22 @@ class SoupEngine:
             self.stats_all = torch.zeros(self.dist.world * 6, dtype=torch.int64, device=dev)
             self.rowflags = torch.zeros(max(self.n, 1), **i32)
 
+    def _perm_table(self):
+        """The generation's SGD epoch permutations, precomputed by one launch before the
+        generation kernel (k_perm_table; nibble Weightwise nets with shuffle, on the device):
+        [severity + train][n] uint64, reallocated when the epoch count grows.  None where the
+        kernels draw them inline (host, other shapes, > 2 GB of table)."""
+        if (self.device.type != "cuda" or self.spec.kind != "weightwise" or self.spec.P > 16 or not self.shuffle
+                or self.generic or not self.execution.perm_table):
+            return None
+        E = max(int(self.params.get("train", 0)), 0) + max(int(self.params.get("learn_from_severity", 1)), 0)
+        if E <= 0 or self.n * E * 8 > (2 << 30):
+            return None
+        t = getattr(self, "_ptab", None)
+        if t is None or t.numel() < self.n * E:
+            self._ptab = t = torch.zeros(self.n * E, dtype=torch.int64, device=self.device)
+        return t
+
     def _init_ordered(self):
         """Buffers of the reference-order generation (csrc/srnn_ordered.h): attack outputs,
         per-turn source versions + level, level work lists, control words."""
@@ -510,6 +526,7 @@ class SoupEngine:
         a.W2 = _p(self.table_in)
         a.W = _p(self.rows_out)
         a.uid = _p(self.uid)
+        a.ptab = _p(self._perm_table())
         a.heads, a.nexts = _p(self.heads[self._p]), _p(self.nexts[self._p])
         a.ballots = _p(self.ballots)
         a.action, a.counterpart, a.loss, a.respawn = _p(self.action), _p(self.counterpart), _p(self.loss), _p(self.respawn)
@@ -734,6 +751,7 @@ class SoupEngine:
                 # ONE launch: post's workgroups first, then n/64 waves evolving every slot
                 rem.flags |= _lib.FLAG_X2_BOTH | _lib.FLAG_X2_POST_FUSED
                 rem.temp2 = _p(self.x_bstat[1 - p])
+                rem.ptab = _p(self._perm_table())  # the generation's permutations, ahead of it
                 loc = None
                 po = None
         self._arg_cache[key] = (pa, po, rem, loc, census)

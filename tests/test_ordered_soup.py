@@ -21,10 +21,13 @@ HOT = dict(attacking_rate=0.3, learn_from_rate=0.3, train=2, learn_from_severity
            remove_zero=True, epsilon=1e-4)
 
 
+def _bits(t):
+    t = t.cpu().contiguous()
+    return t.view(torch.int32) if t.dtype == torch.float32 else t.view(torch.int16)
+
+
 def _same(ordered: SoupEngine, seq: SequentialSoupEngine, P: int):
-    W = ordered.local_rows()[:, :P].cpu()
-    assert torch.equal(W.view(torch.int32) if W.dtype == torch.float32 else W.view(torch.int16),
-                       seq.W[:, :P].view(torch.int32) if seq.W.dtype == torch.float32 else seq.W[:, :P].view(torch.int16))
+    assert torch.equal(_bits(ordered.local_rows()[:, :P]), _bits(seq.W[:, :P]))
     assert torch.equal(ordered.uid.cpu(), seq.uid.cpu())
     assert int(ordered.next_uid[0]) == int(seq.next_uid[0])
     assert torch.equal(ordered.action.cpu(), seq.action.cpu())
@@ -122,12 +125,13 @@ def test_ordered_soup_records_reference_states():
 @pytest.mark.gpu
 @pytest.mark.parametrize("spec", SPECS, ids=IDS)
 def test_device_ordered_generation_is_the_serial_loop(spec):
-    """device OP_SOUP_ORDERED (plan / levels / level launches / tail / close) == the host serial
-    loop bitwise, eager and captured in hipGraphs"""
+    """device OP_SOUP_ORDERED (plan / levels / level launches / tail / close) == the serial loop
+    on the same device (k_soup_seq, one lane) bitwise, eager and captured in hipGraphs (device
+    and host code contract a*b+c differently, so the comparison is device against device)"""
     n, seed = 3000, 7
     for graphs in (False, True):
         o = SoupEngine(spec, n, HOT, device="cuda", seed=seed, order="sequential")
-        s = SequentialSoupEngine(spec, n, HOT, seed=seed)
+        s = SequentialSoupEngine(spec, n, HOT, seed=seed, device="cuda")
         if graphs:
             assert o.capture(warmup=1)
             s.evolve(1)  # capture runs one warmup generation eagerly
@@ -145,7 +149,7 @@ def test_device_ordered_tail_and_bf16_tables():
     spec = ArchSpec.weightwise(2, 2)
     o = SoupEngine(spec, 2000, HOT, device="cuda", seed=2, order="sequential", dtype=torch.bfloat16,
                    execution=ExecConfig(order_levels=1))
-    s = SequentialSoupEngine(spec, 2000, HOT, seed=2, dtype=torch.bfloat16)
+    s = SequentialSoupEngine(spec, 2000, HOT, seed=2, dtype=torch.bfloat16, device="cuda")
     for _ in range(3):
         o.evolve(1)
         s.evolve(1)
@@ -154,14 +158,14 @@ def test_device_ordered_tail_and_bf16_tables():
 
 
 @pytest.mark.gpu
-def test_device_ordered_headline_soup_matches_host_ordered():
-    """100k particles at the bench's parameters: device == host level-scheduled generation"""
+def test_device_ordered_headline_soup_matches_serial_loop():
+    """the bench's parameters (train 20, attack 0.1, learn 0.1, respawn) at 20k particles: the
+    level-scheduled generation == the device serial loop, and most turns run at level 0"""
     spec = ArchSpec.weightwise(2, 2)
     p = dict(attacking_rate=0.1, learn_from_rate=0.1, train=20, remove_divergent=True, remove_zero=True, epsilon=1e-4)
-    o = SoupEngine(spec, 100_000, p, device="cuda", seed=0, order="sequential")
-    h = SoupEngine(spec, 100_000, p, device="cpu", seed=0, order="sequential")
+    o = SoupEngine(spec, 20_000, p, device="cuda", seed=0, order="sequential")
+    s = SequentialSoupEngine(spec, 20_000, p, seed=0, device="cuda")
     o.evolve(2)
-    h.evolve(2)
-    assert torch.equal(o.local_rows().cpu().view(torch.int32), h.local_rows().view(torch.int32))
-    assert torch.equal(o.uid.cpu(), h.uid)
-    assert o.count() == h.count()
+    s.evolve(2)
+    _same(o, s, spec.P)
+    assert o.ordered_levels()["levels"][0] > 0.8 * 20_000

@@ -70,14 +70,17 @@ def test_mixed_soup_curve(tmp_path):
     assert np.max(np.abs(np.array(ww["zs"]) - pub)) < 1.6
     assert np.all(np.array(agg["zs"]) == 0)  # aggregating soups never reach non-zero fixpoints
     # aggregating zero fixpoints per 10-particle soup (code/results/exp-mixed-soup-*/log.txt:6):
-    # published 0.8, 0.4, 0.4, 0.3, 0.2, 0.2, 0.2, 0.2, 0.2, 0.4, 0.3 from 10 soups per point
-    # (standard error ~0.17 per point); here ~0.3 at every train count.  The level is pinned;
-    # the published first point (0.8) sits ~3 standard errors above it.
+    # published 0.8, 0.4, 0.4, 0.3, 0.2, 0.2, 0.2, 0.2, 0.2, 0.4, 0.3 from 10 soups per point.
+    # In the reference's order (the setup's default since the level-scheduled generation) the
+    # rate is ~0.41 per soup at every train count (the synchronous generation gives ~0.31).  A
+    # published point averages 10 soups of ~Binomial(10, 0.041) counts: standard error ~0.2, so
+    # the first point (0.8) is ~2 standard errors above 0.41 -- every point, that one included,
+    # is asserted within 2.5 standard errors, the level within ~1.3 standard errors of the mean.
     pub_agg = np.array([0.8, 0.4, 0.4, 0.3, 0.2, 0.2, 0.2, 0.2, 0.2, 0.4, 0.3])
     agg_y = np.array(agg["ys"])
     assert np.all(agg_y > 0)
     assert abs(agg_y.mean() - pub_agg.mean()) < 0.12
-    assert np.max(np.abs(agg_y[1:] - pub_agg[1:])) < 0.35
+    assert np.max(np.abs(agg_y - pub_agg)) < 0.5
 
 
 def test_mixed_self_fixpoints_curve(tmp_path):
