@@ -51,6 +51,10 @@ def parse_args(argv=None):
     ap.add_argument("--order", choices=["sequential", "synchronous"], default="synchronous",
                     help="sequential: the reference's in-place, index-ordered generation (level-scheduled, "
                          "single rank); synchronous: every read from the generation-start table (shardable)")
+    ap.add_argument("--reference-order-steps", type=int, default=None,
+                    help="single rank, synchronous headline: ALSO time this many generations of the same soup in the "
+                         "reference's sequential order (reported under config.reference_order; default: --steps at "
+                         "N=1, 0 at N>1)")
     ap.add_argument("--train", type=int, default=20)
     ap.add_argument("--attacking-rate", type=float, default=0.1)
     ap.add_argument("--learn-from-rate", type=float, default=0.1)
@@ -179,6 +183,27 @@ def main(argv=None):
         allr = allr.view(d.world, 2).cpu().tolist()
         comm = {"library": d.native.library, "rccl_nranks": [r[0] for r in allr],
                 "rccl_user_ranks": [r[1] for r in allr]}
+    # the same soup in the reference's order (level-scheduled, single rank), timed after the
+    # headline's region: a second number, never part of the headline value
+    ref_order = None
+    k_ref = args.reference_order_steps if args.reference_order_steps is not None else (
+        args.steps if d.world == 1 and args.order == "synchronous" else 0)
+    if k_ref > 0 and d.world == 1 and args.order == "synchronous":
+        eng.release_graphs()
+        ro = SoupEngine(spec, n_total, params, device=dev, seed=args.seed, dist=d, execution=execution,
+                        order="sequential")
+        ro.stats = not args.no_stats
+        if on_gpu and not args.no_graph:
+            ro.capture(warmup=1)
+        ro.evolve(args.warmup)
+        sync()
+        t1 = time.perf_counter()
+        ro.evolve(k_ref)
+        sync()
+        dt_ref = time.perf_counter() - t1
+        ref_order = {"steps": k_ref, "ms_per_step": dt_ref / k_ref * 1e3, "value": n_total * k_ref / dt_ref,
+                     "final_census": ro.count(), "levels": ro.ordered_levels()}
+        ro.release_graphs()
     if d.rank == 0:
         print(json.dumps({
             "metric": "self-application steps/sec (whole node) for 100k-particle soup",
@@ -203,7 +228,8 @@ def main(argv=None):
                        "overlap": getattr(eng, "overlap", False),
                        "sharded_schedule": getattr(eng, "schedule", None) if getattr(eng, "x2", False) else None,
                        "census_every_step": eng.stats, "final_census": census, "order": args.order,
-                       "ordered_levels": eng.ordered_levels() if args.order == "sequential" else None},
+                       "ordered_levels": eng.ordered_levels() if args.order == "sequential" else None,
+                       "reference_order": ref_order},
         }), flush=True)
     eng.release_graphs()  # graph executables reference the RCCL communicator
     d.close()

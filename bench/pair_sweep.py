@@ -20,7 +20,7 @@ def main():
     ap.add_argument("--sizes", default="8192,12500,16384,25000,32768,50000,65536,100000")
     ap.add_argument("--gens", type=int, default=20)
     ap.add_argument("--orders", default="synchronous,sequential")
-    ap.add_argument("--tables", default="1,0")
+    ap.add_argument("--tables", default="1")
     args = ap.parse_args()
     import torch
     from self_replicating_neural_networks_amd.arch import ArchSpec
@@ -38,7 +38,7 @@ def main():
                 for lanes in (1, 2):
                     _lib.set_knob("soup_lanes", lanes)
                     e = SoupEngine(spec, n, params, device=dev, seed=0, order=order,
-                                   execution=ExecConfig(perm_table=bool(table)))
+                                   execution=ExecConfig(perm_table=bool(table), graph_chunks=(20,)))
                     e.stats = True
                     e.capture(warmup=1)
                     e.evolve(4)

@@ -1786,6 +1786,160 @@ __device__ float ww_epochs(const GShape& s, const WWave& g, const WWGroup& R, co
   return loss;
 }
 
+
+// ---------------------------------------------------------------------------------------------
+// ww_epochs with the particle's weights in VGPRs (compile-time width W, depth D; U = 4 lanes per
+// particle for W <= 4, 16 for W <= 16).  Lane u keeps column u of the input layer, column u AND
+// row u of every hidden layer (the diagonal twice, both copies updated by the same fma), and the
+// whole output layer (replicated; its own entry also as kd_own): the forward dot products read
+// the other units' values through DPP broadcasts within the group (quad_perm for U = 4,
+// row_newbcast for U = 16), the backward pass the other units' steps the same way.  Same fma
+// sequence per value as ww_epochs / g_train_epochs (bitwise, tests/test_ww_wave_gpu.py); no LDS
+// traffic and no barriers inside the SGD step (the LDS form waited on LDS 4.6x its issue time,
+// profiles/r3d).  Samples, the permutation and the coordinates stay in LDS.  live = false: the
+// epochs run but the weights in LDS are left as they were (a soup's non-learners).
+template <int U, int R_>
+__device__ __forceinline__ float wr_bcast(float v) {
+  if constexpr (U == 4) return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), R_ * 0x55, 0xF, 0xF, true));
+  else return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x150 + R_, 0xF, 0xF, true));
+}
+template <int U, int W, int R_ = 0>
+__device__ __forceinline__ void wr_bcast_all(float v, float* out) {
+  if constexpr (R_ < W) {
+    out[R_] = wr_bcast<U, R_>(v);
+    wr_bcast_all<U, W, R_ + 1>(v, out);
+  }
+}
+template <int W, int D>
+__device__ float ww_epochs_reg(const GShape& s, const WWave& g, const WWGroup& R, const float* coords, int u, bool live,
+                               int E, bool self, uint64_t uid, uint32_t& ctr, float lr, bool shuffle, const Rng& rng) {
+  constexpr int U = W <= 4 ? 4 : 16;
+  constexpr int H = D - 1 > 0 ? D - 1 : 1;  // hidden layers (at least one array slot)
+  const bool on = u < W;
+  const int uu = on ? u : 0;
+  float k0[4], kc[H][W], kr[H][W], kd[W], kd_own;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) k0[i] = R.w[g.poff[0] + i * g.pst[0] + uu];
+#pragma unroll
+  for (int l = 1; l < D; ++l)
+#pragma unroll
+    for (int r = 0; r < W; ++r) {
+      kc[l - 1][r] = R.w[g.poff[l] + r * g.pst[l] + uu];
+      kr[l - 1][r] = R.w[g.poff[l] + uu * g.pst[l] + r];
+    }
+#pragma unroll
+  for (int r = 0; r < W; ++r) kd[r] = R.w[g.poff[D] + r * g.pst[D]];
+  kd_own = R.w[g.poff[D] + uu * g.pst[D]];
+  const float lr2 = 2.0f * lr;
+  float loss = 0.f;
+  for (int e = 0; e < E; ++e) {
+    if (self && on) {  // samples = the weights at the epoch start (flat, row-major)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) R.sv[s.off[0] + i * W + u] = k0[i];
+#pragma unroll
+      for (int l = 1; l < D; ++l)
+#pragma unroll
+        for (int r = 0; r < W; ++r) R.sv[s.off[l] + r * W + u] = kc[l - 1][r];
+      R.sv[s.off[D] + u] = kd_own;
+    }
+    __syncthreads();
+    if (shuffle) {  // the permutation: exactly ww_epochs' (lane 0 of the particle)
+      for (int k = u; k < s.P; k += g.U) R.perm[k] = k;
+      __syncthreads();
+      if (u == 0 && live) {
+        U4 r{0, 0, 0, 0};
+        int used = 4;
+        uint32_t blk = 0;
+        for (int t = s.P - 1; t > 0; --t) {
+          if (used == 4) {
+            r = rng.draw(uid, ctr, P_SHUFFLE + (blk << 8));
+            ++blk;
+            used = 0;
+          }
+          const uint32_t x = used == 0 ? r.x : used == 1 ? r.y : used == 2 ? r.z : r.w;
+          ++used;
+          int j = (int)(u01(x) * (float)(t + 1));
+          if (j > t) j = t;
+          const int pt = R.perm[t];
+          R.perm[t] = R.perm[j];
+          R.perm[j] = pt;
+        }
+      }
+      __syncthreads();
+    }
+    float acc = 0.f;
+    for (int q = 0; q < s.P; ++q) {
+      const int idx = shuffle ? R.perm[q] : q;
+      const float x0 = R.sv[idx];
+      const float x1 = coords[3 * idx], x2 = coords[3 * idx + 1], x3 = coords[3 * idx + 2];
+      float hin[D][W], hown[D];
+      float h = x0 * k0[0];
+      h = fmaf(x1, k0[1], h);
+      h = fmaf(x2, k0[2], h);
+      h = fmaf(x3, k0[3], h);
+      hown[0] = h;
+      wr_bcast_all<U, W>(h, hin[0]);
+#pragma unroll
+      for (int l = 1; l < D; ++l) {  // hidden layer l: column u
+        float z = hin[l - 1][0] * kc[l - 1][0];
+#pragma unroll
+        for (int r = 1; r < W; ++r) z = fmaf(hin[l - 1][r], kc[l - 1][r], z);
+        hown[l] = z;
+        wr_bcast_all<U, W>(z, hin[l]);
+      }
+      float y = hin[D - 1][0] * kd[0];  // the output unit's chain (every lane, same order)
+#pragma unroll
+      for (int r = 1; r < W; ++r) y = fmaf(hin[D - 1][r], kd[r], y);
+      const float err = y - x0;
+      acc += err * err;
+      const float so = -lr2 * err;
+      float si = kd_own * so;  // pre-update K_D[u]
+      kd_own = fmaf(hown[D - 1], so, kd_own);
+#pragma unroll
+      for (int r = 0; r < W; ++r) kd[r] = fmaf(hin[D - 1][r], so, kd[r]);
+#pragma unroll
+      for (int l = D - 1; l >= 1; --l) {  // hidden layers: row u with the pre-update row
+        float sall[W];
+        wr_bcast_all<U, W>(si, sall);
+        float sacc = kr[l - 1][0] * sall[0];
+#pragma unroll
+        for (int c = 1; c < W; ++c) sacc = fmaf(kr[l - 1][c], sall[c], sacc);
+#pragma unroll
+        for (int r = 0; r < W; ++r) kc[l - 1][r] = fmaf(hin[l - 1][r], si, kc[l - 1][r]);
+#pragma unroll
+        for (int c = 0; c < W; ++c) kr[l - 1][c] = fmaf(hown[l - 1], sall[c], kr[l - 1][c]);
+        si = sacc;
+      }
+      k0[0] = fmaf(x0, si, k0[0]);
+      k0[1] = fmaf(x1, si, k0[1]);
+      k0[2] = fmaf(x2, si, k0[2]);
+      k0[3] = fmaf(x3, si, k0[3]);
+    }
+    loss = acc / (float)s.P;
+    ctr += 1;
+  }
+  __syncthreads();  // every lane read the LDS weights before any write-back
+  if (live && on) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) R.w[g.poff[0] + i * g.pst[0] + u] = k0[i];
+#pragma unroll
+    for (int l = 1; l < D; ++l)
+#pragma unroll
+      for (int r = 0; r < W; ++r) R.w[g.poff[l] + r * g.pst[l] + u] = kc[l - 1][r];
+    R.w[g.poff[D] + u * g.pst[D]] = kd_own;
+  }
+  __syncthreads();
+  return loss;
+}
+// E epochs on the register form for the instantiated shapes (WT > 0), else the LDS form
+template <int WT, int DT>
+__device__ __forceinline__ float ww_epochs_any(const GShape& s, const WWave& g, const WWGroup& R, const float* coords,
+                                               int u, bool live, int E, bool self, uint64_t uid, uint32_t& ctr,
+                                               float lr, bool shuffle, const Rng& rng) {
+  if constexpr (WT > 0) return ww_epochs_reg<WT, DT>(s, g, R, coords, u, live, E, self, uid, ctr, lr, shuffle, rng);
+  else return ww_epochs(s, g, R, coords, u, live, E, self, uid, ctr, lr, shuffle, rng);
+}
+
 __device__ void ww_load(const GShape& s, const WWave& g, float* pw, const char* row, int u) {
   for (int k = u; k < s.P; k += g.U) pw[ww_pidx(s, g, k)] = g_dec(row, k, s.dtype);
 }
@@ -1797,7 +1951,7 @@ __device__ void ww_store(const GShape& s, const WWave& g, const float* pw, char*
   }
 }
 
-template <int OP>
+template <int OP, int WT = 0, int DT = 0>
 __global__ __launch_bounds__(64) void k_ww_wave(GShape s, WWave g, SrnnArgs a) {
   extern __shared__ float sm[];
   float* coords = sm;  // [P][3], whole block
@@ -1818,7 +1972,7 @@ __global__ __launch_bounds__(64) void k_ww_wave(GShape s, WWave g, SrnnArgs a) {
     }
     __syncthreads();
     uint32_t ctr = a.ctr;
-    const float loss = ww_epochs(s, g, R, coords, u, active, a.epochs, OP == OP_TRAIN,
+    const float loss = ww_epochs_any<WT, DT>(s, g, R, coords, u, active, a.epochs, OP == OP_TRAIN,
                                  active ? GItem::uid_of(a, i) : 0, ctr, a.lr, shuffle, rng);
     if (active) {
       ww_store(s, g, R.w, GItem::rowp(s, a.W, i), u);
@@ -1833,6 +1987,7 @@ __global__ __launch_bounds__(64) void k_ww_wave(GShape s, WWave g, SrnnArgs a) {
 // victim's P weight points, lanes over the points), learn_from, self-train, respawn with
 // inline re-init; respawn flags per row (SRNN_F_ROW_FLAGS) or OR-ed into the 64-row ballots
 // (zeroed by their consumer, k_g_respawn_seq).
+template <int WT = 0, int DT = 0>
 __global__ __launch_bounds__(64) void k_ww_wave_soup(GShape s, WWave g, SrnnArgs a) {
   extern __shared__ float sm[];
   float* coords = sm;
@@ -1927,13 +2082,14 @@ __global__ __launch_bounds__(64) void k_ww_wave_soup(GShape s, WWave g, SrnnArgs
     // the groups of a wave learn together (a group without a teacher runs the epochs on its own
     // samples with its lanes masked out of every write: live = false keeps its state)
     if (__ballot(learn) != 0ull && a.severity > 0) {
-      const float l2 = ww_epochs(s, g, R, coords, u, learn, a.severity, false, (uint64_t)gs, ctr, a.lr, shuffle, rng);
+      const float l2 =
+          ww_epochs_any<WT, DT>(s, g, R, coords, u, learn, a.severity, false, (uint64_t)gs, ctr, a.lr, shuffle, rng);
       if (learn) loss = l2;
     }
     if (learn) act = A_LEARN_FROM, cp = te;
     if (a.epochs > 0) {
       uint32_t c2 = (uint32_t)gen * 1024u + 512u + (learn ? (uint32_t)a.severity : 0u);
-      loss = ww_epochs(s, g, R, coords, u, active, a.epochs, true, (uint64_t)gs, c2, a.lr, shuffle, rng);
+      loss = ww_epochs_any<WT, DT>(s, g, R, coords, u, active, a.epochs, true, (uint64_t)gs, c2, a.lr, shuffle, rng);
       act = A_TRAIN_SELF;
       cp = -1;
     }
@@ -1996,15 +2152,30 @@ static bool ww_serves(int op, const GShape& s, const SrnnArgs& a, WWave& g) {
   if (op != OP_TRAIN && op != OP_LEARN) return false;
   return ww_wave_geom(s, g) && ww_wave_lds(s, g) <= 64 * 1024;
 }
+template <int WT, int DT>
+static void ww_launch_shape(int op, dim3 grid, size_t lds, hipStream_t st, const GShape& s, const WWave& g,
+                            const SrnnArgs& a) {
+  if (op == OP_TRAIN) hipLaunchKernelGGL((k_ww_wave<OP_TRAIN, WT, DT>), grid, dim3(64), lds, st, s, g, a);
+  else if (op == OP_LEARN) hipLaunchKernelGGL((k_ww_wave<OP_LEARN, WT, DT>), grid, dim3(64), lds, st, s, g, a);
+  else hipLaunchKernelGGL((k_ww_wave_soup<WT, DT>), grid, dim3(64), lds, st, s, g, a);
+}
 static int ww_launch(int op, const GShape& s, const WWave& g, const SrnnArgs& a) {
   if (a.n <= 0) return 0;
   int64_t blocks = (a.n + g.G - 1) / g.G;
   blocks = blocks < 65536 ? blocks : 65536;
   const size_t lds = ww_wave_lds(s, g);
   hipStream_t st = (hipStream_t)a.stream;
-  if (op == OP_TRAIN) hipLaunchKernelGGL((k_ww_wave<OP_TRAIN>), dim3((unsigned)blocks), dim3(64), lds, st, s, g, a);
-  else if (op == OP_LEARN) hipLaunchKernelGGL((k_ww_wave<OP_LEARN>), dim3((unsigned)blocks), dim3(64), lds, st, s, g, a);
-  else hipLaunchKernelGGL(k_ww_wave_soup, dim3((unsigned)blocks), dim3(64), lds, st, s, g, a);
+  const dim3 grid((unsigned)blocks);
+  // register-resident SGD for the instantiated shapes (knob SRNN_KNOB_WW_WAVE = 2: the LDS form)
+  const bool reg = knob(SRNN_KNOB_WW_WAVE, 1) != 2;
+  const int w = reg ? s.W : 0, d = reg ? s.D : 0;
+  if (w == 3 && d == 3 && g.U == 4) ww_launch_shape<3, 3>(op, grid, lds, st, s, g, a);
+  else if (w == 3 && d == 4 && g.U == 4) ww_launch_shape<3, 4>(op, grid, lds, st, s, g, a);
+  else if (w == 10 && d == 2 && g.U == 16) ww_launch_shape<10, 2>(op, grid, lds, st, s, g, a);
+  else if (w == 10 && d == 3 && g.U == 16) ww_launch_shape<10, 3>(op, grid, lds, st, s, g, a);
+  else if (w == 16 && d == 2 && g.U == 16) ww_launch_shape<16, 2>(op, grid, lds, st, s, g, a);
+  else if (w == 16 && d == 3 && g.U == 16) ww_launch_shape<16, 3>(op, grid, lds, st, s, g, a);
+  else ww_launch_shape<0, 0>(op, grid, lds, st, s, g, a);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) {
     set_error(hipGetErrorString(e));

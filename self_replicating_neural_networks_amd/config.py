@@ -88,7 +88,8 @@ class ExecConfig:
     native_comm: bool = True                # SRNN_NATIVE_COMM: the soup's own RCCL communicator
     loopback: bool = False                  # SRNN_LOOPBACK: one-rank all-to-all as a device copy
     force_generic: Optional[bool] = None    # SRNN_FORCE_GENERIC
-    ww_wave: Optional[bool] = None          # SRNN_WW_WAVE
+    ww_wave: Optional[int] = None           # SRNN_WW_WAVE: 0 lane path, 1 waves (register SGD where
+                                            # instantiated), 2 waves with the LDS SGD
     rnn_wave: Optional[bool] = None         # SRNN_RNN_WAVE
     rnn_spec: Optional[bool] = None         # SRNN_RNN_SPEC
     rnn_soup: Optional[bool] = None         # SRNN_RNN_SOUP
@@ -139,7 +140,7 @@ class ExecConfig:
                 kw[f.name] = v
             elif f.name == "x2_emulate_remote":
                 kw[f.name] = float(v)
-            elif f.name in ("soup_lanes", "order_levels"):
+            elif f.name in ("soup_lanes", "order_levels", "ww_wave"):
                 kw[f.name] = int(v)
             else:
                 kw[f.name] = _env_bool(env, bool(cur))

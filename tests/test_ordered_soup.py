@@ -169,3 +169,28 @@ def test_device_ordered_headline_soup_matches_serial_loop():
     s.evolve(2)
     _same(o, s, spec.P)
     assert o.ordered_levels()["levels"][0] > 0.8 * 20_000
+
+
+def test_ordered_records_equal_native_records():
+    """the recorded trajectories (reference state schema: weights, time, action, counterpart uid as
+    of the turn, fitted, loss) of a level-scheduled soup equal the serial loop's record, state for
+    state -- counterparts that respawned at an earlier turn of the generation are the newborns"""
+    params = dict(attacking_rate=0.3, learn_from_rate=0.3, train=1, remove_divergent=True, remove_zero=True)
+    soups = []
+    for mode in ("native", "ordered"):
+        N.ParticleDecorator.next_uid = 0
+        s = Soup(120, _ww_trainer, mode=mode, seed=8, device="cpu").with_params(**params)
+        s.seed()
+        s.evolve(4)
+        soups.append(s)
+    a, b = soups
+    assert sorted(a.historical_particles) == sorted(b.historical_particles)
+    n_cp = 0
+    for uid in a.historical_particles:
+        sa, sb = a.historical_particles[uid].get_states(), b.historical_particles[uid].get_states()
+        assert len(sa) == len(sb), uid
+        for x, y in zip(sa, sb):
+            assert set(x) == set(y) and x["action"] == y["action"] and x.get("counterpart") == y.get("counterpart")
+            assert x.get("time") == y.get("time") and np.array_equal(x["weights"].view(np.int32), y["weights"].view(np.int32))
+            n_cp += x.get("counterpart") is not None
+    assert n_cp > 0

@@ -105,3 +105,30 @@ def test_ww_wave_soup_equals_lane_path(cuda, w, d, dtype):
     g = _soup(spec, cuda, dtype, graphs=True)
     for k, (x, y) in enumerate(zip(g[:6], a[:6])):
         assert torch.equal(bits(x), bits(y)), k
+
+
+@pytest.mark.parametrize("w,d", [(3, 3), (10, 3), (16, 2), (3, 4), (10, 2), (16, 3)])
+def test_ww_register_form_equals_lds_form(cuda, w, d):
+    """the register-resident SGD (ww_epochs_reg) == the LDS form (knob ww_wave = 2), bitwise, for
+    training, learn_from and whole single-rank soup generations"""
+    from self_replicating_neural_networks_amd.soup_engine import SoupEngine
+    spec = ArchSpec.weightwise(w, d)
+    outs = []
+    for knob in (1, 2):
+        _lib.set_knob("ww_wave", knob)
+        try:
+            r = _train_learn(spec, cuda, torch.float32, n=300)[0]
+            e = SoupEngine(spec, 640, dict(attacking_rate=0.2, learn_from_rate=0.2, train=2, learn_from_severity=1,
+                                           remove_divergent=True, remove_zero=True, epsilon=1e-4),
+                           device=cuda, seed=5)
+            e.evolve(3)
+            torch.cuda.synchronize()
+            r["soup"] = e.local_rows().clone()
+            r["uid"] = e.uid.clone()
+            outs.append(r)
+        finally:
+            _lib.set_knob("ww_wave", -1)
+    a, b = outs
+    bits = lambda t: t.contiguous().view(torch.uint8)
+    bad = [k for k in a if not torch.equal(bits(a[k]), bits(b[k]))]
+    assert not bad, bad
