@@ -51,10 +51,9 @@ def parse_args(argv=None):
     ap.add_argument("--order", choices=["sequential", "synchronous"], default="synchronous",
                     help="sequential: the reference's in-place, index-ordered generation (level-scheduled, "
                          "single rank); synchronous: every read from the generation-start table (shardable)")
-    ap.add_argument("--reference-order-steps", type=int, default=None,
+    ap.add_argument("--reference-order-steps", type=int, default=0,
                     help="single rank, synchronous headline: ALSO time this many generations of the same soup in the "
-                         "reference's sequential order (reported under config.reference_order; default: --steps at "
-                         "N=1, 0 at N>1)")
+                         "reference's sequential order (reported under config.reference_order; -1: --steps)")
     ap.add_argument("--train", type=int, default=20)
     ap.add_argument("--attacking-rate", type=float, default=0.1)
     ap.add_argument("--learn-from-rate", type=float, default=0.1)
@@ -186,8 +185,7 @@ def main(argv=None):
     # the same soup in the reference's order (level-scheduled, single rank), timed after the
     # headline's region: a second number, never part of the headline value
     ref_order = None
-    k_ref = args.reference_order_steps if args.reference_order_steps is not None else (
-        args.steps if d.world == 1 and args.order == "synchronous" else 0)
+    k_ref = args.steps if args.reference_order_steps < 0 else args.reference_order_steps
     if k_ref > 0 and d.world == 1 and args.order == "synchronous":
         eng.release_graphs()
         ro = SoupEngine(spec, n_total, params, device=dev, seed=args.seed, dist=d, execution=execution,

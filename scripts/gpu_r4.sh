@@ -19,7 +19,7 @@ timeout -k 10 600 python -u -m pytest tests/test_ordered_soup.py tests/test_pair
   --timeout 240 --timeout-method thread > gpurun_out/pytest_$TAG.log 2>&1
 rc=$?; grep -E "passed|failed|error" gpurun_out/pytest_$TAG.log | tail -3
 if [ $rc -ne 0 ]; then grep -B5 -A30 "FAILED\|Error" gpurun_out/pytest_$TAG.log | head -60; echo "pytest rc=$rc: stopping"; exit $rc; fi
-timeout -k 10 300 python bench.py --steps 20 --warmup 5 > gpurun_out/bench_$TAG.log 2>&1 || exit 1
+timeout -k 10 300 python bench.py --steps 20 --warmup 5 --reference-order-steps -1 > gpurun_out/bench_$TAG.log 2>&1 || exit 1
 tail -1 gpurun_out/bench_$TAG.log | cut -c1-400
 # strong-scaling model of one rank at N = 2 / 4 / 8 (100k / N slots, the remote-dependent fraction
 # of an N-rank soup emulated at one rank: 1 - exp(-0.1 (N-1)/N) + 0.1 (N-1)/N)

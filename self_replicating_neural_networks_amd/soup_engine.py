@@ -305,6 +305,7 @@ class SoupEngine:
             local[:, : w.shape[1]] = w.to(dev, dtype)
         elif init:
             K.init_rows(spec, local, self.uid, self.seed)
+        self._perm_table()  # allocated here, never inside a graph capture
 
     # ------------------------------------------------------------------ state
     def _init_single_or_allgather(self, nb):
@@ -914,6 +915,9 @@ class SoupEngine:
         err = self.exchange_error()
         if err:
             raise RuntimeError(f"soup row exchange failed ({err}): results are invalid")
+        if self.order == "sequential" and self.ordered_levels()["error"]:
+            raise RuntimeError("reference-order generation: a dependency chain exceeded the level DFS stack; "
+                               "results are invalid")
         c = torch.zeros(6, dtype=torch.int64, device=self.device)
         cls, _ = K.classify(self.spec, self.local_rows(), self.eps, with_sec, uid=None, seed=self.seed,
                             scratch=self._scratch, ctr=0x7FFFFFF0, counts=c, key_offset=self.lo)
