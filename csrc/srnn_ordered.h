@@ -16,46 +16,58 @@
 //                  E(k) = k's row at turn end  (after learn / train / respawn)
 //
 // Writes to a row r happen at "times" j (A(j) for each attacker j of r) and r + 1/2 (E(r)).
-// Keeping every written version (A(j) in table W3 row j, E(j) in W row j, the generation
-// start in W2) removes the write-after-read hazards, so only read-after-write edges remain:
-// turn k depends on the turns that produced the versions it reads.  That DAG is shallow
-// (longest path ~ log n: 5-6 levels at 100k particles, 86 % of the turns at level 0), so a
+// Keeping every written version (E(j) in W row j, the generation start in W2) removes the
+// write-after-read hazards, so only read-after-write edges remain: turn k depends on the
+// turns that produced the versions it reads.  An attack output A(j) is cheap (one forward
+// of 14 points for WW(2,2), against 20 epochs of SGD for the turn), so it is not an edge by
+// itself: a turn that reads A(j) recomputes it from A(j)'s own inputs (up to RB nested
+// attack outputs deep), and only the attack outputs past that depth are stored (W3 row j,
+// flagged by k_ord_mark).  A turn then waits only for the TRAINING of the turns it reads;
+// the DAG is shallow (100k particles: 95 % level 0, 4.8 % level 1, ~160 turns at level 2,
+// a handful at 3; storing every A(j) gives 86 / 12.5 / 1.6 % and 5-6 levels), so a
 // generation runs as
 //
 //   k_ord_plan    per turn: decisions, the source version of each of its reads (src codes)
+//   k_ord_mark    per turn / row: flags the attack outputs reached past the recompute depth
 //   k_ord_levels  per turn: level = 1 + max level of its producers (memoised DFS over the
 //                 src codes), appended to its level's work list (one atomic per wave+level)
-//   k_ord_level   x C launches: the turns of level L, one lane per turn
+//   k_ord_level   x C launches: the turns of level L, one lane (WW(2,2): a lane pair) per turn
 //   k_ord_tail    one wave: the turns of levels >= C in rounds (fence + barrier per round)
 //   k_ord_close   per row: its final version (a row attacked after its own turn ends the
 //                 generation as that attack's output), census class, the next generation's
 //                 decisions linked, block stats for the finish (newborn uids in slot order)
 //
 // Every turn runs the serial loop's per-particle code with the same Philox streams (attack
-// keyed (k, gen*1024+1), SGD (k, gen*1024+512), newborn init respawn_key(gen, k)), so a
-// generation equals OP_SOUP_SEQ bitwise (tests/test_ordered_soup.py, host and device).  No
-// workgroup waits for another: levels are separated by kernel boundaries, the tail's rounds
-// by one wave's own barrier.
+// keyed (k, gen*1024+1), SGD (k, gen*1024+512), newborn init respawn_key(gen, k)), and a
+// recomputed attack output is the same function of the same versions, so a generation
+// equals OP_SOUP_SEQ bitwise (tests/test_ordered_soup.py, host and device).  No workgroup
+// waits for another: levels are separated by kernel boundaries, the tail's rounds by one
+// wave's own barrier.
 #pragma once
 
 namespace ord {
 
-// src codes: >= 0 a version written this generation (2j: A(j) in W3, 2j+1: E(j) in W);
-// -(r+1): the generation-start row r (W2); SELF / ATK: the turn's own current row / its own
-// attack output (learn_from of itself / of its victim); NONE: no such read
+// src codes: >= 0 a version written this generation (2j: A(j), 2j+1: E(j) in W); -(r+1): the
+// generation-start row r (W2); SELF: the turn's own current row (s[1]: a self-attack, s[2]:
+// learn_from itself); ATK: its own attack output (learn_from its victim); NONE: no such read
 constexpr int32_t SRC_SELF = INT32_MIN;
 constexpr int32_t SRC_ATK = INT32_MIN + 1;
 constexpr int32_t SRC_NONE = INT32_MIN + 2;
 constexpr int MAXD = 64;        // DFS stack of the level computation (error bit 1 past it)
 constexpr int MAX_LEVELS = 16;  // parallel level launches per generation (the rest: the tail)
 // o_ctl words: [0, C) list lengths of levels 0..C-1, [C] tail length, [C+1] max level,
-// [C+2] error bits (1: dependency chain deeper than MAXD)
+// [C+2] error bits (1: dependency chain deeper than MAXD, 2: an unstored attack output past
+// the recompute depth -- a marking bug)
 constexpr int CTL_WORDS = MAX_LEVELS + 3;
+// o_src layout: [n][4] {own, victim, teacher, level} then [n] stored flags of A(j)
+constexpr int NPROD = 12;  // producers of one turn: 3 reads x 2^RB leaves
 
 SRNN_HD int32_t code_A(int64_t j) { return (int32_t)(2 * j); }
 SRNN_HD int32_t code_E(int64_t j) { return (int32_t)(2 * j + 1); }
 SRNN_HD int32_t code_G(int64_t r) { return (int32_t)(-(r + 1)); }
-SRNN_HD int64_t producer(int32_t c) { return c >= 0 ? (int64_t)(c >> 1) : -1; }
+SRNN_HD bool is_A(int32_t c) { return c >= 0 && !(c & 1); }
+// a read of a row version (not NONE / SELF / ATK)
+SRNN_HD bool is_row(int32_t c) { return c > SRC_NONE; }
 
 // the last attacker j < k of row r this generation (-1: none); the list is unordered
 SRNN_HD int64_t last_attacker_before(const SrnnArgs& a, int64_t r, int64_t k) {
@@ -74,10 +86,53 @@ SRNN_HD int32_t latest(const SrnnArgs& a, int64_t r, int64_t k) {
   return ja >= 0 ? code_A(ja) : code_G(r);
 }
 
+SRNN_HD const int32_t* src_of(const SrnnArgs& a, int64_t k) { return a.o_src + 4 * k; }
+SRNN_HD bool stored(const SrnnArgs& a, int64_t j) { return a.o_src[4 * a.n + j] != 0; }
+// turn k computes A(k): it attacked, and the attack output is its own row (self-attack),
+// its teacher (learn_from the victim) or read by a turn past the recompute depth
+SRNN_HD bool needs_A(const SrnnArgs& a, int64_t k, const int32_t* s) {
+  return s[1] != SRC_NONE && (s[1] == SRC_SELF || s[2] == SRC_ATK || stored(a, k));
+}
+
+// flag every attack output that the recompute of version `code` (budget B) reaches at depth B
+template <int B>
+SRNN_HD void mark_version(const SrnnArgs& a, int32_t code) {
+  if (!is_A(code)) return;
+  const int64_t j = code >> 1;
+  if constexpr (B == 0) {
+    a.o_src[4 * a.n + j] = 1;
+  } else {
+    const int32_t* sj = src_of(a, j);
+    mark_version<B - 1>(a, sj[0]);
+    if (sj[1] != SRC_SELF) mark_version<B - 1>(a, sj[1]);
+  }
+}
+// the turns whose outputs the materialisation of `code` (budget B) reads; error on an
+// unstored attack output at depth B
+template <int B>
+SRNN_HD void collect(const SrnnArgs& a, int32_t code, int64_t* pr, int& np, bool& bad) {
+  if (code < 0) return;
+  const int64_t j = code >> 1;
+  if ((code & 1) || stored(a, j)) {
+    pr[np++] = j;
+    return;
+  }
+  if constexpr (B == 0) {
+    bad = true;
+  } else {
+    const int32_t* sj = src_of(a, j);
+    collect<B - 1>(a, sj[0], pr, np, bad);
+    if (sj[1] != SRC_SELF) collect<B - 1>(a, sj[1], pr, np, bad);
+  }
+}
+
 template <class Net, class S>
 struct Ord {
   using I = Item<Net, S>;
   static constexpr int P = Net::P;
+  // recompute depth of the attack outputs: two nested outputs for the small nets, one for
+  // the rest (each level doubles the inlined forwards of a read)
+  static constexpr int RB = P <= 20 ? 2 : 1;
 
   SRNN_HD static void read_version(const SrnnArgs& a, int32_t code, float* w) {
     if (code >= 0) {
@@ -88,18 +143,61 @@ struct Ord {
     }
   }
 
-  // src codes of turn k (generation gen) -> o_src[k] = {own, victim, teacher, level = -1}
+  // version `code` into w: a stored version is loaded, an unstored attack output A(j) is
+  // recomputed as f_j(victim) from its own two reads (ap(x, t, o, j): the attack's forward)
+  template <int B, class AP>
+  SRNN_HD static void mat(const SrnnArgs& a, int32_t code, float* w, const AP& ap) {
+    if constexpr (B > 0) {
+      if (is_A(code) && !stored(a, code >> 1)) {
+        const int64_t j = code >> 1;
+        const int32_t* sj = src_of(a, j);
+        float x[P], t[P];
+        mat<B - 1>(a, sj[0], x, ap);
+        if (sj[1] == SRC_SELF) I::copy(t, x);
+        else mat<B - 1>(a, sj[1], t, ap);
+        ap(x, t, w, j);
+        I::q(w);
+        return;
+      }
+    }
+    read_version(a, code, w);
+  }
+
+  // src codes of turn k (generation gen) -> o_src[k] = {own, victim, teacher, level = -1};
+  // its stored flag cleared
   SRNN_HD static void plan(const SrnnArgs& a, int64_t k, int32_t gen) {
     int64_t at, te;
     I::decision(a, k, gen, at, te);
     int32_t* s = a.o_src + 4 * k;
     s[0] = latest(a, k, k);
-    s[1] = (at >= 0 && at != k) ? latest(a, at, k) : SRC_NONE;
+    s[1] = at < 0 ? SRC_NONE : at == k ? SRC_SELF : latest(a, at, k);
     if (te < 0) s[2] = SRC_NONE;
     else if (te == k) s[2] = SRC_SELF;
     else if (te == at) s[2] = SRC_ATK;
     else s[2] = latest(a, te, k);
     s[3] = -1;
+    a.o_src[4 * a.n + k] = 0;
+  }
+
+  // the attack outputs turn k and the close of row k reach past the recompute depth (every
+  // attacker's victim read is walked: whether A(k) is needed depends on these flags)
+  SRNN_HD static void mark(const SrnnArgs& a, int64_t k) {
+    const int32_t* s = src_of(a, k);
+    mark_version<RB>(a, s[0]);
+    if (is_row(s[1])) mark_version<RB>(a, s[1]);
+    if (is_row(s[2])) mark_version<RB>(a, s[2]);
+    const int64_t ja = last_attacker_before(a, k, a.n);
+    if (ja > k) mark_version<RB>(a, code_A(ja));
+  }
+
+  // the turns turn k waits for (after mark)
+  SRNN_HD static int producers(const SrnnArgs& a, int64_t k, int64_t* pr, bool& bad) {
+    const int32_t* s = src_of(a, k);
+    int np = 0;
+    collect<RB>(a, s[0], pr, np, bad);
+    if (needs_A(a, k, s) && is_row(s[1])) collect<RB>(a, s[1], pr, np, bad);
+    if (is_row(s[2])) collect<RB>(a, s[2], pr, np, bad);
+    return np;
   }
 
   // turn k: the serial loop's particle step (soup_seq_one) reading the versions of its plan
@@ -107,17 +205,22 @@ struct Ord {
     const int32_t* s = a.o_src + 4 * k;
     int64_t at, te;
     I::decision(a, k, gen, at, te);
+    auto ap = [&](const float* x, const float* t, float* o, int64_t j) {
+      Net::apply(x, t, o, I::actx(a, c, (uint64_t)j, (uint32_t)gen * 1024u + 1u, perm));
+    };
     float w[P], f[P], o[P];
-    read_version(a, s[0], w);
+    mat<RB>(a, s[0], w, ap);
     int8_t act = A_NONE;
     int64_t cp = -1;
     if (at >= 0) {  // 1. attack: the victim's row becomes f_k(victim) (A(k))
-      if (at == k) I::copy(f, w);
-      else read_version(a, s[1], f);
-      Net::apply(w, f, o, I::actx(a, c, (uint64_t)k, (uint32_t)gen * 1024u + 1u, perm));
-      I::q(o);
-      I::store(I::rowp(a.W3, k), o);
-      if (at == k) I::copy(w, o);
+      if (needs_A(a, k, s)) {
+        if (at == k) I::copy(f, w);
+        else mat<RB>(a, s[1], f, ap);
+        ap(w, f, o, k);
+        I::q(o);
+        if (stored(a, k)) I::store(I::rowp(a.W3, k), o);
+        if (at == k) I::copy(w, o);
+      }
       act = A_ATTACKING;
       cp = at;
     }
@@ -140,7 +243,7 @@ struct Ord {
     if (te >= 0) {  // 2. learn_from the teacher's current row
       if (s[2] == SRC_SELF) I::copy(f, w);
       else if (s[2] == SRC_ATK) I::copy(f, o);
-      else read_version(a, s[2], f);
+      else mat<RB>(a, s[2], f, ap);
       if constexpr (Net::KIND == 0) {
         if (a.severity > 0) loss = Net::template train_epochs<false>(w, f, a.severity, tc);
       } else {
@@ -176,11 +279,14 @@ struct Ord {
 
   // row r after the generation: the last attack after its own turn, else E(r) (in W);
   // consumes r's attack list.  w receives the final row as a reload would see it.
-  SRNN_HD static void close_row(const SrnnArgs& a, int64_t r, float* w) {
+  SRNN_HD static void close_row(const SrnnCfg& c, const SrnnArgs& a, int64_t r, int32_t gen, uint8_t* perm, float* w) {
     const int64_t ja = last_attacker_before(a, r, a.n);
     a.heads[r] = SRNN_NIL;  // consumed: NIL for the generation after next
     if (ja > r) {
-      I::load(I::rowp(a.W3, ja), w);
+      auto ap = [&](const float* x, const float* t, float* o, int64_t j) {
+        Net::apply(x, t, o, I::actx(a, c, (uint64_t)j, (uint32_t)gen * 1024u + 1u, perm));
+      };
+      mat<RB>(a, code_A(ja), w, ap);
       I::store(I::rowp(a.W, r), w);
     } else {
       I::load(I::rowp(a.W, r), w);
@@ -201,6 +307,12 @@ __global__ __launch_bounds__(TB) void k_ord_plan(SrnnCfg, SrnnArgs a) {
   if (k < a.n) ord::Ord<Net, S>::plan(a, k, Item<Net, S>::gen_of(a));
 }
 
+template <class Net, class S>
+__global__ __launch_bounds__(TB) void k_ord_mark(SrnnCfg, SrnnArgs a) {
+  const int64_t k = (int64_t)blockIdx.x * TB + threadIdx.x;
+  if (k < a.n) ord::Ord<Net, S>::mark(a, k);
+}
+
 // level of every turn (memoised DFS: a producer's level another lane already stored is
 // reused, a missing one is computed here -- both give the same value) + the level lists
 template <class Net, class S>
@@ -215,7 +327,7 @@ __global__ __launch_bounds__(TB) void k_ord_levels(SrnnCfg, SrnnArgs a) {
     int32_t stk[ord::MAXD];
     int sp = 0;
     stk[sp++] = (int32_t)k;
-    bool bad = false;
+    bool bad = false, err2 = false;
     while (sp > 0) {
       const int64_t j = stk[sp - 1];
       if (ord::ld_level(src + 4 * j + 3) >= 0) {
@@ -224,10 +336,10 @@ __global__ __launch_bounds__(TB) void k_ord_levels(SrnnCfg, SrnnArgs a) {
       }
       int32_t best = -1;
       bool pushed = false;
-#pragma unroll
-      for (int q = 0; q < 3; ++q) {
-        const int64_t p = ord::producer(src[4 * j + q]);
-        if (p < 0 || pushed) continue;
+      int64_t pr[ord::NPROD];
+      const int np = ord::Ord<Net, S>::producers(a, j, pr, err2);
+      for (int q = 0; q < np && !pushed; ++q) {
+        const int64_t p = pr[q];
         const int32_t lp = ord::ld_level(src + 4 * p + 3);
         if (lp < 0) {
           if (sp == ord::MAXD) {
@@ -246,6 +358,7 @@ __global__ __launch_bounds__(TB) void k_ord_levels(SrnnCfg, SrnnArgs a) {
         --sp;
       }
     }
+    if (err2) atomicOr(a.o_ctl + C + 2, 2);
     if (bad) {
       atomicOr(a.o_ctl + C + 2, 1);
       lv = 0;
@@ -339,7 +452,7 @@ __global__ __launch_bounds__(TB) void k_ord_close(SrnnCfg c, SrnnArgs a) {
   int8_t k = -1;
   if (r < a.n) {
     float w[Net::P];
-    ord::Ord<Net, S>::close_row(a, r, w);
+    ord::Ord<Net, S>::close_row(c, a, r, gen, perm, w);
     rs = a.respawn[r] != 0;
     int64_t at, te;
     I::decision(a, r, gen + 1, at, te);
@@ -367,7 +480,7 @@ __global__ __launch_bounds__(TB) void k_ord_close(SrnnCfg c, SrnnArgs a) {
 
 // OP_SOUP_ORDERED: one sequential (reference-order) generation of a single-rank table.
 // W2: generation-start rows, W: the generation's rows (E versions, then the final table),
-// W3: attack outputs, o_src [n][4], o_list [(C+1) n], o_ctl [CTL_WORDS], o_levels = C;
+// W3: the stored attack outputs, o_src [n][4] + [n] stored flags, o_list [(C+1) n], o_ctl [CTL_WORDS], o_levels = C;
 // heads / nexts: this generation's attack lists (consumed), heads_next / nexts_next: the
 // next generation's (linked here).  Device: the block stats of the two-phase fused
 // generation in temp (SRNN_F_TWO_PHASE); host: the finish inline (uids, census, counter).
@@ -390,16 +503,18 @@ int soup_ordered(const SrnnCfg& c, const SrnnArgs& a) {
     const int32_t gen = I::gen_of(a);
     for (int w = 0; w < ord::CTL_WORDS; ++w) a.o_ctl[w] = 0;
     host_parallel(a.n, [&](int64_t k) { O::plan(a, k, gen); });
+    for (int64_t k = 0; k < a.n; ++k) O::mark(a, k);
     // levels in index order (every producer precedes its consumer)
     std::vector<std::vector<int64_t>> lists((size_t)C + 1);
     int32_t maxl = 0;
     for (int64_t k = 0; k < a.n; ++k) {
       int32_t* s = a.o_src + 4 * k;
+      int64_t pr[ord::NPROD];
+      bool bad = false;
+      const int np = O::producers(a, k, pr, bad);
+      if (bad) a.o_ctl[C + 2] |= 2;
       int32_t lv = 0;
-      for (int q = 0; q < 3; ++q) {
-        const int64_t p = ord::producer(s[q]);
-        if (p >= 0) lv = std::max(lv, a.o_src[4 * p + 3] + 1);
-      }
+      for (int q = 0; q < np; ++q) lv = std::max(lv, a.o_src[4 * pr[q] + 3] + 1);
       s[3] = lv;
       maxl = std::max(maxl, lv);
       lists[(size_t)std::min(lv, C)].push_back(k);
@@ -426,7 +541,7 @@ int soup_ordered(const SrnnCfg& c, const SrnnArgs& a) {
     host_parallel(a.n, [&](int64_t r) {
       float w[Net::P];
       uint8_t perm[Net::P + 4];
-      O::close_row(a, r, w);
+      O::close_row(c, a, r, gen, perm, w);
       if (census)
         ks[(size_t)r] = I::classify_w(w, a.eps, (a.flags & SRNN_F_FIX_SEC) != 0,
                                       I::actx(a, c, (uint64_t)r, 0x7FFFFFF0u, perm));
@@ -466,6 +581,7 @@ int soup_ordered(const SrnnCfg& c, const SrnnArgs& a) {
   hipStream_t st = (hipStream_t)a.stream;
   perm_table<Net>(a);
   hipLaunchKernelGGL((k_ord_plan<Net, S>), dim3((unsigned)nb), dim3(TB), 0, st, c, a);
+  hipLaunchKernelGGL((k_ord_mark<Net, S>), dim3((unsigned)nb), dim3(TB), 0, st, c, a);
   hipLaunchKernelGGL((k_ord_levels<Net, S>), dim3((unsigned)nb), dim3(TB), 0, st, c, a);
   constexpr bool ww22 = std::is_same_v<Net, Weightwise<2, 2>>;
   for (int32_t L = 0; L < C; ++L) {

@@ -311,17 +311,20 @@ __device__ __forceinline__ void turn(const SrnnCfg& c, const SrnnArgs& a, int64_
   const int32_t* s = a.o_src + 4 * k;
   int64_t at, te;
   I::decision(a, k, gen, at, te);
+  auto ap = [&](const float* x, const float* t, float* o, int64_t) { apply(x, t, o, u); };
   float w[P], f[P], o[P];
-  O::read_version(a, s[0], w);
+  O::template mat<O::RB>(a, s[0], w, ap);
   int8_t act = A_NONE;
   int64_t cp = -1;
   if (at >= 0) {
-    if (at == k) I::copy(f, w);
-    else O::read_version(a, s[1], f);
-    apply(w, f, o, u);
-    I::q(o);
-    I::store(I::rowp(a.W3, k), o);
-    if (at == k) I::copy(w, o);
+    if (ord::needs_A(a, k, s)) {
+      if (at == k) I::copy(f, w);
+      else O::template mat<O::RB>(a, s[1], f, ap);
+      apply(w, f, o, u);
+      I::q(o);
+      if (ord::stored(a, k)) I::store(I::rowp(a.W3, k), o);
+      if (at == k) I::copy(w, o);
+    }
     act = A_ATTACKING;
     cp = at;
   }
@@ -330,7 +333,7 @@ __device__ __forceinline__ void turn(const SrnnCfg& c, const SrnnArgs& a, int64_
   if (te >= 0) {
     if (s[2] == ord::SRC_SELF) I::copy(f, w);
     else if (s[2] == ord::SRC_ATK) I::copy(f, o);
-    else O::read_version(a, s[2], f);
+    else O::template mat<O::RB>(a, s[2], f, ap);
   }
   const float loss = learn_and_train<S>(a, w, f, te >= 0, tc, u, sp);
   if (te >= 0) {

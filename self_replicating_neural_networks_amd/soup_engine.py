@@ -369,17 +369,20 @@ class SoupEngine:
         C = int(self.execution.order_levels)
         self.order_levels = C
         self._abuf = torch.zeros((self.n, self.spec.PP), dtype=self.dtype, device=dev)
-        self._osrc = torch.zeros(4 * max(self.n, 1), dtype=torch.int32, device=dev)
+        self._osrc = torch.zeros(5 * max(self.n, 1), dtype=torch.int32, device=dev)  # [n][4] + stored flags
         self._olist = torch.zeros((C + 1) * max(self.n, 1), dtype=torch.int32, device=dev)
         self._octl = torch.zeros(_lib.ORD_CTL_WORDS, dtype=torch.int32, device=dev)
         self._rec_rows = None  # recording: every particle's state before any respawn
 
     def ordered_levels(self) -> Dict[str, int]:
         """Dependency levels of the last reference-order generation: turns per parallel level,
-        the tail's turns, the deepest level, error bits (1: a chain deeper than the DFS stack)."""
+        the tail's turns, the deepest level, error bits (1: a chain deeper than the DFS stack,
+        2: an attack output past the recompute depth left unstored), and how many attack outputs
+        were stored for later turns (the others are recomputed by the turns that read them)."""
         c = self._octl.cpu().tolist()
         C = self.order_levels
-        return dict(levels=c[:C], tail=c[C], max_level=c[C + 1], error=c[C + 2])
+        stored = int(self._osrc[4 * self.n:5 * self.n].sum().item()) if self.n else 0
+        return dict(levels=c[:C], tail=c[C], max_level=c[C + 1], error=c[C + 2], stored_attacks=stored)
 
     def _init_x2(self, n_links):
         dev, R = self.device, self.dist.world
@@ -915,9 +918,12 @@ class SoupEngine:
         err = self.exchange_error()
         if err:
             raise RuntimeError(f"soup row exchange failed ({err}): results are invalid")
-        if self.order == "sequential" and self.ordered_levels()["error"]:
-            raise RuntimeError("reference-order generation: a dependency chain exceeded the level DFS stack; "
-                               "results are invalid")
+        if self.order == "sequential":
+            e = int(self._octl[self.order_levels + 2].item())
+            if e:
+                raise RuntimeError(f"reference-order generation: error bits {e} (1: a dependency chain exceeded the "
+                                   "level DFS stack, 2: an unstored attack output past the recompute depth); "
+                                   "results are invalid")
         c = torch.zeros(6, dtype=torch.int64, device=self.device)
         cls, _ = K.classify(self.spec, self.local_rows(), self.eps, with_sec, uid=None, seed=self.seed,
                             scratch=self._scratch, ctr=0x7FFFFFF0, counts=c, key_offset=self.lo)
