@@ -15,10 +15,13 @@ mkdir -p gpurun_out
 export TMPDIR=/tmp
 TAG=${1:-r4}
 timeout -k 10 600 python -u -m pytest tests/test_ordered_soup.py tests/test_pair_soup_gpu.py tests/test_ww_wave_gpu.py \
-  tests/test_sharded_gpu.py tests/test_sharded_multirank_gpu.py tests/test_kernels_gpu.py -m gpu -x -v \
+  tests/test_sharded_gpu.py tests/test_sharded_multirank_gpu.py tests/test_kernels_gpu.py -m gpu --maxfail=6 -v \
   --timeout 240 --timeout-method thread > gpurun_out/pytest_$TAG.log 2>&1
 rc=$?; grep -E "passed|failed|error" gpurun_out/pytest_$TAG.log | tail -3
-if [ $rc -ne 0 ]; then grep -B5 -A30 "FAILED\|Error" gpurun_out/pytest_$TAG.log | head -60; echo "pytest rc=$rc: stopping"; exit $rc; fi
+# test failures (rc 1) are reported and the measurements still run; anything else (a fault,
+# an abort, a timeout) ends the script
+if [ $rc -ne 0 ]; then grep -E "^(FAILED|ERROR)" gpurun_out/pytest_$TAG.log | head -20; fi
+if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "pytest rc=$rc: stopping"; exit $rc; fi
 timeout -k 10 300 python bench.py --steps 20 --warmup 5 --reference-order-steps -1 > gpurun_out/bench_$TAG.log 2>&1 || exit 1
 tail -1 gpurun_out/bench_$TAG.log | cut -c1-400
 # strong-scaling model of one rank at N = 2 / 4 / 8 (100k / N slots, the remote-dependent fraction

@@ -131,7 +131,8 @@ def test_device_ordered_generation_is_the_serial_loop(spec):
     n, seed = 3000, 7
     for graphs in (False, True):
         o = SoupEngine(spec, n, HOT, device="cuda", seed=seed, order="sequential")
-        s = SequentialSoupEngine(spec, n, HOT, seed=seed, device="cuda")
+        # the same starting rows (the device init contracts a*b+c, the host's does not)
+        s = SequentialSoupEngine(spec, n, HOT, seed=seed, device="cuda", weights=o.local_rows()[:, :spec.P].cpu())
         if graphs:
             assert o.capture(warmup=1)
             s.evolve(1)  # capture runs one warmup generation eagerly
@@ -149,7 +150,8 @@ def test_device_ordered_tail_and_bf16_tables():
     spec = ArchSpec.weightwise(2, 2)
     o = SoupEngine(spec, 2000, HOT, device="cuda", seed=2, order="sequential", dtype=torch.bfloat16,
                    execution=ExecConfig(order_levels=1))
-    s = SequentialSoupEngine(spec, 2000, HOT, seed=2, dtype=torch.bfloat16, device="cuda")
+    s = SequentialSoupEngine(spec, 2000, HOT, seed=2, dtype=torch.bfloat16, device="cuda",
+                             weights=o.local_rows()[:, :spec.P].cpu())
     for _ in range(3):
         o.evolve(1)
         s.evolve(1)
@@ -164,7 +166,7 @@ def test_device_ordered_headline_soup_matches_serial_loop():
     spec = ArchSpec.weightwise(2, 2)
     p = dict(attacking_rate=0.1, learn_from_rate=0.1, train=20, remove_divergent=True, remove_zero=True, epsilon=1e-4)
     o = SoupEngine(spec, 20_000, p, device="cuda", seed=0, order="sequential")
-    s = SequentialSoupEngine(spec, 20_000, p, seed=0, device="cuda")
+    s = SequentialSoupEngine(spec, 20_000, p, seed=0, device="cuda", weights=o.local_rows()[:, :spec.P].cpu())
     o.evolve(2)
     s.evolve(2)
     _same(o, s, spec.P)
