@@ -223,6 +223,7 @@ def main(argv=None):
                        "collectives": comm if comm is not None
                        else (f"torch.distributed ({backend})" if d.enabled else None),
                        "world_size": d.world, "execution": execution.in_force(),
+                       "perm_table_in_use": eng._perm_table() is not None,
                        "overlap": getattr(eng, "overlap", False),
                        "sharded_schedule": getattr(eng, "schedule", None) if getattr(eng, "x2", False) else None,
                        "census_every_step": eng.stats, "final_census": census, "order": args.order,

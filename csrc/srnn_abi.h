@@ -189,7 +189,7 @@ enum SrnnOp {
                         // bitwise OP_SOUP_SEQ, every particle of a level in parallel (srnn_ordered.h)
 };
 
-int srnn_abi_version();  // 20
+int srnn_abi_version();  // 21
 int64_t srnn_args_size();  // sizeof(SrnnArgs): the ctypes mirror checks its layout against it
 int64_t srnn_cfg_size();
 int srnn_has_config(const SrnnCfg* cfg);

@@ -200,7 +200,7 @@ static int with_scratch(int op, const SrnnCfg* c, const SrnnArgs* a) {
 
 extern "C" {
 
-int srnn_abi_version() { return 20; }
+int srnn_abi_version() { return 21; }
 
 // layout check of the ctypes mirror (ops/_lib.py): sizeof(SrnnArgs) / sizeof(SrnnCfg)
 int64_t srnn_args_size() { return (int64_t)sizeof(SrnnArgs); }

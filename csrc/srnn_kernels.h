@@ -749,10 +749,9 @@ constexpr int TBP = 256;
 template <class Net>
 __global__ __launch_bounds__(TBP) void k_perm_table(SrnnArgs a, int32_t E) {
   constexpr int P = Net::P;
-  const int64_t npair = (E + 1) / 2;
-  const int64_t t = (int64_t)blockIdx.x * TBP + threadIdx.x;
-  if (t >= a.n * npair) return;
-  const int64_t row = t % a.n, p = t / a.n;
+  // grid (rows, epoch pairs): no 64-bit division on the index
+  const int64_t row = (int64_t)blockIdx.x * TBP + threadIdx.x, p = blockIdx.y;
+  if (row >= a.n) return;
   const int32_t gen = a.gen_ptr ? a.gen_ptr[0] : a.gen;
   const uint32_t c0 = (uint32_t)gen * 1024u + 512u + 2u * (uint32_t)p;  // even: one draw, two epochs
   const Rng rng{(uint32_t)a.seed, (uint32_t)(a.seed >> 32)};
@@ -768,9 +767,8 @@ int perm_table(const SrnnArgs& a) {
   } else {
     const int32_t E = (a.severity > 0 ? a.severity : 0) + (a.epochs > 0 ? a.epochs : 0);
     if (!a.ptab || !a.dev || !(a.flags & SRNN_F_SHUFFLE) || E <= 0 || a.n <= 0) return 0;
-    const int64_t threads = a.n * ((E + 1) / 2);
-    hipLaunchKernelGGL((k_perm_table<Net>), dim3((unsigned)((threads + TBP - 1) / TBP)), dim3(TBP), 0,
-                       (hipStream_t)a.stream, a, E);
+    hipLaunchKernelGGL((k_perm_table<Net>), dim3((unsigned)((a.n + TBP - 1) / TBP), (unsigned)((E + 1) / 2)),
+                       dim3(TBP), 0, (hipStream_t)a.stream, a, E);
     return 0;
   }
 }

@@ -29,10 +29,13 @@
 //
 //   k_ord_plan    per turn: decisions, the source version of each of its reads (src codes)
 //   k_ord_mark    per turn / row: flags the attack outputs reached past the recompute depth
-//   k_ord_levels  per turn: level = 1 + max level of its producers (memoised DFS over the
-//                 src codes), appended to its level's work list (one atomic per wave+level)
-//   k_ord_level   x C launches: the turns of level L, one lane (WW(2,2): a lane pair) per turn
-//   k_ord_tail    one wave: the turns of levels >= C in rounds (fence + barrier per round)
+//   k_ord_sort    per turn: its producers; none -> level 0's list, else a pending record
+//                 {turn, producers} (one atomic per wave and list)
+//   k_ord_level   L = 0: the level-0 list, one lane per turn; L = 1..C-1: a pass over the
+//                 pending records -- a record whose producers all ran at levels < L runs now
+//                 (WW(2,2): on a lane pair); no level is computed ahead, no DFS
+//   k_ord_tail    one workgroup: the records still pending after C-1, in rounds (fence +
+//                 barrier per round)
 //   k_ord_close   per row: its final version (a row attacked after its own turn ends the
 //                 generation as that attack's output), census class, the next generation's
 //                 decisions linked, block stats for the finish (newborn uids in slot order)
@@ -53,14 +56,18 @@ namespace ord {
 constexpr int32_t SRC_SELF = INT32_MIN;
 constexpr int32_t SRC_ATK = INT32_MIN + 1;
 constexpr int32_t SRC_NONE = INT32_MIN + 2;
-constexpr int MAXD = 64;        // DFS stack of the level computation (error bit 1 past it)
 constexpr int MAX_LEVELS = 16;  // parallel level launches per generation (the rest: the tail)
-// o_ctl words: [0, C) list lengths of levels 0..C-1, [C] tail length, [C+1] max level,
-// [C+2] error bits (1: dependency chain deeper than MAXD, 2: an unstored attack output past
-// the recompute depth -- a marking bug)
-constexpr int CTL_WORDS = MAX_LEVELS + 3;
-// o_src layout: [n][4] {own, victim, teacher, level} then [n] stored flags of A(j)
+// o_ctl words: [0, C) turns run at levels 0..C-1, [TAILW] turns run by the tail, [MAXLW] max
+// level, [ERRW] error bits (2: an unstored attack output past the recompute depth -- a marking
+// bug, 4: the tail found no runnable turn among the pending ones), [REM0 + L] turns still
+// pending after level launch L (L = 0: the sort pass; also the pending records' append counter)
+constexpr int TAILW = MAX_LEVELS, MAXLW = MAX_LEVELS + 1, ERRW = MAX_LEVELS + 2, REM0 = MAX_LEVELS + 3;
+constexpr int CTL_WORDS = 2 * MAX_LEVELS + 3;
+// o_src layout: [n][4] {own, victim, teacher, level} | [n] stored flags of A(j) | [n][16]
+// pending records {turn, producer count, producers...}; o_list: [n] level-0 turns | [n] the
+// tail's records
 constexpr int NPROD = 12;  // producers of one turn: 3 reads x 2^RB leaves
+constexpr int REC = 16;
 
 SRNN_HD int32_t code_A(int64_t j) { return (int32_t)(2 * j); }
 SRNN_HD int32_t code_E(int64_t j) { return (int32_t)(2 * j + 1); }
@@ -87,6 +94,7 @@ SRNN_HD int32_t latest(const SrnnArgs& a, int64_t r, int64_t k) {
 }
 
 SRNN_HD const int32_t* src_of(const SrnnArgs& a, int64_t k) { return a.o_src + 4 * k; }
+SRNN_HD int32_t* pend(const SrnnArgs& a, int64_t q) { return a.o_src + 5 * a.n + REC * q; }
 SRNN_HD bool stored(const SrnnArgs& a, int64_t j) { return a.o_src[4 * a.n + j] != 0; }
 // turn k computes A(k): it attacked, and the attack output is its own row (self-attack),
 // its teacher (learn_from the victim) or read by a turn past the recompute depth
@@ -110,11 +118,12 @@ SRNN_HD void mark_version(const SrnnArgs& a, int32_t code) {
 // the turns whose outputs the materialisation of `code` (budget B) reads; error on an
 // unstored attack output at depth B
 template <int B>
-SRNN_HD void collect(const SrnnArgs& a, int32_t code, int64_t* pr, int& np, bool& bad) {
+SRNN_HD void collect(const SrnnArgs& a, int32_t code, int32_t* pr, int& np, bool& bad) {
   if (code < 0) return;
   const int64_t j = code >> 1;
   if ((code & 1) || stored(a, j)) {
-    pr[np++] = j;
+    if (pr) pr[np] = (int32_t)j;  // (nullptr: count only)
+    ++np;
     return;
   }
   if constexpr (B == 0) {
@@ -191,7 +200,7 @@ struct Ord {
   }
 
   // the turns turn k waits for (after mark)
-  SRNN_HD static int producers(const SrnnArgs& a, int64_t k, int64_t* pr, bool& bad) {
+  SRNN_HD static int producers(const SrnnArgs& a, int64_t k, int32_t* pr, bool& bad) {
     const int32_t* s = src_of(a, k);
     int np = 0;
     collect<RB>(a, s[0], pr, np, bad);
@@ -297,6 +306,129 @@ struct Ord {
 __device__ __forceinline__ int32_t ld_level(const int32_t* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
+__device__ __forceinline__ void st_level(int32_t* p, int32_t v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ int32_t ld_ctl(const int32_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// all producers of pending record rec have levels in [0, L)
+__device__ __forceinline__ bool ready(const SrnnArgs& a, const int32_t* rec, int32_t L) {
+  const int np = rec[1];
+  bool ok = true;
+  for (int q = 0; q < np; ++q) {
+    const int32_t lp = ld_level(a.o_src + 4 * (int64_t)rec[2 + q] + 3);
+    ok = ok && lp >= 0 && lp < L;
+  }
+  return ok;
+}
+
+// wave-aggregated append: this lane's position among the wave's `want` lanes after one
+// atomicAdd on ctr (every lane of the wave calls it)
+__device__ __forceinline__ int32_t wave_append(int32_t* ctr, bool want) {
+  const unsigned long long m = __ballot(want);
+  if (!m) return -1;
+  const int lane = threadIdx.x & 63, leader = __ffsll((long long)m) - 1;
+  int32_t base = 0;
+  if (lane == leader) base = atomicAdd(ctr, (int32_t)__popcll(m));
+  base = __shfl(base, leader);
+  return want ? base + (int32_t)__popcll(m & ((1ull << lane) - 1ull)) : -1;
+}
+__device__ __forceinline__ int32_t wave_sum(int32_t v) {
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+  return v;
+}
+
+// level launch L >= 1 over the pending records, TPT threads per turn (1: lane, 2: pair):
+// a record whose producers all have levels < L runs now (its level becomes L); the others stay
+// pending (counted in REM(L); the last parallel launch also lists them for the tail)
+template <int TPT, class F>
+__device__ __forceinline__ void pending_pass(const SrnnArgs& a, int32_t L, F&& run) {
+  if (ld_ctl(a.o_ctl + REM0 + L - 1) == 0) return;  // nothing left: REM(L) stays 0
+  const bool last = L == a.o_levels - 1;
+  const int64_t P = ld_ctl(a.o_ctl + REM0);
+  const int slots = (int)blockDim.x / TPT, slot = (int)threadIdx.x / TPT, sub = (int)threadIdx.x % TPT;
+  int32_t ex = 0;
+  for (int64_t base = (int64_t)blockIdx.x * slots; base < P; base += (int64_t)gridDim.x * slots) {
+    const int64_t q = base + slot;
+    bool left = false;
+    if (q < P) {
+      const int32_t* rec = pend(a, q);
+      const int64_t k = rec[0];
+      if (ld_level(a.o_src + 4 * k + 3) < 0) {
+        if (ready(a, rec, L)) {
+          run(k);
+          if (sub == 0) {
+            st_level(a.o_src + 4 * k + 3, L);
+            ++ex;
+          }
+        } else {
+          left = sub == 0;
+        }
+      }
+    }
+    const int32_t pos = wave_append(a.o_ctl + REM0 + L, left);
+    if (last && left) a.o_list[a.n + pos] = (int32_t)q;  // the tail's list
+  }
+  ex = wave_sum(ex);
+  if ((threadIdx.x & 63) == 0 && ex) {
+    atomicAdd(a.o_ctl + L, ex);
+    atomicMax(a.o_ctl + MAXLW, L);
+  }
+}
+
+// levels >= C in one workgroup, round by round over the tail's list: the rows a round writes
+// are released before the barrier and the L1 is invalidated after it.  A round that runs
+// nothing while turns are left (no DAG: a bug) sets error bit 4 and stops -- never a hang.
+template <int TPT, class F>
+__device__ __forceinline__ void tail_rounds(const SrnnArgs& a, F&& run) {
+  const int C = a.o_levels;
+  const int64_t T = ld_ctl(a.o_ctl + REM0 + C - 1);
+  if (T == 0) return;
+  __shared__ int32_t s_cnt[2];
+  const int slots = (int)blockDim.x / TPT, slot = (int)threadIdx.x / TPT, sub = (int)threadIdx.x % TPT;
+  const int32_t* tl = a.o_list + a.n;
+  for (int32_t lv = C;; ++lv) {
+    if (threadIdx.x == 0) s_cnt[0] = s_cnt[1] = 0;
+    __syncthreads();
+    int32_t ex = 0, left = 0;
+    for (int64_t q0 = 0; q0 < T; q0 += slots) {
+      const int64_t q = q0 + slot;
+      if (q < T) {
+        const int32_t* rec = pend(a, tl[q]);
+        const int64_t k = rec[0];
+        if (ld_level(a.o_src + 4 * k + 3) < 0) {
+          if (ready(a, rec, lv)) {
+            run(k);
+            if (sub == 0) {
+              st_level(a.o_src + 4 * k + 3, lv);
+              ++ex;
+            }
+          } else if (sub == 0) {
+            ++left;
+          }
+        }
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    if (ex) atomicAdd(&s_cnt[0], ex);
+    if (left) atomicAdd(&s_cnt[1], left);
+    __syncthreads();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    const int32_t ext = s_cnt[0], lt = s_cnt[1];
+    if (threadIdx.x == 0 && ext) {
+      a.o_ctl[TAILW] += ext;
+      a.o_ctl[MAXLW] = lv;
+    }
+    if (lt == 0) break;
+    if (ext == 0) {
+      if (threadIdx.x == 0) atomicOr(a.o_ctl + ERRW, 4);
+      break;
+    }
+    __syncthreads();  // s_cnt is reset by the next round
+  }
+}
 
 }  // namespace ord
 
@@ -304,6 +436,7 @@ template <class Net, class S>
 __global__ __launch_bounds__(TB) void k_ord_plan(SrnnCfg, SrnnArgs a) {
   const int64_t k = (int64_t)blockIdx.x * TB + threadIdx.x;
   if (blockIdx.x == 0 && threadIdx.x < ord::CTL_WORDS) a.o_ctl[threadIdx.x] = 0;  // read from the next launch on
+  if (blockIdx.x == 0 && threadIdx.x + TB < ord::CTL_WORDS) a.o_ctl[threadIdx.x + TB] = 0;
   if (k < a.n) ord::Ord<Net, S>::plan(a, k, Item<Net, S>::gen_of(a));
 }
 
@@ -313,81 +446,31 @@ __global__ __launch_bounds__(TB) void k_ord_mark(SrnnCfg, SrnnArgs a) {
   if (k < a.n) ord::Ord<Net, S>::mark(a, k);
 }
 
-// level of every turn (memoised DFS: a producer's level another lane already stored is
-// reused, a missing one is computed here -- both give the same value) + the level lists
+// the turns without producers -> level 0 (list 0); the others -> pending records (their
+// producers counted, then written straight into the record: no private arrays)
 template <class Net, class S>
-__global__ __launch_bounds__(TB) void k_ord_levels(SrnnCfg, SrnnArgs a) {
+__global__ __launch_bounds__(TB) void k_ord_sort(SrnnCfg, SrnnArgs a) {
+  using O = ord::Ord<Net, S>;
   const int64_t k = (int64_t)blockIdx.x * TB + threadIdx.x;
-  const int lane = threadIdx.x;
-  const int C = a.o_levels;
   const bool valid = k < a.n;
-  int32_t lv = 0;
-  if (valid) {
-    int32_t* src = a.o_src;
-    int32_t stk[ord::MAXD];
-    int sp = 0;
-    stk[sp++] = (int32_t)k;
-    bool bad = false, err2 = false;
-    while (sp > 0) {
-      const int64_t j = stk[sp - 1];
-      if (ord::ld_level(src + 4 * j + 3) >= 0) {
-        --sp;
-        continue;
-      }
-      int32_t best = -1;
-      bool pushed = false;
-      int64_t pr[ord::NPROD];
-      const int np = ord::Ord<Net, S>::producers(a, j, pr, err2);
-      for (int q = 0; q < np && !pushed; ++q) {
-        const int64_t p = pr[q];
-        const int32_t lp = ord::ld_level(src + 4 * p + 3);
-        if (lp < 0) {
-          if (sp == ord::MAXD) {
-            bad = true;
-            break;
-          }
-          stk[sp++] = (int32_t)p;
-          pushed = true;
-        } else {
-          best = lp > best ? lp : best;
-        }
-      }
-      if (bad) break;
-      if (!pushed) {
-        __hip_atomic_store(src + 4 * j + 3, best + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        --sp;
-      }
-    }
-    if (err2) atomicOr(a.o_ctl + C + 2, 2);
-    if (bad) {
-      atomicOr(a.o_ctl + C + 2, 1);
-      lv = 0;
-    } else {
-      lv = ord::ld_level(src + 4 * k + 3);
-    }
+  int np = 0;
+  bool bad = false;
+  if (valid) np = O::producers(a, k, nullptr, bad);
+  if (bad) atomicOr(a.o_ctl + ord::ERRW, 2);
+  if (valid && np == 0) ord::st_level(a.o_src + 4 * k + 3, 0);
+  const int32_t p0 = ord::wave_append(a.o_ctl + 0, valid && np == 0);
+  if (p0 >= 0) a.o_list[p0] = (int32_t)k;
+  const int32_t pq = ord::wave_append(a.o_ctl + ord::REM0, valid && np > 0);
+  if (pq >= 0) {
+    int32_t* rec = ord::pend(a, pq);
+    rec[0] = (int32_t)k;
+    bool bad2 = false;
+    rec[1] = O::producers(a, k, rec + 2, bad2);
+    if (a.o_levels == 1) a.o_list[a.n + pq] = pq;  // no parallel level after 0: all to the tail
   }
-  // append to the list of min(level, C): one atomic per (wave, list)
-  const int32_t L = lv < C ? lv : C;
-  unsigned long long rem = __ballot(valid);
-  while (rem) {
-    const int leader = __ffsll((long long)rem) - 1;
-    const int32_t Ll = __shfl(L, leader);
-    const unsigned long long m = __ballot(valid && L == Ll);
-    int32_t base = 0;
-    if (lane == leader) base = atomicAdd(a.o_ctl + Ll, (int32_t)__popcll(m));
-    base = __shfl(base, leader);
-    if (valid && L == Ll) a.o_list[(int64_t)Ll * a.n + base + __popcll(m & ((1ull << lane) - 1ull))] = (int32_t)k;
-    rem &= ~m;
-  }
-  int32_t mx = valid ? lv : 0;
-  for (int off = 32; off > 0; off >>= 1) {
-    const int32_t y = __shfl_xor(mx, off);
-    mx = y > mx ? y : mx;
-  }
-  if (lane == 0 && mx >= C) atomicMax(a.o_ctl + C + 1, mx);
 }
 
-// the turns of level L (grid-stride over its list)
+// level L: L = 0 the list of turns without producers, L >= 1 a pass over the pending records
 template <class Net, class S>
 __global__ __launch_bounds__(TB) void k_ord_level(SrnnCfg c, SrnnArgs a, int32_t L) {
   using I = Item<Net, S>;
@@ -397,18 +480,20 @@ __global__ __launch_bounds__(TB) void k_ord_level(SrnnCfg c, SrnnArgs a, int32_t
   __shared__ uint8_t s_perm[TB * PERM];
   const int lane = threadIdx.x;
   const int32_t gen = I::gen_of(a);
-  const int64_t cnt = *(volatile const int32_t*)(a.o_ctl + L);
-  const int32_t* list = a.o_list + (int64_t)L * a.n;
-  for (int64_t base = (int64_t)blockIdx.x * TB; base < cnt; base += (int64_t)gridDim.x * TB) {
-    const int64_t q = base + lane;
-    if (q < cnt)
-      ord::Ord<Net, S>::turn(c, a, list[q], gen, samp_lane<Net>(s_samp, lane), s_perm + lane * PERM);
+  float4* samp = samp_lane<Net>(s_samp, lane);
+  uint8_t* perm = s_perm + lane * PERM;
+  if (L == 0) {
+    const int64_t cnt = ord::ld_ctl(a.o_ctl);
+    for (int64_t base = (int64_t)blockIdx.x * TB; base < cnt; base += (int64_t)gridDim.x * TB) {
+      const int64_t q = base + lane;
+      if (q < cnt) ord::Ord<Net, S>::turn(c, a, a.o_list[q], gen, samp, perm);
+    }
+    return;
   }
+  ord::pending_pass<1>(a, L, [&](int64_t k) { ord::Ord<Net, S>::turn(c, a, k, gen, samp, perm); });
 }
 
-// levels >= C: one wave, level by level; the versions a round writes are released before the
-// barrier and the wave's L1 is invalidated after it (rows share cache lines with rows
-// written by earlier rounds)
+// levels >= C: one wave
 template <class Net, class S>
 __global__ __launch_bounds__(TB) void k_ord_tail(SrnnCfg c, SrnnArgs a) {
   using I = Item<Net, S>;
@@ -417,22 +502,10 @@ __global__ __launch_bounds__(TB) void k_ord_tail(SrnnCfg c, SrnnArgs a) {
   __shared__ float4 s_samp[TB * SAMP];
   __shared__ uint8_t s_perm[TB * PERM];
   const int lane = threadIdx.x;
-  const int C = a.o_levels;
-  const int64_t cnt = *(volatile const int32_t*)(a.o_ctl + C);
-  if (cnt == 0) return;
-  const int32_t maxl = *(volatile const int32_t*)(a.o_ctl + C + 1);
   const int32_t gen = I::gen_of(a);
-  const int32_t* list = a.o_list + (int64_t)C * a.n;
-  for (int32_t lv = C; lv <= maxl; ++lv) {
-    for (int64_t q = lane; q < cnt; q += TB) {
-      const int64_t k = list[q];
-      if (ord::ld_level(a.o_src + 4 * k + 3) == lv)
-        ord::Ord<Net, S>::turn(c, a, k, gen, samp_lane<Net>(s_samp, lane), s_perm + lane * PERM);
-    }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    __syncthreads();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-  }
+  float4* samp = samp_lane<Net>(s_samp, lane);
+  uint8_t* perm = s_perm + lane * PERM;
+  ord::tail_rounds<1>(a, [&](int64_t k) { ord::Ord<Net, S>::turn(c, a, k, gen, samp, perm); });
 }
 
 // final rows, census, next decisions, block stats (the fused generation's two-phase form:
@@ -509,18 +582,19 @@ int soup_ordered(const SrnnCfg& c, const SrnnArgs& a) {
     int32_t maxl = 0;
     for (int64_t k = 0; k < a.n; ++k) {
       int32_t* s = a.o_src + 4 * k;
-      int64_t pr[ord::NPROD];
+      int32_t pr[ord::NPROD];
       bool bad = false;
       const int np = O::producers(a, k, pr, bad);
-      if (bad) a.o_ctl[C + 2] |= 2;
+      if (bad) a.o_ctl[ord::ERRW] |= 2;
       int32_t lv = 0;
-      for (int q = 0; q < np; ++q) lv = std::max(lv, a.o_src[4 * pr[q] + 3] + 1);
+      for (int q = 0; q < np; ++q) lv = std::max(lv, a.o_src[4 * (int64_t)pr[q] + 3] + 1);
       s[3] = lv;
       maxl = std::max(maxl, lv);
       lists[(size_t)std::min(lv, C)].push_back(k);
     }
-    for (int32_t L = 0; L <= C; ++L) a.o_ctl[L] = (int32_t)lists[(size_t)L].size();
-    a.o_ctl[C + 1] = maxl;
+    for (int32_t L = 0; L < C; ++L) a.o_ctl[L] = (int32_t)lists[(size_t)L].size();
+    a.o_ctl[ord::TAILW] = (int32_t)lists[(size_t)C].size();
+    a.o_ctl[ord::MAXLW] = maxl;
     auto run_turn = [&](int64_t k) {
       float4 samp[Net::P + 1];
       uint8_t perm[Net::P + 4];
@@ -582,26 +656,27 @@ int soup_ordered(const SrnnCfg& c, const SrnnArgs& a) {
   perm_table<Net>(a);
   hipLaunchKernelGGL((k_ord_plan<Net, S>), dim3((unsigned)nb), dim3(TB), 0, st, c, a);
   hipLaunchKernelGGL((k_ord_mark<Net, S>), dim3((unsigned)nb), dim3(TB), 0, st, c, a);
-  hipLaunchKernelGGL((k_ord_levels<Net, S>), dim3((unsigned)nb), dim3(TB), 0, st, c, a);
+  hipLaunchKernelGGL((k_ord_sort<Net, S>), dim3((unsigned)nb), dim3(TB), 0, st, c, a);
   constexpr bool ww22 = std::is_same_v<Net, Weightwise<2, 2>>;
-  for (int32_t L = 0; L < C; ++L) {
-    // level L holds ~n / 7^L turns at the reference's rates: a grid that covers it in one
-    // pass, grid-stride beyond (any count is processed); the small levels of WW(2,2) run on
-    // lane pairs (latency-bound: srnn_pair.h)
-    int64_t blocks = L == 0 ? nb : std::max<int64_t>(64, nb >> (2 * L));
-    blocks = std::min(blocks, nb);
-    bool pairs = false;
-    if constexpr (ww22) pairs = L > 0 && use_pairs(a.n >> (2 * L + 1));
+  hipLaunchKernelGGL((k_ord_level<Net, S>), dim3((unsigned)nb), dim3(TB), 0, st, c, a, 0);
+  // levels >= 1 pass over the pending records (~5 % of the turns at the reference's rates, most
+  // of them level 1): a grid covering 8 % of n in one pass, grid-stride beyond; WW(2,2) on lane
+  // pairs (latency-bound: srnn_pair.h)
+  const int64_t est = std::max<int64_t>(a.n / 12, 1);
+  bool pairs = false;
+  if constexpr (ww22) pairs = use_pairs(a.n / 20);
+  for (int32_t L = 1; L < C; ++L) {
     if (pairs) {
-      if constexpr (ww22)
+      if constexpr (ww22) {
+        const int64_t blocks = std::min<int64_t>(std::max<int64_t>(16, (est + 63) / 64), (a.n + 63) / 64);
         hipLaunchKernelGGL((k_ord_level2<S>), dim3((unsigned)blocks), dim3(pair::TBW), 0, st, c, a, L);
+      }
     } else {
+      const int64_t blocks = std::min<int64_t>(std::max<int64_t>(16, (est + TB - 1) / TB), nb);
       hipLaunchKernelGGL((k_ord_level<Net, S>), dim3((unsigned)blocks), dim3(TB), 0, st, c, a, L);
     }
   }
-  bool tail_pairs = false;
-  if constexpr (ww22) tail_pairs = use_pairs(0);
-  if (tail_pairs) {
+  if (pairs) {
     if constexpr (ww22) hipLaunchKernelGGL((k_ord_tail2<S>), dim3(1), dim3(pair::TBW), 0, st, c, a);
   } else {
     hipLaunchKernelGGL((k_ord_tail<Net, S>), dim3(1), dim3(TB), 0, st, c, a);

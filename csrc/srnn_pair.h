@@ -421,46 +421,25 @@ __global__ __launch_bounds__(pair::TBW) void k_soup_gen2(SrnnCfg c, SrnnArgs a) 
   }
 }
 
-// reference-order level L on pairs (grid-stride over the level's list, 64 turns per workgroup)
+// reference-order level L >= 1 on pairs (a pass over the pending records, 64 turns per
+// workgroup; level 0 runs on lanes)
 template <class S>
 __global__ __launch_bounds__(pair::TBW) void k_ord_level2(SrnnCfg c, SrnnArgs a, int32_t L) {
   using I = Item<pair::WW22, S>;
   __shared__ float4 s_samp[pair::P * 64];
   const int tid = threadIdx.x, u = tid & 1, pi = tid >> 1;
   const int32_t gen = I::gen_of(a);
-  const int64_t cnt = *(volatile const int32_t*)(a.o_ctl + L);
-  const int32_t* list = a.o_list + (int64_t)L * a.n;
-  for (int64_t base = (int64_t)blockIdx.x * 64; base < cnt; base += (int64_t)gridDim.x * 64) {
-    const int64_t q = base + pi;
-    if (q < cnt) pair::turn<S>(c, a, list[q], gen, u, s_samp + pi);
-  }
+  ord::pending_pass<2>(a, L, [&](int64_t k) { pair::turn<S>(c, a, k, gen, u, s_samp + pi); });
 }
 
-// the reference-order tail (levels >= C) on pairs: one workgroup, level by level
+// the reference-order tail (levels >= C) on pairs: one workgroup, round by round
 template <class S>
 __global__ __launch_bounds__(pair::TBW) void k_ord_tail2(SrnnCfg c, SrnnArgs a) {
   using I = Item<pair::WW22, S>;
   __shared__ float4 s_samp[pair::P * 64];
   const int tid = threadIdx.x, u = tid & 1, pi = tid >> 1;
-  const int C = a.o_levels;
-  const int64_t cnt = *(volatile const int32_t*)(a.o_ctl + C);
-  if (cnt == 0) return;
-  const int32_t maxl = *(volatile const int32_t*)(a.o_ctl + C + 1);
   const int32_t gen = I::gen_of(a);
-  const int32_t* list = a.o_list + (int64_t)C * a.n;
-  for (int32_t lv = C; lv <= maxl; ++lv) {
-    // compact this level's turns into the workgroup's 64 particle slots, round by round
-    for (int64_t q0 = 0; q0 < cnt; q0 += 64) {
-      const int64_t q = q0 + pi;
-      if (q < cnt) {
-        const int64_t k = list[q];
-        if (ord::ld_level(a.o_src + 4 * k + 3) == lv) pair::turn<S>(c, a, k, gen, u, s_samp + pi);
-      }
-    }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    __syncthreads();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-  }
+  ord::tail_rounds<2>(a, [&](int64_t k) { pair::turn<S>(c, a, k, gen, u, s_samp + pi); });
 }
 
 // lanes per particle of a WW(2,2) launch over `count` particles: knob SRNN_KNOB_SOUP_LANES

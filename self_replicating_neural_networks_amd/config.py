@@ -98,8 +98,10 @@ class ExecConfig:
     soup_lanes: Optional[int] = None        # SRNN_SOUP_LANES (None / 0: by population size)
     order_levels: int = 4                   # SRNN_ORDER_LEVELS: parallel level launches of a reference-order
                                             # generation (deeper levels run in its one-wave tail)
-    perm_table: bool = True                 # SRNN_PERM_TABLE: a generation's SGD permutations precomputed by
-                                            # one launch ahead of it (nibble Weightwise nets on the device)
+    perm_table: Optional[bool] = None       # SRNN_PERM_TABLE: a generation's SGD permutations precomputed by
+                                            # one launch ahead of it (nibble Weightwise nets on the device;
+                                            # None: where the launches are latency-bound -- reference-order
+                                            # generations and < 65,536 slots per launch)
 
     _ENV = dict(finish_mode="SRNN_FINISH_MODE", finish_par="SRNN_FINISH_PAR", graph_chunks="SRNN_GRAPH_CHUNKS",
                 x2_schedule="SRNN_X2_SCHEDULE", x2_prio="SRNN_X2_PRIO", x2_emulate_remote="SRNN_X2_EMULATE_REMOTE",

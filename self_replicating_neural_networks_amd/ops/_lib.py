@@ -20,7 +20,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 # SRNN_LIB: load another build of the library (A/B of compiler flags on the GPU box)
 LIB_PATH = os.environ.get("SRNN_LIB") or os.path.join(_HERE, "libsrnn.so")
 CSRC = os.path.normpath(os.path.join(_HERE, "..", "..", "csrc"))
-ABI_VERSION = 20
+ABI_VERSION = 21
 
 # SrnnOp (csrc/srnn_abi.h)
 OP_INIT = 0
@@ -42,7 +42,8 @@ OP_SOUP_SEQ = 19  # sequential (Gauss-Seidel) soup generations
 OP_X2_PACK = 20   # sharded soup, all-to-all exchange: finish + next decisions + rows (csrc/srnn_shard.hip)
 OP_X2_POST = 21   # sharded soup: uids, census, received notices / requests
 OP_SOUP_ORDERED = 22  # reference-order (sequential) generation, level-scheduled (csrc/srnn_ordered.h)
-ORD_CTL_WORDS = 19    # o_ctl words of an ordered generation
+ORD_CTL_WORDS = 35    # o_ctl words of an ordered generation (csrc/srnn_ordered.h)
+ORD_TAILW, ORD_MAXLW, ORD_ERRW = 16, 17, 18
 
 # SrnnFlag bits (csrc/srnn_abi.h: one meaning each)
 FLAG_SHUFFLE = 1 << 0

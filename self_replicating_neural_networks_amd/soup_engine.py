@@ -335,13 +335,23 @@ class SoupEngine:
             self.stats_all = torch.zeros(self.dist.world * 6, dtype=torch.int64, device=dev)
             self.rowflags = torch.zeros(max(self.n, 1), **i32)
 
+    def _use_perm_table(self) -> bool:
+        """ExecConfig.perm_table, auto (None): the table pays where the generation's launches are
+        latency-bound -- the reference order's small level launches, populations below one wave
+        per SIMD -- and costs more than it saves on a throughput-bound 100k launch (MI355X,
+        profiles/r4b_*: the table launch vs the permutation work it removes from the SGD chain)."""
+        pt = self.execution.perm_table
+        if pt is not None:
+            return bool(pt)
+        return self.order == "sequential" or self.n < 65536
+
     def _perm_table(self):
         """The generation's SGD epoch permutations, precomputed by one launch before the
         generation kernel (k_perm_table; nibble Weightwise nets with shuffle, on the device):
         [severity + train][n] uint64, reallocated when the epoch count grows.  None where the
         kernels draw them inline (host, other shapes, > 2 GB of table)."""
         if (self.device.type != "cuda" or self.spec.kind != "weightwise" or self.spec.P > 16 or not self.shuffle
-                or self.generic or not self.execution.perm_table):
+                or self.generic or not self._use_perm_table()):
             return None
         E = max(int(self.params.get("train", 0)), 0) + max(int(self.params.get("learn_from_severity", 1)), 0)
         if E <= 0 or self.n * E * 8 > (2 << 30):
@@ -369,20 +379,22 @@ class SoupEngine:
         C = int(self.execution.order_levels)
         self.order_levels = C
         self._abuf = torch.zeros((self.n, self.spec.PP), dtype=self.dtype, device=dev)
-        self._osrc = torch.zeros(5 * max(self.n, 1), dtype=torch.int32, device=dev)  # [n][4] + stored flags
-        self._olist = torch.zeros((C + 1) * max(self.n, 1), dtype=torch.int32, device=dev)
+        # [n][4] source codes + level | [n] stored-attack flags | [n][16] pending records
+        self._osrc = torch.zeros(21 * max(self.n, 1), dtype=torch.int32, device=dev)
+        self._olist = torch.zeros(2 * max(self.n, 1), dtype=torch.int32, device=dev)  # level 0 | the tail's records
         self._octl = torch.zeros(_lib.ORD_CTL_WORDS, dtype=torch.int32, device=dev)
         self._rec_rows = None  # recording: every particle's state before any respawn
 
     def ordered_levels(self) -> Dict[str, int]:
         """Dependency levels of the last reference-order generation: turns per parallel level,
-        the tail's turns, the deepest level, error bits (1: a chain deeper than the DFS stack,
-        2: an attack output past the recompute depth left unstored), and how many attack outputs
-        were stored for later turns (the others are recomputed by the turns that read them)."""
+        the tail's turns, the deepest level, error bits (2: an attack output past the recompute
+        depth left unstored, 4: the tail found no runnable turn), and how many attack outputs were
+        stored for later turns (the others are recomputed by the turns that read them)."""
         c = self._octl.cpu().tolist()
         C = self.order_levels
         stored = int(self._osrc[4 * self.n:5 * self.n].sum().item()) if self.n else 0
-        return dict(levels=c[:C], tail=c[C], max_level=c[C + 1], error=c[C + 2], stored_attacks=stored)
+        return dict(levels=c[:C], tail=c[_lib.ORD_TAILW], max_level=c[_lib.ORD_MAXLW], error=c[_lib.ORD_ERRW],
+                    stored_attacks=stored)
 
     def _init_x2(self, n_links):
         dev, R = self.device, self.dist.world
@@ -919,11 +931,10 @@ class SoupEngine:
         if err:
             raise RuntimeError(f"soup row exchange failed ({err}): results are invalid")
         if self.order == "sequential":
-            e = int(self._octl[self.order_levels + 2].item())
+            e = int(self._octl[_lib.ORD_ERRW].item())
             if e:
-                raise RuntimeError(f"reference-order generation: error bits {e} (1: a dependency chain exceeded the "
-                                   "level DFS stack, 2: an unstored attack output past the recompute depth); "
-                                   "results are invalid")
+                raise RuntimeError(f"reference-order generation: error bits {e} (2: an unstored attack output past "
+                                   "the recompute depth, 4: the tail found no runnable turn); results are invalid")
         c = torch.zeros(6, dtype=torch.int64, device=self.device)
         cls, _ = K.classify(self.spec, self.local_rows(), self.eps, with_sec, uid=None, seed=self.seed,
                             scratch=self._scratch, ctr=0x7FFFFFF0, counts=c, key_offset=self.lo)
