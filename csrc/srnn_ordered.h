@@ -29,11 +29,11 @@
 //
 //   k_ord_plan    per turn: decisions, the source version of each of its reads (src codes)
 //   k_ord_mark    per turn / row: flags the attack outputs reached past the recompute depth
-//   k_ord_sort    per turn: its producers; none -> level 0's list, else a pending record
-//                 {turn, producers} (one atomic per wave and list)
-//   k_ord_level   L = 0: the level-0 list, one lane per turn; L = 1..C-1: a pass over the
-//                 pending records -- a record whose producers all ran at levels < L runs now
-//                 (WW(2,2): on a lane pair); no level is computed ahead, no DFS
+//   k_ord_level0  per turn: its producers; none -> the turn runs now (level 0), else a pending
+//                 record {turn, producers} in the workgroup's partition (+ its permutations)
+//   k_ord_level   L = 1..C-1: a pass over the pending records -- a record whose producers all
+//                 ran at levels < L runs now (WW(2,2): on a lane pair); no level is computed
+//                 ahead, no DFS
 //   k_ord_tail    one workgroup: the records still pending after C-1, in rounds (fence +
 //                 barrier per round)
 //   k_ord_close   per row: its final version (a row attacked after its own turn ends the
@@ -57,14 +57,18 @@ constexpr int32_t SRC_SELF = INT32_MIN;
 constexpr int32_t SRC_ATK = INT32_MIN + 1;
 constexpr int32_t SRC_NONE = INT32_MIN + 2;
 constexpr int MAX_LEVELS = 16;  // parallel level launches per generation (the rest: the tail)
-// o_ctl words: [0, C) turns run at levels 0..C-1, [TAILW] turns run by the tail, [MAXLW] max
-// level, [ERRW] error bits (2: an unstored attack output past the recompute depth -- a marking
-// bug, 4: the tail found no runnable turn among the pending ones), [REM0 + L] turns still
-// pending after level launch L (L = 0: the sort pass; also the pending records' append counter)
+// o_ctl words: [TAILW] turns run by the tail, [MAXLW] max level, [ERRW] error bits (2: an
+// unstored attack output past the recompute depth -- a marking bug, 4: the tail found no
+// runnable turn among the pending ones), [REM0 + L] turns still pending after level launch L
+// (turns run at level L = REM(L-1) - REM(L), level 0: n - REM(0)), [PART0 + p] records of
+// partition p
 constexpr int TAILW = MAX_LEVELS, MAXLW = MAX_LEVELS + 1, ERRW = MAX_LEVELS + 2, REM0 = MAX_LEVELS + 3;
-constexpr int CTL_WORDS = 2 * MAX_LEVELS + 3;
-// o_src layout: [n][4] {own, victim, teacher, level} | [n] stored flags of A(j) | [n][16]
-// pending records {turn, producer count, producers...}; o_list: [n] level-0 turns | [n] the
+// pending records live in NPART partitions (partition p: the level-0 workgroups b = p mod NPART,
+// appended by one counter each at PART0 + p: no chip-wide contended counter)
+constexpr int NPART = 64, PART0 = 2 * MAX_LEVELS + 3;
+constexpr int CTL_WORDS = PART0 + NPART;
+// o_src layout: [n][4] {own, victim, teacher, level} | [n] stored flags of A(j) |
+// [rec_total(n)][16] pending records {turn, producer count, producers...}; o_list: [n] the
 // tail's records
 constexpr int NPROD = 12;  // producers of one turn: 3 reads x 2^RB leaves
 constexpr int REC = 16;
@@ -95,6 +99,9 @@ SRNN_HD int32_t latest(const SrnnArgs& a, int64_t r, int64_t k) {
 
 SRNN_HD const int32_t* src_of(const SrnnArgs& a, int64_t k) { return a.o_src + 4 * k; }
 SRNN_HD int32_t* pend(const SrnnArgs& a, int64_t q) { return a.o_src + 5 * a.n + REC * q; }
+// records per partition (each level-0 workgroup of TB turns appends to its partition only)
+SRNN_HD int64_t rec_cap(int64_t n) { return ((n + TB - 1) / TB + NPART - 1) / NPART * TB; }
+SRNN_HD int64_t rec_total(int64_t n) { return NPART * rec_cap(n); }
 SRNN_HD bool stored(const SrnnArgs& a, int64_t j) { return a.o_src[4 * a.n + j] != 0; }
 // turn k computes A(k): it attacked, and the attack output is its own row (self-attack),
 // its teacher (learn_from the victim) or read by a turn past the recompute depth
@@ -210,7 +217,10 @@ struct Ord {
   }
 
   // turn k: the serial loop's particle step (soup_seq_one) reading the versions of its plan
-  SRNN_HD static void turn(const SrnnCfg& c, const SrnnArgs& a, int64_t k, int32_t gen, float4* samp, uint8_t* perm) {
+  // (prow >= 0: the turn's epoch permutations are row prow of the pending records' table, stride
+  // rec_total; else drawn inline)
+  SRNN_HD static void turn(const SrnnCfg& c, const SrnnArgs& a, int64_t k, int32_t gen, float4* samp, uint8_t* perm,
+                           int64_t prow = -1) {
     const int32_t* s = a.o_src + 4 * k;
     int64_t at, te;
     I::decision(a, k, gen, at, te);
@@ -243,9 +253,9 @@ struct Ord {
     tc.shuffle = (a.flags & SRNN_F_SHUFFLE) != 0;
     tc.stride = SAMP_STRIDE;
     tc.aggregator = c.aggregator;
-    if (a.ptab && a.dev) {  // this generation's permutations, precomputed (k_perm_table)
-      tc.ptab = a.ptab + k;
-      tc.pstride = a.n;
+    if (a.ptab && a.dev && prow >= 0) {  // precomputed by the level-0 launch
+      tc.ptab = a.ptab + prow;
+      tc.pstride = rec_total(a.n);
       tc.pbase = tc.ctr;
     }
     float loss = 0.f;
@@ -340,25 +350,28 @@ __device__ __forceinline__ int32_t wave_sum(int32_t v) {
   return v;
 }
 
-// level launch L >= 1 over the pending records, TPT threads per turn (1: lane, 2: pair):
-// a record whose producers all have levels < L runs now (its level becomes L); the others stay
-// pending (counted in REM(L); the last parallel launch also lists them for the tail)
+// level launch L >= 1 over the pending records, TPT threads per turn (1: lane, 2: pair),
+// workgroup b on partition b mod NPART: a record whose producers all have levels < L runs now
+// (its level becomes L); the others stay pending (REM(L), a fire-and-forget count; the last
+// parallel launch also lists them for the tail).  run(k, q): turn k of record q.
 template <int TPT, class F>
 __device__ __forceinline__ void pending_pass(const SrnnArgs& a, int32_t L, F&& run) {
   if (ld_ctl(a.o_ctl + REM0 + L - 1) == 0) return;  // nothing left: REM(L) stays 0
   const bool last = L == a.o_levels - 1;
-  const int64_t P = ld_ctl(a.o_ctl + REM0);
+  const int part = (int)(blockIdx.x % NPART);
+  const int64_t bpp = gridDim.x / NPART, j = blockIdx.x / NPART;
+  const int64_t cnt = ld_ctl(a.o_ctl + PART0 + part), q0 = part * rec_cap(a.n);
   const int slots = (int)blockDim.x / TPT, slot = (int)threadIdx.x / TPT, sub = (int)threadIdx.x % TPT;
-  int32_t ex = 0;
-  for (int64_t base = (int64_t)blockIdx.x * slots; base < P; base += (int64_t)gridDim.x * slots) {
-    const int64_t q = base + slot;
+  int32_t ex = 0, nleft = 0;
+  for (int64_t base = j * slots; base < cnt; base += bpp * slots) {
+    const int64_t i = base + slot, q = q0 + i;
     bool left = false;
-    if (q < P) {
+    if (i < cnt) {
       const int32_t* rec = pend(a, q);
       const int64_t k = rec[0];
       if (ld_level(a.o_src + 4 * k + 3) < 0) {
         if (ready(a, rec, L)) {
-          run(k);
+          run(k, q);
           if (sub == 0) {
             st_level(a.o_src + 4 * k + 3, L);
             ++ex;
@@ -368,19 +381,25 @@ __device__ __forceinline__ void pending_pass(const SrnnArgs& a, int32_t L, F&& r
         }
       }
     }
-    const int32_t pos = wave_append(a.o_ctl + REM0 + L, left);
-    if (last && left) a.o_list[a.n + pos] = (int32_t)q;  // the tail's list
+    if (last) {
+      const int32_t pos = wave_append(a.o_ctl + REM0 + L, left);
+      if (left) a.o_list[pos] = (int32_t)q;  // the tail's list
+    } else {
+      nleft += left;
+    }
   }
+  nleft = wave_sum(nleft);
   ex = wave_sum(ex);
-  if ((threadIdx.x & 63) == 0 && ex) {
-    atomicAdd(a.o_ctl + L, ex);
-    atomicMax(a.o_ctl + MAXLW, L);
+  if ((threadIdx.x & 63) == 0) {
+    if (nleft) atomicAdd(a.o_ctl + REM0 + L, nleft);
+    if (ex) atomicMax(a.o_ctl + MAXLW, L);
   }
 }
 
-// levels >= C in one workgroup, round by round over the tail's list: the rows a round writes
-// are released before the barrier and the L1 is invalidated after it.  A round that runs
-// nothing while turns are left (no DAG: a bug) sets error bit 4 and stops -- never a hang.
+// levels >= C in one workgroup, round by round over the tail's records (C = 1: every pending
+// record, partition by partition): the rows a round writes are released before the barrier
+// and the L1 is invalidated after it.  A round that runs nothing while turns are left (no DAG:
+// a bug) sets error bit 4 and stops -- never a hang.
 template <int TPT, class F>
 __device__ __forceinline__ void tail_rounds(const SrnnArgs& a, F&& run) {
   const int C = a.o_levels;
@@ -388,27 +407,34 @@ __device__ __forceinline__ void tail_rounds(const SrnnArgs& a, F&& run) {
   if (T == 0) return;
   __shared__ int32_t s_cnt[2];
   const int slots = (int)blockDim.x / TPT, slot = (int)threadIdx.x / TPT, sub = (int)threadIdx.x % TPT;
-  const int32_t* tl = a.o_list + a.n;
+  const int64_t cap = rec_cap(a.n);
   for (int32_t lv = C;; ++lv) {
     if (threadIdx.x == 0) s_cnt[0] = s_cnt[1] = 0;
     __syncthreads();
     int32_t ex = 0, left = 0;
-    for (int64_t q0 = 0; q0 < T; q0 += slots) {
-      const int64_t q = q0 + slot;
-      if (q < T) {
-        const int32_t* rec = pend(a, tl[q]);
-        const int64_t k = rec[0];
-        if (ld_level(a.o_src + 4 * k + 3) < 0) {
-          if (ready(a, rec, lv)) {
-            run(k);
-            if (sub == 0) {
-              st_level(a.o_src + 4 * k + 3, lv);
-              ++ex;
-            }
-          } else if (sub == 0) {
-            ++left;
+    auto visit = [&](int64_t q) {
+      const int32_t* rec = pend(a, q);
+      const int64_t k = rec[0];
+      if (ld_level(a.o_src + 4 * k + 3) < 0) {
+        if (ready(a, rec, lv)) {
+          run(k, q);
+          if (sub == 0) {
+            st_level(a.o_src + 4 * k + 3, lv);
+            ++ex;
           }
+        } else if (sub == 0) {
+          ++left;
         }
+      }
+    };
+    if (C > 1) {
+      for (int64_t i0 = 0; i0 < T; i0 += slots)
+        if (i0 + slot < T) visit(a.o_list[i0 + slot]);
+    } else {
+      for (int p = 0; p < NPART; ++p) {
+        const int64_t cnt = ld_ctl(a.o_ctl + PART0 + p);
+        for (int64_t i0 = 0; i0 < cnt; i0 += slots)
+          if (i0 + slot < cnt) visit(p * cap + i0 + slot);
       }
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
@@ -446,31 +472,48 @@ __global__ __launch_bounds__(TB) void k_ord_mark(SrnnCfg, SrnnArgs a) {
   if (k < a.n) ord::Ord<Net, S>::mark(a, k);
 }
 
-// the turns without producers -> level 0 (list 0); the others -> pending records (their
-// producers counted, then written straight into the record: no private arrays)
+// level 0: every turn counts its producers; a turn without any runs now (permutations drawn
+// inline), the others become pending records of this workgroup's partition (producers written
+// straight into the record; with a table, the turn's epoch permutations too -- computed by the
+// lanes that have no turn to run, beside the ones that do)
 template <class Net, class S>
-__global__ __launch_bounds__(TB) void k_ord_sort(SrnnCfg, SrnnArgs a) {
+__global__ __launch_bounds__(TB) void k_ord_level0(SrnnCfg c, SrnnArgs a) {
+  using I = Item<Net, S>;
   using O = ord::Ord<Net, S>;
-  const int64_t k = (int64_t)blockIdx.x * TB + threadIdx.x;
+  constexpr int SAMP = samp_slots<Net>();
+  constexpr int PERM = (Net::P + 4) & ~3;
+  __shared__ float4 s_samp[TB * SAMP];
+  __shared__ uint8_t s_perm[TB * PERM];
+  const int lane = threadIdx.x;
+  const int64_t k = (int64_t)blockIdx.x * TB + lane;
   const bool valid = k < a.n;
+  const int32_t gen = I::gen_of(a);
   int np = 0;
   bool bad = false;
   if (valid) np = O::producers(a, k, nullptr, bad);
   if (bad) atomicOr(a.o_ctl + ord::ERRW, 2);
-  if (valid && np == 0) ord::st_level(a.o_src + 4 * k + 3, 0);
-  const int32_t p0 = ord::wave_append(a.o_ctl + 0, valid && np == 0);
-  if (p0 >= 0) a.o_list[p0] = (int32_t)k;
-  const int32_t pq = ord::wave_append(a.o_ctl + ord::REM0, valid && np > 0);
-  if (pq >= 0) {
-    int32_t* rec = ord::pend(a, pq);
+  const bool pend = valid && np > 0;
+  const int part = (int)(blockIdx.x % ord::NPART);
+  const int32_t i = ord::wave_append(a.o_ctl + ord::PART0 + part, pend);
+  if (pend) {
+    const int64_t q = part * ord::rec_cap(a.n) + i;
+    int32_t* rec = ord::pend(a, q);
     rec[0] = (int32_t)k;
     bool bad2 = false;
     rec[1] = O::producers(a, k, rec + 2, bad2);
-    if (a.o_levels == 1) a.o_list[a.n + pq] = pq;  // no parallel level after 0: all to the tail
+    if constexpr (Net::KIND == 0 && Net::P <= 16) {
+      const int32_t E = (a.severity > 0 ? a.severity : 0) + (a.epochs > 0 ? a.epochs : 0);
+      if (a.ptab && (a.flags & SRNN_F_SHUFFLE) && E > 0) perm_row<Net>(a, E, k, a.ptab, q, ord::rec_total(a.n));
+    }
+  } else if (valid) {
+    ord::st_level(a.o_src + 4 * k + 3, 0);
+    O::turn(c, a, k, gen, samp_lane<Net>(s_samp, lane), s_perm + lane * PERM);
   }
+  const int32_t npend = ord::wave_sum(pend ? 1 : 0);
+  if (lane == 0 && npend) atomicAdd(a.o_ctl + ord::REM0, npend);  // fire and forget
 }
 
-// level L: L = 0 the list of turns without producers, L >= 1 a pass over the pending records
+// levels 1..C-1: a pass over the pending records
 template <class Net, class S>
 __global__ __launch_bounds__(TB) void k_ord_level(SrnnCfg c, SrnnArgs a, int32_t L) {
   using I = Item<Net, S>;
@@ -482,15 +525,7 @@ __global__ __launch_bounds__(TB) void k_ord_level(SrnnCfg c, SrnnArgs a, int32_t
   const int32_t gen = I::gen_of(a);
   float4* samp = samp_lane<Net>(s_samp, lane);
   uint8_t* perm = s_perm + lane * PERM;
-  if (L == 0) {
-    const int64_t cnt = ord::ld_ctl(a.o_ctl);
-    for (int64_t base = (int64_t)blockIdx.x * TB; base < cnt; base += (int64_t)gridDim.x * TB) {
-      const int64_t q = base + lane;
-      if (q < cnt) ord::Ord<Net, S>::turn(c, a, a.o_list[q], gen, samp, perm);
-    }
-    return;
-  }
-  ord::pending_pass<1>(a, L, [&](int64_t k) { ord::Ord<Net, S>::turn(c, a, k, gen, samp, perm); });
+  ord::pending_pass<1>(a, L, [&](int64_t k, int64_t q) { ord::Ord<Net, S>::turn(c, a, k, gen, samp, perm, q); });
 }
 
 // levels >= C: one wave
@@ -505,7 +540,7 @@ __global__ __launch_bounds__(TB) void k_ord_tail(SrnnCfg c, SrnnArgs a) {
   const int32_t gen = I::gen_of(a);
   float4* samp = samp_lane<Net>(s_samp, lane);
   uint8_t* perm = s_perm + lane * PERM;
-  ord::tail_rounds<1>(a, [&](int64_t k) { ord::Ord<Net, S>::turn(c, a, k, gen, samp, perm); });
+  ord::tail_rounds<1>(a, [&](int64_t k, int64_t q) { ord::Ord<Net, S>::turn(c, a, k, gen, samp, perm, q); });
 }
 
 // final rows, census, next decisions, block stats (the fused generation's two-phase form:
@@ -592,7 +627,12 @@ int soup_ordered(const SrnnCfg& c, const SrnnArgs& a) {
       maxl = std::max(maxl, lv);
       lists[(size_t)std::min(lv, C)].push_back(k);
     }
-    for (int32_t L = 0; L < C; ++L) a.o_ctl[L] = (int32_t)lists[(size_t)L].size();
+    // the device's control words: turns pending after each parallel level, the tail's count
+    int64_t rem = a.n;
+    for (int32_t L = 0; L < C; ++L) {
+      rem -= (int64_t)lists[(size_t)L].size();
+      a.o_ctl[ord::REM0 + L] = (int32_t)rem;
+    }
     a.o_ctl[ord::TAILW] = (int32_t)lists[(size_t)C].size();
     a.o_ctl[ord::MAXLW] = maxl;
     auto run_turn = [&](int64_t k) {
@@ -653,27 +693,25 @@ int soup_ordered(const SrnnCfg& c, const SrnnArgs& a) {
   const int64_t nb = (a.n + TB - 1) / TB;
   if (nb <= 0) return 0;
   hipStream_t st = (hipStream_t)a.stream;
-  perm_table<Net>(a);
   hipLaunchKernelGGL((k_ord_plan<Net, S>), dim3((unsigned)nb), dim3(TB), 0, st, c, a);
   hipLaunchKernelGGL((k_ord_mark<Net, S>), dim3((unsigned)nb), dim3(TB), 0, st, c, a);
-  hipLaunchKernelGGL((k_ord_sort<Net, S>), dim3((unsigned)nb), dim3(TB), 0, st, c, a);
   constexpr bool ww22 = std::is_same_v<Net, Weightwise<2, 2>>;
-  hipLaunchKernelGGL((k_ord_level<Net, S>), dim3((unsigned)nb), dim3(TB), 0, st, c, a, 0);
+  hipLaunchKernelGGL((k_ord_level0<Net, S>), dim3((unsigned)nb), dim3(TB), 0, st, c, a);
   // levels >= 1 pass over the pending records (~5 % of the turns at the reference's rates, most
-  // of them level 1): a grid covering 8 % of n in one pass, grid-stride beyond; WW(2,2) on lane
-  // pairs (latency-bound: srnn_pair.h)
-  const int64_t est = std::max<int64_t>(a.n / 12, 1);
+  // of them level 1): per partition, workgroups covering 8 % of its share in one pass (grid-
+  // stride beyond); WW(2,2) on lane pairs (latency-bound: srnn_pair.h)
+  const int64_t est = std::max<int64_t>(a.n / 12 / ord::NPART, 1);
   bool pairs = false;
   if constexpr (ww22) pairs = use_pairs(a.n / 20);
   for (int32_t L = 1; L < C; ++L) {
     if (pairs) {
       if constexpr (ww22) {
-        const int64_t blocks = std::min<int64_t>(std::max<int64_t>(16, (est + 63) / 64), (a.n + 63) / 64);
-        hipLaunchKernelGGL((k_ord_level2<S>), dim3((unsigned)blocks), dim3(pair::TBW), 0, st, c, a, L);
+        const int64_t bpp = (est + 63) / 64;
+        hipLaunchKernelGGL((k_ord_level2<S>), dim3((unsigned)(bpp * ord::NPART)), dim3(pair::TBW), 0, st, c, a, L);
       }
     } else {
-      const int64_t blocks = std::min<int64_t>(std::max<int64_t>(16, (est + TB - 1) / TB), nb);
-      hipLaunchKernelGGL((k_ord_level<Net, S>), dim3((unsigned)blocks), dim3(TB), 0, st, c, a, L);
+      const int64_t bpp = (est + TB - 1) / TB;
+      hipLaunchKernelGGL((k_ord_level<Net, S>), dim3((unsigned)(bpp * ord::NPART)), dim3(TB), 0, st, c, a, L);
     }
   }
   if (pairs) {

@@ -238,7 +238,10 @@ __device__ __forceinline__ float learn_and_train(const SrnnArgs& a, float* w, co
   return loss;
 }
 
-__device__ __forceinline__ void train_ctx(const SrnnArgs& a, TrainCtx& tc, uint64_t uid, int32_t gen, int64_t row) {
+// (row >= 0 with a table: the particle's permutations are column `row` of a.ptab, stride
+// pstride (default n); row < 0: drawn inline)
+__device__ __forceinline__ void train_ctx(const SrnnArgs& a, TrainCtx& tc, uint64_t uid, int32_t gen, int64_t row,
+                                          int64_t pstride = -1) {
   tc.lr = a.lr;
   tc.rng = Rng{(uint32_t)a.seed, (uint32_t)(a.seed >> 32)};
   tc.uid = uid;
@@ -248,9 +251,9 @@ __device__ __forceinline__ void train_ctx(const SrnnArgs& a, TrainCtx& tc, uint6
   tc.shuffle = (a.flags & SRNN_F_SHUFFLE) != 0;
   tc.stride = 64;  // particles per workgroup: sample slot k of particle pi at sp[k * 64]
   tc.aggregator = 0;
-  if (a.ptab) {
+  if (a.ptab && row >= 0) {
     tc.ptab = a.ptab + row;
-    tc.pstride = a.n;
+    tc.pstride = pstride >= 0 ? pstride : a.n;
     tc.pbase = tc.ctr;
   }
 }
@@ -304,7 +307,8 @@ __device__ __forceinline__ int8_t evolve(const SrnnArgs& a, int64_t i, int32_t g
 
 // reference-order turn k (Ord::turn) on the pair
 template <class S>
-__device__ __forceinline__ void turn(const SrnnCfg& c, const SrnnArgs& a, int64_t k, int32_t gen, int u, float4* sp) {
+__device__ __forceinline__ void turn(const SrnnCfg& c, const SrnnArgs& a, int64_t k, int32_t gen, int u, float4* sp,
+                                     int64_t prow) {
   using I = Item<WW22, S>;
   using O = ord::Ord<WW22, S>;
   (void)c;
@@ -329,7 +333,7 @@ __device__ __forceinline__ void turn(const SrnnCfg& c, const SrnnArgs& a, int64_
     cp = at;
   }
   TrainCtx tc;
-  train_ctx(a, tc, (uint64_t)k, gen, k);
+  train_ctx(a, tc, (uint64_t)k, gen, prow, ord::rec_total(a.n));
   if (te >= 0) {
     if (s[2] == ord::SRC_SELF) I::copy(f, w);
     else if (s[2] == ord::SRC_ATK) I::copy(f, o);
@@ -429,7 +433,7 @@ __global__ __launch_bounds__(pair::TBW) void k_ord_level2(SrnnCfg c, SrnnArgs a,
   __shared__ float4 s_samp[pair::P * 64];
   const int tid = threadIdx.x, u = tid & 1, pi = tid >> 1;
   const int32_t gen = I::gen_of(a);
-  ord::pending_pass<2>(a, L, [&](int64_t k) { pair::turn<S>(c, a, k, gen, u, s_samp + pi); });
+  ord::pending_pass<2>(a, L, [&](int64_t k, int64_t q) { pair::turn<S>(c, a, k, gen, u, s_samp + pi, q); });
 }
 
 // the reference-order tail (levels >= C) on pairs: one workgroup, round by round
@@ -439,7 +443,7 @@ __global__ __launch_bounds__(pair::TBW) void k_ord_tail2(SrnnCfg c, SrnnArgs a) 
   __shared__ float4 s_samp[pair::P * 64];
   const int tid = threadIdx.x, u = tid & 1, pi = tid >> 1;
   const int32_t gen = I::gen_of(a);
-  ord::tail_rounds<2>(a, [&](int64_t k) { pair::turn<S>(c, a, k, gen, u, s_samp + pi); });
+  ord::tail_rounds<2>(a, [&](int64_t k, int64_t q) { pair::turn<S>(c, a, k, gen, u, s_samp + pi, q); });
 }
 
 // lanes per particle of a WW(2,2) launch over `count` particles: knob SRNN_KNOB_SOUP_LANES

@@ -42,8 +42,15 @@ OP_SOUP_SEQ = 19  # sequential (Gauss-Seidel) soup generations
 OP_X2_PACK = 20   # sharded soup, all-to-all exchange: finish + next decisions + rows (csrc/srnn_shard.hip)
 OP_X2_POST = 21   # sharded soup: uids, census, received notices / requests
 OP_SOUP_ORDERED = 22  # reference-order (sequential) generation, level-scheduled (csrc/srnn_ordered.h)
-ORD_CTL_WORDS = 35    # o_ctl words of an ordered generation (csrc/srnn_ordered.h)
-ORD_TAILW, ORD_MAXLW, ORD_ERRW = 16, 17, 18
+ORD_CTL_WORDS = 99    # o_ctl words of an ordered generation (csrc/srnn_ordered.h)
+ORD_TAILW, ORD_MAXLW, ORD_ERRW, ORD_REM0 = 16, 17, 18, 19
+ORD_NPART = 64        # partitions of the pending records
+
+
+def ord_rec_total(n: int) -> int:
+    """Pending-record capacity of an n-turn ordered generation (ord::rec_total: NPART partitions
+    of ceil(ceil(n / 64) / NPART) * 64 records)."""
+    return ORD_NPART * ((-(-n // 64) + ORD_NPART - 1) // ORD_NPART) * 64
 
 # SrnnFlag bits (csrc/srnn_abi.h: one meaning each)
 FLAG_SHUFFLE = 1 << 0

@@ -354,11 +354,12 @@ class SoupEngine:
                 or self.generic or not self._use_perm_table()):
             return None
         E = max(int(self.params.get("train", 0)), 0) + max(int(self.params.get("learn_from_severity", 1)), 0)
-        if E <= 0 or self.n * E * 8 > (2 << 30):
+        if E <= 0 or (self.n + 4096) * E * 8 > (2 << 30):
             return None
+        rows = _lib.ord_rec_total(self.n) if self.order == "sequential" else self.n  # (pending records)
         t = getattr(self, "_ptab", None)
-        if t is None or t.numel() < self.n * E:
-            self._ptab = t = torch.zeros(self.n * E, dtype=torch.int64, device=self.device)
+        if t is None or t.numel() < rows * E:
+            self._ptab = t = torch.zeros(rows * E, dtype=torch.int64, device=self.device)
         return t
 
     def _init_ordered(self):
@@ -379,9 +380,10 @@ class SoupEngine:
         C = int(self.execution.order_levels)
         self.order_levels = C
         self._abuf = torch.zeros((self.n, self.spec.PP), dtype=self.dtype, device=dev)
-        # [n][4] source codes + level | [n] stored-attack flags | [n][16] pending records
-        self._osrc = torch.zeros(21 * max(self.n, 1), dtype=torch.int32, device=dev)
-        self._olist = torch.zeros(2 * max(self.n, 1), dtype=torch.int32, device=dev)  # level 0 | the tail's records
+        # [n][4] source codes + level | [n] stored-attack flags | [rec_total][16] pending records
+        self._osrc = torch.zeros(5 * max(self.n, 1) + 16 * _lib.ord_rec_total(max(self.n, 1)), dtype=torch.int32,
+                                 device=dev)
+        self._olist = torch.zeros(max(self.n, 1), dtype=torch.int32, device=dev)  # the tail's records
         self._octl = torch.zeros(_lib.ORD_CTL_WORDS, dtype=torch.int32, device=dev)
         self._rec_rows = None  # recording: every particle's state before any respawn
 
@@ -393,8 +395,9 @@ class SoupEngine:
         c = self._octl.cpu().tolist()
         C = self.order_levels
         stored = int(self._osrc[4 * self.n:5 * self.n].sum().item()) if self.n else 0
-        return dict(levels=c[:C], tail=c[_lib.ORD_TAILW], max_level=c[_lib.ORD_MAXLW], error=c[_lib.ORD_ERRW],
-                    stored_attacks=stored)
+        rem = [self.n] + c[_lib.ORD_REM0:_lib.ORD_REM0 + C]  # turns pending before / after each level
+        return dict(levels=[rem[L] - rem[L + 1] for L in range(C)], tail=c[_lib.ORD_TAILW],
+                    max_level=c[_lib.ORD_MAXLW], error=c[_lib.ORD_ERRW], stored_attacks=stored)
 
     def _init_x2(self, n_links):
         dev, R = self.device, self.dist.world
