@@ -746,20 +746,6 @@ __global__ __launch_bounds__(TB) void k_op(SrnnCfg c, SrnnArgs a) {
 // row's global slot) and stores both nibble permutations -- exactly what train_epochs would
 // compute inline, moved off the latency-bound SGD chains into one fully parallel launch.
 constexpr int TBP = 256;
-// the E epoch permutations of slot `key` (global slot a.lo + key) into tab[e * stride + idx]
-template <class Net>
-__device__ __forceinline__ void perm_row(const SrnnArgs& a, int32_t E, int64_t key, uint64_t* tab, int64_t idx,
-                                         int64_t stride) {
-  constexpr int P = Net::P;
-  const int32_t gen = a.gen_ptr ? a.gen_ptr[0] : a.gen;
-  const Rng rng{(uint32_t)a.seed, (uint32_t)(a.seed >> 32)};
-  for (int32_t p = 0; 2 * p < E; ++p) {
-    const uint32_t c0 = (uint32_t)gen * 1024u + 512u + 2u * (uint32_t)p;  // even: one draw, two epochs
-    const U4 r = perm_draw(rng, (uint64_t)(a.lo + key), c0, P_SHUFFLE);
-    tab[2 * p * stride + idx] = perm_from_bits<P>(perm_bits(r, c0));
-    if (2 * p + 1 < E) tab[(2 * p + 1) * stride + idx] = perm_from_bits<P>(perm_bits(r, c0 + 1u));
-  }
-}
 template <class Net>
 __global__ __launch_bounds__(TBP) void k_perm_table(SrnnArgs a, int32_t E) {
   constexpr int P = Net::P;

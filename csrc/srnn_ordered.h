@@ -474,8 +474,7 @@ __global__ __launch_bounds__(TB) void k_ord_mark(SrnnCfg, SrnnArgs a) {
 
 // level 0: every turn counts its producers; a turn without any runs now (permutations drawn
 // inline), the others become pending records of this workgroup's partition (producers written
-// straight into the record; with a table, the turn's epoch permutations too -- computed by the
-// lanes that have no turn to run, beside the ones that do)
+// straight into the record)
 template <class Net, class S>
 __global__ __launch_bounds__(TB) void k_ord_level0(SrnnCfg c, SrnnArgs a) {
   using I = Item<Net, S>;
@@ -501,16 +500,33 @@ __global__ __launch_bounds__(TB) void k_ord_level0(SrnnCfg c, SrnnArgs a) {
     rec[0] = (int32_t)k;
     bool bad2 = false;
     rec[1] = O::producers(a, k, rec + 2, bad2);
-    if constexpr (Net::KIND == 0 && Net::P <= 16) {
-      const int32_t E = (a.severity > 0 ? a.severity : 0) + (a.epochs > 0 ? a.epochs : 0);
-      if (a.ptab && (a.flags & SRNN_F_SHUFFLE) && E > 0) perm_row<Net>(a, E, k, a.ptab, q, ord::rec_total(a.n));
-    }
   } else if (valid) {
     ord::st_level(a.o_src + 4 * k + 3, 0);
     O::turn(c, a, k, gen, samp_lane<Net>(s_samp, lane), s_perm + lane * PERM);
   }
   const int32_t npend = ord::wave_sum(pend ? 1 : 0);
   if (lane == 0 && npend) atomicAdd(a.o_ctl + ord::REM0, npend);  // fire and forget
+}
+
+// the epoch permutations of the pending records (their turns run on the latency-bound level
+// launches, where an inline draw sits on the chain): thread (record, epoch pair), workgroup
+// row y = partition * pairs + pair, grid-stride over the partition's records
+template <class Net>
+__global__ __launch_bounds__(TB) void k_ord_ptab(SrnnArgs a, int32_t E) {
+  constexpr int P = Net::P;
+  const int npair = (E + 1) / 2;
+  const int part = (int)blockIdx.y / npair, p = (int)blockIdx.y % npair;
+  const int64_t cnt = ord::ld_ctl(a.o_ctl + ord::PART0 + part), q0 = part * ord::rec_cap(a.n);
+  const int64_t stride = ord::rec_total(a.n);
+  const int32_t gen = a.gen_ptr ? a.gen_ptr[0] : a.gen;
+  const Rng rng{(uint32_t)a.seed, (uint32_t)(a.seed >> 32)};
+  const uint32_t c0 = (uint32_t)gen * 1024u + 512u + 2u * (uint32_t)p;  // even: one draw, two epochs
+  for (int64_t i = (int64_t)blockIdx.x * TB + threadIdx.x; i < cnt; i += (int64_t)gridDim.x * TB) {
+    const int64_t q = q0 + i, k = ord::pend(a, q)[0];
+    const U4 r = perm_draw(rng, (uint64_t)(a.lo + k), c0, P_SHUFFLE);
+    a.ptab[2 * p * stride + q] = perm_from_bits<P>(perm_bits(r, c0));
+    if (2 * p + 1 < E) a.ptab[(2 * p + 1) * stride + q] = perm_from_bits<P>(perm_bits(r, c0 + 1u));
+  }
 }
 
 // levels 1..C-1: a pass over the pending records
@@ -697,6 +713,14 @@ int soup_ordered(const SrnnCfg& c, const SrnnArgs& a) {
   hipLaunchKernelGGL((k_ord_mark<Net, S>), dim3((unsigned)nb), dim3(TB), 0, st, c, a);
   constexpr bool ww22 = std::is_same_v<Net, Weightwise<2, 2>>;
   hipLaunchKernelGGL((k_ord_level0<Net, S>), dim3((unsigned)nb), dim3(TB), 0, st, c, a);
+  if constexpr (Net::KIND == 0 && Net::P <= 16) {
+    const int32_t E = (a.severity > 0 ? a.severity : 0) + (a.epochs > 0 ? a.epochs : 0);
+    if (a.ptab && (a.flags & SRNN_F_SHUFFLE) && E > 0) {
+      const int64_t est = std::max<int64_t>(a.n / 12 / ord::NPART, 1);
+      hipLaunchKernelGGL((k_ord_ptab<Net>), dim3((unsigned)((est + TB - 1) / TB), (unsigned)(ord::NPART * ((E + 1) / 2))),
+                         dim3(TB), 0, st, a, E);
+    }
+  }
   // levels >= 1 pass over the pending records (~5 % of the turns at the reference's rates, most
   // of them level 1): per partition, workgroups covering 8 % of its share in one pass (grid-
   // stride beyond); WW(2,2) on lane pairs (latency-bound: srnn_pair.h)
