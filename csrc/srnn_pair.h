@@ -21,7 +21,7 @@ namespace pair {
 using WW22 = Weightwise<2, 2>;
 constexpr int P = WW22::P;  // 14
 constexpr int TBW = 128;    // threads per workgroup: 64 particles = one 64-row block
-constexpr int64_t PAIR_MAX_N = 40960;  // auto: pairs for populations (levels) up to this size
+constexpr int64_t PAIR_MAX_N = 20480;  // auto: pairs for populations (levels) up to this size
 
 // DPP quad permutations (quad_perm encodings): the value of pair lane 0 / 1, the partner's
 __device__ __forceinline__ float pb0(float v) {
