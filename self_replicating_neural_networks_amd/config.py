@@ -100,8 +100,7 @@ class ExecConfig:
                                             # generation (deeper levels run in its one-wave tail)
     perm_table: Optional[bool] = None       # SRNN_PERM_TABLE: a generation's SGD permutations precomputed by
                                             # one launch ahead of it (nibble Weightwise nets on the device;
-                                            # None: where the launches are latency-bound -- reference-order
-                                            # generations and < 65,536 slots per launch)
+                                            # None: the reference order's pending turns only)
 
     _ENV = dict(finish_mode="SRNN_FINISH_MODE", finish_par="SRNN_FINISH_PAR", graph_chunks="SRNN_GRAPH_CHUNKS",
                 x2_schedule="SRNN_X2_SCHEDULE", x2_prio="SRNN_X2_PRIO", x2_emulate_remote="SRNN_X2_EMULATE_REMOTE",

@@ -336,14 +336,14 @@ class SoupEngine:
             self.rowflags = torch.zeros(max(self.n, 1), **i32)
 
     def _use_perm_table(self) -> bool:
-        """ExecConfig.perm_table, auto (None): the table pays where the generation's launches are
-        latency-bound -- the reference order's small level launches, populations below one wave
-        per SIMD -- and costs more than it saves on a throughput-bound 100k launch (MI355X,
-        profiles/r4b_*: the table launch vs the permutation work it removes from the SGD chain)."""
+        """ExecConfig.perm_table, auto (None): the reference order's pending turns only (their
+        latency-bound level launches on lane pairs, k_ord_ptab: ~5 % of the slots).  A whole
+        generation's table (k_perm_table) costs more than the permutation work it removes from
+        the SGD chains at 25k-100k slots and breaks even at 12.5k (MI355X, profiles/r4b_*)."""
         pt = self.execution.perm_table
         if pt is not None:
             return bool(pt)
-        return self.order == "sequential" or self.n < 65536
+        return self.order == "sequential"
 
     def _perm_table(self):
         """The generation's SGD epoch permutations, precomputed by one launch before the
