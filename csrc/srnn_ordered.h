@@ -30,12 +30,13 @@
 //   k_ord_plan    per turn: decisions, the source version of each of its reads (src codes)
 //   k_ord_mark    per turn / row: flags the attack outputs reached past the recompute depth
 //   k_ord_level0  per turn: its producers; none -> the turn runs now (level 0), else a pending
-//                 record {turn, producers} in the workgroup's partition (+ its permutations)
+//                 record {turn, producers} in the workgroup's partition
+//   k_ord_ptab    the pending records' epoch permutations (with a table)
 //   k_ord_level   L = 1..C-1: a pass over the pending records -- a record whose producers all
 //                 ran at levels < L runs now (WW(2,2): on a lane pair); no level is computed
 //                 ahead, no DFS
-//   k_ord_tail    one workgroup: the records still pending after C-1, in rounds (fence +
-//                 barrier per round)
+//   k_ord_tail    the records still pending after level C-1, in rounds (fence + barrier per
+//                 round): the last workgroup of launch C-1 to finish, or its own launch (C = 1)
 //   k_ord_close   per row: its final version (a row attacked after its own turn ends the
 //                 generation as that attack's output), census class, the next generation's
 //                 decisions linked, block stats for the finish (newborn uids in slot order)
@@ -62,6 +63,7 @@ constexpr int MAX_LEVELS = 16;  // parallel level launches per generation (the r
 // runnable turn among the pending ones), [REM0 + L] turns still pending after level launch L
 // (turns run at level L = REM(L-1) - REM(L), level 0: n - REM(0)), [PART0 + p] records of
 // partition p
+constexpr int TICKW = 0;  // the last parallel level launch's workgroup tickets
 constexpr int TAILW = MAX_LEVELS, MAXLW = MAX_LEVELS + 1, ERRW = MAX_LEVELS + 2, REM0 = MAX_LEVELS + 3;
 // pending records live in NPART partitions (partition p: the level-0 workgroups b = p mod NPART,
 // appended by one counter each at PART0 + p: no chip-wide contended counter)
@@ -456,6 +458,23 @@ __device__ __forceinline__ void tail_rounds(const SrnnArgs& a, F&& run) {
   }
 }
 
+// the last parallel level launch (L = C-1 >= 1) runs the tail in its LAST workgroup to finish
+// (a ticket, no waiting): every other workgroup's turns are released before its ticket, so
+// the tail's rounds see them -- one launch less per generation
+template <int TPT, class F>
+__device__ __forceinline__ void level_then_tail(const SrnnArgs& a, int32_t L, F&& run) {
+  pending_pass<TPT>(a, L, run);
+  if (L != a.o_levels - 1) return;
+  __shared__ int32_t s_last;
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+  __syncthreads();
+  if (threadIdx.x == 0) s_last = atomicAdd(a.o_ctl + TICKW, 1) == (int32_t)gridDim.x - 1;
+  __syncthreads();
+  if (!s_last) return;
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  tail_rounds<TPT>(a, run);
+}
+
 }  // namespace ord
 
 template <class Net, class S>
@@ -541,7 +560,7 @@ __global__ __launch_bounds__(TB) void k_ord_level(SrnnCfg c, SrnnArgs a, int32_t
   const int32_t gen = I::gen_of(a);
   float4* samp = samp_lane<Net>(s_samp, lane);
   uint8_t* perm = s_perm + lane * PERM;
-  ord::pending_pass<1>(a, L, [&](int64_t k, int64_t q) { ord::Ord<Net, S>::turn(c, a, k, gen, samp, perm, q); });
+  ord::level_then_tail<1>(a, L, [&](int64_t k, int64_t q) { ord::Ord<Net, S>::turn(c, a, k, gen, samp, perm, q); });
 }
 
 // levels >= C: one wave
@@ -738,10 +757,12 @@ int soup_ordered(const SrnnCfg& c, const SrnnArgs& a) {
       hipLaunchKernelGGL((k_ord_level<Net, S>), dim3((unsigned)(bpp * ord::NPART)), dim3(TB), 0, st, c, a, L);
     }
   }
-  if (pairs) {
-    if constexpr (ww22) hipLaunchKernelGGL((k_ord_tail2<S>), dim3(1), dim3(pair::TBW), 0, st, c, a);
-  } else {
-    hipLaunchKernelGGL((k_ord_tail<Net, S>), dim3(1), dim3(TB), 0, st, c, a);
+  if (C == 1) {  // (C >= 2: the last level launch runs the tail in its last workgroup)
+    if (pairs) {
+      if constexpr (ww22) hipLaunchKernelGGL((k_ord_tail2<S>), dim3(1), dim3(pair::TBW), 0, st, c, a);
+    } else {
+      hipLaunchKernelGGL((k_ord_tail<Net, S>), dim3(1), dim3(TB), 0, st, c, a);
+    }
   }
   hipLaunchKernelGGL((k_ord_close<Net, S>), dim3((unsigned)nb), dim3(TB), 0, st, c, a);
   if (!(a.flags & SRNN_F_GEN_COUNTS)) {

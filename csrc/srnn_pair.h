@@ -433,7 +433,7 @@ __global__ __launch_bounds__(pair::TBW) void k_ord_level2(SrnnCfg c, SrnnArgs a,
   __shared__ float4 s_samp[pair::P * 64];
   const int tid = threadIdx.x, u = tid & 1, pi = tid >> 1;
   const int32_t gen = I::gen_of(a);
-  ord::pending_pass<2>(a, L, [&](int64_t k, int64_t q) { pair::turn<S>(c, a, k, gen, u, s_samp + pi, q); });
+  ord::level_then_tail<2>(a, L, [&](int64_t k, int64_t q) { pair::turn<S>(c, a, k, gen, u, s_samp + pi, q); });
 }
 
 // the reference-order tail (levels >= C) on pairs: one workgroup, round by round

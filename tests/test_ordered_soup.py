@@ -146,10 +146,13 @@ def test_device_ordered_generation_is_the_serial_loop(spec):
 
 
 @pytest.mark.gpu
-def test_device_ordered_tail_and_bf16_tables():
+@pytest.mark.parametrize("levels", [1, 2])
+def test_device_ordered_tail_and_bf16_tables(levels):
+    """the tail: its own launch (1 parallel level) or the last workgroup of the last level
+    launch (2)"""
     spec = ArchSpec.weightwise(2, 2)
     o = SoupEngine(spec, 2000, HOT, device="cuda", seed=2, order="sequential", dtype=torch.bfloat16,
-                   execution=ExecConfig(order_levels=1))
+                   execution=ExecConfig(order_levels=levels))
     s = SequentialSoupEngine(spec, 2000, HOT, seed=2, dtype=torch.bfloat16, device="cuda",
                              weights=o.local_rows()[:, :spec.P].cpu())
     for _ in range(3):
