@@ -537,7 +537,8 @@ struct Item {
   // a generation never waits for the uids of the previous generation's newborns.
   // SINGLE: single-rank source rows (no exchange); tk: the received row of a remote teacher
   // (SRNN_F_X2).  Returns the respawn code (also in respawn[j]).
-  template <bool SINGLE = false>
+  // TAB = false compiles the permutation-table path out (the launches that never get one)
+  template <bool SINGLE = false, bool TAB = true>
   SRNN_HD static int8_t soup_evolve(const SrnnCfg& c, const SrnnArgs& a, int64_t j, float4* samp, uint8_t* perm,
                                     uint32_t tk = SRNN_NIL, float* wout = nullptr) {
     const int64_t g = a.lo + j;
@@ -575,7 +576,7 @@ struct Item {
     tc.shuffle = (a.flags & SRNN_F_SHUFFLE) != 0;
     tc.stride = SAMP_STRIDE;
     tc.aggregator = c.aggregator;
-    if (a.ptab && a.dev) {  // this generation's permutations, precomputed (k_perm_table)
+    if (TAB && a.ptab && a.dev) {  // this generation's permutations, precomputed (k_perm_table)
       tc.ptab = a.ptab + j;
       tc.pstride = a.n;
       tc.pbase = tc.ctr;
@@ -857,7 +858,7 @@ SRNN_HD int64_t x2_remote_blocks(const SrnnArgs& a) {
 //    over a bounded grid; the last wave re-arms the list counter
 //  X2 evolves accumulate the generation's block stats (temp), with SRNN_F_FUSED_CENSUS the
 //  census class of each stored row too.
-template <class Net, class S>
+template <class Net, class S, bool TAB = false>
 __global__ __launch_bounds__(TB) void k_soup_evolve(SrnnCfg c, SrnnArgs a) {
   using I = Item<Net, S>;
   constexpr int P = Net::P;
@@ -881,7 +882,7 @@ __global__ __launch_bounds__(TB) void k_soup_evolve(SrnnCfg c, SrnnArgs a) {
   if (!(a.flags & SRNN_F_X2)) {
     const int64_t i = (int64_t)blockIdx.x * TB + lane;
     bool rs = false;
-    if (i < a.n) rs = I::soup_evolve(c, a, i, samp, perm) != 0;
+    if (i < a.n) rs = I::template soup_evolve<false, TAB>(c, a, i, samp, perm) != 0;
     if (a.flags & SRNN_F_ROW_FLAGS) {
       if (i < a.n && a.rowflags) a.rowflags[i] = rs ? 1 : 0;
     } else if (a.ballots) {
@@ -927,7 +928,7 @@ __global__ __launch_bounds__(TB) void k_soup_evolve(SrnnCfg c, SrnnArgs a) {
     int8_t k = -1;
     if (on) {
       float w[P];
-      rs = I::soup_evolve(c, a, j, samp, perm, tk, w) != 0;
+      rs = I::template soup_evolve<false, TAB>(c, a, j, samp, perm, tk, w) != 0;
       if (census) k = classify_w_(w, j);
     }
     const int64_t wd = eb * 2 + lane;
@@ -951,7 +952,7 @@ __global__ __launch_bounds__(TB) void k_soup_evolve(SrnnCfg c, SrnnArgs a) {
     int8_t k = -1;
     if (on) {
       float w[P];
-      rs = I::soup_evolve(c, a, i, samp, perm, SRNN_NIL, w) != 0;
+      rs = I::template soup_evolve<false, TAB>(c, a, i, samp, perm, SRNN_NIL, w) != 0;
       if (census) k = classify_w_(w, i);
     }
     // this wave's two dependency words are consumed (every lane read its bit above)
@@ -967,7 +968,7 @@ __global__ __launch_bounds__(TB) void k_soup_evolve(SrnnCfg c, SrnnArgs a) {
     if (q < cnt) {
       const int64_t j = a.x_rlist[2 * q];
       const uint32_t tk = a.x_rlist[2 * q + 1];
-      const bool rs = I::soup_evolve(c, a, j, samp, perm, tk) != 0;
+      const bool rs = I::template soup_evolve<false, TAB>(c, a, j, samp, perm, tk) != 0;
       const int8_t k = census ? classify_stored(j) : (int8_t)-1;
       bs_publish_lane(bs, j, rs, k);
     }
@@ -998,7 +999,7 @@ __global__ __launch_bounds__(TB) void k_soup_evolve(SrnnCfg c, SrnnArgs a) {
 //    ballots in slot order, assigns the newborns' uids, writes the census (counts[0..4]),
 //    advances next_uid and the generation counter and re-arms the ticket.
 // ----------------------------------------------------------------------------------
-template <class Net, class S>
+template <class Net, class S, bool TAB = false>
 __global__ __launch_bounds__(TB) void k_soup_gen(SrnnCfg c, SrnnArgs a) {
   using I = Item<Net, S>;
   constexpr int P = Net::P;
@@ -1016,7 +1017,7 @@ __global__ __launch_bounds__(TB) void k_soup_gen(SrnnCfg c, SrnnArgs a) {
   int8_t k = -1;
   if (i < a.n) {
     float w[P];  // the stored row (no reload of what this lane just wrote)
-    rs = I::template soup_evolve<true>(c, a, i, samp_lane<Net>(s_samp, lane), perm, SRNN_NIL, w) != 0;
+    rs = I::template soup_evolve<true, TAB>(c, a, i, samp_lane<Net>(s_samp, lane), perm, SRNN_NIL, w) != 0;
     int64_t at, te;
     I::decision(a, i, gen + 1, at, te);
     if (at >= 0) I::link(a.heads_next, a.nexts_next, at, (uint32_t)i);
@@ -1500,7 +1501,14 @@ int soup_gen(const SrnnCfg& c, const SrnnArgs& a) {
     if constexpr (std::is_same_v<Net, Weightwise<2, 2>>)
       hipLaunchKernelGGL((k_soup_gen2<S>), dim3((unsigned)blocks), dim3(pair::TBW), 0, (hipStream_t)a.stream, c, a);
   } else {
-    hipLaunchKernelGGL((k_soup_gen<Net, S>), dim3((unsigned)blocks), dim3(TB), 0, (hipStream_t)a.stream, c, a);
+    bool tab = false;
+    if constexpr (Net::KIND == 0 && Net::P <= 16) tab = a.ptab != nullptr;
+    if (tab) {
+      if constexpr (Net::KIND == 0 && Net::P <= 16)
+        hipLaunchKernelGGL((k_soup_gen<Net, S, true>), dim3((unsigned)blocks), dim3(TB), 0, (hipStream_t)a.stream, c, a);
+    } else {
+      hipLaunchKernelGGL((k_soup_gen<Net, S, false>), dim3((unsigned)blocks), dim3(TB), 0, (hipStream_t)a.stream, c, a);
+    }
   }
   if ((a.flags & SRNN_F_TWO_PHASE) && !(a.flags & SRNN_F_GEN_COUNTS)) {
     constexpr int FNT = SRNN_FINISH_NT;
@@ -1685,7 +1693,7 @@ int launch(const SrnnCfg& c, const SrnnArgs& a) {
     if (a.ptab && !whole) {
       SrnnArgs b = a;
       b.ptab = nullptr;
-      hipLaunchKernelGGL((k_soup_evolve<Net, S>), dim3((unsigned)blocks), dim3(TB), 0, st, c, b);
+      hipLaunchKernelGGL((k_soup_evolve<Net, S, false>), dim3((unsigned)blocks), dim3(TB), 0, st, c, b);
       hipError_t e = hipGetLastError();
       if (e != hipSuccess) {
         set_error(hipGetErrorString(e));
@@ -1707,7 +1715,14 @@ int launch(const SrnnCfg& c, const SrnnArgs& a) {
         return 0;
       }
     }
-    hipLaunchKernelGGL((k_soup_evolve<Net, S>), dim3((unsigned)blocks), dim3(TB), 0, st, c, a);
+    bool tab = false;
+    if constexpr (Net::KIND == 0 && Net::P <= 16) tab = a.ptab != nullptr;
+    if (tab) {
+      if constexpr (Net::KIND == 0 && Net::P <= 16)
+        hipLaunchKernelGGL((k_soup_evolve<Net, S, true>), dim3((unsigned)blocks), dim3(TB), 0, st, c, a);
+    } else {
+      hipLaunchKernelGGL((k_soup_evolve<Net, S, false>), dim3((unsigned)blocks), dim3(TB), 0, st, c, a);
+    }
   } else if (OP == OP_CLASSIFY && a.counts) {
     hipLaunchKernelGGL((k_classify_count<Net, S>), dim3((unsigned)((items + TBC - 1) / TBC)), dim3(TBC), 0, st, c, a);
   } else {
