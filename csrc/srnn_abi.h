@@ -190,9 +190,6 @@ enum SrnnOp {
 };
 
 int srnn_abi_version();  // 21
-// mismatches between the grouped Fisher-Yates decode (perm_from_bits) and its step-by-step
-// definition (perm_from_bits_ref) over `reps` 64-bit draws per permutation size 2..16 (host)
-int64_t srnn_check_perm_decode(int reps);
 int64_t srnn_args_size();  // sizeof(SrnnArgs): the ctypes mirror checks its layout against it
 int64_t srnn_cfg_size();
 int srnn_has_config(const SrnnCfg* cfg);

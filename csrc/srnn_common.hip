@@ -198,30 +198,10 @@ static int with_scratch(int op, const SrnnCfg* c, const SrnnArgs* a) {
   return dispatch(op, c, &b);
 }
 
-namespace {
-template <int N>
-int64_t perm_decode_mismatches(int reps) {
-  uint64_t u = 0x9E3779B97F4A7C15ull * (uint64_t)N;
-  int64_t bad = 0;
-  for (int r = 0; r < reps; ++r) {
-    u = u * 6364136223846793005ull + 1442695040888963407ull;
-    const uint64_t v = r == 0 ? 0ull : r == 1 ? ~0ull : r == 2 ? (1ull << 63) : u;
-    bad += srnn::perm_from_bits<N>(v) != srnn::perm_from_bits_ref<N>(v);
-  }
-  return bad;
-}
-template <int N>
-int64_t perm_decode_all(int reps) {
-  if constexpr (N < 2) return 0;
-  else return perm_decode_mismatches<N>(reps) + perm_decode_all<N - 1>(reps);
-}
-}  // namespace
-
 extern "C" {
 
 int srnn_abi_version() { return 21; }
 
-int64_t srnn_check_perm_decode(int reps) { return perm_decode_all<16>(reps); }
 
 // layout check of the ctypes mirror (ops/_lib.py): sizeof(SrnnArgs) / sizeof(SrnnCfg)
 int64_t srnn_args_size() { return (int64_t)sizeof(SrnnArgs); }

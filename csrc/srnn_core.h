@@ -85,99 +85,8 @@ SRNN_HD uint64_t perm_bits(const U4& r, uint32_t step) {
 SRNN_HD U4 perm_draw(const Rng& rng, uint64_t id, uint32_t step, uint32_t purpose) {
   return rng.draw(id, (step >> 1) * 64u, purpose);
 }
-// floor(x / D) for x < XMAX with one 24-bit multiply and a shift (exact over the range:
-// m = ceil(2^s / D), e = m D - 2^s, e (XMAX - 1) < 2^s); D = 1: x
-constexpr uint32_t div_small_shift(uint32_t d, uint32_t xmax) {
-  for (uint32_t s = 0; s < 32; ++s) {
-    const uint64_t m = ((1ull << s) + d - 1) / d, e = m * d - (1ull << s);
-    if (m < (1ull << 24) && (uint64_t)(xmax - 1) * m < (1ull << 32) && e * (xmax - 1) < (1ull << s)) return s;
-  }
-  return 99;
-}
-template <uint32_t D, uint32_t XMAX>
-SRNN_HD uint32_t div_small(uint32_t x) {
-  if constexpr (D == 1) {
-    return x;
-  } else {
-    constexpr uint32_t S = div_small_shift(D, XMAX);
-    static_assert(S < 32, "no 24-bit multiply-shift divides this range");
-    constexpr uint32_t M = (uint32_t)(((1ull << S) + D - 1) / D);
-#if defined(__HIP_DEVICE_COMPILE__)
-    return __umul24(x, M) >> S;
-#else
-    return (x * M) >> S;
-#endif
-  }
-}
-SRNN_HD uint32_t mul_small(uint32_t x, uint32_t m) {
-#if defined(__HIP_DEVICE_COMPILE__)
-  return __umul24(x, m);
-#else
-  return x * m;
-#endif
-}
-// Fisher-Yates step i (compile-time) with swap index j: nibbles i and j of (phi:plo)
-template <int I>
-SRNN_HD void fy_swap(uint32_t j, uint32_t& plo, uint32_t& phi) {
-  if constexpr (I < 8) {
-    const uint32_t ni = (plo >> (4 * I)) & 15u;
-    const uint32_t nj = (plo >> (4 * j)) & 15u;
-    const uint32_t x = ni ^ nj;
-    plo ^= (x << (4 * I)) | (x << (4 * j));
-  } else {
-    uint64_t p = ((uint64_t)phi << 32) | plo;
-    const uint64_t ni = (p >> (4 * I)) & 15u;
-    const uint64_t nj = (p >> (4 * j)) & 15u;
-    const uint64_t x = ni ^ nj;
-    p ^= (x << (4 * I)) | (x << (4 * j));
-    plo = (uint32_t)p;
-    phi = (uint32_t)(p >> 32);
-  }
-}
-// steps I, I-1, I-2 (those > 0) from ONE 64-bit multiply by (I+1) I (I-1): the product's top
-// word J = d1 I (I-1) + d2 (I-1) + d3 holds the three mixed-radix digits the step-by-step
-// decode (perm_from_bits_ref) draws, and its low 64 bits the same remainder (exact integer
-// identity), so the permutation is the same; two 64-bit multiplies per three steps instead of
-// six
-template <int I>
-SRNN_HD void fy_group(uint32_t& ul, uint32_t& uh, uint32_t& plo, uint32_t& phi) {
-  if constexpr (I > 0) {
-    constexpr int G = I >= 3 ? 3 : I;
-    constexpr uint32_t m2 = G >= 2 ? (uint32_t)I : 1u, m3 = G >= 3 ? (uint32_t)(I - 1) : 1u;
-    constexpr uint32_t M = (uint32_t)(I + 1) * m2 * m3;
-    const uint64_t lo = (uint64_t)ul * M;
-    const uint64_t hi = (uint64_t)uh * M + (lo >> 32);
-    const uint32_t J = (uint32_t)(hi >> 32);
-    ul = (uint32_t)lo;
-    uh = (uint32_t)hi;
-    const uint32_t d1 = div_small<m2 * m3, M>(J);
-    fy_swap<I>(d1, plo, phi);
-    if constexpr (G >= 2) {
-      const uint32_t r1 = J - mul_small(d1, m2 * m3);
-      const uint32_t d2 = div_small<m3, m2 * m3>(r1);
-      fy_swap<I - 1>(d2, plo, phi);
-      if constexpr (G >= 3) fy_swap<I - 2>(r1 - mul_small(d2, m3), plo, phi);
-    }
-    fy_group<I - G>(ul, uh, plo, phi);
-  }
-}
 template <int N>
 SRNN_HD uint64_t perm_from_bits(uint64_t u) {
-  static_assert(N <= 16, "nibble permutation holds at most 16 entries");
-  uint32_t plo = 0, phi = 0;
-#pragma unroll
-  for (int k = 0; k < N; ++k) {
-    if (k < 8) plo |= (uint32_t)k << (4 * k);
-    else phi |= (uint32_t)k << (4 * (k - 8));
-  }
-  uint32_t ul = (uint32_t)u, uh = (uint32_t)(u >> 32);
-  fy_group<N - 1>(ul, uh, plo, phi);
-  return ((uint64_t)phi << 32) | plo;
-}
-// the step-by-step decode (one 64-bit multiply per step): the definition perm_from_bits is
-// checked against (csrc/tests/host_selftest.cpp)
-template <int N>
-SRNN_HD uint64_t perm_from_bits_ref(uint64_t u) {
   static_assert(N <= 16, "nibble permutation holds at most 16 entries");
   // nibbles 0-7 in plo, 8-15 in phi.  j <= i, so for i < 8 (i is a compile-time constant
   // after unrolling) both nibbles live in plo and the swap is 32-bit (v_bfe_u32 + shifts)

@@ -308,7 +308,6 @@ static void seq_soup(const SrnnCfg& c, int64_t n, int steps) {
 
 int main() {
   CHECK(srnn_abi_version() == 21);
-  CHECK(srnn_check_perm_decode(100000) == 0);  // grouped Fisher-Yates decode == step by step
   seq_soup(ww22(), 257, 4);
   seq_soup(agg422(), 129, 3);
   ops_smoke(ww22(), 1000);

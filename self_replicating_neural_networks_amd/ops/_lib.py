@@ -195,8 +195,6 @@ def lib():
         L.srnn_comm_library.restype = ctypes.c_char_p
         L.srnn_storage_encode.argtypes = [vp, vp, i64, ctypes.c_int, vp]
         L.srnn_storage_encode.restype = ctypes.c_int
-        L.srnn_check_perm_decode.argtypes = [ctypes.c_int]
-        L.srnn_check_perm_decode.restype = ctypes.c_int64
         v = L.srnn_abi_version()
         if v != ABI_VERSION:
             raise NativeLibraryError(f"libsrnn ABI {v} != expected {ABI_VERSION}: rebuild with `make -C csrc`")

@@ -87,9 +87,3 @@ def test_plan_returns_the_engine_arguments_it_assumed():
     p = plan_population(ArchSpec.weightwise(2, 2), torch.float16, world=8)
     assert p["engine_kwargs"]["diagnostics"] is False and p["engine_kwargs"]["dtype"] == torch.float16
 
-
-def test_grouped_permutation_decode_is_the_step_by_step_decode():
-    """perm_from_bits (three Fisher-Yates digits per 64-bit multiply, csrc/srnn_core.h) draws
-    exactly the permutation of the step-by-step definition for every size 2..16"""
-    from self_replicating_neural_networks_amd.ops import _lib
-    assert _lib.lib().srnn_check_perm_decode(20000) == 0
