@@ -548,6 +548,17 @@ struct Item {
     const int32_t gen = gen_of(a);
     ApplyCtx x = actx(a, c, uid, (uint32_t)gen * 1024u, perm);
     const bool x2 = !SINGLE && (a.flags & SRNN_F_X2);
+    // this slot's decisions and its teacher's row first: the teacher's load is in flight
+    // while the attacks are applied (generation-start rows: nothing of this generation
+    // writes them)
+    int64_t my_at, te;
+    decision(a, g, gen, my_at, te);
+    float tw[P];
+    const char* tr = nullptr;
+    if (te >= 0) {
+      tr = SINGLE ? rowp(a.W2, te) : teacher_row(a, te, tk, RB);
+      load(tr, tw);
+    }
     // 1. attacks received, in ascending attacker slot order (generation-start attacker rows)
     for_each_attacker<SINGLE>(a, j, [&](uint32_t e, int64_t slot) {
       const char* r = SINGLE ? rowp(a.W2, (int64_t)e) : ent_row(a, e, RB);
@@ -558,8 +569,6 @@ struct Item {
       x.ctr += 1;
       copy(w, o);
     });
-    int64_t my_at, te;
-    decision(a, g, gen, my_at, te);
     int8_t act = A_NONE;
     int64_t cp = -1;
     if (my_at >= 0) {
@@ -584,9 +593,8 @@ struct Item {
     float loss = 0.f;
     // 2. learn_from a teacher (its generation-start weights)
     if (te >= 0) {
-      const char* r = SINGLE ? rowp(a.W2, te) : teacher_row(a, te, tk, RB);
-      if (x2 && tk != SRNN_NIL) x2_check(a, r, RB, te, gen);
-      load(r, f);
+      if (x2 && tk != SRNN_NIL) x2_check(a, tr, RB, te, gen);
+      copy(f, tw);
       if constexpr (Net::KIND == 0) {
         if (a.severity > 0) loss = Net::template train_epochs<false>(w, f, a.severity, tc);
       } else {
@@ -1016,11 +1024,14 @@ __global__ __launch_bounds__(TB) void k_soup_gen(SrnnCfg c, SrnnArgs a) {
   bool rs = false;
   int8_t k = -1;
   if (i < a.n) {
-    float w[P];  // the stored row (no reload of what this lane just wrote)
-    rs = I::template soup_evolve<true, TAB>(c, a, i, samp_lane<Net>(s_samp, lane), perm, SRNN_NIL, w) != 0;
+    // the next generation's attack first (its own lists: the atomic's round trip overlaps
+    // this generation's loads instead of ending the wave; list order is irrelevant, attacks
+    // are applied in ascending attacker order)
     int64_t at, te;
     I::decision(a, i, gen + 1, at, te);
     if (at >= 0) I::link(a.heads_next, a.nexts_next, at, (uint32_t)i);
+    float w[P];  // the stored row (no reload of what this lane just wrote)
+    rs = I::template soup_evolve<true, TAB>(c, a, i, samp_lane<Net>(s_samp, lane), perm, SRNN_NIL, w) != 0;
     if (census)
       k = I::classify_w(w, a.eps, (a.flags & SRNN_F_FIX_SEC) != 0,
                         I::actx(a, c, (uint64_t)(a.lo + i), 0x7FFFFFF0u, perm));
