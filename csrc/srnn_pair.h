@@ -263,8 +263,12 @@ __device__ __forceinline__ void train_ctx(const SrnnArgs& a, TrainCtx& tc, uint6
 template <class S>
 __device__ __forceinline__ int8_t evolve(const SrnnArgs& a, int64_t i, int32_t gen, int u, float4* sp, float* w) {
   using I = Item<WW22, S>;
-  float f[P], o[P];
+  float f[P], o[P], tw[P];
   I::load(I::rowp(a.W2, i), w);
+  // the decisions and the teacher's generation-start row first (its load overlaps the attacks)
+  int64_t my_at, te;
+  I::decision(a, i, gen, my_at, te);
+  if (te >= 0) I::load(I::rowp(a.W2, te), tw);
   // 1. attacks received, ascending attacker slot, generation-start attacker rows (the list is
   // consumed by both lanes of the pair: same wave, the loads precede the NIL store)
   for_each_attacker<true>(a, i, [&](uint32_t e, int64_t) {
@@ -273,14 +277,11 @@ __device__ __forceinline__ int8_t evolve(const SrnnArgs& a, int64_t i, int32_t g
     I::q(o);
     I::copy(w, o);
   });
-  int64_t my_at, te;
-  I::decision(a, i, gen, my_at, te);
   int8_t act = my_at >= 0 ? A_ATTACKING : A_NONE;
   int64_t cp = my_at >= 0 ? my_at : -1;
   TrainCtx tc;
   train_ctx(a, tc, (uint64_t)i, gen, i);
-  if (te >= 0) I::load(I::rowp(a.W2, te), f);  // 2. learn_from: the teacher's generation-start row
-  const float loss = learn_and_train<S>(a, w, f, te >= 0, tc, u, sp);
+  const float loss = learn_and_train<S>(a, w, tw, te >= 0, tc, u, sp);  // 2. learn_from, 3. self-train
   if (te >= 0) {
     act = A_LEARN_FROM;
     cp = te;
@@ -391,13 +392,13 @@ __global__ __launch_bounds__(pair::TBW) void k_soup_gen2(SrnnCfg c, SrnnArgs a) 
   bool rs = false;
   int8_t k = -1;
   if (i < a.n) {
-    float w[pair::P];
-    rs = pair::evolve<S>(a, i, gen, u, s_samp + pi, w) != 0;
-    if (u == 0) {
+    if (u == 0) {  // the next generation's attack first (the atomic overlaps this generation)
       int64_t at, te;
       I::decision(a, i, gen + 1, at, te);
       if (at >= 0) I::link(a.heads_next, a.nexts_next, at, (uint32_t)i);
     }
+    float w[pair::P];
+    rs = pair::evolve<S>(a, i, gen, u, s_samp + pi, w) != 0;
     if (census) k = pair::classify<S>(w, a.eps, (a.flags & SRNN_F_FIX_SEC) != 0, u);
   }
   if ((a.flags & SRNN_F_GEN_COUNTS) && gb == 0 && tid == 0) I::set_gen(a, gen + 1);
@@ -464,8 +465,15 @@ __device__ __forceinline__ int8_t evolve_x2(const SrnnArgs& a, int64_t j, uint32
   constexpr int64_t RB = I::RB;
   const int64_t g = a.lo + j;
   const int32_t gen = I::gen_of(a);
-  float f[P], o[P];
+  float f[P], o[P], tw[P];
   I::load(I::rowp(a.W2, j), w);
+  int64_t my_at, te;  // (the teacher's row load overlaps the attacks)
+  I::decision(a, g, gen, my_at, te);
+  const char* tr = nullptr;
+  if (te >= 0) {
+    tr = teacher_row(a, te, tk, RB);
+    I::load(tr, tw);
+  }
   for_each_attacker<false>(a, j, [&](uint32_t e, int64_t slot) {
     const char* r = ent_row(a, e, RB);
     if ((int64_t)e >= a.n) x2_check(a, r, RB, slot, gen);
@@ -474,18 +482,12 @@ __device__ __forceinline__ int8_t evolve_x2(const SrnnArgs& a, int64_t j, uint32
     I::q(o);
     I::copy(w, o);
   });
-  int64_t my_at, te;
-  I::decision(a, g, gen, my_at, te);
   int8_t act = my_at >= 0 ? A_ATTACKING : A_NONE;
   int64_t cp = my_at >= 0 ? my_at : -1;
   TrainCtx tc;
   train_ctx(a, tc, (uint64_t)g, gen, j);
-  if (te >= 0) {
-    const char* r = teacher_row(a, te, tk, RB);
-    if (tk != SRNN_NIL) x2_check(a, r, RB, te, gen);
-    I::load(r, f);
-  }
-  const float loss = learn_and_train<S>(a, w, f, te >= 0, tc, u, sp);
+  if (te >= 0 && tk != SRNN_NIL) x2_check(a, tr, RB, te, gen);
+  const float loss = learn_and_train<S>(a, w, tw, te >= 0, tc, u, sp);
   if (te >= 0) {
     act = A_LEARN_FROM;
     cp = te;
