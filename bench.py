@@ -51,9 +51,10 @@ def parse_args(argv=None):
     ap.add_argument("--order", choices=["sequential", "synchronous"], default="synchronous",
                     help="sequential: the reference's in-place, index-ordered generation (level-scheduled, "
                          "single rank); synchronous: every read from the generation-start table (shardable)")
-    ap.add_argument("--reference-order-steps", type=int, default=0,
-                    help="single rank, synchronous headline: ALSO time this many generations of the same soup in the "
-                         "reference's sequential order (reported under config.reference_order; -1: --steps)")
+    ap.add_argument("--reference-order-steps", type=int, default=None,
+                    help="synchronous headline: ALSO time this many generations of the same soup in the reference's "
+                         "sequential order (reported under config.reference_order); -1: --steps; default: --steps on "
+                         "one rank, 0 on several (the reference order is single-rank)")
     ap.add_argument("--train", type=int, default=20)
     ap.add_argument("--attacking-rate", type=float, default=0.1)
     ap.add_argument("--learn-from-rate", type=float, default=0.1)
@@ -185,7 +186,10 @@ def main(argv=None):
     # the same soup in the reference's order (level-scheduled, single rank), timed after the
     # headline's region: a second number, never part of the headline value
     ref_order = None
-    k_ref = args.steps if args.reference_order_steps < 0 else args.reference_order_steps
+    k_ref = args.reference_order_steps
+    if k_ref is None:
+        k_ref = -1 if d.world == 1 else 0
+    k_ref = args.steps if k_ref < 0 else k_ref
     if k_ref > 0 and d.world == 1 and args.order == "synchronous":
         eng.release_graphs()
         ro = SoupEngine(spec, n_total, params, device=dev, seed=args.seed, dist=d, execution=execution,
@@ -199,14 +203,19 @@ def main(argv=None):
         ro.evolve(k_ref)
         sync()
         dt_ref = time.perf_counter() - t1
-        ref_order = {"steps": k_ref, "ms_per_step": dt_ref / k_ref * 1e3, "value": n_total * k_ref / dt_ref,
-                     "final_census": ro.count(), "levels": ro.ordered_levels()}
+        ref_order = {"semantics": "reference-order", "steps": k_ref, "warmup": args.warmup,
+                     "ms_per_step": dt_ref / k_ref * 1e3, "value": n_total * k_ref / dt_ref,
+                     "unit": "particle-generations/s", "final_census": ro.count(), "levels": ro.ordered_levels()}
         ro.release_graphs()
     if d.rank == 0:
         print(json.dumps({
             "metric": "self-application steps/sec (whole node) for 100k-particle soup",
             "value": value,
             "unit": "particle-generations/s",
+            # which soup semantics `value` measures: "jacobi" (synchronous: every read from the
+            # generation-start table) or "reference-order" (code/soup.py:51-87, in place, index order);
+            # a jacobi headline carries the reference-order number under config.reference_order
+            "semantics": "reference-order" if args.order == "sequential" else "jacobi",
             "n_gpus": d.world,
             "steps": args.steps,
             "warmup": args.warmup,

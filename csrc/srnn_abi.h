@@ -47,6 +47,8 @@ enum SrnnFlag : uint32_t {
                                      // generation's exchange (block stats of the last one in temp2)
   SRNN_F_X2_PRIO = 1u << 19,         // X2 pack / post / remote evolve: raised wave issue priority (the
                                      // exchange chain wins the SIMDs it shares with the local evolve)
+  SRNN_F_ORD_CRIT = 1u << 22,        // ordered run: turns in the run order of k_ord_order (internal: set by
+                                     // the library from SRNN_KNOB_ORD_CRIT)
 };
 
 // Attack-list entries (uint32, SRNN_NIL ends a list).  Single rank: the attacker's row
@@ -151,10 +153,14 @@ struct SrnnArgs {
   int64_t scratch_bytes;  // the library's own cached device buffer (not inside a graph capture)
   // ---- ordered (reference-order) generation, OP_SOUP_ORDERED (srnn_ordered.h)
   float* W3;            // [n][pp] attack outputs A(k) of this generation
-  int32_t* o_src;       // [n][4] source versions of each turn's reads + its level
-  int32_t* o_list;      // [(o_levels + 1) * n] work lists of levels 0..o_levels-1 and the tail
-  int32_t* o_ctl;       // [19] list lengths, max level, error bits (zeroed by the plan kernel)
-  int32_t o_levels;     // parallel level launches per generation (1..16); deeper turns: the tail
+  int32_t* o_src;       // [n][4] source versions of each turn's reads + its level | [n] stored-attack
+                        // flags | [n] consumer-list heads | [ord::rec_total(n)][32] pending records |
+                        // [ord::rec_total(n)] run order of the turns without producers
+  int32_t* o_list;      // [n] the pending record of each turn (-1: no producer)
+  int32_t* o_ctl;       // [ord::CTL_WORDS = 227] record / run-order counts per partition, pending turns, max level
+                        // (host), error bits (sticky: the plan kernel clears every word but that one)
+  int32_t o_levels;     // dependency levels the host path reports one by one (1..16; the device
+                        // schedules turns by continuation, not by level)
   int32_t pad3;
   // ---- precomputed SGD epoch permutations of a soup generation (nibble Weightwise nets, shuffle
   // on): [severity + epochs][n] uint64, epoch e of local row j at ptab[e * n + j] (counter
@@ -185,11 +191,12 @@ enum SrnnOp {
                         // (links, notices, requests) + the rows of this generation's exchange
   OP_X2_POST = 21,      // after the all-to-all: uids of the previous generation's newborns, global
                         // census, received notices linked for the next generation, requests kept
-  OP_SOUP_ORDERED = 22, // one reference-order (sequential, in-place) generation, level-scheduled:
-                        // bitwise OP_SOUP_SEQ, every particle of a level in parallel (srnn_ordered.h)
+  OP_SOUP_ORDERED = 22, // one reference-order (sequential, in-place) generation scheduled by its
+                        // dependency DAG: bitwise OP_SOUP_SEQ, every turn as soon as its producers
+                        // are done (srnn_ordered.h)
 };
 
-int srnn_abi_version();  // 21
+int srnn_abi_version();  // 22
 int64_t srnn_args_size();  // sizeof(SrnnArgs): the ctypes mirror checks its layout against it
 int64_t srnn_cfg_size();
 int srnn_has_config(const SrnnCfg* cfg);
@@ -211,7 +218,9 @@ enum SrnnKnob {
   SRNN_KNOB_BIG_WAVE = 5,       // SRNN_BIG_WAVE: P = 280 nets on the wave kernels instead of row kernels (default 0)
   SRNN_KNOB_FIX_GROUP = 6,      // SRNN_FIX_GROUP: 16-lane run_fixpoint (1), lane (0), by population size (-1)
   SRNN_KNOB_SOUP_LANES = 7,     // SRNN_SOUP_LANES: lanes per particle of WW(2,2) soup generations (0 = by size)
-  SRNN_KNOB_COUNT = 8
+  SRNN_KNOB_ORD_CRIT = 8,       // SRNN_ORD_CRIT: reference-order generations run the producers of later turns
+                                // first, at raised wave priority (default 1)
+  SRNN_KNOB_COUNT = 9
 };
 void srnn_set_knob(int knob, int value);
 int srnn_get_knob(int knob);

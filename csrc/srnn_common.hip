@@ -112,8 +112,8 @@ static int dispatch_special(int op, const SrnnCfg* c, const SrnnArgs* a) {
 namespace {
 const char* const g_knob_env[SRNN_KNOB_COUNT] = {"SRNN_FORCE_GENERIC", "SRNN_RNN_WAVE", "SRNN_RNN_SPEC",
                                                  "SRNN_RNN_SOUP",      "SRNN_WW_WAVE",  "SRNN_BIG_WAVE",
-                                                 "SRNN_FIX_GROUP",     "SRNN_SOUP_LANES"};
-int g_knob[SRNN_KNOB_COUNT] = {-1, -1, -1, -1, -1, -1, -1, -1};
+                                                 "SRNN_FIX_GROUP",     "SRNN_SOUP_LANES", "SRNN_ORD_CRIT"};
+int g_knob[SRNN_KNOB_COUNT] = {-1, -1, -1, -1, -1, -1, -1, -1, -1};
 }  // namespace
 namespace srnn {
 int knob(int id, int dflt) {
@@ -200,7 +200,7 @@ static int with_scratch(int op, const SrnnCfg* c, const SrnnArgs* a) {
 
 extern "C" {
 
-int srnn_abi_version() { return 21; }
+int srnn_abi_version() { return 22; }
 
 
 // layout check of the ctypes mirror (ops/_lib.py): sizeof(SrnnArgs) / sizeof(SrnnCfg)

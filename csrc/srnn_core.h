@@ -128,6 +128,21 @@ SRNN_HD uint64_t shuffle16(const Rng& rng, uint64_t id, uint32_t step, uint32_t 
 }
 
 // ----------------------------------------------------------------------------------
+// The permutation-table SGD paths load epoch e+1's permutation word at the top of epoch e and
+// consume it at the next epoch.  The first word is loaded right before the epoch loop; left
+// pending into the loop header, it makes the compiler's wait insertion put an
+// `s_waitcnt vmcnt(0)` at the top of EVERY epoch, right behind the next word's load -- a
+// whole global-memory latency per epoch on a latency-bound chain (30 % of a lone wave's
+// cycles).  Draining it before the loop leaves each word in flight for a whole epoch.
+SRNN_HD void perm_prologue_wait() {
+#if defined(__HIP_DEVICE_COMPILE__)
+  // the builtin (not inline asm): the wait-insertion pass must SEE this wait to know the
+  // word is no longer pending at the loop header.  gfx9 encoding: vmcnt(0) expcnt(7) lgkmcnt(15)
+  __builtin_amdgcn_s_waitcnt(0x0F70);
+#endif
+}
+
+// ----------------------------------------------------------------------------------
 // Dense layer helpers (row-major (IN, OUT) kernel, y = x . K, fma chain over i).
 // ----------------------------------------------------------------------------------
 template <int IN, int OUT>
@@ -592,6 +607,7 @@ struct Weightwise {
       c.samp[k * c.stride] = make_float4(SELF ? w[k] : t[k], coords.c[k][0], coords.c[k][1], coords.c[k][2]);
     const uint64_t* pt = c.ptab + (int64_t)(c.ctr - c.pbase) * c.pstride;
     uint64_t pn = pt[0];
+    perm_prologue_wait();
     const float lr2 = 2.0f * c.lr;  // folded step -(2 lr) * err (train_epoch)
     float loss = 0.f;
     for (int e = 0; e < E; ++e) {

@@ -23,20 +23,22 @@
 // itself: a turn that reads A(j) recomputes it from A(j)'s own inputs (up to RB nested
 // attack outputs deep), and only the attack outputs past that depth are stored (W3 row j,
 // flagged by k_ord_mark).  A turn then waits only for the TRAINING of the turns it reads;
-// the DAG is shallow (100k particles: 95 % level 0, 4.8 % level 1, ~160 turns at level 2,
-// a handful at 3; storing every A(j) gives 86 / 12.5 / 1.6 % and 5-6 levels), so a
-// generation runs as
+// the DAG is shallow (100k particles: 95 % of the turns have no producer, 4.8 % are one hop
+// deep, ~170 two, a handful three).  A generation on the device runs as
 //
 //   k_ord_plan    per turn: decisions, the source version of each of its reads (src codes)
 //   k_ord_mark    per turn / row: flags the attack outputs reached past the recompute depth
-//   k_ord_level0  per turn: its producers; none -> the turn runs now (level 0), else a pending
-//                 record {turn, producers} in the workgroup's partition
+//   k_ord_count   per turn: its producers; a turn with producers becomes a pending record
+//                 {turn, producers, remaining count} and is pushed onto every producer's
+//                 consumer list (lock-free: no turn runs in this launch, so the lists are
+//                 complete before any is walked)
 //   k_ord_ptab    the pending records' epoch permutations (with a table)
-//   k_ord_level   L = 1..C-1: a pass over the pending records -- a record whose producers all
-//                 ran at levels < L runs now (WW(2,2): on a lane pair); no level is computed
-//                 ahead, no DFS
-//   k_ord_tail    the records still pending after level C-1, in rounds (fence + barrier per
-//                 round): the last workgroup of launch C-1 to finish, or its own launch (C = 1)
+//   k_ord_run     ONE launch for every turn: a lane runs its own turn if it has no producer;
+//                 a lane that finishes a turn with consumers releases its rows and counts
+//                 down each consumer's record -- the lane whose decrement reaches zero runs
+//                 that consumer next, right away (continuation scheduling: a dependent turn
+//                 starts when ITS producers are done, not when a level launch could start it;
+//                 no workgroup ever waits for another, no level launches, no tail)
 //   k_ord_close   per row: its final version (a row attacked after its own turn ends the
 //                 generation as that attack's output), census class, the next generation's
 //                 decisions linked, block stats for the finish (newborn uids in slot order)
@@ -44,9 +46,8 @@
 // Every turn runs the serial loop's per-particle code with the same Philox streams (attack
 // keyed (k, gen*1024+1), SGD (k, gen*1024+512), newborn init respawn_key(gen, k)), and a
 // recomputed attack output is the same function of the same versions, so a generation
-// equals OP_SOUP_SEQ bitwise (tests/test_ordered_soup.py, host and device).  No workgroup
-// waits for another: levels are separated by kernel boundaries, the tail's rounds by one
-// wave's own barrier.
+// equals OP_SOUP_SEQ bitwise whatever order its turns run in (tests/test_ordered_soup.py,
+// host and device).  The host path runs the same DAG level by level.
 #pragma once
 
 namespace ord {
@@ -57,23 +58,27 @@ namespace ord {
 constexpr int32_t SRC_SELF = INT32_MIN;
 constexpr int32_t SRC_ATK = INT32_MIN + 1;
 constexpr int32_t SRC_NONE = INT32_MIN + 2;
-constexpr int MAX_LEVELS = 16;  // parallel level launches per generation (the rest: the tail)
-// o_ctl words: [TAILW] turns run by the tail, [MAXLW] max level, [ERRW] error bits (2: an
-// unstored attack output past the recompute depth -- a marking bug, 4: the tail found no
-// runnable turn among the pending ones), [REM0 + L] turns still pending after level launch L
-// (turns run at level L = REM(L-1) - REM(L), level 0: n - REM(0)), [PART0 + p] records of
-// partition p
-constexpr int TICKW = 0;  // the last parallel level launch's workgroup tickets
-constexpr int TAILW = MAX_LEVELS, MAXLW = MAX_LEVELS + 1, ERRW = MAX_LEVELS + 2, REM0 = MAX_LEVELS + 3;
-// pending records live in NPART partitions (partition p: the level-0 workgroups b = p mod NPART,
-// appended by one counter each at PART0 + p: no chip-wide contended counter)
+constexpr int MAX_LEVELS = 16;  // dependency levels reported one by one (deeper: one bin)
+// o_ctl words: [MAXLW] deepest level (host path), [ERRW] error bits -- STICKY: set by any
+// generation, never cleared by the next one (2: an unstored attack output past the recompute
+// depth, a marking bug; 4: a turn that never ran), [PEND] pending turns of the generation,
+// [PART0 + p] records of partition p, [CRIT0 + p] / [BULK0 + p] turns without producers of
+// partition p that have consumers (run first) / have none
+constexpr int MAXLW = 17, ERRW = 18, PEND = 19;
+// pending records (and the run order) live in NPART partitions (partition p: the workgroups
+// b = p mod NPART, appended by one counter each: no chip-wide contended counter)
 constexpr int NPART = 64, PART0 = 2 * MAX_LEVELS + 3;
-constexpr int CTL_WORDS = PART0 + NPART;
-// o_src layout: [n][4] {own, victim, teacher, level} | [n] stored flags of A(j) |
-// [rec_total(n)][16] pending records {turn, producer count, producers...}; o_list: [n] the
-// tail's records
+constexpr int CRIT0 = PART0 + NPART, BULK0 = CRIT0 + NPART;
+constexpr int CTL_WORDS = BULK0 + NPART;
+// o_src layout: [n][4] {own, victim, teacher, level} | [n] stored flags of A(j) | [n] consumer-list
+// heads (pending records reading E(j) / A(j), EMPTY-terminated) | [rec_total(n)][REC] pending
+// records | [rec_total(n)] run order (partition p: its critical turns from the front of its
+// rec_cap slots, the others from the back); o_list: [n] the record of each pending turn (-1: none)
 constexpr int NPROD = 12;  // producers of one turn: 3 reads x 2^RB leaves
-constexpr int REC = 16;
+constexpr int REC = 32;    // record words: {turn, np, producers[NPROD], count, ready-next, next[NPROD], -}
+constexpr int R_PROD = 2, R_CNT = R_PROD + NPROD, R_RDY = R_CNT + 1, R_NEXT = R_RDY + 1;
+constexpr int32_t EMPTY = -1;
+static_assert(R_NEXT + NPROD <= REC, "record layout");
 
 SRNN_HD int32_t code_A(int64_t j) { return (int32_t)(2 * j); }
 SRNN_HD int32_t code_E(int64_t j) { return (int32_t)(2 * j + 1); }
@@ -100,11 +105,13 @@ SRNN_HD int32_t latest(const SrnnArgs& a, int64_t r, int64_t k) {
 }
 
 SRNN_HD const int32_t* src_of(const SrnnArgs& a, int64_t k) { return a.o_src + 4 * k; }
-SRNN_HD int32_t* pend(const SrnnArgs& a, int64_t q) { return a.o_src + 5 * a.n + REC * q; }
-// records per partition (each level-0 workgroup of TB turns appends to its partition only)
+SRNN_HD int32_t* cons_head(const SrnnArgs& a) { return a.o_src + 5 * a.n; }
+SRNN_HD int32_t* pend(const SrnnArgs& a, int64_t q) { return a.o_src + 6 * a.n + REC * q; }
+// records per partition (each count workgroup of TB turns appends to its partition only)
 SRNN_HD int64_t rec_cap(int64_t n) { return ((n + TB - 1) / TB + NPART - 1) / NPART * TB; }
 SRNN_HD int64_t rec_total(int64_t n) { return NPART * rec_cap(n); }
 SRNN_HD bool stored(const SrnnArgs& a, int64_t j) { return a.o_src[4 * a.n + j] != 0; }
+SRNN_HD int32_t* run_order(const SrnnArgs& a) { return a.o_src + 6 * a.n + REC * rec_total(a.n); }
 // turn k computes A(k): it attacked, and the attack output is its own row (self-attack),
 // its teacher (learn_from the victim) or read by a turn past the recompute depth
 SRNN_HD bool needs_A(const SrnnArgs& a, int64_t k, const int32_t* s) {
@@ -182,7 +189,7 @@ struct Ord {
   }
 
   // src codes of turn k (generation gen) -> o_src[k] = {own, victim, teacher, level = -1};
-  // its stored flag cleared
+  // its stored flag cleared, its consumer list emptied, no record
   SRNN_HD static void plan(const SrnnArgs& a, int64_t k, int32_t gen) {
     int64_t at, te;
     I::decision(a, k, gen, at, te);
@@ -195,6 +202,8 @@ struct Ord {
     else s[2] = latest(a, te, k);
     s[3] = -1;
     a.o_src[4 * a.n + k] = 0;
+    cons_head(a)[k] = EMPTY;
+    if (a.o_list) a.o_list[k] = -1;
   }
 
   // the attack outputs turn k and the close of row k reach past the recompute depth (every
@@ -208,7 +217,7 @@ struct Ord {
     if (ja > k) mark_version<RB>(a, code_A(ja));
   }
 
-  // the turns turn k waits for (after mark)
+  // the turns turn k waits for (after mark; a producer may appear more than once)
   SRNN_HD static int producers(const SrnnArgs& a, int64_t k, int32_t* pr, bool& bad) {
     const int32_t* s = src_of(a, k);
     int np = 0;
@@ -255,7 +264,7 @@ struct Ord {
     tc.shuffle = (a.flags & SRNN_F_SHUFFLE) != 0;
     tc.stride = SAMP_STRIDE;
     tc.aggregator = c.aggregator;
-    if (a.ptab && a.dev && prow >= 0) {  // precomputed by the level-0 launch
+    if (a.ptab && a.dev && prow >= 0) {  // precomputed by k_ord_ptab
       tc.ptab = a.ptab + prow;
       tc.pstride = rec_total(a.n);
       tc.pbase = tc.ctr;
@@ -315,25 +324,22 @@ struct Ord {
   }
 };
 
+// the distinct entries of pr[0..np) moved to its front (order of first appearance)
+SRNN_HD int dedupe(int32_t* pr, int np) {
+  int m = 0;
+  for (int q = 0; q < np; ++q) {
+    bool seen = false;
+    for (int t = 0; t < m; ++t) seen = seen || pr[t] == pr[q];
+    if (!seen) pr[m++] = pr[q];
+  }
+  return m;
+}
+
 __device__ __forceinline__ int32_t ld_level(const int32_t* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 __device__ __forceinline__ void st_level(int32_t* p, int32_t v) {
   __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ int32_t ld_ctl(const int32_t* p) {
-  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-// all producers of pending record rec have levels in [0, L)
-__device__ __forceinline__ bool ready(const SrnnArgs& a, const int32_t* rec, int32_t L) {
-  const int np = rec[1];
-  bool ok = true;
-  for (int q = 0; q < np; ++q) {
-    const int32_t lp = ld_level(a.o_src + 4 * (int64_t)rec[2 + q] + 3);
-    ok = ok && lp >= 0 && lp < L;
-  }
-  return ok;
 }
 
 // wave-aggregated append: this lane's position among the wave's `want` lanes after one
@@ -352,127 +358,30 @@ __device__ __forceinline__ int32_t wave_sum(int32_t v) {
   return v;
 }
 
-// level launch L >= 1 over the pending records, TPT threads per turn (1: lane, 2: pair),
-// workgroup b on partition b mod NPART: a record whose producers all have levels < L runs now
-// (its level becomes L); the others stay pending (REM(L), a fire-and-forget count; the last
-// parallel launch also lists them for the tail).  run(k, q): turn k of record q.
-template <int TPT, class F>
-__device__ __forceinline__ void pending_pass(const SrnnArgs& a, int32_t L, F&& run) {
-  if (ld_ctl(a.o_ctl + REM0 + L - 1) == 0) return;  // nothing left: REM(L) stays 0
-  const bool last = L == a.o_levels - 1;
-  const int part = (int)(blockIdx.x % NPART);
-  const int64_t bpp = gridDim.x / NPART, j = blockIdx.x / NPART;
-  const int64_t cnt = ld_ctl(a.o_ctl + PART0 + part), q0 = part * rec_cap(a.n);
-  const int slots = (int)blockDim.x / TPT, slot = (int)threadIdx.x / TPT, sub = (int)threadIdx.x % TPT;
-  int32_t ex = 0, nleft = 0;
-  for (int64_t base = j * slots; base < cnt; base += bpp * slots) {
-    const int64_t i = base + slot, q = q0 + i;
-    bool left = false;
-    if (i < cnt) {
-      const int32_t* rec = pend(a, q);
-      const int64_t k = rec[0];
-      if (ld_level(a.o_src + 4 * k + 3) < 0) {
-        if (ready(a, rec, L)) {
-          run(k, q);
-          if (sub == 0) {
-            st_level(a.o_src + 4 * k + 3, L);
-            ++ex;
-          }
-        } else {
-          left = sub == 0;
-        }
-      }
-    }
-    if (last) {
-      const int32_t pos = wave_append(a.o_ctl + REM0 + L, left);
-      if (left) a.o_list[pos] = (int32_t)q;  // the tail's list
-    } else {
-      nleft += left;
-    }
-  }
-  nleft = wave_sum(nleft);
-  ex = wave_sum(ex);
-  if ((threadIdx.x & 63) == 0) {
-    if (nleft) atomicAdd(a.o_ctl + REM0 + L, nleft);
-    if (ex) atomicMax(a.o_ctl + MAXLW, L);
-  }
-}
-
-// levels >= C in one workgroup, round by round over the tail's records (C = 1: every pending
-// record, partition by partition): the rows a round writes are released before the barrier
-// and the L1 is invalidated after it.  A round that runs nothing while turns are left (no DAG:
-// a bug) sets error bit 4 and stops -- never a hang.
-template <int TPT, class F>
-__device__ __forceinline__ void tail_rounds(const SrnnArgs& a, F&& run) {
-  const int C = a.o_levels;
-  const int64_t T = ld_ctl(a.o_ctl + REM0 + C - 1);
-  if (T == 0) return;
-  __shared__ int32_t s_cnt[2];
-  const int slots = (int)blockDim.x / TPT, slot = (int)threadIdx.x / TPT, sub = (int)threadIdx.x % TPT;
-  const int64_t cap = rec_cap(a.n);
-  for (int32_t lv = C;; ++lv) {
-    if (threadIdx.x == 0) s_cnt[0] = s_cnt[1] = 0;
-    __syncthreads();
-    int32_t ex = 0, left = 0;
-    auto visit = [&](int64_t q) {
-      const int32_t* rec = pend(a, q);
-      const int64_t k = rec[0];
-      if (ld_level(a.o_src + 4 * k + 3) < 0) {
-        if (ready(a, rec, lv)) {
-          run(k, q);
-          if (sub == 0) {
-            st_level(a.o_src + 4 * k + 3, lv);
-            ++ex;
-          }
-        } else if (sub == 0) {
-          ++left;
-        }
-      }
-    };
-    if (C > 1) {
-      for (int64_t i0 = 0; i0 < T; i0 += slots)
-        if (i0 + slot < T) visit(a.o_list[i0 + slot]);
-    } else {
-      for (int p = 0; p < NPART; ++p) {
-        const int64_t cnt = ld_ctl(a.o_ctl + PART0 + p);
-        for (int64_t i0 = 0; i0 < cnt; i0 += slots)
-          if (i0 + slot < cnt) visit(p * cap + i0 + slot);
-      }
-    }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    if (ex) atomicAdd(&s_cnt[0], ex);
-    if (left) atomicAdd(&s_cnt[1], left);
-    __syncthreads();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    const int32_t ext = s_cnt[0], lt = s_cnt[1];
-    if (threadIdx.x == 0 && ext) {
-      a.o_ctl[TAILW] += ext;
-      a.o_ctl[MAXLW] = lv;
-    }
-    if (lt == 0) break;
-    if (ext == 0) {
-      if (threadIdx.x == 0) atomicOr(a.o_ctl + ERRW, 4);
-      break;
-    }
-    __syncthreads();  // s_cnt is reset by the next round
-  }
-}
-
-// the last parallel level launch (L = C-1 >= 1) runs the tail in its LAST workgroup to finish
-// (a ticket, no waiting): every other workgroup's turns are released before its ticket, so
-// the tail's rounds see them -- one launch less per generation
-template <int TPT, class F>
-__device__ __forceinline__ void level_then_tail(const SrnnArgs& a, int32_t L, F&& run) {
-  pending_pass<TPT>(a, L, run);
-  if (L != a.o_levels - 1) return;
-  __shared__ int32_t s_last;
+// Turn `k` is done: publish it to its consumers (pending records pushed onto its list by
+// k_ord_count).  Its rows were stored with plain stores; they are drained and released at
+// agent scope (the consumers may run on any CU / XCD) BEFORE the counts go down.  Every
+// record whose count this lane takes to zero joins the lane's ready list (linked through the
+// records' R_RDY words): this lane runs those turns next.
+__device__ __forceinline__ void publish(const SrnnArgs& a, int64_t k, int32_t& ready) {
+  const int32_t h = cons_head(a)[k];
+  if (h == EMPTY) return;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-  __syncthreads();
-  if (threadIdx.x == 0) s_last = atomicAdd(a.o_ctl + TICKW, 1) == (int32_t)gridDim.x - 1;
-  __syncthreads();
-  if (!s_last) return;
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-  tail_rounds<TPT>(a, run);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (kept: ROCm 7.2 may drop the fence's own wait)
+  for (int32_t q = h; q != EMPTY;) {
+    int32_t* rec = pend(a, q);
+    const int np = rec[1];
+    int s = 0;
+    for (int t = 0; t < np; ++t)
+      if (rec[R_PROD + t] == (int32_t)k) s = t;
+    const int32_t nxt = rec[R_NEXT + s];
+    if (__hip_atomic_fetch_add(rec + R_CNT, -1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 1) {
+      rec[R_RDY] = ready;
+      ready = q;
+    }
+    q = nxt;
+  }
 }
 
 }  // namespace ord
@@ -480,8 +389,10 @@ __device__ __forceinline__ void level_then_tail(const SrnnArgs& a, int32_t L, F&
 template <class Net, class S>
 __global__ __launch_bounds__(TB) void k_ord_plan(SrnnCfg, SrnnArgs a) {
   const int64_t k = (int64_t)blockIdx.x * TB + threadIdx.x;
-  if (blockIdx.x == 0 && threadIdx.x < ord::CTL_WORDS) a.o_ctl[threadIdx.x] = 0;  // read from the next launch on
-  if (blockIdx.x == 0 && threadIdx.x + TB < ord::CTL_WORDS) a.o_ctl[threadIdx.x + TB] = 0;
+  // control words for the next launches (the error word is sticky: never cleared here)
+  if (blockIdx.x == 0)
+    for (int w = threadIdx.x; w < ord::CTL_WORDS; w += TB)
+      if (w != ord::ERRW) a.o_ctl[w] = 0;
   if (k < a.n) ord::Ord<Net, S>::plan(a, k, Item<Net, S>::gen_of(a));
 }
 
@@ -491,21 +402,16 @@ __global__ __launch_bounds__(TB) void k_ord_mark(SrnnCfg, SrnnArgs a) {
   if (k < a.n) ord::Ord<Net, S>::mark(a, k);
 }
 
-// level 0: every turn counts its producers; a turn without any runs now (permutations drawn
-// inline), the others become pending records of this workgroup's partition (producers written
-// straight into the record)
+// every turn counts its producers; a turn with producers becomes a pending record of this
+// workgroup's partition (producers written straight into the record, deduplicated) and is
+// pushed onto each producer's consumer list.  No turn runs here, so every list is complete
+// before k_ord_run walks any of them.
 template <class Net, class S>
-__global__ __launch_bounds__(TB) void k_ord_level0(SrnnCfg c, SrnnArgs a) {
-  using I = Item<Net, S>;
+__global__ __launch_bounds__(TB) void k_ord_count(SrnnCfg, SrnnArgs a) {
   using O = ord::Ord<Net, S>;
-  constexpr int SAMP = samp_slots<Net>();
-  constexpr int PERM = (Net::P + 4) & ~3;
-  __shared__ float4 s_samp[TB * SAMP];
-  __shared__ uint8_t s_perm[TB * PERM];
   const int lane = threadIdx.x;
   const int64_t k = (int64_t)blockIdx.x * TB + lane;
   const bool valid = k < a.n;
-  const int32_t gen = I::gen_of(a);
   int np = 0;
   bool bad = false;
   if (valid) np = O::producers(a, k, nullptr, bad);
@@ -516,26 +422,29 @@ __global__ __launch_bounds__(TB) void k_ord_level0(SrnnCfg c, SrnnArgs a) {
   if (pend) {
     const int64_t q = part * ord::rec_cap(a.n) + i;
     int32_t* rec = ord::pend(a, q);
-    rec[0] = (int32_t)k;
     bool bad2 = false;
-    rec[1] = O::producers(a, k, rec + 2, bad2);
-  } else if (valid) {
-    ord::st_level(a.o_src + 4 * k + 3, 0);
-    O::turn(c, a, k, gen, samp_lane<Net>(s_samp, lane), s_perm + lane * PERM);
+    int32_t* pr = rec + ord::R_PROD;
+    const int m = ord::dedupe(pr, O::producers(a, k, pr, bad2));
+    rec[0] = (int32_t)k;
+    rec[1] = m;
+    rec[ord::R_CNT] = m;
+    a.o_list[k] = (int32_t)q;
+    int32_t* heads = ord::cons_head(a);
+    for (int s = 0; s < m; ++s) rec[ord::R_NEXT + s] = atomicExch(heads + pr[s], (int32_t)q);
   }
   const int32_t npend = ord::wave_sum(pend ? 1 : 0);
-  if (lane == 0 && npend) atomicAdd(a.o_ctl + ord::REM0, npend);  // fire and forget
+  if (lane == 0 && npend) atomicAdd(a.o_ctl + ord::PEND, npend);  // fire and forget
 }
 
-// the epoch permutations of the pending records (their turns run on the latency-bound level
-// launches, where an inline draw sits on the chain): thread (record, epoch pair), workgroup
-// row y = partition * pairs + pair, grid-stride over the partition's records
+// the epoch permutations of the pending records (their turns run as continuations, lone
+// chains where an inline draw sits on the critical path): thread (record, epoch pair),
+// workgroup row y = partition * pairs + pair, grid-stride over the partition's records
 template <class Net>
 __global__ __launch_bounds__(TB) void k_ord_ptab(SrnnArgs a, int32_t E) {
   constexpr int P = Net::P;
   const int npair = (E + 1) / 2;
   const int part = (int)blockIdx.y / npair, p = (int)blockIdx.y % npair;
-  const int64_t cnt = ord::ld_ctl(a.o_ctl + ord::PART0 + part), q0 = part * ord::rec_cap(a.n);
+  const int64_t cnt = ord::ld_level(a.o_ctl + ord::PART0 + part), q0 = part * ord::rec_cap(a.n);
   const int64_t stride = ord::rec_total(a.n);
   const int32_t gen = a.gen_ptr ? a.gen_ptr[0] : a.gen;
   const Rng rng{(uint32_t)a.seed, (uint32_t)(a.seed >> 32)};
@@ -548,34 +457,114 @@ __global__ __launch_bounds__(TB) void k_ord_ptab(SrnnArgs a, int32_t E) {
   }
 }
 
-// levels 1..C-1: a pass over the pending records
+// the run order of the turns without producers: those with consumers (the first links of the
+// generation's dependency chains) ahead of the rest, each group partitioned like the records
 template <class Net, class S>
-__global__ __launch_bounds__(TB) void k_ord_level(SrnnCfg c, SrnnArgs a, int32_t L) {
-  using I = Item<Net, S>;
-  constexpr int SAMP = samp_slots<Net>();
-  constexpr int PERM = (Net::P + 4) & ~3;
-  __shared__ float4 s_samp[TB * SAMP];
-  __shared__ uint8_t s_perm[TB * PERM];
-  const int lane = threadIdx.x;
-  const int32_t gen = I::gen_of(a);
-  float4* samp = samp_lane<Net>(s_samp, lane);
-  uint8_t* perm = s_perm + lane * PERM;
-  ord::level_then_tail<1>(a, L, [&](int64_t k, int64_t q) { ord::Ord<Net, S>::turn(c, a, k, gen, samp, perm, q); });
+__global__ __launch_bounds__(TB) void k_ord_order(SrnnCfg, SrnnArgs a) {
+  const int64_t k = (int64_t)blockIdx.x * TB + threadIdx.x;
+  const bool root = k < a.n && a.o_list[k] < 0;
+  const bool crit = root && ord::cons_head(a)[k] != ord::EMPTY;
+  const int part = (int)(blockIdx.x % ord::NPART);
+  const int64_t cap = ord::rec_cap(a.n);
+  int32_t* order = ord::run_order(a);
+  const int32_t i = ord::wave_append(a.o_ctl + ord::CRIT0 + part, crit);
+  const int32_t j = ord::wave_append(a.o_ctl + ord::BULK0 + part, root && !crit);
+  if (crit) order[part * cap + i] = (int32_t)k;
+  else if (root) order[(part + 1) * cap - 1 - j] = (int32_t)k;
 }
 
-// levels >= C: one wave
+// the turn at position g of the run order (-1: past its end); the wave's exclusive prefixes
+// of the partitions' critical / other counts in s_c / s_b (64 partitions = one per lane)
+__device__ __forceinline__ int64_t ord_turn_at(const SrnnArgs& a, int64_t g, int32_t* s_c, int32_t* s_b,
+                                               int64_t& ncrit) {
+  const int lane = threadIdx.x & 63;
+  const int32_t c = ord::ld_level(a.o_ctl + ord::CRIT0 + lane), b = ord::ld_level(a.o_ctl + ord::BULK0 + lane);
+  int32_t ic = c, ib = b;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const int32_t vc = __shfl_up(ic, off), vb = __shfl_up(ib, off);
+    if (lane >= off) {
+      ic += vc;
+      ib += vb;
+    }
+  }
+  s_c[lane] = ic - c;
+  s_b[lane] = ib - b;
+  const int64_t C = __shfl(ic, 63), B = __shfl(ib, 63);
+  ncrit = C;
+  __syncthreads();
+  const int64_t cap = ord::rec_cap(a.n);
+  const int32_t* order = ord::run_order(a);
+  const bool isc = g < C;
+  if (!isc && g >= C + B) return -1;
+  const int64_t h = isc ? g : g - C;
+  const int32_t* pre = isc ? s_c : s_b;
+  int p = 0;  // the last partition whose prefix is <= h (a partition with entries)
+#pragma unroll
+  for (int step = 32; step > 0; step >>= 1)
+    if (pre[p + step] <= h) p += step;
+  const int64_t off = h - pre[p];
+  return isc ? order[p * cap + off] : order[(p + 1) * cap - 1 - off];
+}
+
+// every turn of the generation: lane k runs turn k if it has no producer (level 0); a lane
+// that completes a turn runs the consumers it made ready (continuations, at raised wave
+// priority: they are the generation's critical path), level = 1 + the deepest producer's
 template <class Net, class S>
-__global__ __launch_bounds__(TB) void k_ord_tail(SrnnCfg c, SrnnArgs a) {
+__global__ __launch_bounds__(TB) void k_ord_run(SrnnCfg c, SrnnArgs a) {
   using I = Item<Net, S>;
+  using O = ord::Ord<Net, S>;
   constexpr int SAMP = samp_slots<Net>();
   constexpr int PERM = (Net::P + 4) & ~3;
   __shared__ float4 s_samp[TB * SAMP];
   __shared__ uint8_t s_perm[TB * PERM];
   const int lane = threadIdx.x;
+  const int64_t k0 = (int64_t)blockIdx.x * TB + lane;
   const int32_t gen = I::gen_of(a);
   float4* samp = samp_lane<Net>(s_samp, lane);
   uint8_t* perm = s_perm + lane * PERM;
-  ord::tail_rounds<1>(a, [&](int64_t k, int64_t q) { ord::Ord<Net, S>::turn(c, a, k, gen, samp, perm, q); });
+  int64_t cur = -1, prow = -1;
+  bool raised = false;
+  if (a.flags & SRNN_F_ORD_CRIT) {  // the run order: producers of later turns first, raised priority
+    __shared__ int32_t s_c[64], s_b[64];
+    int64_t ncrit = 0;
+    cur = ord_turn_at(a, k0, s_c, s_b, ncrit);
+    if ((int64_t)blockIdx.x * TB < ncrit) {
+      __builtin_amdgcn_s_setprio(2);
+      raised = true;
+    }
+  } else if (k0 < a.n && a.o_list[k0] < 0) {
+    cur = k0;
+  }
+  if (cur >= 0) ord::st_level(a.o_src + 4 * cur + 3, 0);
+  int32_t ready = ord::EMPTY;
+  for (;;) {
+    if (cur < 0) {
+      if (ready == ord::EMPTY) break;
+      const int32_t q = ready;
+      const int32_t* rec = ord::pend(a, q);
+      ready = rec[ord::R_RDY];
+      // the producers' rows (released before their decrements) are visible after this
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if (!raised) {
+        __builtin_amdgcn_s_setprio(2);
+        raised = true;
+      }
+      cur = rec[0];
+      prow = q;
+      int32_t lv = 0;
+      for (int t = 0; t < rec[1]; ++t) {
+        const int32_t lp = ord::ld_level(a.o_src + 4 * (int64_t)rec[ord::R_PROD + t] + 3);
+        lv = lv > lp ? lv : lp;
+      }
+      ord::st_level(a.o_src + 4 * cur + 3, lv + 1);
+    }
+    O::turn(c, a, cur, gen, samp, perm, prow);
+    ord::publish(a, cur, ready);
+    cur = -1;
+    prow = -1;
+  }
 }
 
 // final rows, census, next decisions, block stats (the fused generation's two-phase form:
@@ -594,6 +583,7 @@ __global__ __launch_bounds__(TB) void k_ord_close(SrnnCfg c, SrnnArgs a) {
   bool rs = false;
   int8_t k = -1;
   if (r < a.n) {
+    if (a.o_src[4 * r + 3] < 0) atomicOr(a.o_ctl + ord::ERRW, 4);  // never ran: a scheduling bug
     float w[Net::P];
     ord::Ord<Net, S>::close_row(c, a, r, gen, perm, w);
     rs = a.respawn[r] != 0;
@@ -623,7 +613,9 @@ __global__ __launch_bounds__(TB) void k_ord_close(SrnnCfg c, SrnnArgs a) {
 
 // OP_SOUP_ORDERED: one sequential (reference-order) generation of a single-rank table.
 // W2: generation-start rows, W: the generation's rows (E versions, then the final table),
-// W3: the stored attack outputs, o_src [n][4] + [n] stored flags, o_list [(C+1) n], o_ctl [CTL_WORDS], o_levels = C;
+// W3: the stored attack outputs, o_src (layout above), o_list [n], o_ctl [CTL_WORDS],
+// o_levels: dependency levels the host path runs as separate passes (the rest: one pass per
+// level as well; the device schedules by continuation and ignores it);
 // heads / nexts: this generation's attack lists (consumed), heads_next / nexts_next: the
 // next generation's (linked here).  Device: the block stats of the two-phase fused
 // generation in temp (SRNN_F_TWO_PHASE); host: the finish inline (uids, census, counter).
@@ -641,14 +633,14 @@ int soup_ordered(const SrnnCfg& c, const SrnnArgs& a) {
               "1 <= o_levels <= 16");
     return -5;
   }
-  const int32_t C = a.o_levels;
   if (!a.dev) {
     const int32_t gen = I::gen_of(a);
-    for (int w = 0; w < ord::CTL_WORDS; ++w) a.o_ctl[w] = 0;
+    for (int w = 0; w < ord::CTL_WORDS; ++w)
+      if (w != ord::ERRW) a.o_ctl[w] = 0;
     host_parallel(a.n, [&](int64_t k) { O::plan(a, k, gen); });
     for (int64_t k = 0; k < a.n; ++k) O::mark(a, k);
     // levels in index order (every producer precedes its consumer)
-    std::vector<std::vector<int64_t>> lists((size_t)C + 1);
+    std::vector<std::vector<int64_t>> lists;
     int32_t maxl = 0;
     for (int64_t k = 0; k < a.n; ++k) {
       int32_t* s = a.o_src + 4 * k;
@@ -660,31 +652,17 @@ int soup_ordered(const SrnnCfg& c, const SrnnArgs& a) {
       for (int q = 0; q < np; ++q) lv = std::max(lv, a.o_src[4 * (int64_t)pr[q] + 3] + 1);
       s[3] = lv;
       maxl = std::max(maxl, lv);
-      lists[(size_t)std::min(lv, C)].push_back(k);
+      if ((size_t)lv >= lists.size()) lists.resize((size_t)lv + 1);
+      lists[(size_t)lv].push_back(k);
+      if (lv > 0) a.o_ctl[ord::PEND] += 1;
     }
-    // the device's control words: turns pending after each parallel level, the tail's count
-    int64_t rem = a.n;
-    for (int32_t L = 0; L < C; ++L) {
-      rem -= (int64_t)lists[(size_t)L].size();
-      a.o_ctl[ord::REM0 + L] = (int32_t)rem;
-    }
-    a.o_ctl[ord::TAILW] = (int32_t)lists[(size_t)C].size();
     a.o_ctl[ord::MAXLW] = maxl;
-    auto run_turn = [&](int64_t k) {
-      float4 samp[Net::P + 1];
-      uint8_t perm[Net::P + 4];
-      O::turn(c, a, k, gen, samp, perm);
-    };
-    for (int32_t L = 0; L < C; ++L) {
-      const auto& li = lists[(size_t)L];
-      host_parallel((int64_t)li.size(), [&](int64_t q) { run_turn(li[(size_t)q]); });
-    }
-    for (int32_t L = C; L <= maxl; ++L) {  // the tail, level by level
-      std::vector<int64_t> li;
-      for (int64_t k : lists[(size_t)C])
-        if (a.o_src[4 * k + 3] == L) li.push_back(k);
-      host_parallel((int64_t)li.size(), [&](int64_t q) { run_turn(li[(size_t)q]); });
-    }
+    for (const auto& li : lists)
+      host_parallel((int64_t)li.size(), [&](int64_t q) {
+        float4 samp[Net::P + 1];
+        uint8_t perm[Net::P + 4];
+        O::turn(c, a, li[(size_t)q], gen, samp, perm);
+      });
     std::vector<int8_t> ks((size_t)a.n, (int8_t)-1);
     const bool census = (a.flags & SRNN_F_FUSED_CENSUS) != 0;
     host_parallel(a.n, [&](int64_t r) {
@@ -730,8 +708,7 @@ int soup_ordered(const SrnnCfg& c, const SrnnArgs& a) {
   hipStream_t st = (hipStream_t)a.stream;
   hipLaunchKernelGGL((k_ord_plan<Net, S>), dim3((unsigned)nb), dim3(TB), 0, st, c, a);
   hipLaunchKernelGGL((k_ord_mark<Net, S>), dim3((unsigned)nb), dim3(TB), 0, st, c, a);
-  constexpr bool ww22 = std::is_same_v<Net, Weightwise<2, 2>>;
-  hipLaunchKernelGGL((k_ord_level0<Net, S>), dim3((unsigned)nb), dim3(TB), 0, st, c, a);
+  hipLaunchKernelGGL((k_ord_count<Net, S>), dim3((unsigned)nb), dim3(TB), 0, st, c, a);
   if constexpr (Net::KIND == 0 && Net::P <= 16) {
     const int32_t E = (a.severity > 0 ? a.severity : 0) + (a.epochs > 0 ? a.epochs : 0);
     if (a.ptab && (a.flags & SRNN_F_SHUFFLE) && E > 0) {
@@ -740,30 +717,12 @@ int soup_ordered(const SrnnCfg& c, const SrnnArgs& a) {
                          dim3(TB), 0, st, a, E);
     }
   }
-  // levels >= 1 pass over the pending records (~5 % of the turns at the reference's rates, most
-  // of them level 1): per partition, workgroups covering 8 % of its share in one pass (grid-
-  // stride beyond); WW(2,2) on lane pairs (latency-bound: srnn_pair.h)
-  const int64_t est = std::max<int64_t>(a.n / 12 / ord::NPART, 1);
-  bool pairs = false;
-  if constexpr (ww22) pairs = use_pairs(a.n / 20);
-  for (int32_t L = 1; L < C; ++L) {
-    if (pairs) {
-      if constexpr (ww22) {
-        const int64_t bpp = (est + 63) / 64;
-        hipLaunchKernelGGL((k_ord_level2<S>), dim3((unsigned)(bpp * ord::NPART)), dim3(pair::TBW), 0, st, c, a, L);
-      }
-    } else {
-      const int64_t bpp = (est + TB - 1) / TB;
-      hipLaunchKernelGGL((k_ord_level<Net, S>), dim3((unsigned)(bpp * ord::NPART)), dim3(TB), 0, st, c, a, L);
-    }
+  SrnnArgs ra = a;
+  if (knob(SRNN_KNOB_ORD_CRIT, 1) != 0) {
+    hipLaunchKernelGGL((k_ord_order<Net, S>), dim3((unsigned)nb), dim3(TB), 0, st, c, a);
+    ra.flags |= SRNN_F_ORD_CRIT;
   }
-  if (C == 1) {  // (C >= 2: the last level launch runs the tail in its last workgroup)
-    if (pairs) {
-      if constexpr (ww22) hipLaunchKernelGGL((k_ord_tail2<S>), dim3(1), dim3(pair::TBW), 0, st, c, a);
-    } else {
-      hipLaunchKernelGGL((k_ord_tail<Net, S>), dim3(1), dim3(TB), 0, st, c, a);
-    }
-  }
+  hipLaunchKernelGGL((k_ord_run<Net, S>), dim3((unsigned)nb), dim3(TB), 0, st, c, ra);
   hipLaunchKernelGGL((k_ord_close<Net, S>), dim3((unsigned)nb), dim3(TB), 0, st, c, a);
   if (!(a.flags & SRNN_F_GEN_COUNTS)) {
     constexpr int FNT = SRNN_FINISH_NT;

@@ -2,8 +2,8 @@
 // particle (lane u of a pair computes hidden unit u).  Included by srnn_kernels.h inside
 // namespace srnn, after srnn_ordered.h.
 //
-// Below one wave per SIMD (a 100k soup strong-scaled over 2-8 GPUs, the deeper levels of a
-// reference-order generation) the lane-per-particle kernels are latency-bound: every SIMD that
+// Below one wave per SIMD (a 100k soup strong-scaled over 2-8 GPUs) the lane-per-particle
+// kernels are latency-bound: every SIMD that
 // has a wave at all runs ONE particle's 280-step SGD chain per lane at ~5 cycles per dependent
 // instruction, and most SIMDs are idle.  Splitting a particle over a lane pair cuts the
 // instructions each lane issues per SGD step from 37 to 25 (the dot products of a unit stay on
@@ -13,7 +13,7 @@
 // kernel (4 weights), column u AND row u of the 2x2 kernel (its diagonal entry twice, updated
 // by the same fma) and the 2-weight output kernel.  Every fma is the lane path's
 // (MLP::forward / backward_update in folded form, Net::apply per point), so results are
-// bitwise equal to k_soup_gen / k_ord_level (tests/test_pair_soup_gpu.py).
+// bitwise equal to k_soup_gen / k_soup_evolve (tests/test_pair_soup_gpu.py).
 #pragma once
 
 namespace pair {
@@ -181,6 +181,7 @@ __device__ __forceinline__ float train(Regs& r, const float* __restrict__ t, int
   uint64_t pn = ident;
   if (tab) {
     pn = pt[0];
+    perm_prologue_wait();
   } else if (c.shuffle) {
     rr = perm_draw(c.rng, c.uid, c.ctr, P_SHUFFLE);
     pn = perm_from_bits<P>(perm_bits(rr, c.ctr));
@@ -306,64 +307,6 @@ __device__ __forceinline__ int8_t evolve(const SrnnArgs& a, int64_t i, int32_t g
   return rs;
 }
 
-// reference-order turn k (Ord::turn) on the pair
-template <class S>
-__device__ __forceinline__ void turn(const SrnnCfg& c, const SrnnArgs& a, int64_t k, int32_t gen, int u, float4* sp,
-                                     int64_t prow) {
-  using I = Item<WW22, S>;
-  using O = ord::Ord<WW22, S>;
-  (void)c;
-  const int32_t* s = a.o_src + 4 * k;
-  int64_t at, te;
-  I::decision(a, k, gen, at, te);
-  auto ap = [&](const float* x, const float* t, float* o, int64_t) { apply(x, t, o, u); };
-  float w[P], f[P], o[P];
-  O::template mat<O::RB>(a, s[0], w, ap);
-  int8_t act = A_NONE;
-  int64_t cp = -1;
-  if (at >= 0) {
-    if (ord::needs_A(a, k, s)) {
-      if (at == k) I::copy(f, w);
-      else O::template mat<O::RB>(a, s[1], f, ap);
-      apply(w, f, o, u);
-      I::q(o);
-      if (ord::stored(a, k)) I::store(I::rowp(a.W3, k), o);
-      if (at == k) I::copy(w, o);
-    }
-    act = A_ATTACKING;
-    cp = at;
-  }
-  TrainCtx tc;
-  train_ctx(a, tc, (uint64_t)k, gen, prow, ord::rec_total(a.n));
-  if (te >= 0) {
-    if (s[2] == ord::SRC_SELF) I::copy(f, w);
-    else if (s[2] == ord::SRC_ATK) I::copy(f, o);
-    else O::template mat<O::RB>(a, s[2], f, ap);
-  }
-  const float loss = learn_and_train<S>(a, w, f, te >= 0, tc, u, sp);
-  if (te >= 0) {
-    act = A_LEARN_FROM;
-    cp = te;
-  }
-  if (a.epochs > 0) {
-    act = A_TRAIN_SELF;
-    cp = -1;
-  }
-  I::q(w);
-  int8_t rs = 0;
-  if ((a.flags & SRNN_F_REMOVE_DIVERGENT) && is_diverged<P>(w)) rs = 1;
-  else if ((a.flags & SRNN_F_REMOVE_ZERO) && is_zero<P>(w, a.eps)) rs = 2;
-  if (a.traj) I::store(I::rowp(a.traj, k), w);
-  if (rs) WW22::init(w, I::rng(a), respawn_key(gen, k));
-  I::store(I::rowp(a.W, k), w);
-  if (u == 0) {
-    if (a.action) a.action[k] = act;
-    if (a.counterpart) a.counterpart[k] = cp;
-    if (a.loss) a.loss[k] = loss;
-    if (a.respawn) a.respawn[k] = rs;
-  }
-}
-
 // even-lane bits of a 64-lane ballot -> 32 bits (pair p at bit p)
 __device__ __forceinline__ uint32_t even_bits(unsigned long long x) {
   x &= 0x5555555555555555ull;
@@ -424,27 +367,6 @@ __global__ __launch_bounds__(pair::TBW) void k_soup_gen2(SrnnCfg c, SrnnArgs a) 
     mine[3] = s_bs[0][3] + s_bs[1][3];
     if ((a.flags & SRNN_F_BORN_TOTAL) && mm) atomicAdd(bs + ((a.n + TB - 1) / TB) * 4, (unsigned long long)__popcll(mm));
   }
-}
-
-// reference-order level L >= 1 on pairs (a pass over the pending records, 64 turns per
-// workgroup; level 0 runs on lanes)
-template <class S>
-__global__ __launch_bounds__(pair::TBW) void k_ord_level2(SrnnCfg c, SrnnArgs a, int32_t L) {
-  using I = Item<pair::WW22, S>;
-  __shared__ float4 s_samp[pair::P * 64];
-  const int tid = threadIdx.x, u = tid & 1, pi = tid >> 1;
-  const int32_t gen = I::gen_of(a);
-  ord::level_then_tail<2>(a, L, [&](int64_t k, int64_t q) { pair::turn<S>(c, a, k, gen, u, s_samp + pi, q); });
-}
-
-// the reference-order tail (levels >= C) on pairs: one workgroup, round by round
-template <class S>
-__global__ __launch_bounds__(pair::TBW) void k_ord_tail2(SrnnCfg c, SrnnArgs a) {
-  using I = Item<pair::WW22, S>;
-  __shared__ float4 s_samp[pair::P * 64];
-  const int tid = threadIdx.x, u = tid & 1, pi = tid >> 1;
-  const int32_t gen = I::gen_of(a);
-  ord::tail_rounds<2>(a, [&](int64_t k, int64_t q) { pair::turn<S>(c, a, k, gen, u, s_samp + pi, q); });
 }
 
 // lanes per particle of a WW(2,2) launch over `count` particles: knob SRNN_KNOB_SOUP_LANES

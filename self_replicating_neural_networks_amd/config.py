@@ -67,6 +67,15 @@ def _env_bool(name: str, default: bool) -> bool:
     return default if v is None or v == "" else v not in ("0", "false", "False", "no")
 
 
+def _tri_state(v: str) -> Optional[bool]:
+    """A tri-state knob's environment value: -1 / auto / none -> None (the built-in choice),
+    0 / false / no / off -> False, anything else -> True."""
+    t = v.strip().lower()
+    if t in ("-1", "auto", "none", "default"):
+        return None
+    return t not in ("0", "false", "no", "off")
+
+
 @dataclasses.dataclass(frozen=True)
 class ExecConfig:
     """Execution knobs: which schedule / kernel family runs, never what is computed (every
@@ -96,8 +105,10 @@ class ExecConfig:
     big_wave: Optional[bool] = None         # SRNN_BIG_WAVE
     fix_group: Optional[bool] = None        # SRNN_FIX_GROUP (None: by population size)
     soup_lanes: Optional[int] = None        # SRNN_SOUP_LANES (None / 0: by population size)
-    order_levels: int = 4                   # SRNN_ORDER_LEVELS: parallel level launches of a reference-order
-                                            # generation (deeper levels run in its one-wave tail)
+    ord_crit: Optional[bool] = None         # SRNN_ORD_CRIT: reference-order generations run the producers of
+                                            # later turns first, at raised wave priority (None: on)
+    order_levels: int = 4                   # SRNN_ORDER_LEVELS: dependency levels a reference-order generation
+                                            # reports one by one (ordered_levels; deeper: the tail bin)
     perm_table: Optional[bool] = None       # SRNN_PERM_TABLE: a generation's SGD permutations precomputed by
                                             # one launch ahead of it (nibble Weightwise nets on the device;
                                             # None: the reference order's pending turns only)
@@ -107,10 +118,14 @@ class ExecConfig:
                 sharded_graph="SRNN_SHARDED_GRAPH", native_comm="SRNN_NATIVE_COMM", loopback="SRNN_LOOPBACK",
                 force_generic="SRNN_FORCE_GENERIC", ww_wave="SRNN_WW_WAVE", rnn_wave="SRNN_RNN_WAVE",
                 rnn_spec="SRNN_RNN_SPEC", rnn_soup="SRNN_RNN_SOUP", big_wave="SRNN_BIG_WAVE",
-                fix_group="SRNN_FIX_GROUP", soup_lanes="SRNN_SOUP_LANES", order_levels="SRNN_ORDER_LEVELS",
+                fix_group="SRNN_FIX_GROUP", soup_lanes="SRNN_SOUP_LANES", ord_crit="SRNN_ORD_CRIT",
+                order_levels="SRNN_ORDER_LEVELS",
                 perm_table="SRNN_PERM_TABLE")
+    # Optional[bool] knobs whose None means "the built-in choice" (by population size, ...)
+    TRI_STATE = ("force_generic", "rnn_wave", "rnn_spec", "rnn_soup", "big_wave", "fix_group", "perm_table",
+                 "ord_crit")
     LIBRARY_KNOBS = ("force_generic", "ww_wave", "rnn_wave", "rnn_spec", "rnn_soup", "big_wave", "fix_group",
-                     "soup_lanes")
+                     "soup_lanes", "ord_crit")
 
     def validate(self):
         if self.finish_mode not in ("batch", "serial"):
@@ -143,6 +158,8 @@ class ExecConfig:
                 kw[f.name] = float(v)
             elif f.name in ("soup_lanes", "order_levels", "ww_wave"):
                 kw[f.name] = int(v)
+            elif f.name in self.TRI_STATE:
+                kw[f.name] = _tri_state(v)
             else:
                 kw[f.name] = _env_bool(env, bool(cur))
         return dataclasses.replace(self, **kw).validate() if kw else self.validate()
@@ -192,6 +209,11 @@ class RunConfig:
     checkpoint_dir: Optional[str] = None   # periodic native checkpoints (exact resume)
     checkpoint_every: int = 0
     collective_timeout_s: float = 600.0    # process-group timeout (failure detection)
+    # soup semantics: "sequential" -- the reference's in-place, index-order Soup.evolve
+    # (code/soup.py:51-87), level-scheduled on the device; "synchronous" -- Jacobi (every read
+    # from the generation-start table), the variant for shapes / rank counts the ordered
+    # generation does not cover.  A checkpoint records it; resuming with the other order raises.
+    order: str = "sequential"
     recorder: RecorderConfig = RecorderConfig()
     execution: ExecConfig = ExecConfig()   # schedules / kernel families (env vars override)
 
@@ -204,6 +226,8 @@ class RunConfig:
             raise ValueError("exchange must be alltoall or allgather")
         if self.device not in ("cuda", "cpu"):
             raise ValueError("device must be cuda or cpu")
+        if self.order not in ("sequential", "synchronous"):
+            raise ValueError("order must be sequential (the reference's) or synchronous (Jacobi)")
         if self.census_every not in (0, 1):
             # the census is fused into the generation kernel: on (every generation) or off
             raise ValueError("census_every must be 0 (final census only) or 1 (every generation)")

@@ -165,7 +165,8 @@ def save_engine(eng, path: str, chunk_bytes: int = CHUNK_BYTES) -> str:
         manifest = dict(format=FORMAT, kind="soup", spec=json.loads(eng.spec.to_json()), n_total=eng.n_total,
                         params={k: v for k, v in eng.params.items()}, seed=eng.seed, lr=eng.lr, shuffle=eng.shuffle,
                         time=eng.time, gen=int(eng.gen_dev.item()), next_uid=int(eng.next_uid.item()),
-                        world=eng.dist.world, dtype=_DTYPE_NAMES[eng.dtype], exchange=eng.exchange)
+                        world=eng.dist.world, dtype=_DTYPE_NAMES[eng.dtype], exchange=eng.exchange,
+                        order=eng.order)
         tmp = os.path.join(path, ".manifest.json")
         with open(tmp, "w") as f:
             json.dump(manifest, f, indent=1, sort_keys=True)
@@ -182,18 +183,32 @@ def _manifest(path: str, kind: str):
     return m
 
 
+def checkpoint_order(path: str) -> str:
+    """The soup order a checkpoint was written in (manifests before the field existed were
+    written by synchronous engines: the runner had no other)."""
+    return _manifest(path, "soup").get("order", "synchronous")
+
+
 def load_engine(path: str, device="cpu", dist: Optional[Dist] = None, chunk_bytes: int = CHUNK_BYTES,
-                diagnostics: bool = True):
-    """Rebuild a SoupEngine from a checkpoint (any rank count).  Each rank streams only its
-    own rows straight into its device table: host memory O(chunk), not O(shard)."""
+                diagnostics: bool = True, order: Optional[str] = None, execution=None):
+    """Rebuild a SoupEngine from a checkpoint (any rank count), in the order it was written
+    in.  ``order``: the order the caller expects -- a different one raises (resuming a
+    reference-order soup with Jacobi generations, or the reverse, would silently change its
+    dynamics).  Each rank streams only its own rows straight into its device table: host
+    memory O(chunk), not O(shard)."""
     from ..soup_engine import SoupEngine
 
     m = _manifest(path, "soup")
+    written = m.get("order", "synchronous")
+    if order is not None and order != written:
+        raise ValueError(f"{path}: checkpoint of a {written!r}-order soup; resuming it with order={order!r} would "
+                         "change its dynamics")
     spec = ArchSpec(**m["spec"])
     d = dist or Dist()
     eng = SoupEngine(spec, m["n_total"], m["params"], device=device, seed=m["seed"], lr=m["lr"],
                      shuffle=m["shuffle"], dist=d, dtype=_DTYPES[m.get("dtype", "float32")],
-                     exchange=m.get("exchange", "alltoall"), init=False, diagnostics=diagnostics)
+                     exchange=m.get("exchange", "alltoall"), init=False, diagnostics=diagnostics,
+                     order=written, execution=execution)
     rows = eng.local_rows()
     rows.zero_()
     _fill_rows(path, eng.lo, eng.hi, spec.P, rows, eng.uid, chunk_bytes)

@@ -20,7 +20,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 # SRNN_LIB: load another build of the library (A/B of compiler flags on the GPU box)
 LIB_PATH = os.environ.get("SRNN_LIB") or os.path.join(_HERE, "libsrnn.so")
 CSRC = os.path.normpath(os.path.join(_HERE, "..", "..", "csrc"))
-ABI_VERSION = 21
+ABI_VERSION = 22
 
 # SrnnOp (csrc/srnn_abi.h)
 OP_INIT = 0
@@ -41,10 +41,19 @@ OP_GEN_FINISH = 17
 OP_SOUP_SEQ = 19  # sequential (Gauss-Seidel) soup generations
 OP_X2_PACK = 20   # sharded soup, all-to-all exchange: finish + next decisions + rows (csrc/srnn_shard.hip)
 OP_X2_POST = 21   # sharded soup: uids, census, received notices / requests
-OP_SOUP_ORDERED = 22  # reference-order (sequential) generation, level-scheduled (csrc/srnn_ordered.h)
-ORD_CTL_WORDS = 99    # o_ctl words of an ordered generation (csrc/srnn_ordered.h)
-ORD_TAILW, ORD_MAXLW, ORD_ERRW, ORD_REM0 = 16, 17, 18, 19
+OP_SOUP_ORDERED = 22  # reference-order (sequential) generation, DAG-scheduled (csrc/srnn_ordered.h)
+ORD_CTL_WORDS = 227   # o_ctl words of an ordered generation (csrc/srnn_ordered.h)
+ORD_MAXLW, ORD_ERRW, ORD_PEND = 17, 18, 19
 ORD_NPART = 64        # partitions of the pending records
+ORD_REC = 32          # int32 words per pending record
+ORD_MAX_LEVELS = 16   # dependency levels reported one by one (deeper: one bin)
+
+
+def ord_src_words(n: int) -> int:
+    """int32 words of an n-turn ordered generation's o_src: [n][4] codes + level, [n] stored flags,
+    [n] consumer-list heads, the pending records, the run order of the turns without producers."""
+    n = max(int(n), 1)
+    return 6 * n + (ORD_REC + 1) * ord_rec_total(n)
 
 
 def ord_rec_total(n: int) -> int:
@@ -234,10 +243,10 @@ def supports(spec, op: int, device: bool, dtype: int = DTYPE_FP32) -> bool:
 # execution knobs (csrc/srnn_abi.h SrnnKnob; config.py ExecConfig): the environment variable
 # of a knob, when set, overrides what is set here
 KNOBS = {"force_generic": 0, "rnn_wave": 1, "rnn_spec": 2, "rnn_soup": 3, "ww_wave": 4, "big_wave": 5,
-         "fix_group": 6, "soup_lanes": 7}
+         "fix_group": 6, "soup_lanes": 7, "ord_crit": 8}
 KNOB_ENV = {"force_generic": "SRNN_FORCE_GENERIC", "rnn_wave": "SRNN_RNN_WAVE", "rnn_spec": "SRNN_RNN_SPEC",
             "rnn_soup": "SRNN_RNN_SOUP", "ww_wave": "SRNN_WW_WAVE", "big_wave": "SRNN_BIG_WAVE",
-            "fix_group": "SRNN_FIX_GROUP", "soup_lanes": "SRNN_SOUP_LANES"}
+            "fix_group": "SRNN_FIX_GROUP", "soup_lanes": "SRNN_SOUP_LANES", "ord_crit": "SRNN_ORD_CRIT"}
 
 
 def set_knob(name: str, value: int) -> None:

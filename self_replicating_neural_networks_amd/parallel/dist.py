@@ -127,10 +127,15 @@ class Dist:
     # ExecConfig (native_comm, loopback); None: the defaults, environment variables override
     execution: Optional[object] = None
     _pad_bufs: dict = dataclasses.field(default_factory=dict, repr=False)
+    _resolved: Optional[object] = dataclasses.field(default=None, repr=False)
 
     def _exec(self):
-        from ..config import ExecConfig
-        return (self.execution or ExecConfig()).resolved()
+        """The ExecConfig in force, resolved (environment overrides) once per Dist: the
+        per-generation collectives read it without re-parsing the environment."""
+        if self._resolved is None:
+            from ..config import ExecConfig
+            self._resolved = (self.execution or ExecConfig()).resolved()
+        return self._resolved
 
     def enable_native_comm(self, device) -> bool:
         """Create the soup's own RCCL communicator on ``device`` (collective over all

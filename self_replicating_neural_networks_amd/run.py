@@ -66,14 +66,19 @@ def write_checkpoint(eng, ckpt_dir: str) -> str:
 
 
 def build_engine(cfg: ExperimentConfig, dist, device, resume: bool = False):
+    """The configured soup (``run.order``: the reference's sequential order or Jacobi), or the
+    latest checkpoint's with ``resume`` -- which must have been written in the same order."""
     r = cfg.run
+    execution = r.execution.resolved()
+    execution.apply_library()
     if resume and r.checkpoint_dir:
         path = latest_checkpoint(r.checkpoint_dir)
         if path is not None:
-            eng = load_engine(path, device=device, dist=dist)
+            eng = load_engine(path, device=device, dist=dist, order=r.order, execution=execution)
             return eng, path
     eng = SoupEngine(cfg.arch, r.n_total, cfg.soup.params(), device=device, seed=r.seed, lr=r.lr,
-                     shuffle=r.shuffle, dist=dist, dtype=r.torch_dtype(), exchange=r.exchange)
+                     shuffle=r.shuffle, dist=dist, dtype=r.torch_dtype(), exchange=r.exchange,
+                     execution=execution, order=r.order)
     return eng, None
 
 
@@ -96,7 +101,7 @@ def run(cfg: ExperimentConfig, resume: bool = False, log=print):
         eng.capture(warmup=1 if d.enabled else 0)  # a sharded warmup initialises the communicator
     if d.rank == 0:
         log(json.dumps(dict(event="start", resumed_from=resumed, time=eng.time, world=d.world,
-                            n_total=eng.n_total, graph=eng._graphs is not None)))
+                            n_total=eng.n_total, order=eng.order, graph=eng._graphs is not None)))
     t0 = time.perf_counter()
     start = eng.time
     seg = r.checkpoint_every if (r.checkpoint_dir and r.checkpoint_every > 0) else max(r.generations - eng.time, 0)
@@ -115,7 +120,7 @@ def run(cfg: ExperimentConfig, resume: bool = False, log=print):
     dt = time.perf_counter() - t0
     census = eng.count()
     gens = eng.time - start
-    out = dict(event="done", time=eng.time, census=census, seconds=dt,
+    out = dict(event="done", time=eng.time, order=eng.order, census=census, seconds=dt,
                particle_generations_per_s=(eng.n_total * gens / dt) if dt > 0 and gens else None)
     if eng.trajectory is not None and r.checkpoint_dir:
         eng.trajectory.save(os.path.join(r.checkpoint_dir, "trajectories"), d.rank)

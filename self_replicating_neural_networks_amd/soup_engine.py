@@ -63,6 +63,8 @@ RESPAWN_NAMES = {1: "divergent_dead", 2: "zweo_dead"}  # sic, reference code/sou
 # list entries are uint32 (csrc/srnn_abi.h): a single-rank or all-gather soup addresses its
 # slots directly; a sharded all-to-all soup addresses local rows + received rows per rank
 MAX_SLOTS_DIRECT = 2 ** 32 - 2
+# rows of a reference-order generation per rank (int32 version codes 2j / 2j+1, csrc/srnn_ordered.h)
+ORDERED_MAX_ROWS = 2 ** 30 - 1
 X2_ERRORS = {1: "exchange capacity overflow (rows, notices or requests dropped)",
              4: "exchange protocol mismatch (row tag / slot range)"}
 
@@ -114,10 +116,28 @@ def _finish_batch(nb: int, chunks) -> int:
     return max(1, min(max(list(chunks) or [1]), (512 << 20) // (nb * 32)))
 
 
+def ordered_bytes(spec: ArchSpec, n: int, dtype=torch.float32, epochs: int = 0) -> int:
+    """Device bytes of the reference-order generation's buffers for ``n`` rows
+    (SoupEngine._init_ordered): the stored attack outputs W3 (n rows of the table), the turns'
+    source codes + levels, the stored flags and the pending records (csrc/srnn_ordered.h
+    o_src), the tail's list, the control words, and -- nibble Weightwise nets with shuffled
+    SGD on the device -- the pending records' epoch permutations (``epochs`` = train +
+    learn_from_severity)."""
+    n1 = max(int(n), 1)
+    rb = spec.PP * torch.empty((), dtype=dtype).element_size()
+    rec = _lib.ord_rec_total(n1)
+    b = n * rb + 4 * _lib.ord_src_words(n1) + 4 * n1 + 4 * _lib.ORD_CTL_WORDS
+    if spec.kind == "weightwise" and spec.P <= 16 and epochs > 0 and (n + 4096) * epochs * 8 <= (2 << 30):
+        b += rec * epochs * 8
+    return int(b)
+
+
 def engine_bytes(spec: ArchSpec, n_total: int, world: int = 1, dtype=torch.float32, exchange: str = "alltoall",
                  attacking_rate: float = 0.1, learn_from_rate: float = 0.1, segment: int = 0,
-                 diagnostics: bool = True) -> int:
-    """Device bytes one rank of a SoupEngine allocates (the tensors of ``__init__``)."""
+                 diagnostics: bool = True, order: str = "synchronous", epochs: int = 0) -> int:
+    """Device bytes one rank of a SoupEngine allocates (the tensors of ``__init__``);
+    ``order="sequential"`` adds the reference-order generation's buffers (``ordered_bytes``,
+    ``epochs`` = train + learn_from_severity for its permutation table)."""
     R = world
     n = -(-n_total // R)
     rb = spec.PP * torch.empty((), dtype=dtype).element_size()
@@ -142,12 +162,15 @@ def engine_bytes(spec: ArchSpec, n_total: int, world: int = 1, dtype=torch.float
         b += 2 * n * 4 + nb * 32  # links, block stats
         # the batched-finish ring, sized as SoupEngine._init_single_or_allgather sizes it
         b += _finish_batch(nb, ExecConfig().resolved().graph_chunks) * (nb * 8 + 2) * 4
+    if order == "sequential":
+        b += ordered_bytes(spec, n, dtype, epochs)
     return int(b)
 
 
 def plan_population(spec: ArchSpec, dtype=torch.float32, exchange: str = "alltoall", world: int = 1,
                     hbm_bytes: int = 288 * 10 ** 9, fill: float = 0.9, attacking_rate: float = 0.1,
-                    learn_from_rate: float = 0.1, diagnostics: bool = False, segment: int = 0) -> Dict:
+                    learn_from_rate: float = 0.1, diagnostics: bool = False, segment: int = 0,
+                    order: str = "synchronous", epochs: int = 0) -> Dict:
     """The largest population whose per-rank engine (``engine_bytes``) fits ``fill`` of each
     GPU's HBM (288 GB HBM3E per MI355X), and what limits it: the HBM, or the uint32 attack-list
     entries (single-rank / all-gather soups address < 2^32 slots; a sharded all-to-all soup
@@ -155,7 +178,7 @@ def plan_population(spec: ArchSpec, dtype=torch.float32, exchange: str = "alltoa
     diagnostics columns (``diagnostics=False``, 13 B per row); the returned ``engine_kwargs``
     are what the planned ``SoupEngine`` must be built with for the plan to hold."""
     kw = dict(world=world, dtype=dtype, exchange=exchange, attacking_rate=attacking_rate,
-              learn_from_rate=learn_from_rate, diagnostics=diagnostics, segment=segment)
+              learn_from_rate=learn_from_rate, diagnostics=diagnostics, segment=segment, order=order, epochs=epochs)
     budget = fill * hbm_bytes
     lo, hi = 1, 1 << 50
     while lo < hi:  # largest n_total with engine_bytes <= budget
@@ -179,12 +202,15 @@ def plan_population(spec: ArchSpec, dtype=torch.float32, exchange: str = "alltoa
         limit = lo2
     else:
         limit = MAX_SLOTS_DIRECT
+    why = "uint32 list entries"
+    if order == "sequential" and ORDERED_MAX_ROWS * world < limit:
+        limit, why = ORDERED_MAX_ROWS * world, "ordered version codes (int32)"
     n_total = min(n_fit, limit)
-    return dict(n_total=n_total, n_total_fit=n_fit, limited_by="hbm" if n_fit <= limit else "uint32 list entries",
+    return dict(n_total=n_total, n_total_fit=n_fit, limited_by="hbm" if n_fit <= limit else why,
                 bytes_per_gpu=engine_bytes(spec, n_total, **kw),
                 bytes_per_particle_per_gpu=engine_bytes(spec, n_total, **kw) / max(n_total, 1),
                 world=world, exchange=exchange, dtype=str(dtype).replace("torch.", ""),
-                engine_kwargs=dict(dtype=dtype, exchange=exchange, diagnostics=diagnostics))
+                engine_kwargs=dict(dtype=dtype, exchange=exchange, diagnostics=diagnostics, order=order))
 
 
 class SoupEngine:
@@ -374,30 +400,40 @@ class SoupEngine:
                 f"no level-scheduled reference-order generation for {self.spec}: it exists for the "
                 "lane-per-particle template shapes; SequentialSoupEngine runs the same order for any shape on the "
                 "host, SoupEngine(order='synchronous') any shape on the device")
-        if self.n >= 1 << 30:
+        if self.n > ORDERED_MAX_ROWS:
             raise ValueError("reference-order generations address < 2^30 slots")
         dev = self.device
         C = int(self.execution.order_levels)
         self.order_levels = C
         self._abuf = torch.zeros((self.n, self.spec.PP), dtype=self.dtype, device=dev)
-        # [n][4] source codes + level | [n] stored-attack flags | [rec_total][16] pending records
-        self._osrc = torch.zeros(5 * max(self.n, 1) + 16 * _lib.ord_rec_total(max(self.n, 1)), dtype=torch.int32,
-                                 device=dev)
-        self._olist = torch.zeros(max(self.n, 1), dtype=torch.int32, device=dev)  # the tail's records
+        # [n][4] source codes + level | [n] stored-attack flags | [n] consumer lists | pending records
+        self._osrc = torch.zeros(_lib.ord_src_words(self.n), dtype=torch.int32, device=dev)
+        self._olist = torch.zeros(max(self.n, 1), dtype=torch.int32, device=dev)  # each turn's record
         self._octl = torch.zeros(_lib.ORD_CTL_WORDS, dtype=torch.int32, device=dev)
         self._rec_rows = None  # recording: every particle's state before any respawn
 
     def ordered_levels(self) -> Dict[str, int]:
-        """Dependency levels of the last reference-order generation: turns per parallel level,
-        the tail's turns, the deepest level, error bits (2: an attack output past the recompute
-        depth left unstored, 4: the tail found no runnable turn), and how many attack outputs were
-        stored for later turns (the others are recomputed by the turns that read them)."""
-        c = self._octl.cpu().tolist()
+        """Dependency levels of the last reference-order generation (a turn's level: 1 + its
+        deepest producer's, 0 without one): turns per level for the first ``order_levels``
+        levels, the turns deeper than those (``tail``), the deepest level, the turns that had
+        producers (``pending``: on the device, run as continuations), the error bits (sticky over
+        the engine's life: 2 -- an attack output past the recompute depth left unstored, 4 -- a
+        turn that never ran), and how many attack outputs were stored for later turns (the others
+        are recomputed by the turns that read them)."""
         C = self.order_levels
-        stored = int(self._osrc[4 * self.n:5 * self.n].sum().item()) if self.n else 0
-        rem = [self.n] + c[_lib.ORD_REM0:_lib.ORD_REM0 + C]  # turns pending before / after each level
-        return dict(levels=[rem[L] - rem[L + 1] for L in range(C)], tail=c[_lib.ORD_TAILW],
-                    max_level=c[_lib.ORD_MAXLW], error=c[_lib.ORD_ERRW], stored_attacks=stored)
+        n = self.n
+        lv = self._osrc[:4 * n].view(n, 4)[:, 3] if n else self._osrc[:0]
+        hist = torch.bincount(lv.clamp(0, _lib.ORD_MAX_LEVELS).long(), minlength=_lib.ORD_MAX_LEVELS + 1)
+        hist = hist.cpu().tolist()
+        c = self._octl.cpu().tolist()
+        err = c[_lib.ORD_ERRW] | (4 if n and int((lv < 0).sum().item()) else 0)
+        stored = int(self._osrc[4 * n:5 * n].sum().item()) if n else 0
+        return dict(levels=hist[:C], tail=sum(hist[C:]), max_level=int(lv.max().item()) if n else 0,
+                    pending=c[_lib.ORD_PEND], error=err, stored_attacks=stored)
+
+    def ordered_error(self) -> int:
+        """The reference-order generations' error bits, sticky over the engine's life (0: none)."""
+        return int(self._octl[_lib.ORD_ERRW].item()) if self.order == "sequential" else 0
 
     def _init_x2(self, n_links):
         dev, R = self.device, self.dist.world
@@ -933,11 +969,10 @@ class SoupEngine:
         err = self.exchange_error()
         if err:
             raise RuntimeError(f"soup row exchange failed ({err}): results are invalid")
-        if self.order == "sequential":
-            e = int(self._octl[_lib.ORD_ERRW].item())
-            if e:
-                raise RuntimeError(f"reference-order generation: error bits {e} (2: an unstored attack output past "
-                                   "the recompute depth, 4: the tail found no runnable turn); results are invalid")
+        e = self.ordered_error()
+        if e:
+            raise RuntimeError(f"reference-order generation: error bits {e} (2: an unstored attack output past "
+                               "the recompute depth, 4: a turn that never ran); results are invalid")
         c = torch.zeros(6, dtype=torch.int64, device=self.device)
         cls, _ = K.classify(self.spec, self.local_rows(), self.eps, with_sec, uid=None, seed=self.seed,
                             scratch=self._scratch, ctr=0x7FFFFFF0, counts=c, key_offset=self.lo)
@@ -1030,7 +1065,8 @@ class SoupEngine:
         names = ["_bufs", "uid", "next_uid", "_gen_ring", "heads", "nexts", "ballots", "rowflags", "action",
                  "counterpart", "loss", "respawn", "counts", "census", "err", "full", "stats_all", "_blockstat",
                  "_done", "_bs_ring", "x_dep", "x_rlist", "x_rcount", "x_rslot", "x_satt", "x_cno", "x_crq",
-                 "x_srep", "x_nsrep", "x_part", "x_ctl", "x_bstat", "x_hpre", "x_hgrp", "sendbuf", "recvbuf"]
+                 "x_srep", "x_nsrep", "x_part", "x_ctl", "x_bstat", "x_hpre", "x_hgrp", "sendbuf", "recvbuf",
+                 "_abuf", "_osrc", "_olist", "_octl", "_ptab"]
         out = []
         for k in names:
             v = getattr(self, k, None)

@@ -61,3 +61,18 @@ def test_bench_world_size_mismatch_exits_nonzero():
                        text=True, timeout=120)
     assert p.returncode != 0
     assert "WORLD_SIZE=2" in p.stderr
+
+
+def test_bench_reports_the_reference_order_by_default():
+    """a 1-rank run (the driver's BENCH form) always carries the same soup timed in the
+    reference's in-place order next to the headline, and says which semantics `value` is"""
+    d = _bench("--particles", "1500")
+    assert d["semantics"] == "jacobi"
+    ro = d["config"]["reference_order"]
+    assert ro is not None and ro["semantics"] == "reference-order" and ro["steps"] == d["steps"]
+    assert ro["ms_per_step"] > 0 and ro["value"] > 0 and sum(ro["final_census"].values()) == 1500
+    assert ro["levels"]["error"] == 0 and sum(ro["levels"]["levels"]) + ro["levels"]["tail"] == 1500
+    off = _bench("--particles", "1500", "--reference-order-steps", "0")
+    assert off["config"]["reference_order"] is None
+    seq = _bench("--particles", "1500", "--order", "sequential")
+    assert seq["semantics"] == "reference-order" and seq["config"]["reference_order"] is None

@@ -101,3 +101,30 @@ def test_streaming_checkpoint_16bit_chunks_and_v1_compat(tmp_path):
     (v1 / "manifest.json").write_text(json.dumps(m))
     f = C.load_engine(str(v1))
     assert torch.equal(f.local_rows(), e.local_rows()) and torch.equal(f.uid, e.uid)
+
+
+def test_reference_order_resume_is_exact_and_order_checked(tmp_path):
+    """an ordered (reference-order) soup checkpointed mid-run resumes in the SAME order, bitwise
+    equal to the uninterrupted run; resuming it as another order raises instead of silently
+    switching to Jacobi dynamics"""
+    import pytest
+
+    spec = ArchSpec.weightwise(2, 2)
+    a = SoupEngine(spec, 300, PARAMS, seed=9, order="sequential")
+    a.evolve(5)
+    b = SoupEngine(spec, 300, PARAMS, seed=9, order="sequential")
+    b.evolve(2)
+    C.save_engine(b, str(tmp_path / "ck"))
+    assert C.checkpoint_order(str(tmp_path / "ck")) == "sequential"
+    c = C.load_engine(str(tmp_path / "ck"))
+    assert c.order == "sequential"
+    c.evolve(3)
+    assert torch.equal(a.uid, c.uid) and int(a.next_uid) == int(c.next_uid) and c.time == 5
+    assert torch.equal(a.local_rows(), c.local_rows())
+    assert torch.equal(a.action, c.action) and torch.equal(a.loss.view(torch.int32), c.loss.view(torch.int32))
+    with pytest.raises(ValueError, match="change its dynamics"):
+        C.load_engine(str(tmp_path / "ck"), order="synchronous")
+    s = SoupEngine(spec, 300, PARAMS, seed=9)
+    C.save_engine(s, str(tmp_path / "cs"))
+    with pytest.raises(ValueError, match="change its dynamics"):
+        C.load_engine(str(tmp_path / "cs"), order="sequential")

@@ -39,6 +39,19 @@ def test_environment_overrides_config(monkeypatch):
     assert r.x2_schedule == "overlap" and r.graph_chunks == (6, 2) and r.finish_par is False
 
 
+@pytest.mark.parametrize("val,want", [("-1", None), ("", "unset"), ("auto", None), ("0", False), ("1", True),
+                                      ("off", False)])
+def test_tri_state_knobs_parse_as_tri_state(monkeypatch, val, want):
+    """SRNN_FIX_GROUP / SRNN_PERM_TABLE: -1 (or auto) is "by population size", not True"""
+    monkeypatch.setenv("SRNN_FIX_GROUP", val)
+    monkeypatch.setenv("SRNN_PERM_TABLE", val)
+    r = ExecConfig(fix_group=True).resolved()
+    if want == "unset":  # empty: the config's own value stays
+        assert r.fix_group is True and r.perm_table is None
+    else:
+        assert r.fix_group is want and r.perm_table is want
+
+
 def test_engine_reads_config_not_environment():
     spec = ArchSpec.weightwise(2, 2)
     e = SoupEngine(spec, 256, dict(train=1), device="cpu", execution=ExecConfig(graph_chunks=(6, 2)))
@@ -70,15 +83,21 @@ def _held_bytes(e: SoupEngine) -> int:
     return total
 
 
+@pytest.mark.parametrize("order", ["synchronous", "sequential"])
 @pytest.mark.parametrize("n,diag", [(1000, True), (5000, False), (64, True)])
-def test_engine_bytes_matches_a_constructed_single_rank_engine(n, diag):
+def test_engine_bytes_matches_a_constructed_single_rank_engine(n, diag, order):
     spec = ArchSpec.weightwise(2, 2)
-    e = SoupEngine(spec, n, dict(train=1), device="cpu", diagnostics=diag)
-    est = engine_bytes(spec, n, diagnostics=diag)
+    e = SoupEngine(spec, n, dict(train=1), device="cpu", diagnostics=diag, order=order)
+    est = engine_bytes(spec, n, diagnostics=diag, order=order, epochs=2)
     held = _held_bytes(e)
     if e._bs_ring is None:  # the batched-finish ring is a GPU-only buffer: add what a GPU engine holds
         nb = max(-(-n // 64), 1)
         held += _finish_batch(nb, e._chunk_sizes()) * (nb * 8 + 2) * 4
+    if order == "sequential":
+        # the pending records' permutation table is a GPU-only buffer too (train 1 + severity 1)
+        assert getattr(e, "_ptab", None) is None
+        held += _lib.ord_rec_total(n) * 2 * 8
+        assert est > engine_bytes(spec, n, diagnostics=diag) + n * spec.PP * 4  # W3 alone is a table
     # the model may round a few small control tensors up; never low by more than 1 %
     assert est >= held * 0.99 and est <= held * 1.05 + 512, (est, held)
 
@@ -86,4 +105,10 @@ def test_engine_bytes_matches_a_constructed_single_rank_engine(n, diag):
 def test_plan_returns_the_engine_arguments_it_assumed():
     p = plan_population(ArchSpec.weightwise(2, 2), torch.float16, world=8)
     assert p["engine_kwargs"]["diagnostics"] is False and p["engine_kwargs"]["dtype"] == torch.float16
+    q = plan_population(ArchSpec.weightwise(2, 2), torch.float16, world=1, order="sequential", epochs=21)
+    s = plan_population(ArchSpec.weightwise(2, 2), torch.float16, world=1)
+    assert q["engine_kwargs"]["order"] == "sequential"
+    # the ordered buffers make a rank hold fewer particles; int32 version codes cap it below 2^30
+    assert q["n_total"] < s["n_total"] and q["n_total"] <= 2 ** 30 - 1
+    assert q["limited_by"] in ("hbm", "ordered version codes (int32)")
 

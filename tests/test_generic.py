@@ -123,7 +123,9 @@ def test_reference_facades_any_shape():
         expect = O.apply(net.spec, before[None], before[None])[0]
         net.self_attack()
         got = net.get_weights_flat()
-        assert np.allclose(got, expect, rtol=1e-4, atol=1e-6), net.spec
+        # the engine fuses a*b+c (host and device alike), the oracle rounds the product: a
+        # 17-step linear recurrence carries that to a few 1e-6 of the row's scale
+        assert np.max(np.abs(got - expect)) <= 1e-5 * max(np.max(np.abs(expect)), 1.0), net.spec
         t = TrainingNeuralNetworkDecorator(net)
         loss = t.compiled().train()
         assert np.isfinite(loss) or net.is_diverged()

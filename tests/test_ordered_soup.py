@@ -199,3 +199,17 @@ def test_ordered_records_equal_native_records():
             assert x.get("time") == y.get("time") and np.array_equal(x["weights"].view(np.int32), y["weights"].view(np.int32))
             n_cp += x.get("counterpart") is not None
     assert n_cp > 0
+
+
+def test_ordered_error_bits_are_sticky():
+    """an error bit of one reference-order generation survives the later generations of the same
+    evolve (the plan of the next generation clears every control word but that one), so count()
+    still refuses the invalid rows"""
+    o = SoupEngine(ArchSpec.weightwise(2, 2), 200, HOT, device="cpu", seed=1, order="sequential")
+    o.evolve(1)
+    assert o.ordered_error() == 0
+    o._octl[_lib.ORD_ERRW] = 2  # as k_ord_count sets it for an unstored attack output
+    o.evolve(3)
+    assert o.ordered_error() == 2 and o.ordered_levels()["error"] == 2
+    with pytest.raises(RuntimeError, match="error bits 2"):
+        o.count()

@@ -133,3 +133,24 @@ def test_profiling_helpers():
     assert cmds[0][:5] == ["timeout", "-k", "10", "120", "rocprofv3"]
     assert all(c[c.index("--") + 1] == "python3" for c in cmds)  # program right after --
     assert not any("--sys-trace" in c for c in cmds)
+
+
+def test_runner_runs_the_reference_order_by_default_and_resumes_it(tmp_path):
+    """RunConfig.order defaults to the reference's sequential order; the runner's checkpoints
+    record it and --resume continues it bitwise; a resume with the other order raises"""
+    assert RunConfig().order == "sequential"
+    straight, out = run(_cfg(tmp_path, generations=5), log=lambda s: None)
+    assert straight.order == "sequential" and out["order"] == "sequential"
+    ref = SoupEngine(ArchSpec.weightwise(2, 2), 150, SOUP.params(), seed=4, order="sequential").evolve(5)
+    assert torch.equal(straight.local_rows(), ref.local_rows())
+    ck = str(tmp_path / "ck")
+    run(_cfg(tmp_path, generations=2, checkpoint_dir=ck, checkpoint_every=2), log=lambda s: None)
+    eng, _ = run(_cfg(tmp_path, generations=5, checkpoint_dir=ck, checkpoint_every=3), resume=True,
+                 log=lambda s: None)
+    assert eng.order == "sequential" and eng.time == 5
+    assert torch.equal(eng.local_rows(), straight.local_rows()) and torch.equal(eng.uid, straight.uid)
+    with pytest.raises(ValueError, match="change its dynamics"):
+        run(_cfg(tmp_path, generations=6, checkpoint_dir=ck, checkpoint_every=3, order="synchronous"), resume=True,
+            log=lambda s: None)
+    with pytest.raises(ValueError):
+        _cfg(tmp_path, order="gauss-seidel")
