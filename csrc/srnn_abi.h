@@ -166,6 +166,9 @@ struct SrnnArgs {
   // on): [severity + epochs][n] uint64, epoch e of local row j at ptab[e * n + j] (counter
   // gen * 1024 + 512 + e); filled by the generation's own k_perm_table launch.  null: inline
   uint64_t* ptab;
+  // ---- ordered generation trace (debug, SoupEngine.ordered_trace): [n][2] s_memrealtime (100 MHz,
+  // chip-wide) at the start and the end (after its publish) of each turn on the device.  null: off
+  uint64_t* o_trace;
 };
 
 #define SRNN_X2_HDR 12  // int64 header words of an X2 exchange block (see srnn_shard.hip)
@@ -196,7 +199,7 @@ enum SrnnOp {
                         // are done (srnn_ordered.h)
 };
 
-int srnn_abi_version();  // 22
+int srnn_abi_version();  // 23
 int64_t srnn_args_size();  // sizeof(SrnnArgs): the ctypes mirror checks its layout against it
 int64_t srnn_cfg_size();
 int srnn_has_config(const SrnnCfg* cfg);

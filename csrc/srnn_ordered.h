@@ -61,10 +61,10 @@ constexpr int32_t SRC_NONE = INT32_MIN + 2;
 constexpr int MAX_LEVELS = 16;  // dependency levels reported one by one (deeper: one bin)
 // o_ctl words: [MAXLW] deepest level (host path), [ERRW] error bits -- STICKY: set by any
 // generation, never cleared by the next one (2: an unstored attack output past the recompute
-// depth, a marking bug; 4: a turn that never ran), [PEND] pending turns of the generation,
-// [PART0 + p] records of partition p, [CRIT0 + p] / [BULK0 + p] turns without producers of
+// depth, a marking bug; 4: a turn that never ran), [PART0 + p] records (pending turns) of
+// partition p, [CRIT0 + p] / [BULK0 + p] turns without producers of
 // partition p that have consumers (run first) / have none
-constexpr int MAXLW = 17, ERRW = 18, PEND = 19;
+constexpr int MAXLW = 17, ERRW = 18;
 // pending records (and the run order) live in NPART partitions (partition p: the workgroups
 // b = p mod NPART, appended by one counter each: no chip-wide contended counter)
 constexpr int NPART = 64, PART0 = 2 * MAX_LEVELS + 3;
@@ -228,8 +228,8 @@ struct Ord {
   }
 
   // turn k: the serial loop's particle step (soup_seq_one) reading the versions of its plan
-  // (prow >= 0: the turn's epoch permutations are row prow of the pending records' table, stride
-  // rec_total; else drawn inline)
+  // (prow >= 0: the turn's epoch permutations are row prow of k_ord_ptab's table, stride
+  // 2 rec_total; else drawn inline)
   SRNN_HD static void turn(const SrnnCfg& c, const SrnnArgs& a, int64_t k, int32_t gen, float4* samp, uint8_t* perm,
                            int64_t prow = -1) {
     const int32_t* s = a.o_src + 4 * k;
@@ -266,7 +266,7 @@ struct Ord {
     tc.aggregator = c.aggregator;
     if (a.ptab && a.dev && prow >= 0) {  // precomputed by k_ord_ptab
       tc.ptab = a.ptab + prow;
-      tc.pstride = rec_total(a.n);
+      tc.pstride = 2 * rec_total(a.n);
       tc.pbase = tc.ctr;
     }
     float loss = 0.f;
@@ -362,8 +362,8 @@ __device__ __forceinline__ int32_t wave_sum(int32_t v) {
 // k_ord_count).  Its rows were stored with plain stores; they are drained and released at
 // agent scope (the consumers may run on any CU / XCD) BEFORE the counts go down.  Every
 // record whose count this lane takes to zero joins the lane's ready list (linked through the
-// records' R_RDY words): this lane runs those turns next.
-__device__ __forceinline__ void publish(const SrnnArgs& a, int64_t k, int32_t& ready) {
+// records' R_RDY words, `nready` long); k_ord_run shares the lists out over its wave.
+__device__ __forceinline__ void publish(const SrnnArgs& a, int64_t k, int32_t& ready, int32_t& nready) {
   const int32_t h = cons_head(a)[k];
   if (h == EMPTY) return;
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -379,6 +379,7 @@ __device__ __forceinline__ void publish(const SrnnArgs& a, int64_t k, int32_t& r
     if (__hip_atomic_fetch_add(rec + R_CNT, -1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 1) {
       rec[R_RDY] = ready;
       ready = q;
+      ++nready;
     }
     q = nxt;
   }
@@ -432,28 +433,30 @@ __global__ __launch_bounds__(TB) void k_ord_count(SrnnCfg, SrnnArgs a) {
     int32_t* heads = ord::cons_head(a);
     for (int s = 0; s < m; ++s) rec[ord::R_NEXT + s] = atomicExch(heads + pr[s], (int32_t)q);
   }
-  const int32_t npend = ord::wave_sum(pend ? 1 : 0);
-  if (lane == 0 && npend) atomicAdd(a.o_ctl + ord::PEND, npend);  // fire and forget
 }
 
-// the epoch permutations of the pending records (their turns run as continuations, lone
-// chains where an inline draw sits on the critical path): thread (record, epoch pair),
-// workgroup row y = partition * pairs + pair, grid-stride over the partition's records
+// the epoch permutations of the turns on the generation's critical paths, drawn in one parallel
+// launch instead of on their latency-bound chains: the pending records (rows q < rec_total) and
+// the roots that have consumers (row rec_total + their run-order slot).  Thread (turn, epoch
+// pair), workgroup row y = (group, partition, pair), grid-stride over the partition's entries.
 template <class Net>
 __global__ __launch_bounds__(TB) void k_ord_ptab(SrnnArgs a, int32_t E) {
   constexpr int P = Net::P;
   const int npair = (E + 1) / 2;
-  const int part = (int)blockIdx.y / npair, p = (int)blockIdx.y % npair;
-  const int64_t cnt = ord::ld_level(a.o_ctl + ord::PART0 + part), q0 = part * ord::rec_cap(a.n);
-  const int64_t stride = ord::rec_total(a.n);
+  const int grp = (int)blockIdx.y / (ord::NPART * npair);  // 0: records, 1: critical roots
+  const int part = ((int)blockIdx.y / npair) % ord::NPART, p = (int)blockIdx.y % npair;
+  const int64_t cap = ord::rec_cap(a.n), stride = 2 * ord::rec_total(a.n);
+  const int64_t cnt = ord::ld_level(a.o_ctl + (grp ? ord::CRIT0 : ord::PART0) + part), q0 = part * cap;
   const int32_t gen = a.gen_ptr ? a.gen_ptr[0] : a.gen;
   const Rng rng{(uint32_t)a.seed, (uint32_t)(a.seed >> 32)};
   const uint32_t c0 = (uint32_t)gen * 1024u + 512u + 2u * (uint32_t)p;  // even: one draw, two epochs
   for (int64_t i = (int64_t)blockIdx.x * TB + threadIdx.x; i < cnt; i += (int64_t)gridDim.x * TB) {
-    const int64_t q = q0 + i, k = ord::pend(a, q)[0];
+    const int64_t q = q0 + i;
+    const int64_t k = grp ? ord::run_order(a)[q] : ord::pend(a, q)[0];
+    const int64_t row = grp ? ord::rec_total(a.n) + q : q;
     const U4 r = perm_draw(rng, (uint64_t)(a.lo + k), c0, P_SHUFFLE);
-    a.ptab[2 * p * stride + q] = perm_from_bits<P>(perm_bits(r, c0));
-    if (2 * p + 1 < E) a.ptab[(2 * p + 1) * stride + q] = perm_from_bits<P>(perm_bits(r, c0 + 1u));
+    a.ptab[2 * p * stride + row] = perm_from_bits<P>(perm_bits(r, c0));
+    if (2 * p + 1 < E) a.ptab[(2 * p + 1) * stride + row] = perm_from_bits<P>(perm_bits(r, c0 + 1u));
   }
 }
 
@@ -476,7 +479,7 @@ __global__ __launch_bounds__(TB) void k_ord_order(SrnnCfg, SrnnArgs a) {
 // the turn at position g of the run order (-1: past its end); the wave's exclusive prefixes
 // of the partitions' critical / other counts in s_c / s_b (64 partitions = one per lane)
 __device__ __forceinline__ int64_t ord_turn_at(const SrnnArgs& a, int64_t g, int32_t* s_c, int32_t* s_b,
-                                               int64_t& ncrit) {
+                                               int64_t& ncrit, int64_t& slot) {
   const int lane = threadIdx.x & 63;
   const int32_t c = ord::ld_level(a.o_ctl + ord::CRIT0 + lane), b = ord::ld_level(a.o_ctl + ord::BULK0 + lane);
   int32_t ic = c, ib = b;
@@ -504,12 +507,17 @@ __device__ __forceinline__ int64_t ord_turn_at(const SrnnArgs& a, int64_t g, int
   for (int step = 32; step > 0; step >>= 1)
     if (pre[p + step] <= h) p += step;
   const int64_t off = h - pre[p];
+  slot = isc ? p * cap + off : -1;  // (critical roots: their run-order slot keys the permutation table)
   return isc ? order[p * cap + off] : order[(p + 1) * cap - 1 - off];
 }
 
-// every turn of the generation: lane k runs turn k if it has no producer (level 0); a lane
-// that completes a turn runs the consumers it made ready (continuations, at raised wave
-// priority: they are the generation's critical path), level = 1 + the deepest producer's
+// every turn of the generation.  A lane first runs a turn without producers: turn k (or, with
+// the run order, the k-th of it: producers of later turns first, their waves at raised priority,
+// their permutations from the table).  Then the wave works in rounds: the records its lanes made
+// ready (each lane's list) are gathered into LDS and handed out one per lane -- a producer whose
+// row several turns read does not run those turns one after another -- each run as a
+// continuation (raised priority, permutations from the table) at level 1 + its deepest
+// producer's.  The wave ends when no lane has a ready record left.
 template <class Net, class S>
 __global__ __launch_bounds__(TB) void k_ord_run(SrnnCfg c, SrnnArgs a) {
   using I = Item<Net, S>;
@@ -518,6 +526,7 @@ __global__ __launch_bounds__(TB) void k_ord_run(SrnnCfg c, SrnnArgs a) {
   constexpr int PERM = (Net::P + 4) & ~3;
   __shared__ float4 s_samp[TB * SAMP];
   __shared__ uint8_t s_perm[TB * PERM];
+  __shared__ int32_t s_q[TB];
   const int lane = threadIdx.x;
   const int64_t k0 = (int64_t)blockIdx.x * TB + lane;
   const int32_t gen = I::gen_of(a);
@@ -527,8 +536,9 @@ __global__ __launch_bounds__(TB) void k_ord_run(SrnnCfg c, SrnnArgs a) {
   bool raised = false;
   if (a.flags & SRNN_F_ORD_CRIT) {  // the run order: producers of later turns first, raised priority
     __shared__ int32_t s_c[64], s_b[64];
-    int64_t ncrit = 0;
-    cur = ord_turn_at(a, k0, s_c, s_b, ncrit);
+    int64_t ncrit = 0, slot = -1;
+    cur = ord_turn_at(a, k0, s_c, s_b, ncrit, slot);
+    if (slot >= 0) prow = ord::rec_total(a.n) + slot;
     if ((int64_t)blockIdx.x * TB < ncrit) {
       __builtin_amdgcn_s_setprio(2);
       raised = true;
@@ -537,22 +547,51 @@ __global__ __launch_bounds__(TB) void k_ord_run(SrnnCfg c, SrnnArgs a) {
     cur = k0;
   }
   if (cur >= 0) ord::st_level(a.o_src + 4 * cur + 3, 0);
-  int32_t ready = ord::EMPTY;
+  int32_t ready = ord::EMPTY, nready = 0;
   for (;;) {
-    if (cur < 0) {
-      if (ready == ord::EMPTY) break;
-      const int32_t q = ready;
-      const int32_t* rec = ord::pend(a, q);
-      ready = rec[ord::R_RDY];
-      // the producers' rows (released before their decrements) are visible after this
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      if (!raised) {
-        __builtin_amdgcn_s_setprio(2);
-        raised = true;
+    if (cur >= 0) {
+      const uint64_t t0 = a.o_trace ? __builtin_amdgcn_s_memrealtime() : 0;
+      O::turn(c, a, cur, gen, samp, perm, prow);
+      ord::publish(a, cur, ready, nready);
+      if (a.o_trace) {
+        a.o_trace[2 * cur] = t0;
+        a.o_trace[2 * cur + 1] = __builtin_amdgcn_s_memrealtime();
       }
+    }
+    // the wave's ready records, one per lane (the rest stay in their lists for the next round)
+    const int32_t total = ord::wave_sum(nready);
+    if (total == 0) break;
+    int32_t pre = nready;  // exclusive prefix of the list lengths
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+      const int32_t v = __shfl_up(pre, off);
+      if (lane >= off) pre += v;
+    }
+    pre -= nready;
+    for (int32_t t = pre; t < TB && nready > 0; ++t) {
+      s_q[t] = ready;
+      ready = ord::pend(a, ready)[ord::R_RDY];
+      --nready;
+    }
+    __syncthreads();
+    cur = -1;
+    prow = -1;
+    if (lane < total) {
+      const int32_t q = s_q[lane];
+      const int32_t* rec = ord::pend(a, q);
       cur = rec[0];
       prow = q;
+    }
+    __syncthreads();  // (s_q is refilled next round)
+    // the producers' rows (released before their decrements) are visible after this
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (!raised) {
+      __builtin_amdgcn_s_setprio(2);
+      raised = true;
+    }
+    if (cur >= 0) {
+      const int32_t* rec = ord::pend(a, prow);
       int32_t lv = 0;
       for (int t = 0; t < rec[1]; ++t) {
         const int32_t lp = ord::ld_level(a.o_src + 4 * (int64_t)rec[ord::R_PROD + t] + 3);
@@ -560,10 +599,6 @@ __global__ __launch_bounds__(TB) void k_ord_run(SrnnCfg c, SrnnArgs a) {
       }
       ord::st_level(a.o_src + 4 * cur + 3, lv + 1);
     }
-    O::turn(c, a, cur, gen, samp, perm, prow);
-    ord::publish(a, cur, ready);
-    cur = -1;
-    prow = -1;
   }
 }
 
@@ -654,7 +689,6 @@ int soup_ordered(const SrnnCfg& c, const SrnnArgs& a) {
       maxl = std::max(maxl, lv);
       if ((size_t)lv >= lists.size()) lists.resize((size_t)lv + 1);
       lists[(size_t)lv].push_back(k);
-      if (lv > 0) a.o_ctl[ord::PEND] += 1;
     }
     a.o_ctl[ord::MAXLW] = maxl;
     for (const auto& li : lists)
@@ -709,18 +743,19 @@ int soup_ordered(const SrnnCfg& c, const SrnnArgs& a) {
   hipLaunchKernelGGL((k_ord_plan<Net, S>), dim3((unsigned)nb), dim3(TB), 0, st, c, a);
   hipLaunchKernelGGL((k_ord_mark<Net, S>), dim3((unsigned)nb), dim3(TB), 0, st, c, a);
   hipLaunchKernelGGL((k_ord_count<Net, S>), dim3((unsigned)nb), dim3(TB), 0, st, c, a);
+  SrnnArgs ra = a;
+  const bool crit = knob(SRNN_KNOB_ORD_CRIT, 1) != 0;
+  if (crit) {
+    hipLaunchKernelGGL((k_ord_order<Net, S>), dim3((unsigned)nb), dim3(TB), 0, st, c, a);
+    ra.flags |= SRNN_F_ORD_CRIT;
+  }
   if constexpr (Net::KIND == 0 && Net::P <= 16) {
     const int32_t E = (a.severity > 0 ? a.severity : 0) + (a.epochs > 0 ? a.epochs : 0);
     if (a.ptab && (a.flags & SRNN_F_SHUFFLE) && E > 0) {
       const int64_t est = std::max<int64_t>(a.n / 12 / ord::NPART, 1);
-      hipLaunchKernelGGL((k_ord_ptab<Net>), dim3((unsigned)((est + TB - 1) / TB), (unsigned)(ord::NPART * ((E + 1) / 2))),
+      hipLaunchKernelGGL((k_ord_ptab<Net>), dim3((unsigned)((est + TB - 1) / TB), (unsigned)((crit ? 2 : 1) * ord::NPART * ((E + 1) / 2))),
                          dim3(TB), 0, st, a, E);
     }
-  }
-  SrnnArgs ra = a;
-  if (knob(SRNN_KNOB_ORD_CRIT, 1) != 0) {
-    hipLaunchKernelGGL((k_ord_order<Net, S>), dim3((unsigned)nb), dim3(TB), 0, st, c, a);
-    ra.flags |= SRNN_F_ORD_CRIT;
   }
   hipLaunchKernelGGL((k_ord_run<Net, S>), dim3((unsigned)nb), dim3(TB), 0, st, c, ra);
   hipLaunchKernelGGL((k_ord_close<Net, S>), dim3((unsigned)nb), dim3(TB), 0, st, c, a);

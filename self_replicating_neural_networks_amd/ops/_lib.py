@@ -20,7 +20,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 # SRNN_LIB: load another build of the library (A/B of compiler flags on the GPU box)
 LIB_PATH = os.environ.get("SRNN_LIB") or os.path.join(_HERE, "libsrnn.so")
 CSRC = os.path.normpath(os.path.join(_HERE, "..", "..", "csrc"))
-ABI_VERSION = 22
+ABI_VERSION = 23
 
 # SrnnOp (csrc/srnn_abi.h)
 OP_INIT = 0
@@ -43,7 +43,7 @@ OP_X2_PACK = 20   # sharded soup, all-to-all exchange: finish + next decisions +
 OP_X2_POST = 21   # sharded soup: uids, census, received notices / requests
 OP_SOUP_ORDERED = 22  # reference-order (sequential) generation, DAG-scheduled (csrc/srnn_ordered.h)
 ORD_CTL_WORDS = 227   # o_ctl words of an ordered generation (csrc/srnn_ordered.h)
-ORD_MAXLW, ORD_ERRW, ORD_PEND = 17, 18, 19
+ORD_MAXLW, ORD_ERRW = 17, 18
 ORD_NPART = 64        # partitions of the pending records
 ORD_REC = 32          # int32 words per pending record
 ORD_MAX_LEVELS = 16   # dependency levels reported one by one (deeper: one bin)
@@ -131,6 +131,8 @@ class SrnnArgs(ctypes.Structure):
         ("W3", _P), ("o_src", _P), ("o_list", _P), ("o_ctl", _P), ("o_levels", _I32), ("pad3", _I32),
         # precomputed SGD epoch permutations of a soup generation
         ("ptab", _P),
+        # ordered generation trace (debug): [n][2] start / end times of each turn (100 MHz)
+        ("o_trace", _P),
     ]
 
 

@@ -128,7 +128,7 @@ def ordered_bytes(spec: ArchSpec, n: int, dtype=torch.float32, epochs: int = 0) 
     rec = _lib.ord_rec_total(n1)
     b = n * rb + 4 * _lib.ord_src_words(n1) + 4 * n1 + 4 * _lib.ORD_CTL_WORDS
     if spec.kind == "weightwise" and spec.P <= 16 and epochs > 0 and (n + 4096) * epochs * 8 <= (2 << 30):
-        b += rec * epochs * 8
+        b += 2 * rec * epochs * 8  # permutation table: pending records + critical roots
     return int(b)
 
 
@@ -361,15 +361,20 @@ class SoupEngine:
             self.stats_all = torch.zeros(self.dist.world * 6, dtype=torch.int64, device=dev)
             self.rowflags = torch.zeros(max(self.n, 1), **i32)
 
+    # synchronous generations up to this many slots per launch draw their SGD permutations in a
+    # launch of their own (profiles/r5a_*: 12.5k 0.0397 vs 0.0426 ms, 25k 0.0432 vs 0.0444)
+    PERM_TABLE_MAX_N = 32768
+
     def _use_perm_table(self) -> bool:
-        """ExecConfig.perm_table, auto (None): the reference order's pending turns only (their
-        latency-bound level launches on lane pairs, k_ord_ptab: ~5 % of the slots).  A whole
-        generation's table (k_perm_table) costs more than the permutation work it removes from
-        the SGD chains at 25k-100k slots and breaks even at 12.5k (MI355X, profiles/r4b_*)."""
+        """ExecConfig.perm_table, auto (None): the reference order's critical-path turns (pending
+        records and the roots with consumers, k_ord_ptab: ~10 % of the slots), and synchronous
+        generations of at most PERM_TABLE_MAX_N slots per launch -- latency-bound, where the lone
+        chains gain more from a permutation-free SGD loop than the table launch (k_perm_table)
+        costs; above that the launch costs more than it removes (MI355X, profiles/r4b_*, r5a_*)."""
         pt = self.execution.perm_table
         if pt is not None:
             return bool(pt)
-        return self.order == "sequential"
+        return self.order == "sequential" or self.n <= self.PERM_TABLE_MAX_N
 
     def _perm_table(self):
         """The generation's SGD epoch permutations, precomputed by one launch before the
@@ -382,7 +387,8 @@ class SoupEngine:
         E = max(int(self.params.get("train", 0)), 0) + max(int(self.params.get("learn_from_severity", 1)), 0)
         if E <= 0 or (self.n + 4096) * E * 8 > (2 << 30):
             return None
-        rows = _lib.ord_rec_total(self.n) if self.order == "sequential" else self.n  # (pending records)
+        # (reference order: the pending records' rows and the critical roots' rows, csrc k_ord_ptab)
+        rows = 2 * _lib.ord_rec_total(self.n) if self.order == "sequential" else self.n
         t = getattr(self, "_ptab", None)
         if t is None or t.numel() < rows * E:
             self._ptab = t = torch.zeros(rows * E, dtype=torch.int64, device=self.device)
@@ -429,7 +435,33 @@ class SoupEngine:
         err = c[_lib.ORD_ERRW] | (4 if n and int((lv < 0).sum().item()) else 0)
         stored = int(self._osrc[4 * n:5 * n].sum().item()) if n else 0
         return dict(levels=hist[:C], tail=sum(hist[C:]), max_level=int(lv.max().item()) if n else 0,
-                    pending=c[_lib.ORD_PEND], error=err, stored_attacks=stored)
+                    pending=n - hist[0], error=err, stored_attacks=stored)
+
+    def ordered_trace(self, on: bool = True) -> None:
+        """Record, on the device, when each turn of the next reference-order generations starts
+        and ends (s_memrealtime, 100 MHz; debug: a few stores per turn).  Read it with
+        ``ordered_timeline()``."""
+        if self.order != "sequential" or self.device.type != "cuda":
+            raise ValueError("the turn trace is a device reference-order generation's")
+        self._otrace = torch.zeros(2 * max(self.n, 1), dtype=torch.int64, device=self.device) if on else None
+        self._arg_cache.clear()
+
+    def ordered_timeline(self) -> Dict[str, list]:
+        """The last traced generation per dependency level: turns, first start and last end (us
+        after the generation's first turn started), mean / max turn duration (us)."""
+        t = self._otrace.view(-1, 2).cpu().double()[:self.n]
+        lv = self._osrc[:4 * self.n].view(self.n, 4)[:, 3].cpu()
+        ok = t[:, 0] > 0
+        t0 = t[ok, 0].min()
+        out = {}
+        for L in range(int(lv.max()) + 1):
+            m = ok & (lv == L)
+            if int(m.sum()) == 0:
+                continue
+            s, e = (t[m, 0] - t0) / 100.0, (t[m, 1] - t0) / 100.0
+            out[L] = dict(turns=int(m.sum()), first_start=float(s.min()), last_start=float(s.max()),
+                          last_end=float(e.max()), mean_us=float((e - s).mean()), max_us=float((e - s).max()))
+        return out
 
     def ordered_error(self) -> int:
         """The reference-order generations' error bits, sticky over the engine's life (0: none)."""
@@ -617,6 +649,7 @@ class SoupEngine:
             if self.order == "sequential":
                 fa.W3, fa.o_src, fa.o_list, fa.o_ctl = _p(self._abuf), _p(self._osrc), _p(self._olist), _p(self._octl)
                 fa.o_levels = self.order_levels
+                fa.o_trace = _p(getattr(self, "_otrace", None))
             ca = fa
         self._arg_cache[key] = (a, ca, a.flags)
         return self._arg_cache[key]

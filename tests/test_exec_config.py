@@ -96,7 +96,7 @@ def test_engine_bytes_matches_a_constructed_single_rank_engine(n, diag, order):
     if order == "sequential":
         # the pending records' permutation table is a GPU-only buffer too (train 1 + severity 1)
         assert getattr(e, "_ptab", None) is None
-        held += _lib.ord_rec_total(n) * 2 * 8
+        held += 2 * _lib.ord_rec_total(n) * 2 * 8
         assert est > engine_bytes(spec, n, diagnostics=diag) + n * spec.PP * 4  # W3 alone is a table
     # the model may round a few small control tensors up; never low by more than 1 %
     assert est >= held * 0.99 and est <= held * 1.05 + 512, (est, held)
