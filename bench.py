@@ -49,12 +49,13 @@ def parse_args(argv=None):
     ap.add_argument("--particles", type=int, default=100_000, help="soup size (strong scaling)")
     ap.add_argument("--particles-per-gpu", type=int, default=100_000, help="per-rank soup size (weak scaling)")
     ap.add_argument("--order", choices=["sequential", "synchronous"], default="synchronous",
-                    help="sequential: the reference's in-place, index-ordered generation (level-scheduled, "
-                         "single rank); synchronous: every read from the generation-start table (shardable)")
+                    help="sequential: the reference's in-place, index-ordered generation (DAG-scheduled; sharded by "
+                         "replicated plan + per-level all-gathers); synchronous: every read from the generation-start "
+                         "table (Jacobi)")
     ap.add_argument("--reference-order-steps", type=int, default=None,
                     help="synchronous headline: ALSO time this many generations of the same soup in the reference's "
-                         "sequential order (reported under config.reference_order); -1: --steps; default: --steps on "
-                         "one rank, 0 on several (the reference order is single-rank)")
+                         "sequential order on the same ranks (reported under config.reference_order); -1 / default: "
+                         "--steps; 0: off")
     ap.add_argument("--train", type=int, default=20)
     ap.add_argument("--attacking-rate", type=float, default=0.1)
     ap.add_argument("--learn-from-rate", type=float, default=0.1)
@@ -143,10 +144,6 @@ def main(argv=None):
     n_total = args.particles if args.scaling == "strong" else args.particles_per_gpu * d.world
     execution = ExecConfig().resolved()
     execution.apply_library()
-    if args.order == "sequential" and d.enabled:
-        print("bench.py: the reference-order generation is single-rank (--order synchronous shards)",
-              file=sys.stderr)
-        sys.exit(2)
     eng = SoupEngine(spec, n_total, params, device=dev, seed=args.seed, dist=d, execution=execution,
                      order=args.order)
     eng.stats = not args.no_stats
@@ -186,23 +183,28 @@ def main(argv=None):
     # the same soup in the reference's order (level-scheduled, single rank), timed after the
     # headline's region: a second number, never part of the headline value
     ref_order = None
-    k_ref = args.reference_order_steps
-    if k_ref is None:
-        k_ref = -1 if d.world == 1 else 0
+    k_ref = -1 if args.reference_order_steps is None else args.reference_order_steps
     k_ref = args.steps if k_ref < 0 else k_ref
-    if k_ref > 0 and d.world == 1 and args.order == "synchronous":
+    if k_ref > 0 and args.order == "synchronous":
         eng.release_graphs()
         ro = SoupEngine(spec, n_total, params, device=dev, seed=args.seed, dist=d, execution=execution,
                         order="sequential")
         ro.stats = not args.no_stats
         if on_gpu and not args.no_graph:
-            ro.capture(warmup=1)
+            ro.capture(warmup=1)  # (single rank: hipGraphs; sharded: eager, its level count is read back)
         ro.evolve(args.warmup)
+        sync()
+        d.barrier()
         sync()
         t1 = time.perf_counter()
         ro.evolve(k_ref)
         sync()
-        dt_ref = time.perf_counter() - t1
+        d.barrier()
+        sync()
+        tr = torch.tensor([time.perf_counter() - t1], dtype=torch.float64, device=dev if backend == "nccl" else "cpu")
+        if d.enabled:
+            dist.all_reduce(tr, op=dist.ReduceOp.MAX)
+        dt_ref = float(tr.item())
         ref_order = {"semantics": "reference-order", "steps": k_ref, "warmup": args.warmup,
                      "ms_per_step": dt_ref / k_ref * 1e3, "value": n_total * k_ref / dt_ref,
                      "unit": "particle-generations/s", "final_census": ro.count(), "levels": ro.ordered_levels()}

@@ -169,6 +169,9 @@ struct SrnnArgs {
   // ---- ordered generation trace (debug, SoupEngine.ordered_trace): [n][2] s_memrealtime (100 MHz,
   // chip-wide) at the start and the end (after its publish) of each turn on the device.  null: off
   uint64_t* o_trace;
+  // ---- the reference-order generation sharded over ranks (OP_SOUP_ORDERED_SH): this rank's turns
+  // [o_lo, o_hi) of the n global ones (every other field in the global view: n = n_total, lo = 0)
+  int64_t o_lo, o_hi;
 };
 
 #define SRNN_X2_HDR 12  // int64 header words of an X2 exchange block (see srnn_shard.hip)
@@ -197,9 +200,14 @@ enum SrnnOp {
   OP_SOUP_ORDERED = 22, // one reference-order (sequential, in-place) generation scheduled by its
                         // dependency DAG: bitwise OP_SOUP_SEQ, every turn as soon as its producers
                         // are done (srnn_ordered.h)
+  OP_SOUP_ORDERED_SH = 23, // one phase (steps) of a reference-order generation sharded over ranks:
+                           // 0 plan + levels of every turn, 1 run this rank's turns of level
+                           // o_levels, 2 pack their outputs, 3 unpack the gathered outputs, 4 close
+                           // this rank's rows, 5 link the next generation's attacks
+                           // (srnn_ordered_sh.h)
 };
 
-int srnn_abi_version();  // 23
+int srnn_abi_version();  // 24
 int64_t srnn_args_size();  // sizeof(SrnnArgs): the ctypes mirror checks its layout against it
 int64_t srnn_cfg_size();
 int srnn_has_config(const SrnnCfg* cfg);

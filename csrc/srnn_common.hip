@@ -77,6 +77,7 @@ const char* op_name(int op) {
     case OP_X2_PACK: return "srnn:x2_pack";
     case OP_X2_POST: return "srnn:x2_post";
     case OP_SOUP_ORDERED: return "srnn:soup_ordered";
+    case OP_SOUP_ORDERED_SH: return "srnn:soup_ordered_sh";
     default: return "srnn:op";
   }
 }
@@ -200,7 +201,7 @@ static int with_scratch(int op, const SrnnCfg* c, const SrnnArgs* a) {
 
 extern "C" {
 
-int srnn_abi_version() { return 23; }
+int srnn_abi_version() { return 24; }
 
 
 // layout check of the ctypes mirror (ops/_lib.py): sizeof(SrnnArgs) / sizeof(SrnnCfg)

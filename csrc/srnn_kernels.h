@@ -1949,6 +1949,7 @@ int run_net_op(int op, const SrnnCfg& c, const SrnnArgs& a) {
     case OP_GEN_FINISH: return gen_finish<Net, S>(c, a);
     case OP_SOUP_SEQ: return soup_seq<Net, S>(c, a);
     case OP_SOUP_ORDERED: return soup_ordered<Net, S>(c, a);
+    case OP_SOUP_ORDERED_SH: return soup_ordered_sh<Net, S>(c, a);
     default: set_error("unknown op"); return -1;
   }
 }

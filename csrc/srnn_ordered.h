@@ -645,6 +645,7 @@ __global__ __launch_bounds__(TB) void k_ord_close(SrnnCfg c, SrnnArgs a) {
 }
 
 #include "srnn_pair.h"
+#include "srnn_ordered_sh.h"
 
 // OP_SOUP_ORDERED: one sequential (reference-order) generation of a single-rank table.
 // W2: generation-start rows, W: the generation's rows (E versions, then the final table),

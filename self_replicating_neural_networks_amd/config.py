@@ -107,6 +107,9 @@ class ExecConfig:
     soup_lanes: Optional[int] = None        # SRNN_SOUP_LANES (None / 0: by population size)
     ord_crit: Optional[bool] = None         # SRNN_ORD_CRIT: reference-order generations run the producers of
                                             # later turns first, at raised wave priority (None: on)
+    ordsh_emulate: int = 0                  # SRNN_ORDSH_EMULATE: one-rank timing model of R ranks of a sharded
+                                            # reference-order generation (the rank runs 1/R of the turns;
+                                            # the other turns never run: timing only, results invalid)
     order_levels: int = 4                   # SRNN_ORDER_LEVELS: dependency levels a reference-order generation
                                             # reports one by one (ordered_levels; deeper: the tail bin)
     perm_table: Optional[bool] = None       # SRNN_PERM_TABLE: a generation's SGD permutations precomputed by
@@ -119,6 +122,7 @@ class ExecConfig:
                 force_generic="SRNN_FORCE_GENERIC", ww_wave="SRNN_WW_WAVE", rnn_wave="SRNN_RNN_WAVE",
                 rnn_spec="SRNN_RNN_SPEC", rnn_soup="SRNN_RNN_SOUP", big_wave="SRNN_BIG_WAVE",
                 fix_group="SRNN_FIX_GROUP", soup_lanes="SRNN_SOUP_LANES", ord_crit="SRNN_ORD_CRIT",
+                ordsh_emulate="SRNN_ORDSH_EMULATE",
                 order_levels="SRNN_ORDER_LEVELS",
                 perm_table="SRNN_PERM_TABLE")
     # Optional[bool] knobs whose None means "the built-in choice" (by population size, ...)
@@ -156,7 +160,7 @@ class ExecConfig:
                 kw[f.name] = v
             elif f.name == "x2_emulate_remote":
                 kw[f.name] = float(v)
-            elif f.name in ("soup_lanes", "order_levels", "ww_wave"):
+            elif f.name in ("soup_lanes", "order_levels", "ww_wave", "ordsh_emulate"):
                 kw[f.name] = int(v)
             elif f.name in self.TRI_STATE:
                 kw[f.name] = _tri_state(v)

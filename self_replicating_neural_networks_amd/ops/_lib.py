@@ -20,7 +20,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 # SRNN_LIB: load another build of the library (A/B of compiler flags on the GPU box)
 LIB_PATH = os.environ.get("SRNN_LIB") or os.path.join(_HERE, "libsrnn.so")
 CSRC = os.path.normpath(os.path.join(_HERE, "..", "..", "csrc"))
-ABI_VERSION = 23
+ABI_VERSION = 24
 
 # SrnnOp (csrc/srnn_abi.h)
 OP_INIT = 0
@@ -42,6 +42,8 @@ OP_SOUP_SEQ = 19  # sequential (Gauss-Seidel) soup generations
 OP_X2_PACK = 20   # sharded soup, all-to-all exchange: finish + next decisions + rows (csrc/srnn_shard.hip)
 OP_X2_POST = 21   # sharded soup: uids, census, received notices / requests
 OP_SOUP_ORDERED = 22  # reference-order (sequential) generation, DAG-scheduled (csrc/srnn_ordered.h)
+OP_SOUP_ORDERED_SH = 23  # one phase of a sharded reference-order generation (csrc/srnn_ordered_sh.h)
+ORDSH_PLAN, ORDSH_LEVEL, ORDSH_PACK, ORDSH_UNPACK, ORDSH_CLOSE, ORDSH_LINK = range(6)
 ORD_CTL_WORDS = 227   # o_ctl words of an ordered generation (csrc/srnn_ordered.h)
 ORD_MAXLW, ORD_ERRW = 17, 18
 ORD_NPART = 64        # partitions of the pending records
@@ -133,6 +135,8 @@ class SrnnArgs(ctypes.Structure):
         ("ptab", _P),
         # ordered generation trace (debug): [n][2] start / end times of each turn (100 MHz)
         ("o_trace", _P),
+        # the sharded reference-order generation: this rank's turns [o_lo, o_hi)
+        ("o_lo", _I64), ("o_hi", _I64),
     ]
 
 

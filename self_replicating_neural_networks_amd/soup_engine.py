@@ -252,7 +252,9 @@ class SoupEngine:
             self.dist.enable_native_comm(self.device)
         self.lo, self.hi = self.dist.shard(self.n_total)
         self.n = self.hi - self.lo
-        self.x2 = self.dist.enabled and exchange == "alltoall"
+        # the reference order shards by replicated plan + per-level all-gathers (srnn_ordered_sh.h),
+        # on the all-gather exchange's buffers
+        self.x2 = self.dist.enabled and exchange == "alltoall" and order != "sequential"
         if not self.x2 and self.n_total > MAX_SLOTS_DIRECT:
             raise ValueError(f"a single-rank or all-gather soup addresses at most {MAX_SLOTS_DIRECT} slots "
                              "(uint32 attack-list entries); shard it with exchange='alltoall'")
@@ -396,25 +398,41 @@ class SoupEngine:
 
     def _init_ordered(self):
         """Buffers of the reference-order generation (csrc/srnn_ordered.h): attack outputs,
-        per-turn source versions + level, level work lists, control words."""
-        if self.dist.enabled:
-            raise NotImplementedError("reference-order (sequential) generations are single-rank: its levels would "
-                                      "need one exchange each; shard with order='synchronous'")
+        per-turn source versions + level, consumer lists and records, control words.  Sharded
+        (srnn_ordered_sh.h): every rank plans all n_total turns and keeps the version tables of
+        all rows (E rows, stored attack outputs) next to the gathered generation-start table."""
         dev_side = self.device.type != "cpu"
         if self.generic or not _lib.supports(self.spec, _lib.OP_SOUP_ORDERED, dev_side, self.dtype_code):
             raise NotImplementedError(
                 f"no level-scheduled reference-order generation for {self.spec}: it exists for the "
                 "lane-per-particle template shapes; SequentialSoupEngine runs the same order for any shape on the "
                 "host, SoupEngine(order='synchronous') any shape on the device")
-        if self.n > ORDERED_MAX_ROWS:
+        sharded = self.dist.enabled
+        N = self.n_total if sharded else self.n  # turns planned on this rank
+        if N > ORDERED_MAX_ROWS:
             raise ValueError("reference-order generations address < 2^30 slots")
+        if sharded and not _lib.supports(self.spec, _lib.OP_SOUP_ORDERED_SH, dev_side, self.dtype_code):
+            raise NotImplementedError(f"no sharded reference-order generation for {self.spec}")
         dev = self.device
         C = int(self.execution.order_levels)
         self.order_levels = C
-        self._abuf = torch.zeros((self.n, self.spec.PP), dtype=self.dtype, device=dev)
-        # [n][4] source codes + level | [n] stored-attack flags | [n] consumer lists | pending records
-        self._osrc = torch.zeros(_lib.ord_src_words(self.n), dtype=torch.int32, device=dev)
-        self._olist = torch.zeros(max(self.n, 1), dtype=torch.int32, device=dev)  # each turn's record
+        self._ord_n = N
+        self._abuf = torch.zeros((N, self.spec.PP), dtype=self.dtype, device=dev)
+        # [N][4] source codes + level | [N] stored-attack flags | [N] consumer lists | pending records
+        self._osrc = torch.zeros(_lib.ord_src_words(N), dtype=torch.int32, device=dev)
+        self._olist = torch.zeros(max(N, 1), dtype=torch.int32, device=dev)  # each turn's record
+        if sharded:
+            i32 = dict(dtype=torch.int32, device=dev)
+            self._fw = torch.zeros((N, self.spec.PP), dtype=self.dtype, device=dev)  # E versions of all rows
+            self._sh_heads = [torch.full((N,), -1, **i32) for _ in range(2)]  # replicated attack lists
+            self._sh_nexts = [torch.full((N,), -1, **i32) for _ in range(2)]
+            self._sh_cnt = torch.zeros(4, **i32)
+            rb = self.spec.PP * self._bufs[0].element_size()
+            self._sh_recb = 16 + 2 * rb  # csrc ordsh::rec_bytes (16-byte slot header, two rows)
+            cap = max(hi - lo for lo, hi in (self.dist.shard_of_rank(r, N) for r in range(self.dist.world)))
+            self._sh_send = torch.zeros(max(cap, 1) * self._sh_recb // 8, dtype=torch.int64, device=dev)
+            self._sh_recv = torch.zeros(self.dist.world * max(cap, 1) * self._sh_recb // 8, dtype=torch.int64,
+                                        device=dev)
         self._octl = torch.zeros(_lib.ORD_CTL_WORDS, dtype=torch.int32, device=dev)
         self._rec_rows = None  # recording: every particle's state before any respawn
 
@@ -427,7 +445,7 @@ class SoupEngine:
         turn that never ran), and how many attack outputs were stored for later turns (the others
         are recomputed by the turns that read them)."""
         C = self.order_levels
-        n = self.n
+        n = self._ord_n
         lv = self._osrc[:4 * n].view(n, 4)[:, 3] if n else self._osrc[:0]
         hist = torch.bincount(lv.clamp(0, _lib.ORD_MAX_LEVELS).long(), minlength=_lib.ORD_MAX_LEVELS + 1)
         hist = hist.cpu().tolist()
@@ -697,6 +715,8 @@ class SoupEngine:
                 # per-generation fixpoint-fraction statistics (reference Soup.count, code/soup.py:89-103)
                 self.classify_local(self.stats_with_sec, zero=False)
             return
+        if self.order == "sequential":
+            return self._ordered_sharded_generation(a, ca, record)
         # ---- sharded, all-gather: decide -> all-gather rows -> evolve -> census + respawn
         #      count (+ generation counter) -> all-gather stats -> uids
         d = self.dist
@@ -747,6 +767,84 @@ class SoupEngine:
             self.classify_local(self.stats_with_sec, zero=False)
         if rec:
             self.recorder.on_evolved(self, rows=self._rec_rows, old_uid=uid0, ordered=True)
+
+    def _sh_args(self, phase: int, level: int = 0) -> _lib.SrnnArgs:
+        """Argument block of a sharded reference-order phase, in the global view (csrc
+        srnn_ordered_sh.h): all n_total turns planned, this rank's [lo, hi) run; per-row columns
+        addressed by global slot through pointers offset by -lo."""
+        key = self._cache_key("ordsh", phase)
+        a = self._arg_cache.get(key)
+        if a is None:
+            N, lo = self.n_total, self.lo
+
+            def shifted(t):
+                return ctypes.c_void_p(t.data_ptr() - lo * t.element_size()) if t is not None else None
+
+            a = self._args()
+            a.n, a.n_total, a.lo = N, N, 0
+            a.o_lo, a.o_hi = self.lo, self.hi
+            em = int(self.execution.ordsh_emulate)
+            if self.dist.world == 1 and em > 1:  # timing model of `em` ranks: this one runs 1/em of the turns
+                a.o_hi = a.o_lo + -(-N // em)
+            a.W2, a.W, a.W3 = _p(self.full), _p(self._fw), _p(self._abuf)
+            a.o_src, a.o_list, a.o_ctl = _p(self._osrc), _p(self._olist), _p(self._octl)
+            a.heads, a.nexts = _p(self._sh_heads[self._p]), _p(self._sh_nexts[self._p])
+            a.heads_next, a.nexts_next = _p(self._sh_heads[1 - self._p]), _p(self._sh_nexts[1 - self._p])
+            a.action, a.counterpart, a.loss = shifted(self.action), shifted(self.counterpart), shifted(self.loss)
+            a.respawn, a.rowflags = shifted(self.respawn), shifted(self.rowflags)
+            a.sendbuf, a.recvbuf, a.x_ctl = _p(self._sh_send), _p(self._sh_recv), _p(self._sh_cnt)
+            a.steps = phase
+            self._arg_cache[key] = a
+        a.o_levels = level if phase in (_lib.ORDSH_LEVEL, _lib.ORDSH_PACK) else self.order_levels
+        return a
+
+    def _ordered_sharded_generation(self, a, ca, record: bool):
+        """One reference-order generation sharded over the ranks (csrc/srnn_ordered_sh.h):
+        all-gather of the generation-start rows -> replicated plan + levels -> per level: this
+        rank's turns, their outputs all-gathered -> close of this rank's rows -> the next
+        generation's lists -> census + respawn count (OP_CLASSIFY) -> uids (flush).  Bitwise the
+        single-rank generation (tests/test_ordered_sharded.py).  Eager: the number of levels is
+        read back every generation."""
+        if record and self.recorder is not None:
+            raise NotImplementedError("recording states of a sharded reference-order soup")
+        spec, cfg, d = self.spec, self.cfg, self.dist
+        N, R = self.n_total, d.world
+
+        def run(phase, level=0, **fields):
+            sa = self._sh_args(phase, level)
+            for k, v in fields.items():
+                setattr(sa, k, v)
+            _lib.run(_lib.OP_SOUP_ORDERED_SH, spec, sa, cfg)
+
+        if not self._lists_ready:  # this generation's attack lists, every slot (the global view)
+            self._sh_heads[self._p].fill_(-1)
+            _lib.run(_lib.OP_SOUP_DECIDE, spec, self._sh_args(_lib.ORDSH_PLAN), cfg)
+        d.all_gather_rows(self.full.view(torch.int32), self.table_in.view(torch.int32), N)
+        run(_lib.ORDSH_PLAN)
+        lv = self._osrc[:4 * N].view(N, 4)[:, 3]
+        maxl = int(self._octl[_lib.ORD_MAXLW].item())
+        counts = torch.stack([torch.bincount(lv[lo:hi].clamp(min=0).long(), minlength=maxl + 1)[:maxl + 1]
+                              for lo, hi in (d.shard_of_rank(r, N) for r in range(R))])
+        caps = counts.max(dim=0).values.cpu().tolist()  # records per rank and level: the same on every rank
+        recw = self._sh_recb // 8
+        for L in range(maxl + 1):
+            run(_lib.ORDSH_LEVEL, L)
+            cap = int(caps[L])
+            if cap == 0:
+                continue
+            send = self._sh_send[:cap * recw]
+            send.view(cap, recw)[:, 0].fill_(-1)
+            run(_lib.ORDSH_PACK, L, x_blk=cap)
+            d.all_gather_into(self._sh_recv[:R * cap * recw], send)
+            run(_lib.ORDSH_UNPACK, x_blk=cap)
+        run(_lib.ORDSH_CLOSE)
+        self.rows_out.copy_(self._fw[self.lo:self.hi])
+        run(_lib.ORDSH_LINK)
+        self._lists_ready = True
+        _lib.run(_lib.OP_CLASSIFY, spec, ca, cfg)  # census + respawn count + the generation counter
+        self._p = 1 - self._p
+        self._pending = True
+        self._flush()
 
     def _finish_pending(self):
         """Batch mode: ONE finish launch for the generations whose block stats wait in the
