@@ -157,7 +157,7 @@ struct SrnnArgs {
                         // flags | [n] consumer-list heads | [ord::rec_total(n)][32] pending records |
                         // [ord::rec_total(n)] run order of the turns without producers
   int32_t* o_list;      // [n] the pending record of each turn (-1: no producer)
-  int32_t* o_ctl;       // [ord::CTL_WORDS = 227] record / run-order counts per partition, pending turns, max level
+  int32_t* o_ctl;       // [ord::CTL_WORDS = 163] record / critical-list counts per partition, pending turns, max level
                         // (host), error bits (sticky: the plan kernel clears every word but that one)
   int32_t o_levels;     // dependency levels the host path reports one by one (1..16; the device
                         // schedules turns by continuation, not by level)

@@ -62,18 +62,18 @@ constexpr int MAX_LEVELS = 16;  // dependency levels reported one by one (deeper
 // o_ctl words: [MAXLW] deepest level (host path), [ERRW] error bits -- STICKY: set by any
 // generation, never cleared by the next one (2: an unstored attack output past the recompute
 // depth, a marking bug; 4: a turn that never ran), [PART0 + p] records (pending turns) of
-// partition p, [CRIT0 + p] / [BULK0 + p] turns without producers of
-// partition p that have consumers (run first) / have none
+// partition p, [CRIT0 + p] producers of later turns in partition p (the producer's block mod
+// NPART; k_ord_count appends a producer when its first consumer registers)
 constexpr int MAXLW = 17, ERRW = 18;
 // pending records (and the run order) live in NPART partitions (partition p: the workgroups
 // b = p mod NPART, appended by one counter each: no chip-wide contended counter)
 constexpr int NPART = 64, PART0 = 2 * MAX_LEVELS + 3;
-constexpr int CRIT0 = PART0 + NPART, BULK0 = CRIT0 + NPART;
-constexpr int CTL_WORDS = BULK0 + NPART;
+constexpr int CRIT0 = PART0 + NPART;
+constexpr int CTL_WORDS = CRIT0 + NPART;
 // o_src layout: [n][4] {own, victim, teacher, level} | [n] stored flags of A(j) | [n] consumer-list
 // heads (pending records reading E(j) / A(j), EMPTY-terminated) | [rec_total(n)][REC] pending
-// records | [rec_total(n)] run order (partition p: its critical turns from the front of its
-// rec_cap slots, the others from the back); o_list: [n] the record of each pending turn (-1: none)
+// records | [rec_total(n)] the critical list (producers of later turns; partition p: the producers
+// of blocks b = p mod NPART, rec_cap(n) slots); o_list: [n] the record of each pending turn (-1: none)
 constexpr int NPROD = 12;  // producers of one turn: 3 reads x 2^RB leaves
 constexpr int REC = 32;    // record words: {turn, np, producers[NPROD], count, ready-next, next[NPROD], -}
 constexpr int R_PROD = 2, R_CNT = R_PROD + NPROD, R_RDY = R_CNT + 1, R_NEXT = R_RDY + 1;
@@ -363,12 +363,17 @@ __device__ __forceinline__ int32_t wave_sum(int32_t v) {
 // agent scope (the consumers may run on any CU / XCD) BEFORE the counts go down.  Every
 // record whose count this lane takes to zero joins the lane's ready list (linked through the
 // records' R_RDY words, `nready` long); k_ord_run shares the lists out over its wave.
+// ROWS = false (level propagation only): nothing but the producer's level -- an agent-scope atomic
+// store -- is handed over, so its completion (vmcnt) before the decrements replaces the release
+template <bool ROWS = true>
 __device__ __forceinline__ void publish(const SrnnArgs& a, int64_t k, int32_t& ready, int32_t& nready) {
   const int32_t h = cons_head(a)[k];
   if (h == EMPTY) return;
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (kept: ROCm 7.2 may drop the fence's own wait)
+  if constexpr (ROWS) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (kept: ROCm 7.2 may drop the fence's own wait)
+  }
   for (int32_t q = h; q != EMPTY;) {
     int32_t* rec = pend(a, q);
     const int np = rec[1];
@@ -431,7 +436,15 @@ __global__ __launch_bounds__(TB) void k_ord_count(SrnnCfg, SrnnArgs a) {
     rec[ord::R_CNT] = m;
     a.o_list[k] = (int32_t)q;
     int32_t* heads = ord::cons_head(a);
-    for (int s = 0; s < m; ++s) rec[ord::R_NEXT + s] = atomicExch(heads + pr[s], (int32_t)q);
+    for (int s = 0; s < m; ++s) {
+      const int32_t old = atomicExch(heads + pr[s], (int32_t)q);
+      rec[ord::R_NEXT + s] = old;
+      if (old == ord::EMPTY && (a.flags & SRNN_F_ORD_CRIT)) {  // pr[s]'s first consumer: a critical turn
+        const int pp = (int)((pr[s] / TB) % ord::NPART);
+        const int32_t pos = atomicAdd(a.o_ctl + ord::CRIT0 + pp, 1);
+        ord::run_order(a)[pp * ord::rec_cap(a.n) + pos] = pr[s];
+      }
+    }
   }
 }
 
@@ -460,55 +473,28 @@ __global__ __launch_bounds__(TB) void k_ord_ptab(SrnnArgs a, int32_t E) {
   }
 }
 
-// the run order of the turns without producers: those with consumers (the first links of the
-// generation's dependency chains) ahead of the rest, each group partitioned like the records
-template <class Net, class S>
-__global__ __launch_bounds__(TB) void k_ord_order(SrnnCfg, SrnnArgs a) {
-  const int64_t k = (int64_t)blockIdx.x * TB + threadIdx.x;
-  const bool root = k < a.n && a.o_list[k] < 0;
-  const bool crit = root && ord::cons_head(a)[k] != ord::EMPTY;
-  const int part = (int)(blockIdx.x % ord::NPART);
-  const int64_t cap = ord::rec_cap(a.n);
-  int32_t* order = ord::run_order(a);
-  const int32_t i = ord::wave_append(a.o_ctl + ord::CRIT0 + part, crit);
-  const int32_t j = ord::wave_append(a.o_ctl + ord::BULK0 + part, root && !crit);
-  if (crit) order[part * cap + i] = (int32_t)k;
-  else if (root) order[(part + 1) * cap - 1 - j] = (int32_t)k;
-}
-
-// the turn at position g of the run order (-1: past its end); the wave's exclusive prefixes
-// of the partitions' critical / other counts in s_c / s_b (64 partitions = one per lane)
-__device__ __forceinline__ int64_t ord_turn_at(const SrnnArgs& a, int64_t g, int32_t* s_c, int32_t* s_b,
-                                               int64_t& ncrit, int64_t& slot) {
+// the g-th entry of the critical list (-1: past its end) and its slot; the wave's exclusive prefix
+// of the partitions' counts in s_c (64 partitions = one per lane)
+__device__ __forceinline__ int64_t ord_crit_at(const SrnnArgs& a, int64_t g, int32_t* s_c, int64_t& slot) {
   const int lane = threadIdx.x & 63;
-  const int32_t c = ord::ld_level(a.o_ctl + ord::CRIT0 + lane), b = ord::ld_level(a.o_ctl + ord::BULK0 + lane);
-  int32_t ic = c, ib = b;
+  const int32_t c = ord::ld_level(a.o_ctl + ord::CRIT0 + lane);
+  int32_t ic = c;
 #pragma unroll
   for (int off = 1; off < 64; off <<= 1) {
-    const int32_t vc = __shfl_up(ic, off), vb = __shfl_up(ib, off);
-    if (lane >= off) {
-      ic += vc;
-      ib += vb;
-    }
+    const int32_t v = __shfl_up(ic, off);
+    if (lane >= off) ic += v;
   }
   s_c[lane] = ic - c;
-  s_b[lane] = ib - b;
-  const int64_t C = __shfl(ic, 63), B = __shfl(ib, 63);
-  ncrit = C;
+  const int64_t C = __shfl(ic, 63);
   __syncthreads();
-  const int64_t cap = ord::rec_cap(a.n);
-  const int32_t* order = ord::run_order(a);
-  const bool isc = g < C;
-  if (!isc && g >= C + B) return -1;
-  const int64_t h = isc ? g : g - C;
-  const int32_t* pre = isc ? s_c : s_b;
-  int p = 0;  // the last partition whose prefix is <= h (a partition with entries)
+  slot = -1;
+  if (g >= C) return -1;
+  int p = 0;  // the last partition whose prefix is <= g (a partition with entries)
 #pragma unroll
   for (int step = 32; step > 0; step >>= 1)
-    if (pre[p + step] <= h) p += step;
-  const int64_t off = h - pre[p];
-  slot = isc ? p * cap + off : -1;  // (critical roots: their run-order slot keys the permutation table)
-  return isc ? order[p * cap + off] : order[(p + 1) * cap - 1 - off];
+    if (s_c[p + step] <= g) p += step;
+  slot = p * ord::rec_cap(a.n) + (g - s_c[p]);
+  return ord::run_order(a)[slot];
 }
 
 // every turn of the generation.  A lane first runs a turn without producers: turn k (or, with
@@ -528,23 +514,27 @@ __global__ __launch_bounds__(TB) void k_ord_run(SrnnCfg c, SrnnArgs a) {
   __shared__ uint8_t s_perm[TB * PERM];
   __shared__ int32_t s_q[TB];
   const int lane = threadIdx.x;
-  const int64_t k0 = (int64_t)blockIdx.x * TB + lane;
   const int32_t gen = I::gen_of(a);
   float4* samp = samp_lane<Net>(s_samp, lane);
   uint8_t* perm = s_perm + lane * PERM;
   int64_t cur = -1, prow = -1;
   bool raised = false;
-  if (a.flags & SRNN_F_ORD_CRIT) {  // the run order: producers of later turns first, raised priority
-    __shared__ int32_t s_c[64], s_b[64];
-    int64_t ncrit = 0, slot = -1;
-    cur = ord_turn_at(a, k0, s_c, s_b, ncrit, slot);
-    if (slot >= 0) prow = ord::rec_total(a.n) + slot;
-    if ((int64_t)blockIdx.x * TB < ncrit) {
+  // with the critical list: its waves first (the grid's first a.x_groups workgroups), at raised
+  // priority, permutations from the table; then every other turn without producers in index order
+  const int64_t ncw = (a.flags & SRNN_F_ORD_CRIT) ? a.x_groups : 0;
+  if ((int64_t)blockIdx.x < ncw) {
+    __shared__ int32_t s_c[64];
+    int64_t slot = -1;
+    cur = ord_crit_at(a, (int64_t)blockIdx.x * TB + lane, s_c, slot);
+    if (cur >= 0 && a.o_list[cur] >= 0) cur = -1;  // a producer with producers of its own: a continuation
+    if (cur >= 0) prow = ord::rec_total(a.n) + slot;
+    if (__ballot(cur >= 0)) {
       __builtin_amdgcn_s_setprio(2);
       raised = true;
     }
-  } else if (k0 < a.n && a.o_list[k0] < 0) {
-    cur = k0;
+  } else {
+    const int64_t k = ((int64_t)blockIdx.x - ncw) * TB + lane;
+    if (k < a.n && a.o_list[k] < 0 && !(ncw && ord::cons_head(a)[k] != ord::EMPTY)) cur = k;
   }
   if (cur >= 0) ord::st_level(a.o_src + 4 * cur + 3, 0);
   int32_t ready = ord::EMPTY, nready = 0;
@@ -743,13 +733,15 @@ int soup_ordered(const SrnnCfg& c, const SrnnArgs& a) {
   hipStream_t st = (hipStream_t)a.stream;
   hipLaunchKernelGGL((k_ord_plan<Net, S>), dim3((unsigned)nb), dim3(TB), 0, st, c, a);
   hipLaunchKernelGGL((k_ord_mark<Net, S>), dim3((unsigned)nb), dim3(TB), 0, st, c, a);
-  hipLaunchKernelGGL((k_ord_count<Net, S>), dim3((unsigned)nb), dim3(TB), 0, st, c, a);
   SrnnArgs ra = a;
   const bool crit = knob(SRNN_KNOB_ORD_CRIT, 1) != 0;
   if (crit) {
-    hipLaunchKernelGGL((k_ord_order<Net, S>), dim3((unsigned)nb), dim3(TB), 0, st, c, a);
     ra.flags |= SRNN_F_ORD_CRIT;
+    // critical-list waves of the run launch: the list holds at most one entry per pending
+    // record's producer slot; the launch's waves past its end return at once
+    ra.x_groups = (int32_t)std::min<int64_t>(nb, (ord::rec_total(a.n) + TB - 1) / TB);
   }
+  hipLaunchKernelGGL((k_ord_count<Net, S>), dim3((unsigned)nb), dim3(TB), 0, st, c, ra);
   if constexpr (Net::KIND == 0 && Net::P <= 16) {
     const int32_t E = (a.severity > 0 ? a.severity : 0) + (a.epochs > 0 ? a.epochs : 0);
     if (a.ptab && (a.flags & SRNN_F_SHUFFLE) && E > 0) {
@@ -758,7 +750,7 @@ int soup_ordered(const SrnnCfg& c, const SrnnArgs& a) {
                          dim3(TB), 0, st, a, E);
     }
   }
-  hipLaunchKernelGGL((k_ord_run<Net, S>), dim3((unsigned)nb), dim3(TB), 0, st, c, ra);
+  hipLaunchKernelGGL((k_ord_run<Net, S>), dim3((unsigned)(nb + (crit ? ra.x_groups : 0))), dim3(TB), 0, st, c, ra);
   hipLaunchKernelGGL((k_ord_close<Net, S>), dim3((unsigned)nb), dim3(TB), 0, st, c, a);
   if (!(a.flags & SRNN_F_GEN_COUNTS)) {
     constexpr int FNT = SRNN_FINISH_NT;

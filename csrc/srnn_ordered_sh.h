@@ -39,15 +39,15 @@ constexpr int64_t rec_bytes() {
 
 // levels of every turn without running any: a root (no producer) is level 0 and counts its
 // consumers down; the lane that takes a record to zero sets its level (1 + its deepest
-// producer's) and counts that turn's consumers down in turn.  Levels are atomics; the release /
-// acquire of ord::publish order them (no rows are handed over here).
+// producer's) and counts that turn's consumers down in turn.  Levels are agent-scope atomics,
+// drained before the decrements (ord::publish<false>: no rows handed over, no release).
 template <class Net, class S>
 __global__ __launch_bounds__(TB) void k_ordsh_levels(SrnnArgs a) {
   const int64_t k = (int64_t)blockIdx.x * TB + threadIdx.x;
   int32_t ready = ord::EMPTY, nready = 0, maxl = 0;
   if (k < a.n && a.o_list[k] < 0) {
     ord::st_level(a.o_src + 4 * k + 3, 0);
-    ord::publish(a, k, ready, nready);
+    ord::publish<false>(a, k, ready, nready);
   }
   while (ready != ord::EMPTY) {
     const int32_t q = ready;
@@ -62,7 +62,7 @@ __global__ __launch_bounds__(TB) void k_ordsh_levels(SrnnArgs a) {
     const int64_t kk = rec[0];
     ord::st_level(a.o_src + 4 * kk + 3, lv + 1);
     maxl = maxl > lv + 1 ? maxl : lv + 1;
-    ord::publish(a, kk, ready, nready);
+    ord::publish<false>(a, kk, ready, nready);
   }
   if (maxl) atomicMax(a.o_ctl + ord::MAXLW, maxl);
 }

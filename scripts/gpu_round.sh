@@ -10,16 +10,12 @@ export TMPDIR=/tmp
 TAG=${1:-round}
 step() { local name=$1 lim=$2; shift 2; timeout -k 10 $lim "$@" > gpurun_out/${name}_$TAG.log 2>&1; local rc=$?;
          echo "[$name rc=$rc] $(tail -1 gpurun_out/${name}_$TAG.log | cut -c1-600)"; return $rc; }
-timeout -k 10 600 python -u -m pytest tests/test_ordered_soup.py tests/test_exact_oracle_gpu.py tests/test_pair_soup_gpu.py -m gpu -x -q --timeout 200 --timeout-method thread > gpurun_out/pytest_$TAG.log 2>&1
+timeout -k 10 600 python -u -m pytest tests/test_ordered_sharded_gpu.py tests/test_ordered_soup.py tests/test_exact_oracle_gpu.py tests/test_pair_soup_gpu.py -m gpu -x -q --timeout 200 --timeout-method thread > gpurun_out/pytest_$TAG.log 2>&1
 rc=$?; tail -2 gpurun_out/pytest_$TAG.log; [ $rc -eq 0 ] || exit $rc
 step tr_crit 300 python bench/ordered_trace.py || exit 1
-SRNN_ORD_CRIT=0 step tr_nocrit 300 python bench/ordered_trace.py || exit 1
-step tr_12k 300 python bench/ordered_trace.py --particles 12500 || exit 1
 step b20 300 python bench.py --steps 20 --warmup 5 || exit 1
-for N in 50000 100000; do
-  for PT in 0 1; do
-    SRNN_PERM_TABLE=$PT step s${N}_t$PT 300 python bench.py --steps 20 --warmup 5 --particles $N --reference-order-steps 0 || exit 1
-  done
-done
+step b20b 300 python bench.py --steps 20 --warmup 5 || exit 1
+SRNN_ORDSH_EMULATE=8 step em8_seq 300 python bench.py --steps 10 --warmup 2 --force-sharded --order sequential || exit 1
 step prof_ro 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_ro_$TAG -o t --output-format csv -- python3 bench.py --steps 20 --warmup 5 --order sequential || exit 1
+SRNN_ORDSH_EMULATE=8 step prof_em8 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_em8_$TAG -o t --output-format csv -- python3 bench.py --steps 10 --warmup 2 --force-sharded --order sequential || exit 1
 echo done

@@ -44,7 +44,7 @@ OP_X2_POST = 21   # sharded soup: uids, census, received notices / requests
 OP_SOUP_ORDERED = 22  # reference-order (sequential) generation, DAG-scheduled (csrc/srnn_ordered.h)
 OP_SOUP_ORDERED_SH = 23  # one phase of a sharded reference-order generation (csrc/srnn_ordered_sh.h)
 ORDSH_PLAN, ORDSH_LEVEL, ORDSH_PACK, ORDSH_UNPACK, ORDSH_CLOSE, ORDSH_LINK = range(6)
-ORD_CTL_WORDS = 227   # o_ctl words of an ordered generation (csrc/srnn_ordered.h)
+ORD_CTL_WORDS = 163   # o_ctl words of an ordered generation (csrc/srnn_ordered.h)
 ORD_MAXLW, ORD_ERRW = 17, 18
 ORD_NPART = 64        # partitions of the pending records
 ORD_REC = 32          # int32 words per pending record
