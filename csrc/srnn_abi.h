@@ -49,6 +49,8 @@ enum SrnnFlag : uint32_t {
                                      // exchange chain wins the SIMDs it shares with the local evolve)
   SRNN_F_ORD_CRIT = 1u << 22,        // ordered run: turns in the run order of k_ord_order (internal: set by
                                      // the library from SRNN_KNOB_ORD_CRIT)
+  SRNN_F_PTAB_READY = 1u << 23,      // ptab already holds this generation's permutations (built by the
+                                     // sharded pack): the generation launch does not rebuild them
 };
 
 // Attack-list entries (uint32, SRNN_NIL ends a list).  Single rank: the attacker's row
@@ -207,7 +209,7 @@ enum SrnnOp {
                            // (srnn_ordered_sh.h)
 };
 
-int srnn_abi_version();  // 24
+int srnn_abi_version();  // 25
 int64_t srnn_args_size();  // sizeof(SrnnArgs): the ctypes mirror checks its layout against it
 int64_t srnn_cfg_size();
 int srnn_has_config(const SrnnCfg* cfg);

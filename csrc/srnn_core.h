@@ -122,6 +122,22 @@ SRNN_HD uint64_t perm_from_bits(uint64_t u) {
   }
   return ((uint64_t)phi << 32) | plo;
 }
+// runtime-n form of perm_from_bits<N> (same permutation; tables built outside a templated kernel)
+SRNN_HD uint64_t perm_from_bits_n(int n, uint64_t u) {
+  uint64_t p = 0;
+  for (int k = 0; k < n; ++k) p |= (uint64_t)k << (4 * k);
+  uint32_t ul = (uint32_t)u, uh = (uint32_t)(u >> 32);
+  for (int i = n - 1; i > 0; --i) {
+    const uint64_t lo = (uint64_t)ul * (uint32_t)(i + 1);
+    const uint64_t hi = (uint64_t)uh * (uint32_t)(i + 1) + (lo >> 32);
+    const uint32_t j = (uint32_t)(hi >> 32);
+    ul = (uint32_t)lo;
+    uh = (uint32_t)hi;
+    const uint64_t ni = (p >> (4 * i)) & 15u, nj = (p >> (4 * j)) & 15u, x = ni ^ nj;
+    p ^= (x << (4 * i)) | (x << (4 * j));
+  }
+  return p;
+}
 template <int N>
 SRNN_HD uint64_t shuffle16(const Rng& rng, uint64_t id, uint32_t step, uint32_t purpose) {
   return perm_from_bits<N>(perm_bits(perm_draw(rng, id, step, purpose), step));

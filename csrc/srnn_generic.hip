@@ -240,22 +240,8 @@ __device__ void make_coords_dev(const GShape& s, float* c) {  // whole block, th
 }
 
 // ---------------------------------------------------------------- permutations
-// nibble permutation of [0, n), n <= 16: the runtime-n form of perm_from_bits<N>
-SRNN_HD uint64_t g_perm_nibbles(int n, uint64_t u) {
-  uint64_t p = 0;
-  for (int k = 0; k < n; ++k) p |= (uint64_t)k << (4 * k);
-  uint32_t ul = (uint32_t)u, uh = (uint32_t)(u >> 32);
-  for (int i = n - 1; i > 0; --i) {
-    const uint64_t lo = (uint64_t)ul * (uint32_t)(i + 1);
-    const uint64_t hi = (uint64_t)uh * (uint32_t)(i + 1) + (lo >> 32);
-    const uint32_t j = (uint32_t)(hi >> 32);
-    ul = (uint32_t)lo;
-    uh = (uint32_t)hi;
-    const uint64_t ni = (p >> (4 * i)) & 15u, nj = (p >> (4 * j)) & 15u, x = ni ^ nj;
-    p ^= (x << (4 * i)) | (x << (4 * j));
-  }
-  return p;
-}
+// nibble permutation of [0, n), n <= 16 (srnn_core.h)
+SRNN_HD uint64_t g_perm_nibbles(int n, uint64_t u) { return perm_from_bits_n(n, u); }
 // Fisher-Yates into a strided vector (fisher_yates of srnn_core.h, same draws)
 SRNN_HD void g_fisher_yates(SV perm, int n, const Rng& rng, uint64_t id, uint32_t step, uint32_t purpose) {
   for (int i = 0; i < n; ++i) perm[i] = (float)i;

@@ -768,14 +768,32 @@ __global__ __launch_bounds__(TBP) void k_perm_table(SrnnArgs a, int32_t E) {
   a.ptab[2 * p * a.n + row] = perm_from_bits<P>(perm_bits(r, c0));
   if (2 * p + 1 < E) a.ptab[(2 * p + 1) * a.n + row] = perm_from_bits<P>(perm_bits(r, c0 + 1u));
 }
-// launch the permutation table of this generation when the caller gave one (nibble nets)
+// the same entries from a shape-independent kernel (the sharded exchange's pack builds the
+// table of the generation it prepares; runtime P, identical permutations)
+__device__ __forceinline__ void perm_table_entry(const SrnnArgs& a, int P, int64_t row, int32_t p, int32_t gen,
+                                                 int32_t E) {
+  const uint32_t c0 = (uint32_t)gen * 1024u + 512u + 2u * (uint32_t)p;
+  const Rng rng{(uint32_t)a.seed, (uint32_t)(a.seed >> 32)};
+  const U4 r = perm_draw(rng, (uint64_t)(a.lo + row), c0, P_SHUFFLE);
+  a.ptab[2 * p * a.n + row] = perm_from_bits_n(P, perm_bits(r, c0));
+  if (2 * p + 1 < E) a.ptab[(2 * p + 1) * a.n + row] = perm_from_bits_n(P, perm_bits(r, c0 + 1u));
+}
+// workgroups of NT threads that build a generation's table inside another launch (0: none --
+// no table given, host, not a nibble Weightwise net, no shuffle, no epochs)
+inline int64_t pack_ptab_blocks(const SrnnCfg& c, const SrnnArgs& a, int NT) {
+  const int32_t E = (a.severity > 0 ? a.severity : 0) + (a.epochs > 0 ? a.epochs : 0);
+  if (!a.ptab || !a.dev || !(a.flags & SRNN_F_SHUFFLE) || c.kind != 0 || c.p > 16 || E <= 0 || a.n <= 0) return 0;
+  return ((a.n + NT - 1) / NT) * ((E + 1) / 2);
+}
+// launch the permutation table of this generation when the caller gave one (nibble nets);
+// SRNN_F_PTAB_READY: an earlier launch of the generation (the sharded pack) built it already
 template <class Net>
 int perm_table(const SrnnArgs& a) {
   if constexpr (Net::KIND != 0 || Net::P > 16) {
     return 0;
   } else {
     const int32_t E = (a.severity > 0 ? a.severity : 0) + (a.epochs > 0 ? a.epochs : 0);
-    if (!a.ptab || !a.dev || !(a.flags & SRNN_F_SHUFFLE) || E <= 0 || a.n <= 0) return 0;
+    if (!a.ptab || !a.dev || !(a.flags & SRNN_F_SHUFFLE) || E <= 0 || a.n <= 0 || (a.flags & SRNN_F_PTAB_READY)) return 0;
     hipLaunchKernelGGL((k_perm_table<Net>), dim3((unsigned)((a.n + TBP - 1) / TBP), (unsigned)((E + 1) / 2)),
                        dim3(TBP), 0, (hipStream_t)a.stream, a, E);
     return 0;

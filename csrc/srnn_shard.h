@@ -157,16 +157,17 @@ SRNN_HD void pack_row(const SrnnArgs& a, const X2Geom& G, int64_t idx, int32_t g
   tag[1] = gen;
 }
 
-// the header words of every peer block that the finish owns
+// the header words of peer q's block that the finish owns
+SRNN_HD void write_stats_peer(const SrnnArgs& a, const X2Geom& G, int q, const int64_t* tot, int32_t gen) {
+  int64_t* h = G.hdr(G.blk(a.sendbuf, a, q));
+  for (int w = 0; w < 6; ++w) h[w] = tot[w];
+  h[H_VALID] = 1;
+  h[H_GEN] = gen;
+  h[H_NREP] = a.x_nsrep ? a.x_nsrep[q] : 0;
+  h[H_NATT] = a.x_cno ? (a.x_cno[q] < a.x_cn ? a.x_cno[q] : a.x_cn) : 0;
+}
 SRNN_HD void write_stats(const SrnnArgs& a, const X2Geom& G, const int64_t* tot, int32_t gen) {
-  for (int q = 0; q < a.world; ++q) {
-    int64_t* h = G.hdr(G.blk(a.sendbuf, a, q));
-    for (int w = 0; w < 6; ++w) h[w] = tot[w];
-    h[H_VALID] = 1;
-    h[H_GEN] = gen;
-    h[H_NREP] = a.x_nsrep ? a.x_nsrep[q] : 0;
-    h[H_NATT] = a.x_cno ? (a.x_cno[q] < a.x_cn ? a.x_cno[q] : a.x_cn) : 0;
-  }
+  for (int q = 0; q < a.world; ++q) write_stats_peer(a, G, q, tot, gen);
 }
 // stats word w of rank r: the gathered array (flush, all-gather exchange) or the header of
 // r's block in the exchange just received (zeros when not valid)

@@ -39,101 +39,98 @@ namespace {
 
 using namespace x2;
 
+// The finish of generation t-1 in ONE workgroup (no ticket, no second pass): its block stats
+// (popcount of the respawn ballots, class counts) -> this rank's totals in every peer's header,
+// the newborns per finish group -> x_part[g * 6] (post's uid workgroups start from them), and
+// the remote-dependent slots of THIS generation per 64-row block (x_dep bits, final since the
+// last post) -> x_hpre[b] = holes before block b, x_hgrp = 0 (the single-launch evolve's waves
+// map their holes onto the remote list with x_hpre[b] + x_hgrp[g]).  One load round trip, LDS
+// reductions, stores: the ticketed form (x_groups workgroups, partials through memory, a last
+// workgroup summing them) was a chain of ~7 dependent memory round trips, ~9.6 us per
+// generation on the sharded critical path (profiles/r5e_*).
+constexpr int X2_MAX_GROUPS = 1024;
+__device__ void pack_finish_wg(const SrnnArgs& a, const X2Geom& G, int32_t gen) {
+  __shared__ int64_t s_red[XT / 64];
+  __shared__ int32_t s_hw[XT / 64];
+  __shared__ int32_t s_born[X2_MAX_GROUPS];
+  const int t = threadIdx.x;
+  // this thread's peers' header words that are not stats (loaded first, stored last)
+  for (int64_t g = t; g < a.x_groups; g += XT) s_born[g] = 0;
+  __syncthreads();
+  const unsigned long long* bs = reinterpret_cast<const unsigned long long*>(a.temp);
+  const int64_t nb = (a.n + 63) / 64, per = (nb + a.x_groups - 1) / a.x_groups, nw = (a.n + 31) / 32;
+  int64_t v[6] = {0, 0, 0, 0, 0, 0};
+  int32_t carry = 0;
+  for (int64_t c0 = 0; c0 < nb; c0 += XT) {
+    const int64_t b = c0 + t;
+    int32_t h = 0;
+    if (b < nb) {
+      const unsigned long long* st = bs + b * 4;
+      const unsigned long long m = st[0], c01 = st[1], c23 = st[2], c4 = st[3];
+      if (a.x_hpre) h = __popc(a.x_dep[2 * b]) + (2 * b + 1 < nw ? __popc(a.x_dep[2 * b + 1]) : 0);
+      const int32_t born = __popcll(m);
+      v[0] += born;
+      v[1] += (uint32_t)c01;
+      v[2] += (uint32_t)(c01 >> 32);
+      v[3] += (uint32_t)c23;
+      v[4] += (uint32_t)(c23 >> 32);
+      v[5] += (uint32_t)c4;
+      if (born) atomicAdd(&s_born[b / per], born);
+    }
+    if (a.x_hpre) {
+      int32_t tot;
+      const int32_t incl = block_incl_scan<XT, int32_t>(h, s_hw, &tot);
+      if (b < nb) a.x_hpre[b] = carry + incl - h;
+      carry += tot;
+      __syncthreads();  // s_hw is reused by the next chunk
+    }
+  }
+  for (int w = 0; w < 6; ++w) v[w] = wg_sum(v[w], s_red);  // (barriers: s_born complete too)
+  for (int64_t g = t; g < a.x_groups; g += XT) {
+    a.x_part[g * 6] = s_born[g];
+    if (a.x_hpre) a.x_hgrp[g] = 0;
+  }
+  int64_t tot[6];  // census[5], born
+  tot[5] = v[0];
+  for (int w = 0; w < 5; ++w) tot[w] = v[1 + w];
+  if (a.counts) {  // census accumulated by a classify launch (nets without a fused census)
+    for (int w = 0; w < 5; ++w) tot[w] += (int64_t)a.counts[w];
+  }
+  __syncthreads();  // every thread read counts before thread 0 clears them
+  if (a.counts && t == 0)
+    for (int w = 0; w < 6; ++w) a.counts[w] = 0;
+  for (int q = t; q < a.world; q += XT) write_stats_peer(a, G, q, tot, gen);
+}
+
 __global__ __launch_bounds__(XT) void k_x2_pack(SrnnCfg c, SrnnArgs a) {
   if (a.flags & SRNN_F_X2_PRIO) __builtin_amdgcn_s_setprio(3);
   const X2Geom G = geom(c);
   const int32_t gen = gen_of(a);
   const bool prime = (a.flags & SRNN_F_X2_PRIME) != 0, fin_only = (a.flags & SRNN_F_X2_FINISH_ONLY) != 0;
   const int64_t nd = fin_only ? 0 : (a.n + XT - 1) / XT;
-  __shared__ int64_t s_red[XT / 64];
-  __shared__ int32_t s_last;
-  __shared__ int32_t s_hw[XT / 64];
-  if ((int64_t)blockIdx.x < a.x_groups) {
-    // ---- finish of generation t-1: this workgroup's blocks -> partial (born, census)
-    int64_t b0, b1;
-    wg_range(a, blockIdx.x, b0, b1);
-    const unsigned long long* bs = reinterpret_cast<const unsigned long long*>(a.temp);
-    int64_t v[6] = {0, 0, 0, 0, 0, 0};
-    for (int64_t b = b0 + threadIdx.x; b < b1; b += XT) {
-      const unsigned long long* st = bs + b * 4;
-      v[0] += __popcll(st[0]);
-      v[1] += (uint32_t)st[1];
-      v[2] += (uint32_t)(st[1] >> 32);
-      v[3] += (uint32_t)st[2];
-      v[4] += (uint32_t)(st[2] >> 32);
-      v[5] += (uint32_t)st[3];
-    }
-    for (int w = 0; w < 6; ++w) v[w] = wg_sum(v[w], s_red);
-    if (a.x_hpre) {
-      // remote-dependent slots (holes) per 64-row block of THIS generation (bits final since
-      // pack / post of the last one): exclusive prefix inside the workgroup's range -> x_hpre,
-      // its total -> x_hgrp (scanned by the last workgroup); the single-launch evolve's waves
-      // map their holes onto the remote list with them
-      const int64_t nw = (a.n + 31) / 32;
-      int32_t carry = 0;
-      for (int64_t c0 = b0; c0 < b1; c0 += XT) {
-        const int64_t b = c0 + threadIdx.x;
-        int32_t h = 0;
-        if (b < b1) h = __popc(a.x_dep[2 * b]) + (2 * b + 1 < nw ? __popc(a.x_dep[2 * b + 1]) : 0);
-        int32_t tot;
-        const int32_t incl = block_incl_scan<XT, int32_t>(h, s_hw, &tot);
-        if (b < b1) a.x_hpre[b] = carry + incl - h;
-        carry += tot;
-        __syncthreads();
-      }
-      if (threadIdx.x == 0) __hip_atomic_store(a.x_hgrp + blockIdx.x, carry, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    if (threadIdx.x == 0) {
-      // partials leave L2 at once (sc1 stores: other XCDs read them), drained before the ticket
-      for (int w = 0; w < 6; ++w)
-        __hip_atomic_store(a.x_part + blockIdx.x * 6 + w, v[w], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      s_last = atomicAdd(a.x_ctl + 0, 1) == a.x_groups - 1;
-    }
-    __syncthreads();
-    if (!s_last) return;
-    // the last workgroup sums every workgroup's partials: one device-scope load round trip per
-    // thread (a serial walk by one thread costs one round trip per workgroup)
-    int64_t pv[6] = {0, 0, 0, 0, 0, 0};
-    for (int64_t g = threadIdx.x; g < a.x_groups; g += XT)
-      for (int w = 0; w < 6; ++w) pv[w] += __hip_atomic_load(a.x_part + g * 6 + w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    for (int w = 0; w < 6; ++w) pv[w] = wg_sum(pv[w], s_red);
-    if (a.x_hpre) {  // exclusive prefix of the workgroups' hole totals, in place
-      int32_t carry = 0;
-      for (int64_t c0 = 0; c0 < a.x_groups; c0 += XT) {
-        const int64_t g = c0 + threadIdx.x;
-        const int32_t h =
-            g < a.x_groups ? __hip_atomic_load(a.x_hgrp + g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0;
-        int32_t tot;
-        const int32_t incl = block_incl_scan<XT, int32_t>(h, s_hw, &tot);
-        if (g < a.x_groups) a.x_hgrp[g] = carry + incl - h;
-        carry += tot;
-        __syncthreads();
-      }
-    }
-    if (threadIdx.x == 0) {
-      int64_t tot[6];  // census[5], born
-      tot[5] = pv[0];
-      for (int w = 0; w < 5; ++w) tot[w] = pv[1 + w];
-      if (a.counts) {  // census accumulated by a classify launch (nets without a fused census)
-        for (int w = 0; w < 5; ++w) tot[w] += (int64_t)a.counts[w];
-        for (int w = 0; w < 6; ++w) a.counts[w] = 0;
-      }
-      write_stats(a, G, tot, gen);
-      a.x_ctl[0] = 0;
-    }
+  const int64_t nr = (fin_only || prime) ? 0 : ((int64_t)a.world * (a.x_cq + a.x_cn) + XT - 1) / XT;
+  if (blockIdx.x == 0) {  // ---- finish of generation t-1
+    pack_finish_wg(a, G, gen);
     return;
   }
-  if ((int64_t)blockIdx.x < a.x_groups + nd) {
+  const int64_t blk = (int64_t)blockIdx.x - 1;
+  if (blk < nd) {
     // ---- decisions of the next generation (PRIME: of this one) for the local slots
-    const int64_t i = ((int64_t)blockIdx.x - a.x_groups) * XT + threadIdx.x;
+    const int64_t i = blk * XT + threadIdx.x;
     __shared__ int32_t s_res[XT / 64 + 1];
     pack_decide_block(a, G, i, i < a.n, prime ? gen : gen + 1, s_res);
     return;
   }
-  // ---- rows of this generation's exchange
-  const int64_t idx = ((int64_t)blockIdx.x - a.x_groups - nd) * XT + threadIdx.x;
-  if (idx < (int64_t)a.world * (a.x_cq + a.x_cn)) pack_row(a, G, idx, gen);
+  if (blk < nd + nr) {  // ---- rows of this generation's exchange
+    const int64_t idx = (blk - nd) * XT + threadIdx.x;
+    if (idx < (int64_t)a.world * (a.x_cq + a.x_cn)) pack_row(a, G, idx, gen);
+    return;
+  }
+  // ---- this generation's SGD epoch permutations (SrnnArgs::ptab, nibble Weightwise nets):
+  // the table launch of the generation kernel folded into pack (pack_ptab_blocks)
+  const int64_t tb = (a.n + XT - 1) / XT, q = blk - nd - nr, p = q / tb;
+  const int64_t row = (q - p * tb) * XT + threadIdx.x;
+  if (row < a.n) perm_table_entry(a, c.p, row, (int32_t)p, gen, (a.severity > 0 ? a.severity : 0) + (a.epochs > 0 ? a.epochs : 0));
 }
 
 __global__ __launch_bounds__(XT) void k_x2_post(SrnnCfg c, SrnnArgs a) {
@@ -253,21 +250,35 @@ __global__ __launch_bounds__(TBU) void k_uid_assign(SrnnArgs a) {
     if (a.census && all > 0)
       for (int w = 0; w < 5; ++w) a.census[w] = cen[w];
   }
-  // per-row flags: thread t walks rows [t*ch, (t+1)*ch)
-  const int64_t ch = (a.n + TBU - 1) / TBU;
-  const int64_t r0 = (int64_t)threadIdx.x * ch < a.n ? (int64_t)threadIdx.x * ch : a.n;
-  const int64_t r1 = r0 + ch < a.n ? r0 + ch : a.n;
-  int32_t cnt = 0;
-  for (int64_t i = r0; i < r1; ++i) cnt += a.rowflags[i] != 0;
-  int32_t total_local;
-  const int32_t incl = block_incl_scan<TBU>(cnt, s_wave, &total_local);  // barrier inside
+  // per-row flags in tiles of TBU * UR rows: thread t takes rows [tile + t*UR, +UR) (the wave's
+  // loads cover consecutive memory), one block scan per tile numbers them in slot order (the
+  // per-thread walk of n / TBU rows took 61 us at 100k rows, profiles/r5e_*)
+  constexpr int UR = 8;
   const int64_t base = *(volatile const int64_t*)a.uid_base;
-  int64_t k = base + s_prefix + incl - cnt;
-  for (int64_t i = r0; i < r1 && cnt; ++i)
-    if (a.rowflags[i]) {
-      a.uid_out[i] = k++;
-      a.rowflags[i] = 0;
+  int64_t k = base;  // (s_prefix added after the first scan's barrier)
+  bool first = true;
+  for (int64_t t0 = 0; t0 < a.n; t0 += (int64_t)TBU * UR) {
+    const int64_t r0 = t0 + (int64_t)threadIdx.x * UR;
+    int32_t f[UR];
+    int32_t cnt = 0;
+#pragma unroll
+    for (int u = 0; u < UR; ++u) {
+      f[u] = r0 + u < a.n ? a.rowflags[r0 + u] : 0;
+      cnt += f[u] != 0;
     }
+    int32_t tile_total;
+    const int32_t incl = block_incl_scan<TBU>(cnt, s_wave, &tile_total);  // barrier inside
+    if (first) k += s_prefix, first = false;
+    int64_t u0 = k + incl - cnt;
+#pragma unroll
+    for (int u = 0; u < UR; ++u)
+      if (f[u]) {
+        a.uid_out[r0 + u] = u0++;
+        a.rowflags[r0 + u] = 0;
+      }
+    k += tile_total;
+    __syncthreads();  // s_wave is reused by the next tile
+  }
   __syncthreads();
   if (threadIdx.x == 0) a.uid_base[0] = base + s_total;
   if (a.counts && threadIdx.x < 6) a.counts[threadIdx.x] = 0;
@@ -325,10 +336,14 @@ extern "C" int srnn_x2_run(int op, const SrnnCfg* c, const SrnnArgs* a) {
       host_pack(*c, *a);
       return 0;
     }
+    if (a->x_groups > X2_MAX_GROUPS) {
+      set_error("X2 pack: at most 1024 finish groups");
+      return -5;
+    }
     const int64_t nd = fin_only ? 0 : (a->n + XT - 1) / XT;
     const bool prime = (a->flags & SRNN_F_X2_PRIME) != 0;
     const int64_t nr = (fin_only || prime) ? 0 : ((int64_t)a->world * (a->x_cq + a->x_cn) + XT - 1) / XT;
-    const int64_t grid = a->x_groups + nd + nr;
+    const int64_t grid = 1 + nd + nr + ((fin_only || prime) ? 0 : pack_ptab_blocks(*c, *a, XT));
     if (grid > 0x7fffffffLL) {
       set_error("grid too large");
       return -2;

@@ -20,7 +20,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 # SRNN_LIB: load another build of the library (A/B of compiler flags on the GPU box)
 LIB_PATH = os.environ.get("SRNN_LIB") or os.path.join(_HERE, "libsrnn.so")
 CSRC = os.path.normpath(os.path.join(_HERE, "..", "..", "csrc"))
-ABI_VERSION = 24
+ABI_VERSION = 25
 
 # SrnnOp (csrc/srnn_abi.h)
 OP_INIT = 0
@@ -86,6 +86,7 @@ FLAG_X2_FINISH_ONLY = 1 << 18
 FLAG_X2_PRIO = 1 << 19
 FLAG_X2_BOTH = 1 << 20
 FLAG_X2_POST_FUSED = 1 << 21
+FLAG_PTAB_READY = 1 << 23  # ptab already holds the generation's permutations (the sharded pack built them)
 
 X2_HDR = 12           # int64 header words of an exchange block
 X2_REMOTE_WAVES = 4096

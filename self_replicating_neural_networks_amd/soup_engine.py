@@ -938,6 +938,9 @@ class SoupEngine:
                 rem.flags |= _lib.FLAG_X2_BOTH | _lib.FLAG_X2_POST_FUSED
                 rem.temp2 = _p(self.x_bstat[1 - p])
                 rem.ptab = _p(self._perm_table())  # the generation's permutations, ahead of it
+                if rem.ptab:  # built by pack's extra workgroups (no table launch on the critical path)
+                    pa.ptab = rem.ptab
+                    rem.flags |= _lib.FLAG_PTAB_READY
                 loc = None
                 po = None
         self._arg_cache[key] = (pa, po, rem, loc, census)
