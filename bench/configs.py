@@ -124,10 +124,17 @@ def config4s(args):
     params = dict(attacking_rate=0.1, learn_from_rate=0.1, learn_from_severity=1, train=args.train4s,
                   remove_divergent=True, remove_zero=True, epsilon=1e-4)
     res = dict(config="4s", name=f"{n} Aggregating(4,10,3) soup", n=n, params=params, gens=gens)
-    for label, shuffler, dtype in (("fp32", "none", torch.float32), ("bf16", "none", torch.bfloat16),
-                                   ("fp32_shuffle_random", "random", torch.float32)):
+    variants = [(label, shuffler, dtype, "synchronous") for label, shuffler, dtype in (
+        ("fp32", "none", torch.float32), ("bf16", "none", torch.bfloat16),
+        ("fp32_shuffle_random", "random", torch.float32))]
+    # the reference's in-place, index-ordered generation of the same soup (csrc/srnn_bignet.h BigOrd)
+    if args.order4s in ("both", "sequential"):
+        variants += [("ref_order_" + label, shuffler, dtype, "sequential") for label, shuffler, dtype, _ in variants]
+    if args.order4s == "sequential":
+        variants = [v for v in variants if v[3] == "sequential"]
+    for label, shuffler, dtype, order in variants:
         spec = ArchSpec.aggregating(4, 10, 3, shuffler=shuffler)
-        eng = SoupEngine(spec, n, params, device=dev, seed=0, dtype=dtype)
+        eng = SoupEngine(spec, n, params, device=dev, seed=0, dtype=dtype, order=order)
         eng.stats = True
         graphed = eng.capture(warmup=1)
         eng.evolve(2)
@@ -141,6 +148,8 @@ def config4s(args):
         res[f"{label}_graph"] = graphed
         res[f"{label}_generic_engine"] = bool(eng.generic)
         res[f"{label}_census"] = eng.count()
+        if order == "sequential":
+            res[f"{label}_levels"] = eng.ordered_levels()
         del eng
         torch.cuda.empty_cache()
     return res
@@ -185,6 +194,8 @@ def main():
     ap.add_argument("--n4s", type=int, default=1_000_000)
     ap.add_argument("--gens4s", type=int, default=5)
     ap.add_argument("--train4s", type=int, default=20)
+    ap.add_argument("--order4s", choices=["synchronous", "sequential", "both"], default="both",
+                    help="config 4s: the synchronous generation, the reference order, or both")
     args = ap.parse_args()
     for c in args.only.split(","):
         fn = {"1": config1, "2": config2, "4": config4, "4s": config4s, "5": config5}[c.strip()]

@@ -1745,6 +1745,294 @@ __global__ __launch_bounds__(TBR) void k_big_respawn_seq(SrnnCfg c, SrnnArgs a) 
   if (a.counts && threadIdx.x < 5) a.counts[threadIdx.x] = 0;
 }
 
+// ------------------------------------------------------------------ reference order
+// The reference's in-place, index-ordered generation (code/soup.py:51-87) of a big
+// aggregating net on the continuation scheduler of srnn_ordered.h (plan / mark / count / run
+// are shape independent; this is the turn and the close).  Recompute depth 1: an unstored
+// attack output A(j) is its attacker's forward on its victim's aggregate, and an aggregating
+// net's output is chunk-constant (shuffled: a permutation of the chunk values), so a version
+// read is either a streamed row or a 4-value chunk state -- the turn's own row is the only
+// 280-float array (as in big_soup_one).  Every step is the serial loop's (the runtime-shape
+// engine's soup_seq_one: attack keyed (attacker, gen*1024+1), learn_from `severity` steps on
+// the teacher's aggregate, `epochs` self-train steps, respawn_key(gen, k)) in the same
+// arithmetic order, so the generation equals OP_SOUP_SEQ bitwise whatever order its turns run in.
+template <class T, class S, bool SHUF>
+struct BigOrd : ord::OrdSched<1> {
+  using R = BRow<T, S>;
+  using Sched = ord::OrdSched<1>;
+  __device__ static float wget(const char* row, int k) {
+    if constexpr (S::ID == 0) return reinterpret_cast<const float*>(row)[k];
+    else return S::dec(reinterpret_cast<const uint16_t*>(row)[k]);
+  }
+  // lmlp with the weights read from a row in memory (same operation order)
+  template <int L>
+  __device__ static void smlp_rec(const char* row, float* x) {
+    constexpr int I = T::rows(L), O = T::cols(L), OFF = T::off(L);
+    float y[T::MAXW];
+#pragma unroll
+    for (int j = 0; j < O; ++j) {
+      float acc = x[0] * wget(row, OFF + j);
+#pragma unroll
+      for (int i = 1; i < I; ++i) acc = fmaf(x[i], wget(row, OFF + i * O + j), acc);
+      y[j] = acc;
+    }
+#pragma unroll
+    for (int j = 0; j < O; ++j) x[j] = y[j];
+    if constexpr (L < T::D) smlp_rec<L + 1>(row, x);
+  }
+  __device__ static void smlp(const char* row, const float* g, float* h) {
+    float x[T::MAXW];
+#pragma unroll
+    for (int i = 0; i < T::A; ++i) x[i] = g[i];
+    smlp_rec<0>(row, x);
+#pragma unroll
+    for (int i = 0; i < T::A; ++i) h[i] = x[i];
+  }
+  // the row of a stored version (E(j) in W, a stored A(j) in W3, the generation start in W2)
+  __device__ static const char* vrow(const SrnnArgs& a, int32_t code) {
+    if (code >= 0) return R::at((code & 1) ? a.W : a.W3, (int64_t)(code >> 1));
+    return R::at(a.W2, -(int64_t)code - 1);
+  }
+  __device__ static Rng rng(const SrnnArgs& a) { return Rng{(uint32_t)a.seed, (uint32_t)(a.seed >> 32)}; }
+  // chunk state of the unstored attack output A(j): the attacker's forward on its victim's aggregate
+  __device__ static void attack_state(const SrnnCfg& c, const SrnnArgs& a, int64_t j, float* h) {
+    const int32_t* sj = ord::src_of(a, j);
+    float gv[T::A];
+    R::stream_aggregate(vrow(a, sj[1] == ord::SRC_SELF ? sj[0] : sj[1]), gv, c.aggregator);
+    smlp(vrow(a, sj[0]), gv, h);
+    R::quant_a(h);
+  }
+  // aggregate of the output expand'(h) of attacker j (no shuffle: h itself, exactly)
+  __device__ static void state_agg(const SrnnCfg& c, const SrnnArgs& a, int64_t j, int32_t gen,
+                                   const ChunkPerm<T>& cp, const float* h, float* g) {
+    if constexpr (SHUF) {
+      cp.draw(rng(a), (uint64_t)j, (uint32_t)gen * 1024u + 1u);
+      aggregate_out<T, SHUF>(h, g, c.aggregator, cp);
+    } else {
+#pragma unroll
+      for (int q = 0; q < T::A; ++q) g[q] = h[q];
+    }
+  }
+  __device__ static void agg_version(const SrnnCfg& c, const SrnnArgs& a, int32_t code, int32_t gen,
+                                     const ChunkPerm<T>& cp, float* g) {
+    if (ord::is_A(code) && !ord::stored(a, code >> 1)) {
+      float h[T::A];
+      attack_state(c, a, code >> 1, h);
+      state_agg(c, a, code >> 1, gen, cp, h, g);
+    } else {
+      R::stream_aggregate(vrow(a, code), g, c.aggregator);
+    }
+  }
+  __device__ static void load_version(const SrnnCfg& c, const SrnnArgs& a, int32_t code, int32_t gen,
+                                      const ChunkPerm<T>& cp, float (&w)[T::P]) {
+    if (ord::is_A(code) && !ord::stored(a, code >> 1)) {
+      float h[T::A];
+      attack_state(c, a, code >> 1, h);
+      if constexpr (SHUF) cp.draw(rng(a), (uint64_t)(code >> 1), (uint32_t)gen * 1024u + 1u);
+      expand_out<T, SHUF>(w, h, cp);
+    } else {
+      R::load(vrow(a, code), w);
+    }
+  }
+  // this lane's stores of a row are complete before it reads the row back
+  __device__ static void own_row_fence() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  }
+  // a stored attack output, written weight by weight from its chunk state
+  __device__ static void store_state(char* row, const float* h, const ChunkPerm<T>& cp) {
+    for (int k = 0; k < T::P; ++k) R::put(row, k, pick<T>(h, SHUF ? cp.cid(k) : T::chunk(k)));
+    for (int k = T::P; k < T::PP; ++k) R::put(row, k, 0.f);
+  }
+
+  __device__ static void turn(const SrnnCfg& c, const SrnnArgs& a, int64_t k, int32_t gen, const ChunkPerm<T>& cp) {
+    const int32_t* s = ord::src_of(a, k);
+    int64_t at, te;
+    Sched::Dec::decision(a, k, gen, at, te);
+    const bool attack = at >= 0 && ord::needs_A(a, k, s);
+    // the aggregates of the versions this turn reads that do not depend on its own row first
+    // (streamed rows and chunk-state forwards: their loads never compete with the 280-float
+    // row for registers)
+    float gv[T::A], gt[T::A];
+    if (attack && at != k) agg_version(c, a, s[1], gen, cp, gv);
+    if (te >= 0 && s[2] != ord::SRC_SELF && s[2] != ord::SRC_ATK) agg_version(c, a, s[2], gen, cp, gt);
+    // the own row is read from memory until the training: an unstored attack output is
+    // materialised into this turn's E slot (W row k: nothing reads it before the turn ends), a
+    // self-attack's output too -- the 280 registers of the row are defined once, by one load
+    char* ek = R::at(a.W, k);
+    const char* p0 = vrow(a, s[0]);
+    if (ord::is_A(s[0]) && !ord::stored(a, s[0] >> 1)) {
+      float h[T::A];
+      attack_state(c, a, s[0] >> 1, h);
+      if constexpr (SHUF) cp.draw(rng(a), (uint64_t)(s[0] >> 1), (uint32_t)gen * 1024u + 1u);
+      store_state(ek, h, cp);
+      own_row_fence();
+      p0 = ek;
+    }
+    int8_t act = A_NONE;
+    int64_t cpart = -1;
+    float ho[T::A];  // the chunk state of A(k)
+    if (at >= 0) {  // 1. attack: the victim's row becomes f_k(victim)
+      if (attack) {
+        if (at == k) R::stream_aggregate(p0, gv, c.aggregator);
+        smlp(p0, gv, ho);
+        R::quant_a(ho);
+        if constexpr (SHUF) cp.draw(rng(a), (uint64_t)k, (uint32_t)gen * 1024u + 1u);
+        if (ord::stored(a, k)) store_state(R::at(a.W3, k), ho, cp);
+        if (at == k) {
+          store_state(ek, ho, cp);
+          own_row_fence();
+          p0 = ek;
+        }
+      }
+      act = A_ATTACKING;
+      cpart = at;
+    }
+    float w[T::P];
+    R::load(p0, w);
+    // 2. learn_from (`severity` steps on the teacher's aggregate), 3. self-train (`epochs` steps
+    // on the own aggregate): one step loop, one register copy of the row (big_soup_one)
+    int nlearn = 0;
+    if (te >= 0) {
+      if (s[2] == ord::SRC_SELF) lrow_aggregate<T>(w, gt, c.aggregator);
+      else if (s[2] == ord::SRC_ATK) state_agg(c, a, k, gen, cp, ho, gt);
+      nlearn = a.severity > 0 ? a.severity : 0;
+      act = A_LEARN_FROM;
+      cpart = te;
+    }
+    if (a.epochs > 0) act = A_TRAIN_SELF, cpart = -1;
+    const int nsteps = nlearn + (a.epochs > 0 ? a.epochs : 0);
+    float loss = 0.f;
+    for (int st = 0; st < nsteps; ++st) {
+      float gs[T::A];
+      if (st < nlearn) {
+#pragma unroll
+        for (int q = 0; q < T::A; ++q) gs[q] = gt[q];
+      } else {
+        lrow_aggregate<T>(w, gs, c.aggregator);
+      }
+      loss = ltrain_step<T>(w, gs, a.lr);
+    }
+    R::quant(w);  // 4. respawn: the stored state decides (tests of big_soup_one)
+    float nz[8], lo[8], hi[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) nz[q] = 0.f, lo[q] = w[0], hi[q] = w[0];
+#pragma unroll
+    for (int i = 0; i < T::P; ++i) {
+      nz[i & 7] = fmaf(w[i], 0.f, nz[i & 7]);
+      lo[i & 7] = fminf(lo[i & 7], w[i]);
+      hi[i & 7] = fmaxf(hi[i & 7], w[i]);
+    }
+#pragma unroll
+    for (int q = 1; q < 8; ++q) nz[0] += nz[q], lo[0] = fminf(lo[0], lo[q]), hi[0] = fmaxf(hi[0], hi[q]);
+    const bool bad = !finitef(nz[0]);
+    const bool zero = !bad && (-a.eps <= lo[0]) && (hi[0] <= a.eps);
+    int8_t rsp = 0;
+    if ((a.flags & SRNN_F_REMOVE_DIVERGENT) && bad) rsp = 1;
+    else if ((a.flags & SRNN_F_REMOVE_ZERO) && zero) rsp = 2;
+    if (a.traj) R::store(R::at(a.traj, k), w);  // recording: the state before any respawn
+    if (rsp) R::init_row(R::at(a.W, k), rng(a), respawn_key(gen, k));  // E(k): a newborn
+    else R::store(R::at(a.W, k), w);                                      // E(k)
+    if (a.action) a.action[k] = act;
+    if (a.counterpart) a.counterpart[k] = cpart;
+    if (a.loss) a.loss[k] = loss;
+    if (a.respawn) a.respawn[k] = rsp;
+  }
+};
+// the run policy of k_ord_run: the chunk ids of the shuffled outputs in LDS (stride TBROW)
+template <class T, class S, bool SHUF>
+struct BigOrdPol {
+  struct Shared {
+    uint32_t cw[SHUF ? ChunkPerm<T>::NW * TBROW : 1];
+  };
+  __device__ static void turn(const SrnnCfg& c, const SrnnArgs& a, int64_t k, int32_t gen, Shared& sh, int64_t) {
+    BigOrd<T, S, SHUF>::turn(c, a, k, gen, ChunkPerm<T>{sh.cw + threadIdx.x});
+  }
+};
+// final rows (the last attack after a row's own turn, else its E version), the next
+// generation's lists, census of the stored rows, block stats (two-phase, as k_ord_close)
+template <class T, class S, bool SHUF>
+__global__ __launch_bounds__(TB) void k_ordbig_close(SrnnCfg c, SrnnArgs a) {
+  using R = BRow<T, S>;
+  using Dec = ord::OrdSched<1>::Dec;
+  __shared__ uint32_t s_cw[SHUF ? ChunkPerm<T>::NW * TBROW : 1];
+  const ChunkPerm<T> cp{s_cw + threadIdx.x};
+  const int64_t gb = blockIdx.x;
+  const int64_t r = gb * TB + threadIdx.x;
+  const int lane = threadIdx.x;
+  const int32_t gen = a.gen_ptr ? a.gen_ptr[0] : a.gen;
+  const bool census = !SHUF && (a.flags & SRNN_F_FUSED_CENSUS) != 0;
+  bool rs = false;
+  int8_t k = -1;
+  if (r < a.n) {
+    if (a.o_src[4 * r + 3] < 0) atomicOr(a.o_ctl + ord::ERRW, 4);  // never ran: a scheduling bug
+    float w[T::P];
+    const int64_t ja = ord::last_attacker_before(a, r, a.n);
+    a.heads[r] = SRNN_NIL;  // consumed: NIL for the generation after next
+    if (ja > r) {
+      BigOrd<T, S, SHUF>::load_version(c, a, ord::code_A(ja), gen, cp, w);
+      R::store(R::at(a.W, r), w);
+    } else {
+      R::load(R::at(a.W, r), w);
+    }
+    rs = a.respawn[r] != 0;
+    int64_t at, te;
+    Dec::decision(a, r, gen + 1, at, te);
+    if (at >= 0) Dec::link(a.heads_next, a.nexts_next, at, (uint32_t)r);
+    if (census) k = sclassify<T, S>(w, RowSummary<T>(w), a.eps, (a.flags & SRNN_F_FIX_SEC) != 0, c.aggregator);
+  }
+  if ((a.flags & SRNN_F_GEN_COUNTS) && gb == 0 && lane == 0) Dec::set_gen(a, gen + 1);
+  const unsigned long long m = __ballot(rs);
+  uint32_t cnt[5];
+#pragma unroll
+  for (int q = 0; q < 5; ++q) cnt[q] = (uint32_t)__popcll(__ballot(k == q));
+  if (lane == 0) {
+    unsigned long long* bs = reinterpret_cast<unsigned long long*>(a.temp);
+    unsigned long long* mine = bs + gb * 4;
+    mine[0] = m;
+    mine[1] = (unsigned long long)cnt[0] | ((unsigned long long)cnt[1] << 32);
+    mine[2] = (unsigned long long)cnt[2] | ((unsigned long long)cnt[3] << 32);
+    mine[3] = (unsigned long long)cnt[4];
+    if ((a.flags & SRNN_F_BORN_TOTAL) && m) atomicAdd(bs + ((a.n + TB - 1) / TB) * 4, (unsigned long long)__popcll(m));
+  }
+}
+// OP_SOUP_ORDERED of a big aggregating net (device): soup_ordered's launch sequence with this
+// family's run policy and close (no permutation table: an aggregating net's SGD step has one
+// sample); the finish (uids, census, counter) follows unless the caller batches it
+template <class T, class S, bool SHUF>
+int big_soup_ordered(const SrnnCfg& c, const SrnnArgs& a) {
+  if (a.world > 1 || a.lo != 0 || a.n_total != a.n || a.n >= (int64_t)(1 << 30)) {
+    set_error("ordered soup generation: one unsharded table of < 2^30 rows");
+    return -5;
+  }
+  if (!a.W || !a.W2 || !a.W3 || !a.o_src || !a.o_list || !a.o_ctl || !a.heads || !a.nexts || !a.heads_next ||
+      !a.nexts_next || !a.respawn || !(a.flags & SRNN_F_TWO_PHASE) || !a.temp) {
+    set_error("ordered soup generation needs W, W2, W3, o_src, o_list, o_ctl, both attack lists, respawn and "
+              "two-phase block stats (temp)");
+    return -5;
+  }
+  const int64_t nb = (a.n + TB - 1) / TB;
+  if (nb <= 0) return 0;
+  hipStream_t st = (hipStream_t)a.stream;
+  hipLaunchKernelGGL((k_ord_plan<1>), dim3((unsigned)nb), dim3(TB), 0, st, c, a);
+  hipLaunchKernelGGL((k_ord_mark<1>), dim3((unsigned)nb), dim3(TB), 0, st, c, a);
+  SrnnArgs ra = a;
+  const bool crit = knob(SRNN_KNOB_ORD_CRIT, 1) != 0;
+  if (crit) {
+    ra.flags |= SRNN_F_ORD_CRIT;
+    ra.x_groups = (int32_t)std::min<int64_t>(nb, (ord::rec_total(a.n) + TB - 1) / TB);
+  }
+  hipLaunchKernelGGL((k_ord_count<1>), dim3((unsigned)nb), dim3(TB), 0, st, c, ra);
+  hipLaunchKernelGGL((k_ord_run<BigOrdPol<T, S, SHUF>>), dim3((unsigned)(nb + (crit ? ra.x_groups : 0))), dim3(TB), 0,
+                     st, c, ra);
+  hipLaunchKernelGGL((k_ordbig_close<T, S, SHUF>), dim3((unsigned)nb), dim3(TB), 0, st, c, a);
+  if (!(a.flags & SRNN_F_GEN_COUNTS)) {
+    constexpr int FNT = SRNN_FINISH_NT;
+    hipLaunchKernelGGL((k_gen_finish<Weightwise<1, 1>, StF32, FNT>), dim3(1), dim3(FNT), 0, st, a, (int32_t)nb);
+  }
+  return 0;
+}
+
 // ops of the big nets that take any storage format / shuffler (everything a soup needs)
 template <class T, class S, bool SHUF>
 int big_run_s(int op, const SrnnCfg& c, const SrnnArgs& a) {
@@ -1770,6 +2058,11 @@ int big_run_s(int op, const SrnnCfg& c, const SrnnArgs& a) {
       break;
     }
     case OP_RESPAWN_SEQ: hipLaunchKernelGGL((k_big_respawn_seq<T, S>), dim3(1), dim3(TBR), 0, st, c, a); break;
+    case OP_SOUP_ORDERED: {
+      const int r = big_soup_ordered<T, S, SHUF>(c, a);
+      if (r) return r;
+      break;
+    }
     case OP_SOUP_DECIDE: {
       // decisions are shape independent: every global slot
       if (a.n_total <= 0) return 0;
@@ -1790,7 +2083,8 @@ int big_run_s(int op, const SrnnCfg& c, const SrnnArgs& a) {
 // true when big_run serves (op, storage, shuffler); the rest goes to the runtime-shape engine
 constexpr bool big_serves(int op, int dtype, int shuffler) {
   if (op == OP_INIT || op == OP_PERTURB || op == OP_RESPAWN || op == OP_APPLY || op == OP_CLASSIFY ||
-      op == OP_TRAIN || op == OP_LEARN || op == OP_SOUP_EVOLVE || op == OP_RESPAWN_SEQ || op == OP_SOUP_DECIDE)
+      op == OP_TRAIN || op == OP_LEARN || op == OP_SOUP_EVOLVE || op == OP_RESPAWN_SEQ || op == OP_SOUP_DECIDE ||
+      op == OP_SOUP_ORDERED)
     return true;
   return op == OP_RUN_FIXPOINT && dtype == 0 && shuffler == 0;
 }

@@ -151,48 +151,18 @@ SRNN_HD void collect(const SrnnArgs& a, int32_t code, int32_t* pr, int& np, bool
   }
 }
 
-template <class Net, class S>
-struct Ord {
-  using I = Item<Net, S>;
-  static constexpr int P = Net::P;
-  // recompute depth of the attack outputs: two nested outputs for the small nets, one for
-  // the rest (each level doubles the inlined forwards of a read)
-  static constexpr int RB = P <= 20 ? 2 : 1;
-
-  SRNN_HD static void read_version(const SrnnArgs& a, int32_t code, float* w) {
-    if (code >= 0) {
-      const int64_t j = code >> 1;
-      I::load((code & 1) ? I::rowp(a.W, j) : I::rowp(a.W3, j), w);
-    } else {
-      I::load(I::rowp(a.W2, (int64_t)(-(int64_t)code - 1)), w);
-    }
-  }
-
-  // version `code` into w: a stored version is loaded, an unstored attack output A(j) is
-  // recomputed as f_j(victim) from its own two reads (ap(x, t, o, j): the attack's forward)
-  template <int B, class AP>
-  SRNN_HD static void mat(const SrnnArgs& a, int32_t code, float* w, const AP& ap) {
-    if constexpr (B > 0) {
-      if (is_A(code) && !stored(a, code >> 1)) {
-        const int64_t j = code >> 1;
-        const int32_t* sj = src_of(a, j);
-        float x[P], t[P];
-        mat<B - 1>(a, sj[0], x, ap);
-        if (sj[1] == SRC_SELF) I::copy(t, x);
-        else mat<B - 1>(a, sj[1], t, ap);
-        ap(x, t, w, j);
-        I::q(w);
-        return;
-      }
-    }
-    read_version(a, code, w);
-  }
+// the schedule of a generation for recompute depth RB (shape independent: decisions, version
+// codes, the stored-output marks and the producer lists of the turns)
+template <int RB_>
+struct OrdSched {
+  static constexpr int RB = RB_;
+  using Dec = Item<Weightwise<1, 1>, StF32>;  // decisions are shape independent
 
   // src codes of turn k (generation gen) -> o_src[k] = {own, victim, teacher, level = -1};
   // its stored flag cleared, its consumer list emptied, no record
   SRNN_HD static void plan(const SrnnArgs& a, int64_t k, int32_t gen) {
     int64_t at, te;
-    I::decision(a, k, gen, at, te);
+    Dec::decision(a, k, gen, at, te);
     int32_t* s = a.o_src + 4 * k;
     s[0] = latest(a, k, k);
     s[1] = at < 0 ? SRC_NONE : at == k ? SRC_SELF : latest(a, at, k);
@@ -225,6 +195,50 @@ struct Ord {
     if (needs_A(a, k, s) && is_row(s[1])) collect<RB>(a, s[1], pr, np, bad);
     if (is_row(s[2])) collect<RB>(a, s[2], pr, np, bad);
     return np;
+  }
+};
+
+// recompute depth of the attack outputs: two nested outputs for the small nets, one for the rest
+// (each level doubles the inlined forwards of a read; the big aggregating nets: srnn_bignet.h)
+template <class Net>
+constexpr int ord_rb() {
+  return Net::P <= 20 ? 2 : 1;
+}
+
+template <class Net, class S>
+struct Ord : OrdSched<ord_rb<Net>()> {
+  using I = Item<Net, S>;
+  using Sched = OrdSched<ord_rb<Net>()>;
+  static constexpr int P = Net::P;
+  static constexpr int RB = Sched::RB;
+
+  SRNN_HD static void read_version(const SrnnArgs& a, int32_t code, float* w) {
+    if (code >= 0) {
+      const int64_t j = code >> 1;
+      I::load((code & 1) ? I::rowp(a.W, j) : I::rowp(a.W3, j), w);
+    } else {
+      I::load(I::rowp(a.W2, (int64_t)(-(int64_t)code - 1)), w);
+    }
+  }
+
+  // version `code` into w: a stored version is loaded, an unstored attack output A(j) is
+  // recomputed as f_j(victim) from its own two reads (ap(x, t, o, j): the attack's forward)
+  template <int B, class AP>
+  SRNN_HD static void mat(const SrnnArgs& a, int32_t code, float* w, const AP& ap) {
+    if constexpr (B > 0) {
+      if (is_A(code) && !stored(a, code >> 1)) {
+        const int64_t j = code >> 1;
+        const int32_t* sj = src_of(a, j);
+        float x[P], t[P];
+        mat<B - 1>(a, sj[0], x, ap);
+        if (sj[1] == SRC_SELF) I::copy(t, x);
+        else mat<B - 1>(a, sj[1], t, ap);
+        ap(x, t, w, j);
+        I::q(w);
+        return;
+      }
+    }
+    read_version(a, code, w);
   }
 
   // turn k: the serial loop's particle step (soup_seq_one) reading the versions of its plan
@@ -392,29 +406,30 @@ __device__ __forceinline__ void publish(const SrnnArgs& a, int64_t k, int32_t& r
 
 }  // namespace ord
 
-template <class Net, class S>
+// (plan / mark / count: shape independent, one instantiation per recompute depth)
+template <int RB>
 __global__ __launch_bounds__(TB) void k_ord_plan(SrnnCfg, SrnnArgs a) {
   const int64_t k = (int64_t)blockIdx.x * TB + threadIdx.x;
   // control words for the next launches (the error word is sticky: never cleared here)
   if (blockIdx.x == 0)
     for (int w = threadIdx.x; w < ord::CTL_WORDS; w += TB)
       if (w != ord::ERRW) a.o_ctl[w] = 0;
-  if (k < a.n) ord::Ord<Net, S>::plan(a, k, Item<Net, S>::gen_of(a));
+  if (k < a.n) ord::OrdSched<RB>::plan(a, k, a.gen_ptr ? a.gen_ptr[0] : a.gen);
 }
 
-template <class Net, class S>
+template <int RB>
 __global__ __launch_bounds__(TB) void k_ord_mark(SrnnCfg, SrnnArgs a) {
   const int64_t k = (int64_t)blockIdx.x * TB + threadIdx.x;
-  if (k < a.n) ord::Ord<Net, S>::mark(a, k);
+  if (k < a.n) ord::OrdSched<RB>::mark(a, k);
 }
 
 // every turn counts its producers; a turn with producers becomes a pending record of this
 // workgroup's partition (producers written straight into the record, deduplicated) and is
 // pushed onto each producer's consumer list.  No turn runs here, so every list is complete
 // before k_ord_run walks any of them.
-template <class Net, class S>
+template <int RB>
 __global__ __launch_bounds__(TB) void k_ord_count(SrnnCfg, SrnnArgs a) {
-  using O = ord::Ord<Net, S>;
+  using O = ord::OrdSched<RB>;
   const int lane = threadIdx.x;
   const int64_t k = (int64_t)blockIdx.x * TB + lane;
   const bool valid = k < a.n;
@@ -504,19 +519,27 @@ __device__ __forceinline__ int64_t ord_crit_at(const SrnnArgs& a, int64_t g, int
 // row several turns read does not run those turns one after another -- each run as a
 // continuation (raised priority, permutations from the table) at level 1 + its deepest
 // producer's.  The wave ends when no lane has a ready record left.
+// (Pol: the turn of a net family and its LDS -- OrdLanePol below, the big aggregating nets'
+// in srnn_bignet.h; the schedule itself is shape independent)
 template <class Net, class S>
+struct OrdLanePol {
+  static constexpr int SAMP = samp_slots<Net>();
+  static constexpr int PERM = (Net::P + 4) & ~3;
+  struct Shared {
+    float4 samp[TB * SAMP];
+    uint8_t perm[TB * PERM];
+  };
+  __device__ static void turn(const SrnnCfg& c, const SrnnArgs& a, int64_t k, int32_t gen, Shared& sh, int64_t prow) {
+    const int lane = threadIdx.x;
+    ord::Ord<Net, S>::turn(c, a, k, gen, samp_lane<Net>(sh.samp, lane), sh.perm + lane * PERM, prow);
+  }
+};
+template <class Pol>
 __global__ __launch_bounds__(TB) void k_ord_run(SrnnCfg c, SrnnArgs a) {
-  using I = Item<Net, S>;
-  using O = ord::Ord<Net, S>;
-  constexpr int SAMP = samp_slots<Net>();
-  constexpr int PERM = (Net::P + 4) & ~3;
-  __shared__ float4 s_samp[TB * SAMP];
-  __shared__ uint8_t s_perm[TB * PERM];
+  __shared__ typename Pol::Shared s_sh;
   __shared__ int32_t s_q[TB];
   const int lane = threadIdx.x;
-  const int32_t gen = I::gen_of(a);
-  float4* samp = samp_lane<Net>(s_samp, lane);
-  uint8_t* perm = s_perm + lane * PERM;
+  const int32_t gen = a.gen_ptr ? a.gen_ptr[0] : a.gen;
   int64_t cur = -1, prow = -1;
   bool raised = false;
   // with the critical list: its waves first (the grid's first a.x_groups workgroups), at raised
@@ -541,7 +564,7 @@ __global__ __launch_bounds__(TB) void k_ord_run(SrnnCfg c, SrnnArgs a) {
   for (;;) {
     if (cur >= 0) {
       const uint64_t t0 = a.o_trace ? __builtin_amdgcn_s_memrealtime() : 0;
-      O::turn(c, a, cur, gen, samp, perm, prow);
+      Pol::turn(c, a, cur, gen, s_sh, prow);
       ord::publish(a, cur, ready, nready);
       if (a.o_trace) {
         a.o_trace[2 * cur] = t0;
@@ -731,8 +754,8 @@ int soup_ordered(const SrnnCfg& c, const SrnnArgs& a) {
   const int64_t nb = (a.n + TB - 1) / TB;
   if (nb <= 0) return 0;
   hipStream_t st = (hipStream_t)a.stream;
-  hipLaunchKernelGGL((k_ord_plan<Net, S>), dim3((unsigned)nb), dim3(TB), 0, st, c, a);
-  hipLaunchKernelGGL((k_ord_mark<Net, S>), dim3((unsigned)nb), dim3(TB), 0, st, c, a);
+  hipLaunchKernelGGL((k_ord_plan<O::RB>), dim3((unsigned)nb), dim3(TB), 0, st, c, a);
+  hipLaunchKernelGGL((k_ord_mark<O::RB>), dim3((unsigned)nb), dim3(TB), 0, st, c, a);
   SrnnArgs ra = a;
   const bool crit = knob(SRNN_KNOB_ORD_CRIT, 1) != 0;
   if (crit) {
@@ -741,7 +764,7 @@ int soup_ordered(const SrnnCfg& c, const SrnnArgs& a) {
     // record's producer slot; the launch's waves past its end return at once
     ra.x_groups = (int32_t)std::min<int64_t>(nb, (ord::rec_total(a.n) + TB - 1) / TB);
   }
-  hipLaunchKernelGGL((k_ord_count<Net, S>), dim3((unsigned)nb), dim3(TB), 0, st, c, ra);
+  hipLaunchKernelGGL((k_ord_count<O::RB>), dim3((unsigned)nb), dim3(TB), 0, st, c, ra);
   if constexpr (Net::KIND == 0 && Net::P <= 16) {
     const int32_t E = (a.severity > 0 ? a.severity : 0) + (a.epochs > 0 ? a.epochs : 0);
     if (a.ptab && (a.flags & SRNN_F_SHUFFLE) && E > 0) {
@@ -750,7 +773,7 @@ int soup_ordered(const SrnnCfg& c, const SrnnArgs& a) {
                          dim3(TB), 0, st, a, E);
     }
   }
-  hipLaunchKernelGGL((k_ord_run<Net, S>), dim3((unsigned)(nb + (crit ? ra.x_groups : 0))), dim3(TB), 0, st, c, ra);
+  hipLaunchKernelGGL((k_ord_run<OrdLanePol<Net, S>>), dim3((unsigned)(nb + (crit ? ra.x_groups : 0))), dim3(TB), 0, st, c, ra);
   hipLaunchKernelGGL((k_ord_close<Net, S>), dim3((unsigned)nb), dim3(TB), 0, st, c, a);
   if (!(a.flags & SRNN_F_GEN_COUNTS)) {
     constexpr int FNT = SRNN_FINISH_NT;

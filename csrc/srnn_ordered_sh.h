@@ -274,9 +274,9 @@ int soup_ordered_sh(const SrnnCfg& c, const SrnnArgs& a) {
   const unsigned nb = (unsigned)((a.n + TB - 1) / TB), nbo = (unsigned)std::max<int64_t>((own + TB - 1) / TB, 1);
   switch (phase) {
     case ordsh::PLAN:
-      hipLaunchKernelGGL((k_ord_plan<Net, S>), dim3(nb), dim3(TB), 0, st, c, a);
-      hipLaunchKernelGGL((k_ord_mark<Net, S>), dim3(nb), dim3(TB), 0, st, c, a);
-      hipLaunchKernelGGL((k_ord_count<Net, S>), dim3(nb), dim3(TB), 0, st, c, a);
+      hipLaunchKernelGGL((k_ord_plan<O::RB>), dim3(nb), dim3(TB), 0, st, c, a);
+      hipLaunchKernelGGL((k_ord_mark<O::RB>), dim3(nb), dim3(TB), 0, st, c, a);
+      hipLaunchKernelGGL((k_ord_count<O::RB>), dim3(nb), dim3(TB), 0, st, c, a);
       hipLaunchKernelGGL((k_ordsh_levels<Net, S>), dim3(nb), dim3(TB), 0, st, a);
       break;
     case ordsh::LEVEL:

@@ -10,14 +10,10 @@ export TMPDIR=/tmp
 TAG=${1:-round}
 step() { local name=$1 lim=$2; shift 2; timeout -k 10 $lim "$@" > gpurun_out/${name}_$TAG.log 2>&1; local rc=$?;
          echo "[$name rc=$rc] $(tail -1 gpurun_out/${name}_$TAG.log | cut -c1-600)"; return $rc; }
-timeout -k 10 600 python -u -m pytest tests/test_sharded_multirank_gpu.py tests/test_sharded_gpu.py tests/test_bench_contract_gpu.py -m gpu -x -q --timeout 200 --timeout-method thread > gpurun_out/pytest_$TAG.log 2>&1
+timeout -k 10 900 python -u -m pytest tests/test_ordered_bignet_gpu.py tests/test_ordered_soup.py tests/test_ordered_sharded_gpu.py tests/test_exact_oracle_gpu.py tests/test_bignet_gpu.py tests/test_sharded_multirank_gpu.py -m gpu -x -v --timeout 300 --timeout-method thread > gpurun_out/pytest_$TAG.log 2>&1
 rc=$?; tail -2 gpurun_out/pytest_$TAG.log; [ $rc -eq 0 ] || exit $rc
-# strong-scaling model of one rank of N (forced-sharded, remote fraction emulated), kernel traces
-for NR in 8:12500:0.164 4:25000:0.141 2:50000:0.093; do
-  IFS=: read R NP FR <<< "$NR"
-  SRNN_X2_EMULATE_REMOTE=$FR step xprof${R} 300 rocprofv3 --kernel-trace --stats -d gpurun_out/xprof${R}_$TAG -o x --output-format csv -- python3 bench.py --steps 20 --warmup 5 --force-sharded --particles $NP --reference-order-steps 0 || exit 1
-  SRNN_X2_EMULATE_REMOTE=$FR step strong${R} 300 python bench.py --steps 20 --warmup 5 --force-sharded --particles $NP --reference-order-steps 0 || exit 1
-  SRNN_X2_EMULATE_REMOTE=$FR step strong${R}b 300 python bench.py --steps 20 --warmup 5 --force-sharded --particles $NP --reference-order-steps 0 || exit 1
-done
+step c4s 600 python bench/configs.py --only 4s --n4s 1000000 --gens4s 5 || exit 1
 step b20 300 python bench.py --steps 20 --warmup 5 || exit 1
+SRNN_ORDSH_EMULATE=8 step em8_seq 300 python bench.py --steps 10 --warmup 2 --force-sharded --order sequential || exit 1
+step prof_c4s 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_c4s_$TAG -o t --output-format csv -- python3 bench/configs.py --only 4s --n4s 1000000 --gens4s 3 --order4s sequential || exit 1
 echo done

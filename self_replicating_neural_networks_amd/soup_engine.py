@@ -402,11 +402,12 @@ class SoupEngine:
         (srnn_ordered_sh.h): every rank plans all n_total turns and keeps the version tables of
         all rows (E rows, stored attack outputs) next to the gathered generation-start table."""
         dev_side = self.device.type != "cpu"
-        if self.generic or not _lib.supports(self.spec, _lib.OP_SOUP_ORDERED, dev_side, self.dtype_code):
+        if not _lib.supports(self.spec, _lib.OP_SOUP_ORDERED, dev_side, self.dtype_code):
             raise NotImplementedError(
-                f"no level-scheduled reference-order generation for {self.spec}: it exists for the "
-                "lane-per-particle template shapes; SequentialSoupEngine runs the same order for any shape on the "
-                "host, SoupEngine(order='synchronous') any shape on the device")
+                f"no scheduled reference-order generation for {self.spec} on {self.device.type}: it exists for "
+                "the lane-per-particle template shapes (host and device) and the big aggregating nets (device, "
+                "csrc/srnn_bignet.h); SequentialSoupEngine runs the same order for any shape on the host, "
+                "SoupEngine(order='synchronous') any shape on the device")
         sharded = self.dist.enabled
         N = self.n_total if sharded else self.n  # turns planned on this rank
         if N > ORDERED_MAX_ROWS:
