@@ -49,6 +49,8 @@ enum SrnnFlag : uint32_t {
                                      // exchange chain wins the SIMDs it shares with the local evolve)
   SRNN_F_ORD_CRIT = 1u << 22,        // ordered run: turns in the run order of k_ord_order (internal: set by
                                      // the library from SRNN_KNOB_ORD_CRIT)
+  SRNN_F_ORD_QUEUE = 1u << 24,       // ordered run: continuations through the generation's ready queue
+                                     // (internal: set by the library from SRNN_KNOB_ORD_QUEUE)
   SRNN_F_PTAB_READY = 1u << 23,      // ptab already holds this generation's permutations (built by the
                                      // sharded pack): the generation launch does not rebuild them
 };
@@ -157,9 +159,11 @@ struct SrnnArgs {
   float* W3;            // [n][pp] attack outputs A(k) of this generation
   int32_t* o_src;       // [n][4] source versions of each turn's reads + its level | [n] stored-attack
                         // flags | [n] consumer-list heads | [ord::rec_total(n)][32] pending records |
-                        // [ord::rec_total(n)] run order of the turns without producers
+                        // [ord::rec_total(n)] critical list (producers of later turns) |
+                        // [ord::rec_total(n)] ready queue (records in the order they became ready)
   int32_t* o_list;      // [n] the pending record of each turn (-1: no producer)
-  int32_t* o_ctl;       // [ord::CTL_WORDS = 163] record / critical-list counts per partition, pending turns, max level
+  int32_t* o_ctl;       // [ord::CTL_WORDS = 165] record / critical-list counts per partition, ready-queue
+                        // head and tail, max level
                         // (host), error bits (sticky: the plan kernel clears every word but that one)
   int32_t o_levels;     // dependency levels the host path reports one by one (1..16; the device
                         // schedules turns by continuation, not by level)
@@ -209,7 +213,7 @@ enum SrnnOp {
                            // (srnn_ordered_sh.h)
 };
 
-int srnn_abi_version();  // 25
+int srnn_abi_version();  // 26
 int64_t srnn_args_size();  // sizeof(SrnnArgs): the ctypes mirror checks its layout against it
 int64_t srnn_cfg_size();
 int srnn_has_config(const SrnnCfg* cfg);
@@ -233,7 +237,9 @@ enum SrnnKnob {
   SRNN_KNOB_SOUP_LANES = 7,     // SRNN_SOUP_LANES: lanes per particle of WW(2,2) soup generations (0 = by size)
   SRNN_KNOB_ORD_CRIT = 8,       // SRNN_ORD_CRIT: reference-order generations run the producers of later turns
                                 // first, at raised wave priority (default 1)
-  SRNN_KNOB_COUNT = 9
+  SRNN_KNOB_ORD_QUEUE = 9,      // SRNN_ORD_QUEUE: reference-order continuations through one ready queue
+                                //   (1, default) or run by the producers' waves (0)
+  SRNN_KNOB_COUNT = 10
 };
 void srnn_set_knob(int knob, int value);
 int srnn_get_knob(int knob);

@@ -2018,6 +2018,7 @@ int big_soup_ordered(const SrnnCfg& c, const SrnnArgs& a) {
   hipLaunchKernelGGL((k_ord_mark<1>), dim3((unsigned)nb), dim3(TB), 0, st, c, a);
   SrnnArgs ra = a;
   const bool crit = knob(SRNN_KNOB_ORD_CRIT, 1) != 0;
+  if (knob(SRNN_KNOB_ORD_QUEUE, 1) != 0) ra.flags |= SRNN_F_ORD_QUEUE;
   if (crit) {
     ra.flags |= SRNN_F_ORD_CRIT;
     ra.x_groups = (int32_t)std::min<int64_t>(nb, (ord::rec_total(a.n) + TB - 1) / TB);

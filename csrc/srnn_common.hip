@@ -113,7 +113,8 @@ static int dispatch_special(int op, const SrnnCfg* c, const SrnnArgs* a) {
 namespace {
 const char* const g_knob_env[SRNN_KNOB_COUNT] = {"SRNN_FORCE_GENERIC", "SRNN_RNN_WAVE", "SRNN_RNN_SPEC",
                                                  "SRNN_RNN_SOUP",      "SRNN_WW_WAVE",  "SRNN_BIG_WAVE",
-                                                 "SRNN_FIX_GROUP",     "SRNN_SOUP_LANES", "SRNN_ORD_CRIT"};
+                                                 "SRNN_FIX_GROUP",     "SRNN_SOUP_LANES", "SRNN_ORD_CRIT",
+                                                 "SRNN_ORD_QUEUE"};
 int g_knob[SRNN_KNOB_COUNT] = {-1, -1, -1, -1, -1, -1, -1, -1, -1};
 }  // namespace
 namespace srnn {
@@ -201,7 +202,7 @@ static int with_scratch(int op, const SrnnCfg* c, const SrnnArgs* a) {
 
 extern "C" {
 
-int srnn_abi_version() { return 25; }
+int srnn_abi_version() { return 26; }
 
 
 // layout check of the ctypes mirror (ops/_lib.py): sizeof(SrnnArgs) / sizeof(SrnnCfg)

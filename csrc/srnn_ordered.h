@@ -69,11 +69,15 @@ constexpr int MAXLW = 17, ERRW = 18;
 // b = p mod NPART, appended by one counter each: no chip-wide contended counter)
 constexpr int NPART = 64, PART0 = 2 * MAX_LEVELS + 3;
 constexpr int CRIT0 = PART0 + NPART;
-constexpr int CTL_WORDS = CRIT0 + NPART;
+// [QH], [QT]: head / tail of the generation's ready queue (SRNN_F_ORD_QUEUE)
+constexpr int QH = CRIT0 + NPART, QT = QH + 1;
+constexpr int CTL_WORDS = QT + 1;
 // o_src layout: [n][4] {own, victim, teacher, level} | [n] stored flags of A(j) | [n] consumer-list
 // heads (pending records reading E(j) / A(j), EMPTY-terminated) | [rec_total(n)][REC] pending
 // records | [rec_total(n)] the critical list (producers of later turns; partition p: the producers
-// of blocks b = p mod NPART, rec_cap(n) slots); o_list: [n] the record of each pending turn (-1: none)
+// of blocks b = p mod NPART, rec_cap(n) slots) | [rec_total(n)] the ready queue (records whose
+// producers are all done, in the order they became ready; EMPTY until written);
+// o_list: [n] the record of each pending turn (-1: none)
 constexpr int NPROD = 12;  // producers of one turn: 3 reads x 2^RB leaves
 constexpr int REC = 32;    // record words: {turn, np, producers[NPROD], count, ready-next, next[NPROD], -}
 constexpr int R_PROD = 2, R_CNT = R_PROD + NPROD, R_RDY = R_CNT + 1, R_NEXT = R_RDY + 1;
@@ -112,6 +116,7 @@ SRNN_HD int64_t rec_cap(int64_t n) { return ((n + TB - 1) / TB + NPART - 1) / NP
 SRNN_HD int64_t rec_total(int64_t n) { return NPART * rec_cap(n); }
 SRNN_HD bool stored(const SrnnArgs& a, int64_t j) { return a.o_src[4 * a.n + j] != 0; }
 SRNN_HD int32_t* run_order(const SrnnArgs& a) { return a.o_src + 6 * a.n + REC * rec_total(a.n); }
+SRNN_HD int32_t* ready_queue(const SrnnArgs& a) { return a.o_src + 6 * a.n + (REC + 1) * rec_total(a.n); }
 // turn k computes A(k): it attacked, and the attack output is its own row (self-attack),
 // its teacher (learn_from the victim) or read by a turn past the recompute depth
 SRNN_HD bool needs_A(const SrnnArgs& a, int64_t k, const int32_t* s) {
@@ -414,7 +419,10 @@ __global__ __launch_bounds__(TB) void k_ord_plan(SrnnCfg, SrnnArgs a) {
   if (blockIdx.x == 0)
     for (int w = threadIdx.x; w < ord::CTL_WORDS; w += TB)
       if (w != ord::ERRW) a.o_ctl[w] = 0;
-  if (k < a.n) ord::OrdSched<RB>::plan(a, k, a.gen_ptr ? a.gen_ptr[0] : a.gen);
+  if (k < a.n) {
+    ord::OrdSched<RB>::plan(a, k, a.gen_ptr ? a.gen_ptr[0] : a.gen);
+    ord::ready_queue(a)[k] = ord::EMPTY;  // (at most one queue entry per pending turn: < n)
+  }
 }
 
 template <int RB>
@@ -571,6 +579,60 @@ __global__ __launch_bounds__(TB) void k_ord_run(SrnnCfg c, SrnnArgs a) {
         a.o_trace[2 * cur + 1] = __builtin_amdgcn_s_memrealtime();
       }
     }
+    if (a.flags & SRNN_F_ORD_QUEUE) {
+      // the generation's ready queue: this wave's ready records are appended (one counter add per
+      // wave), then the wave claims up to TB entries, whoever made them ready -- every
+      // continuation round runs a full wave of turns instead of the few its own producers freed.
+      // A record is appended by a wave that claims afterwards, so none is left behind when the
+      // others have left; a claimed slot is written right after its tail add (the spin is short).
+      int32_t* qa = ord::ready_queue(a);
+      const int32_t total = ord::wave_sum(nready);
+      if (total) {
+        int32_t pre = nready;
+#pragma unroll
+        for (int off = 1; off < 64; off <<= 1) {
+          const int32_t v = __shfl_up(pre, off);
+          if (lane >= off) pre += v;
+        }
+        pre -= nready;
+        int32_t base = 0;
+        if (lane == 0) base = __hip_atomic_fetch_add(a.o_ctl + ord::QT, total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        base = __shfl(base, 0);
+        for (int32_t t = base + pre; nready > 0; ++t) {
+          ord::st_level(qa + t, ready);
+          ready = ord::pend(a, ready)[ord::R_RDY];
+          --nready;
+        }
+      }
+      int32_t qb = 0, m = 0;
+      if (lane == 0) {
+        for (;;) {
+          int32_t h = ord::ld_level(a.o_ctl + ord::QH);
+          const int32_t avail = ord::ld_level(a.o_ctl + ord::QT) - h;
+          if (avail <= 0) break;
+          const int32_t want = avail < TB ? avail : TB;
+          if (__hip_atomic_compare_exchange_strong(a.o_ctl + ord::QH, &h, h + want, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                   __HIP_MEMORY_SCOPE_AGENT)) {
+            qb = h;
+            m = want;
+            break;
+          }
+        }
+      }
+      qb = __shfl(qb, 0);
+      m = __shfl(m, 0);
+      if (m == 0) break;
+      cur = -1;
+      prow = -1;
+      if (lane < m) {
+        int32_t q;
+        while ((q = ord::ld_level(qa + qb + lane)) == ord::EMPTY) __builtin_amdgcn_s_sleep(1);
+        prow = q;
+      }
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if (lane < m) cur = ord::pend(a, prow)[0];
+    } else {
     // the wave's ready records, one per lane (the rest stay in their lists for the next round)
     const int32_t total = ord::wave_sum(nready);
     if (total == 0) break;
@@ -599,6 +661,7 @@ __global__ __launch_bounds__(TB) void k_ord_run(SrnnCfg c, SrnnArgs a) {
     // the producers' rows (released before their decrements) are visible after this
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
     if (!raised) {
       __builtin_amdgcn_s_setprio(2);
       raised = true;
@@ -758,6 +821,7 @@ int soup_ordered(const SrnnCfg& c, const SrnnArgs& a) {
   hipLaunchKernelGGL((k_ord_mark<O::RB>), dim3((unsigned)nb), dim3(TB), 0, st, c, a);
   SrnnArgs ra = a;
   const bool crit = knob(SRNN_KNOB_ORD_CRIT, 1) != 0;
+  if (knob(SRNN_KNOB_ORD_QUEUE, 1) != 0) ra.flags |= SRNN_F_ORD_QUEUE;
   if (crit) {
     ra.flags |= SRNN_F_ORD_CRIT;
     // critical-list waves of the run launch: the list holds at most one entry per pending

@@ -307,7 +307,7 @@ static void seq_soup(const SrnnCfg& c, int64_t n, int steps) {
 }
 
 int main() {
-  CHECK(srnn_abi_version() == 25);
+  CHECK(srnn_abi_version() == 26);
   seq_soup(ww22(), 257, 4);
   seq_soup(agg422(), 129, 3);
   ops_smoke(ww22(), 1000);

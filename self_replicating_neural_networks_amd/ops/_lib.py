@@ -20,7 +20,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 # SRNN_LIB: load another build of the library (A/B of compiler flags on the GPU box)
 LIB_PATH = os.environ.get("SRNN_LIB") or os.path.join(_HERE, "libsrnn.so")
 CSRC = os.path.normpath(os.path.join(_HERE, "..", "..", "csrc"))
-ABI_VERSION = 25
+ABI_VERSION = 26
 
 # SrnnOp (csrc/srnn_abi.h)
 OP_INIT = 0
@@ -44,7 +44,7 @@ OP_X2_POST = 21   # sharded soup: uids, census, received notices / requests
 OP_SOUP_ORDERED = 22  # reference-order (sequential) generation, DAG-scheduled (csrc/srnn_ordered.h)
 OP_SOUP_ORDERED_SH = 23  # one phase of a sharded reference-order generation (csrc/srnn_ordered_sh.h)
 ORDSH_PLAN, ORDSH_LEVEL, ORDSH_PACK, ORDSH_UNPACK, ORDSH_CLOSE, ORDSH_LINK = range(6)
-ORD_CTL_WORDS = 163   # o_ctl words of an ordered generation (csrc/srnn_ordered.h)
+ORD_CTL_WORDS = 165   # o_ctl words of an ordered generation (csrc/srnn_ordered.h)
 ORD_MAXLW, ORD_ERRW = 17, 18
 ORD_NPART = 64        # partitions of the pending records
 ORD_REC = 32          # int32 words per pending record
@@ -53,9 +53,9 @@ ORD_MAX_LEVELS = 16   # dependency levels reported one by one (deeper: one bin)
 
 def ord_src_words(n: int) -> int:
     """int32 words of an n-turn ordered generation's o_src: [n][4] codes + level, [n] stored flags,
-    [n] consumer-list heads, the pending records, the run order of the turns without producers."""
+    [n] consumer-list heads, the pending records, the critical list, the ready queue."""
     n = max(int(n), 1)
-    return 6 * n + (ORD_REC + 1) * ord_rec_total(n)
+    return 6 * n + (ORD_REC + 2) * ord_rec_total(n)
 
 
 def ord_rec_total(n: int) -> int:
@@ -250,10 +250,11 @@ def supports(spec, op: int, device: bool, dtype: int = DTYPE_FP32) -> bool:
 # execution knobs (csrc/srnn_abi.h SrnnKnob; config.py ExecConfig): the environment variable
 # of a knob, when set, overrides what is set here
 KNOBS = {"force_generic": 0, "rnn_wave": 1, "rnn_spec": 2, "rnn_soup": 3, "ww_wave": 4, "big_wave": 5,
-         "fix_group": 6, "soup_lanes": 7, "ord_crit": 8}
+         "fix_group": 6, "soup_lanes": 7, "ord_crit": 8, "ord_queue": 9}
 KNOB_ENV = {"force_generic": "SRNN_FORCE_GENERIC", "rnn_wave": "SRNN_RNN_WAVE", "rnn_spec": "SRNN_RNN_SPEC",
             "rnn_soup": "SRNN_RNN_SOUP", "ww_wave": "SRNN_WW_WAVE", "big_wave": "SRNN_BIG_WAVE",
-            "fix_group": "SRNN_FIX_GROUP", "soup_lanes": "SRNN_SOUP_LANES", "ord_crit": "SRNN_ORD_CRIT"}
+            "fix_group": "SRNN_FIX_GROUP", "soup_lanes": "SRNN_SOUP_LANES", "ord_crit": "SRNN_ORD_CRIT",
+            "ord_queue": "SRNN_ORD_QUEUE"}
 
 
 def set_knob(name: str, value: int) -> None:
