@@ -1588,21 +1588,33 @@ __device__ __forceinline__ int8_t big_soup_one(const SrnnCfg& c, const SrnnArgs&
   const int64_t g = a.lo + j;
   const int32_t gen = a.gen_ptr ? a.gen_ptr[0] : a.gen;
   const bool x2 = (a.flags & SRNN_F_X2) != 0;
-  // the own row stays a per-lane load (the generation is SGD-bound: staging it through LDS
-  // measured slower, profiles/r2j_staged_rows_finish_par.md)
+  // Attacks received: after the first one the victim's row is chunk-constant (its shuffled form:
+  // a permutation of the chunk values), so the victim is carried as its 4-value state h and the
+  // row registers hold only the current attacker's row; the victim's row is defined ONCE after the
+  // attacks (expanded from h, or its generation-start row), so no 280-float array is carried
+  // through the attack loop.  The same arithmetic: the aggregate of expand'(h) is h exactly
+  // (shuffled: aggregate_out, the materialised vector's sums).
   float w[T::P];
-  R::load(R::at(a.W2, j), w);
+  float h[T::A];
+  bool attacked = false;
   uint32_t ctr = (uint32_t)gen * 1024u;
   for_each_attacker<false>(a, j, [&](uint32_t e, int64_t slot) {
-    float gv[T::A], h[T::A];
-    lrow_aggregate<T>(w, gv, c.aggregator);
+    float gv[T::A];
+    if (!attacked) {
+      R::stream_aggregate(R::at(a.W2, j), gv, c.aggregator);
+    } else if constexpr (SHUF) {
+      aggregate_out<T, SHUF>(h, gv, c.aggregator, cp);  // cp: the previous attack's permutation
+    } else {
+#pragma unroll
+      for (int q = 0; q < T::A; ++q) gv[q] = h[q];
+    }
     const char* r = ent_row(a, e, R::RB);
     if (x2 && (int64_t)e >= a.n) x2_check(a, r, R::RB, slot, gen);
     R::load(r, w);
     lmlp<T>(w, gv, h);
     R::quant_a(h);
     if constexpr (SHUF) cp.draw(rng, (uint64_t)g, ctr);
-    expand_out<T, SHUF>(w, h, cp);
+    attacked = true;
     ctr += 1;
   });
   int64_t my_at, te;
@@ -1623,6 +1635,10 @@ __device__ __forceinline__ int8_t big_soup_one(const SrnnCfg& c, const SrnnArgs&
     act = A_LEARN_FROM;
     cpart = te;
   }
+  // the own row (the generation is SGD-bound: a per-lane load; staging it through LDS measured
+  // slower, profiles/r2j_staged_rows_finish_par.md)
+  if (attacked) expand_out<T, SHUF>(w, h, cp);
+  else R::load(R::at(a.W2, j), w);
   if (a.epochs > 0) act = A_TRAIN_SELF, cpart = -1;
   const int nsteps = nlearn + (a.epochs > 0 ? a.epochs : 0);
   float loss = 0.f;
@@ -1673,36 +1689,45 @@ __global__ __launch_bounds__(TBROW) void k_big_soup_evolve(SrnnCfg c, SrnnArgs a
   __shared__ uint32_t s_cw[SHUF ? ChunkPerm<T>::NW * TBROW : 1];
   const ChunkPerm<T> cp{s_cw + threadIdx.x};
   const bool x2 = (a.flags & SRNN_F_X2) != 0;
+  const bool remote = x2 && (a.flags & SRNN_F_X2_REMOTE);
   unsigned long long* bs = reinterpret_cast<unsigned long long*>(a.temp);
-  if (x2 && (a.flags & SRNN_F_X2_REMOTE)) {
-    const int64_t cnt = *(volatile const int32_t*)a.x_rcount;
-    for (int64_t q = (int64_t)blockIdx.x * TBROW + threadIdx.x; q - threadIdx.x < cnt;
-         q += (int64_t)gridDim.x * TBROW) {
-      if (q < cnt) {
-        const int64_t j = a.x_rlist[2 * q];
-        const bool rs = big_soup_one<T, S, SHUF>(c, a, cp, j, a.x_rlist[2 * q + 1]) != 0;
-        bs_publish_lane(bs, j, rs, -1);
-      }
+  // ONE call site of the inlined particle step for both forms (two inlined copies doubled the
+  // kernel's code: 19.6k vs 13.6k lines of ISA)
+  const int64_t cnt = remote ? (int64_t) * (volatile const int32_t*)a.x_rcount : 0;
+  int64_t q = (int64_t)blockIdx.x * TBROW + threadIdx.x;
+  for (;;) {
+    if (remote && q - threadIdx.x >= cnt) break;  // (workgroup-uniform)
+    int64_t j = q;
+    uint32_t tk = SRNN_NIL;
+    bool on;
+    if (remote) {
+      on = q < cnt;
+      if (on) j = a.x_rlist[2 * q], tk = a.x_rlist[2 * q + 1];
+    } else {
+      on = j < a.n && !(x2 && x2_dep(a, j));
     }
-    __syncthreads();
-    if (threadIdx.x == 0 && atomicAdd(a.x_ctl + 3, 1) == (int32_t)gridDim.x - 1) {
-      *a.x_rcount = 0;
-      a.x_ctl[3] = 0;
+    const bool rs = on ? big_soup_one<T, S, SHUF>(c, a, cp, j, tk) != 0 : false;
+    if (remote) {
+      if (on) bs_publish_lane(bs, j, rs, -1);
+      q += (int64_t)gridDim.x * TBROW;
+      continue;
+    }
+    if (x2) {
+      const int64_t wd = (j >> 6) * 2 + (threadIdx.x & 63);
+      if ((threadIdx.x & 63) < 2 && wd * 32 < a.n) a.x_dep[wd] = 0u;
+      bs_publish_wave(bs, j >> 6, rs, -1);
+    } else if (a.flags & SRNN_F_ROW_FLAGS) {
+      if (j < a.n && a.rowflags) a.rowflags[j] = rs ? 1 : 0;
+    } else if (a.ballots) {
+      const unsigned long long m = __ballot(rs);
+      if ((threadIdx.x & 63) == 0) a.ballots[j >> 6] = m;
     }
     return;
   }
-  const int64_t j = (int64_t)blockIdx.x * TBROW + threadIdx.x;
-  bool rs = false;
-  if (j < a.n && !(x2 && x2_dep(a, j))) rs = big_soup_one<T, S, SHUF>(c, a, cp, j, SRNN_NIL) != 0;
-  if (x2) {
-    const int64_t wd = (j >> 6) * 2 + (threadIdx.x & 63);
-    if ((threadIdx.x & 63) < 2 && wd * 32 < a.n) a.x_dep[wd] = 0u;
-    bs_publish_wave(bs, j >> 6, rs, -1);
-  } else if (a.flags & SRNN_F_ROW_FLAGS) {
-    if (j < a.n && a.rowflags) a.rowflags[j] = rs ? 1 : 0;
-  } else if (a.ballots) {
-    const unsigned long long m = __ballot(rs);
-    if ((threadIdx.x & 63) == 0) a.ballots[j >> 6] = m;
+  __syncthreads();
+  if (threadIdx.x == 0 && atomicAdd(a.x_ctl + 3, 1) == (int32_t)gridDim.x - 1) {
+    *a.x_rcount = 0;
+    a.x_ctl[3] = 0;
   }
 }
 
