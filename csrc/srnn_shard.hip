@@ -50,16 +50,21 @@ using namespace x2;
 // generation on the sharded critical path (profiles/r5e_*).
 constexpr int X2_MAX_GROUPS = 1024;
 __device__ void pack_finish_wg(const SrnnArgs& a, const X2Geom& G, int32_t gen) {
-  __shared__ int64_t s_red[XT / 64];
+  __shared__ int64_t s_red[XT / 64][6];
   __shared__ int32_t s_hw[XT / 64];
   __shared__ int32_t s_born[X2_MAX_GROUPS];
   const int t = threadIdx.x;
-  // this thread's peers' header words that are not stats (loaded first, stored last)
   for (int64_t g = t; g < a.x_groups; g += XT) s_born[g] = 0;
+  int64_t v[6] = {0, 0, 0, 0, 0, 0};  // born, census[5]
+  if (a.counts && t == 0) {
+    // census accumulated by a classify launch (nets without a fused census): read and cleared
+    // by this thread alone, before anything waits
+    for (int w = 0; w < 5; ++w) v[1 + w] = (int64_t)a.counts[w];
+    for (int w = 0; w < 6; ++w) a.counts[w] = 0;
+  }
   __syncthreads();
   const unsigned long long* bs = reinterpret_cast<const unsigned long long*>(a.temp);
   const int64_t nb = (a.n + 63) / 64, per = (nb + a.x_groups - 1) / a.x_groups, nw = (a.n + 31) / 32;
-  int64_t v[6] = {0, 0, 0, 0, 0, 0};
   int32_t carry = 0;
   for (int64_t c0 = 0; c0 < nb; c0 += XT) {
     const int64_t b = c0 + t;
@@ -85,20 +90,22 @@ __device__ void pack_finish_wg(const SrnnArgs& a, const X2Geom& G, int32_t gen) 
       __syncthreads();  // s_hw is reused by the next chunk
     }
   }
-  for (int w = 0; w < 6; ++w) v[w] = wg_sum(v[w], s_red);  // (barriers: s_born complete too)
+  // the six totals in one exchange (wave shuffles, one barrier; s_born complete after it too)
+#pragma unroll
+  for (int w = 0; w < 6; ++w)
+    for (int off = 32; off > 0; off >>= 1) v[w] += __shfl_xor(v[w], off);
+  if ((t & 63) == 0)
+    for (int w = 0; w < 6; ++w) s_red[t >> 6][w] = v[w];
+  __syncthreads();
+  int64_t tot[6] = {0, 0, 0, 0, 0, 0};  // census[5], born
+  for (int q = 0; q < XT / 64; ++q) {
+    tot[5] += s_red[q][0];
+    for (int w = 0; w < 5; ++w) tot[w] += s_red[q][1 + w];
+  }
   for (int64_t g = t; g < a.x_groups; g += XT) {
     a.x_part[g * 6] = s_born[g];
     if (a.x_hpre) a.x_hgrp[g] = 0;
   }
-  int64_t tot[6];  // census[5], born
-  tot[5] = v[0];
-  for (int w = 0; w < 5; ++w) tot[w] = v[1 + w];
-  if (a.counts) {  // census accumulated by a classify launch (nets without a fused census)
-    for (int w = 0; w < 5; ++w) tot[w] += (int64_t)a.counts[w];
-  }
-  __syncthreads();  // every thread read counts before thread 0 clears them
-  if (a.counts && t == 0)
-    for (int w = 0; w < 6; ++w) a.counts[w] = 0;
   for (int q = t; q < a.world; q += XT) write_stats_peer(a, G, q, tot, gen);
 }
 
