@@ -54,8 +54,9 @@ def parse_args(argv=None):
                          "table (Jacobi)")
     ap.add_argument("--reference-order-steps", type=int, default=None,
                     help="synchronous headline: ALSO time this many generations of the same soup in the reference's "
-                         "sequential order on the same ranks (reported under config.reference_order); -1 / default: "
-                         "--steps; 0: off")
+                         "sequential order on the same ranks (reported under config.reference_order); -1: --steps; "
+                         "default: --steps on one GPU, off on several (the sharded reference order all-gathers per "
+                         "dependency level: it is measured on request, never at the cost of the headline run); 0: off")
     ap.add_argument("--train", type=int, default=20)
     ap.add_argument("--attacking-rate", type=float, default=0.1)
     ap.add_argument("--learn-from-rate", type=float, default=0.1)
@@ -219,7 +220,9 @@ def main(argv=None):
     # the same soup in the reference's order (DAG-scheduled; sharded over the same ranks), timed
     # after the headline's region: a second number, never part of the headline value
     ref_order = None
-    k_ref = -1 if args.reference_order_steps is None else args.reference_order_steps
+    k_ref = args.reference_order_steps
+    if k_ref is None:
+        k_ref = -1 if d.world == 1 else 0
     k_ref = args.steps if k_ref < 0 else k_ref
     if k_ref > 0 and args.order == "synchronous":
         eng.release_graphs()

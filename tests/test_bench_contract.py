@@ -80,11 +80,12 @@ def test_bench_reports_the_reference_order_by_default():
 
 def test_bench_reference_order_on_two_ranks():
     """the reference order shards: --gpus 2 --order sequential runs, and a 2-rank Jacobi headline
-    carries the same soup in the reference order, with the census of the 1-rank run (bitwise the
-    same soup on any rank count)"""
+    carries the same soup in the reference order on request, with the census of the 1-rank run
+    (bitwise the same soup on any rank count)"""
     two = _bench("--gpus", "2", "--particles", "1200", "--order", "sequential")
     assert two["n_gpus"] == 2 and two["semantics"] == "reference-order"
     one = _bench("--particles", "1200", "--order", "sequential")
     assert two["config"]["final_census"] == one["config"]["final_census"]
-    side = _bench("--gpus", "2", "--particles", "1200")
+    side = _bench("--gpus", "2", "--particles", "1200", "--reference-order-steps", "-1")
     assert side["config"]["reference_order"]["final_census"] == one["config"]["final_census"]
+    assert _bench("--gpus", "2", "--particles", "1200")["config"]["reference_order"] is None  # on request only
