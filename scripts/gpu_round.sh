@@ -14,7 +14,7 @@ timeout -k 10 900 python -u -m pytest tests/test_ordered_soup.py tests/test_orde
 rc=$?; tail -2 gpurun_out/pytest_$TAG.log; [ $rc -eq 0 ] || exit $rc
 step b20 300 python bench.py --steps 20 --warmup 5 || exit 1
 step b20b 300 python bench.py --steps 20 --warmup 5 || exit 1
+step b20c 300 python bench.py --steps 20 --warmup 5 || exit 1
 step prof_ro 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_ro_$TAG -o t --output-format csv -- python3 bench.py --steps 20 --warmup 5 --order sequential || exit 1
 step tr_crit 300 python bench/ordered_trace.py || exit 1
-step c4s 600 python bench/configs.py --only 4s --n4s 1000000 --gens4s 3 --order4s sequential || exit 1
 echo done
