@@ -1315,14 +1315,15 @@ struct BRow {
 };
 
 // chunk ids of the shuffled output (4 bits per weight) in LDS, word w of lane L at
-// cw[w * TBROW + L] (consecutive lanes -> consecutive banks)
+// cw[w * st + L] (st = the workgroup size; consecutive lanes -> consecutive banks)
 template <class T>
 struct ChunkPerm {
   static constexpr int NW = (T::P + 7) / 8;
   static_assert(T::A <= 16, "chunk ids are 4-bit");
   uint32_t* cw;
-  __device__ uint32_t word(int w) const { return cw[w * TBROW]; }
-  __device__ int cid(int k) const { return (int)((cw[(k >> 3) * TBROW] >> (4 * (k & 7))) & 15u); }
+  int st = TBROW;  // LDS words between a lane's consecutive chunk-id words (= the workgroup size)
+  __device__ uint32_t word(int w) const { return cw[w * st]; }
+  __device__ int cid(int k) const { return (int)((cw[(k >> 3) * st] >> (4 * (k & 7))) & 15u); }
   // fisher_yates(perm, P, rng, id, step, P_AGGSHUF) applied to chunk(perm[k])
   __device__ void draw(const Rng& rng, uint64_t id, uint32_t step) const {
 #pragma unroll
@@ -1331,7 +1332,7 @@ struct ChunkPerm {
 #pragma unroll
       for (int e = 0; e < 8; ++e)
         if (8 * w + e < T::P) x |= (uint32_t)T::chunk_c(8 * w + e) << (4 * e);
-      cw[w * TBROW] = x;
+      cw[w * st] = x;
     }
     U4 r{0, 0, 0, 0};
     int used = 4;
@@ -1347,13 +1348,13 @@ struct ChunkPerm {
       int j = (int)(u01(x) * (float)(i + 1));
       if (j > i) j = i;
       const int wi = i >> 3, wj = j >> 3, si = 4 * (i & 7), sj = 4 * (j & 7);
-      const uint32_t xi = cw[wi * TBROW], xj = cw[wj * TBROW];
+      const uint32_t xi = cw[wi * st], xj = cw[wj * st];
       const uint32_t d = ((xi >> si) ^ (xj >> sj)) & 15u;
       if (wi == wj) {
-        cw[wi * TBROW] = xi ^ (d << si) ^ (d << sj);
+        cw[wi * st] = xi ^ (d << si) ^ (d << sj);
       } else {
-        cw[wi * TBROW] = xi ^ (d << si);
-        cw[wj * TBROW] = xj ^ (d << sj);
+        cw[wi * st] = xi ^ (d << si);
+        cw[wj * st] = xj ^ (d << sj);
       }
     }
   }
@@ -1968,10 +1969,10 @@ struct BigOrd : ord::OrdSched<1> {
 template <class T, class S, bool SHUF>
 struct BigOrdPol {
   struct Shared {
-    uint32_t cw[SHUF ? ChunkPerm<T>::NW * TBROW : 1];
+    uint32_t cw[SHUF ? ChunkPerm<T>::NW * TB : 1];
   };
   __device__ static void turn(const SrnnCfg& c, const SrnnArgs& a, int64_t k, int32_t gen, Shared& sh, int64_t) {
-    BigOrd<T, S, SHUF>::turn(c, a, k, gen, ChunkPerm<T>{sh.cw + threadIdx.x});
+    BigOrd<T, S, SHUF>::turn(c, a, k, gen, ChunkPerm<T>{sh.cw + threadIdx.x, TB});
   }
 };
 // final rows (the last attack after a row's own turn, else its E version), the next
@@ -1980,8 +1981,8 @@ template <class T, class S, bool SHUF>
 __global__ __launch_bounds__(TB) void k_ordbig_close(SrnnCfg c, SrnnArgs a) {
   using R = BRow<T, S>;
   using Dec = ord::OrdSched<1>::Dec;
-  __shared__ uint32_t s_cw[SHUF ? ChunkPerm<T>::NW * TBROW : 1];
-  const ChunkPerm<T> cp{s_cw + threadIdx.x};
+  __shared__ uint32_t s_cw[SHUF ? ChunkPerm<T>::NW * TB : 1];
+  const ChunkPerm<T> cp{s_cw + threadIdx.x, TB};
   const int64_t gb = blockIdx.x;
   const int64_t r = gb * TB + threadIdx.x;
   const int lane = threadIdx.x;
@@ -1989,16 +1990,18 @@ __global__ __launch_bounds__(TB) void k_ordbig_close(SrnnCfg c, SrnnArgs a) {
   const bool census = !SHUF && (a.flags & SRNN_F_FUSED_CENSUS) != 0;
   bool rs = false;
   int8_t k = -1;
+  // the E rows through the wave's staging area (coalesced passes, as the synchronous soup's
+  // census: a lane-per-row load touches 64 rows 1120 B apart per instruction)
+  __shared__ uint4 s_stg[R::G::WAVE_U4];
+  float w[T::P];
+  R::load_staged(a.W, r < a.n ? (int32_t)r : -1, w, s_stg);
   if (r < a.n) {
     if (a.o_src[4 * r + 3] < 0) atomicOr(a.o_ctl + ord::ERRW, 4);  // never ran: a scheduling bug
-    float w[T::P];
     const int64_t ja = ord::last_attacker_before(a, r, a.n);
     a.heads[r] = SRNN_NIL;  // consumed: NIL for the generation after next
-    if (ja > r) {
+    if (ja > r) {  // attacked after its own turn: the last attack's output
       BigOrd<T, S, SHUF>::load_version(c, a, ord::code_A(ja), gen, cp, w);
       R::store(R::at(a.W, r), w);
-    } else {
-      R::load(R::at(a.W, r), w);
     }
     rs = a.respawn[r] != 0;
     int64_t at, te;
