@@ -31,14 +31,14 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, out_dir, dtype, chunks):
+def _worker(rank, world, port, out_dir, dtype, chunks, n_total=N_TOTAL):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), SRNN_SHARE_DEVICE="1")
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         dev = torch.device("cuda", 0)
         torch.cuda.set_device(dev)
         d = Dist(rank, world, 0, None)
-        e = SoupEngine(ArchSpec.weightwise(2, 2), N_TOTAL, PARAMS, device=dev, seed=21, dist=d, dtype=DTYPES[dtype],
+        e = SoupEngine(ArchSpec.weightwise(2, 2), n_total, PARAMS, device=dev, seed=21, dist=d, dtype=DTYPES[dtype],
                        order="sequential")
         e.stats = True
         for k in chunks:
@@ -52,13 +52,15 @@ def _worker(rank, world, port, out_dir, dtype, chunks):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,dtype,chunks", [(2, "float32", (3,)), (3, "float32", (1, 2)), (2, "bfloat16", (3,))])
-def test_device_sharded_reference_order_equals_single_rank(tmp_path, world, dtype, chunks):
-    ref = SoupEngine(ArchSpec.weightwise(2, 2), N_TOTAL, PARAMS, device="cuda", seed=21, dtype=DTYPES[dtype],
+@pytest.mark.parametrize("world,dtype,chunks,n_total", [(2, "float32", (3,), N_TOTAL), (3, "float32", (1, 2), N_TOTAL),
+                                                       (2, "bfloat16", (3,), N_TOTAL), (2, "float32", (2,), 20011)])
+def test_device_sharded_reference_order_equals_single_rank(tmp_path, world, dtype, chunks, n_total):
+    """(20,011 particles: > 8192 rows per rank, the uid assignment's multi-tile path)"""
+    ref = SoupEngine(ArchSpec.weightwise(2, 2), n_total, PARAMS, device="cuda", seed=21, dtype=DTYPES[dtype],
                      order="sequential")
     ref.evolve(sum(chunks))
     ref_counts = ref.count()
-    mp.start_processes(_worker, args=(world, _free_port(), str(tmp_path), dtype, chunks), nprocs=world,
+    mp.start_processes(_worker, args=(world, _free_port(), str(tmp_path), dtype, chunks, n_total), nprocs=world,
                        start_method="spawn", join=True)
     parts = [np.load(os.path.join(tmp_path, f"r{r}.npz")) for r in range(world)]
     W = np.concatenate([p["W"] for p in parts])
