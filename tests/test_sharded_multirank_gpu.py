@@ -57,12 +57,14 @@ def _worker(rank, world, port, spec_json, out_dir, dtype, chunks, schedule):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,dtype,chunks,schedule", [
-    (2, "float32", (2, 4), "serial"), (3, "float32", (6,), "serial"), (2, "bfloat16", (3, 3), "serial"),
-    (2, "float32", (2, 4), "overlap"), (3, "float32", (6,), "overlap")])
-def test_multirank_device_soup_equals_single_rank(cuda, tmp_path, world, dtype, chunks, schedule):
-    """both generation schedules: one stream, or the local slots beside the exchange"""
-    spec = ArchSpec.weightwise(2, 2)
+@pytest.mark.parametrize("world,dtype,chunks,schedule,shape", [
+    (2, "float32", (2, 4), "serial", (2, 2)), (3, "float32", (6,), "serial", (2, 2)),
+    (2, "bfloat16", (3, 3), "serial", (2, 2)), (2, "float32", (2, 4), "overlap", (2, 2)),
+    (3, "float32", (6,), "overlap", (2, 2)), (2, "float32", (3,), "serial", (2, 1)), (2, "float32", (3,), "serial", (1, 1))])
+def test_multirank_device_soup_equals_single_rank(cuda, tmp_path, world, dtype, chunks, schedule, shape):
+    """both generation schedules: one stream, or the local slots beside the exchange; WW(2,1) /
+    WW(1,1): the permutation table built by pack for other nibble shapes (runtime P)"""
+    spec = ArchSpec.weightwise(*shape)
     ref = SoupEngine(spec, N_TOTAL, PARAMS, device=cuda, seed=21, dtype=DTYPES[dtype])
     ref.stats = True
     ref.evolve(sum(chunks))
