@@ -62,3 +62,19 @@ def test_device_ordered_big_net_graphs_equal_eager():
     b.evolve(3)
     torch.cuda.synchronize()
     assert torch.equal(_bits(a.local_rows()), _bits(b.local_rows())) and torch.equal(a.uid, b.uid)
+
+
+@pytest.mark.parametrize("shape", [(4, 8, 2), (4, 16, 2)], ids=["agg-4-8-2", "agg-4-16-2"])
+def test_device_ordered_other_big_shapes(shape):
+    """the other instantiated big aggregating shapes (P = 128, 384) in the reference order"""
+    spec = ArchSpec.aggregating(*shape)
+    n, seed = 1200, 5
+    o = SoupEngine(spec, n, HOT, device="cuda", seed=seed, order="sequential")
+    s = SequentialSoupEngine(spec, n, HOT, seed=seed, weights=o.local_rows()[:, :spec.P].float().cpu())
+    for g in range(2):
+        o.evolve(1)
+        s.evolve(1)
+        torch.cuda.synchronize()
+        assert torch.equal(_bits(o.local_rows()[:, :spec.P]), _bits(s.W[:, :spec.P])), g
+        assert torch.equal(o.uid.cpu(), s.uid.cpu()) and torch.equal(o.respawn.cpu(), s.respawn.cpu())
+    assert o.ordered_levels()["error"] == 0
