@@ -61,7 +61,7 @@ constexpr int32_t SRC_NONE = INT32_MIN + 2;
 constexpr int MAX_LEVELS = 16;  // dependency levels reported one by one (deeper: one bin)
 // o_ctl words: [MAXLW] deepest level (host path), [ERRW] error bits -- STICKY: set by any
 // generation, never cleared by the next one (2: an unstored attack output past the recompute
-// depth, a marking bug; 4: a turn that never ran), [PART0 + p] records (pending turns) of
+// depth, a marking bug; 4: a turn that never ran; 8: a ready-queue entry never written), [PART0 + p] records (pending turns) of
 // partition p, [CRIT0 + p] producers of later turns in partition p (the producer's block mod
 // NPART; k_ord_count appends a producer when its first consumer registers)
 constexpr int MAXLW = 17, ERRW = 18;
@@ -625,13 +625,16 @@ __global__ __launch_bounds__(TB) void k_ord_run(SrnnCfg c, SrnnArgs a) {
       cur = -1;
       prow = -1;
       if (lane < m) {
-        int32_t q;
-        while ((q = ord::ld_level(qa + qb + lane)) == ord::EMPTY) __builtin_amdgcn_s_sleep(1);
-        prow = q;
+        // (bounded: a slot still unwritten after ~2^24 polls is a scheduling bug -- error bit 8
+        // and the entry skipped, rather than a wave that never ends)
+        int32_t q, polls = 0;
+        while ((q = ord::ld_level(qa + qb + lane)) == ord::EMPTY && ++polls < (1 << 24)) __builtin_amdgcn_s_sleep(1);
+        if (q == ord::EMPTY) atomicOr(a.o_ctl + ord::ERRW, 8);
+        else prow = q;
       }
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      if (lane < m) cur = ord::pend(a, prow)[0];
+      if (lane < m && prow >= 0) cur = ord::pend(a, prow)[0];
     } else {
     // the wave's ready records, one per lane (the rest stay in their lists for the next round)
     const int32_t total = ord::wave_sum(nready);

@@ -443,7 +443,7 @@ class SoupEngine:
         levels, the turns deeper than those (``tail``), the deepest level, the turns that had
         producers (``pending``: on the device, run as continuations), the error bits (sticky over
         the engine's life: 2 -- an attack output past the recompute depth left unstored, 4 -- a
-        turn that never ran), and how many attack outputs were stored for later turns (the others
+        turn that never ran, 8 -- a ready-queue entry never written), and how many attack outputs were stored for later turns (the others
         are recomputed by the turns that read them)."""
         C = self.order_levels
         n = self._ord_n
