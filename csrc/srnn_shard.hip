@@ -291,6 +291,76 @@ __global__ __launch_bounds__(TBU) void k_uid_assign(SrnnArgs a) {
   if (a.counts && threadIdx.x < 6) a.counts[threadIdx.x] = 0;
 }
 
+// The same assignment over the whole grid in two launches (SrnnArgs::temp: int32 count per
+// UCH-row chunk, then int64 this rank's first uid): chunk counts (workgroup 0 also takes the
+// census and the rank's uid base and advances next_uid), then every chunk numbers its flagged
+// rows after the prefix of the chunks before it.  The one-workgroup form walks n rows in
+// sequence (60 us at 100k rows, profiles/r5q_*).
+constexpr int UCH = 4 * TBU;
+SRNN_HD int64_t uid_chunks(int64_t n) { return (n + UCH - 1) / UCH; }
+SRNN_HD int64_t uid_temp_bytes(int64_t n) { return ((uid_chunks(n) * 4 + 7) / 8) * 8 + 8; }
+__device__ __forceinline__ int64_t* uid_first(const SrnnArgs& a) {
+  return reinterpret_cast<int64_t*>(reinterpret_cast<char*>(a.temp) + ((uid_chunks(a.n) * 4 + 7) / 8) * 8);
+}
+__device__ __forceinline__ int32_t block_sum_tbu(int32_t v, int32_t* s_wave) {
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+  if ((threadIdx.x & 63) == 0) s_wave[threadIdx.x >> 6] = v;
+  __syncthreads();
+  int32_t t = 0;
+  for (int w = 0; w < TBU / 64; ++w) t += s_wave[w];
+  return t;
+}
+__global__ __launch_bounds__(TBU) void k_uid_count(SrnnArgs a) {
+  __shared__ int32_t s_wave[TBU / 64];
+  const int64_t r0 = (int64_t)blockIdx.x * UCH + (int64_t)threadIdx.x * 4;
+  int32_t c = 0;
+#pragma unroll
+  for (int u = 0; u < 4; ++u) c += (r0 + u < a.n && a.rowflags[r0 + u] != 0) ? 1 : 0;
+  const int32_t tot = block_sum_tbu(c, s_wave);
+  if (threadIdx.x == 0) reinterpret_cast<int32_t*>(a.temp)[blockIdx.x] = tot;
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    int64_t pre = 0, all_born = 0, cen[5] = {0, 0, 0, 0, 0}, all = 0;
+    for (int r = 0; r < a.world; ++r) {
+      const int64_t k = a.stats[r * 6 + 5];
+      if (r < a.rank) pre += k;
+      all_born += k;
+      for (int w = 0; w < 5; ++w) cen[w] += a.stats[r * 6 + w];
+    }
+    for (int w = 0; w < 5; ++w) all += cen[w];
+    if (a.census && all > 0)
+      for (int w = 0; w < 5; ++w) a.census[w] = cen[w];
+    const int64_t base = a.uid_base[0];
+    *uid_first(a) = base + pre;
+    a.uid_base[0] = base + all_born;
+    if (a.counts)
+      for (int w = 0; w < 6; ++w) a.counts[w] = 0;
+  }
+}
+__global__ __launch_bounds__(TBU) void k_uid_write(SrnnArgs a) {
+  __shared__ int32_t s_wave[TBU / 64];
+  const int32_t* cnt = reinterpret_cast<const int32_t*>(a.temp);
+  int32_t p = 0;  // flagged rows of the chunks before this one
+  for (int64_t j = threadIdx.x; j < (int64_t)blockIdx.x; j += TBU) p += cnt[j];
+  const int64_t before = block_sum_tbu(p, s_wave);
+  __syncthreads();  // s_wave is reused by the scan
+  const int64_t r0 = (int64_t)blockIdx.x * UCH + (int64_t)threadIdx.x * 4;
+  int32_t f[4], c = 0;
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    f[u] = r0 + u < a.n ? a.rowflags[r0 + u] : 0;
+    c += f[u] != 0;
+  }
+  int32_t tot;
+  const int32_t incl = block_incl_scan<TBU>(c, s_wave, &tot);
+  int64_t k = *uid_first(a) + before + incl - c;
+#pragma unroll
+  for (int u = 0; u < 4; ++u)
+    if (f[u]) {
+      a.uid_out[r0 + u] = k++;
+      a.rowflags[r0 + u] = 0;
+    }
+}
+
 int check(hipError_t e) {
   if (e != hipSuccess) {
     set_error(hipGetErrorString(e));
@@ -313,6 +383,12 @@ extern "C" int srnn_x2_run(int op, const SrnnCfg* c, const SrnnArgs* a) {
     if (!a->dev) {
       host_uid_assign(*a);
       return 0;
+    }
+    if (a->temp && a->temp_bytes >= uid_temp_bytes(a->n) && a->n > UCH) {  // the grid-wide form
+      const unsigned g = (unsigned)uid_chunks(a->n);
+      hipLaunchKernelGGL(k_uid_count, dim3(g), dim3(TBU), 0, (hipStream_t)a->stream, *a);
+      hipLaunchKernelGGL(k_uid_write, dim3(g), dim3(TBU), 0, (hipStream_t)a->stream, *a);
+      return check(hipGetLastError());
     }
     hipLaunchKernelGGL(k_uid_assign, dim3(1), dim3(TBU), 0, (hipStream_t)a->stream, *a);
     return check(hipGetLastError());

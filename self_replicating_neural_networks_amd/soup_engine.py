@@ -1065,6 +1065,17 @@ class SoupEngine:
         else:
             a, _, flags = self._gen_args()
             self.dist.all_gather_into(self.stats_all, self.counts)
+            if self.device.type == "cuda":
+                # the grid-wide assignment's scratch (csrc uid_temp_bytes: a count per 4096-row
+                # chunk + this rank's first uid); allocated once, outside graph captures
+                nb = (-(-self.n // 4096) * 4 + 7) // 8 * 8 + 8
+                t = getattr(self, "_uid_tmp", None)
+                if t is None or t.numel() * 8 < nb:
+                    self._uid_tmp = t = torch.zeros(nb // 8, dtype=torch.int64, device=self.device)
+                ua = self._args()
+                ctypes.pointer(ua)[0] = a
+                ua.temp, ua.temp_bytes = _p(t), t.numel() * 8
+                a = ua
             _lib.run(_lib.OP_UID_ASSIGN, self.spec, a, self.cfg)
         self._pending = False
 
