@@ -107,6 +107,8 @@ class ExecConfig:
     soup_lanes: Optional[int] = None        # SRNN_SOUP_LANES (None / 0: by population size)
     ord_crit: Optional[bool] = None         # SRNN_ORD_CRIT: reference-order generations run the producers of
                                             # later turns first, at raised wave priority (None: on)
+    ord_queue: Optional[bool] = None        # SRNN_ORD_QUEUE: reference-order continuations through one ready
+                                            # queue per generation (None: on; off: per-wave lists)
     ordsh_emulate: int = 0                  # SRNN_ORDSH_EMULATE: one-rank timing model of R ranks of a sharded
                                             # reference-order generation (the rank runs 1/R of the turns;
                                             # the other turns never run: timing only, results invalid)
@@ -121,15 +123,15 @@ class ExecConfig:
                 sharded_graph="SRNN_SHARDED_GRAPH", native_comm="SRNN_NATIVE_COMM", loopback="SRNN_LOOPBACK",
                 force_generic="SRNN_FORCE_GENERIC", ww_wave="SRNN_WW_WAVE", rnn_wave="SRNN_RNN_WAVE",
                 rnn_spec="SRNN_RNN_SPEC", rnn_soup="SRNN_RNN_SOUP", big_wave="SRNN_BIG_WAVE",
-                fix_group="SRNN_FIX_GROUP", soup_lanes="SRNN_SOUP_LANES", ord_crit="SRNN_ORD_CRIT",
+                fix_group="SRNN_FIX_GROUP", soup_lanes="SRNN_SOUP_LANES", ord_crit="SRNN_ORD_CRIT", ord_queue="SRNN_ORD_QUEUE",
                 ordsh_emulate="SRNN_ORDSH_EMULATE",
                 order_levels="SRNN_ORDER_LEVELS",
                 perm_table="SRNN_PERM_TABLE")
     # Optional[bool] knobs whose None means "the built-in choice" (by population size, ...)
     TRI_STATE = ("force_generic", "rnn_wave", "rnn_spec", "rnn_soup", "big_wave", "fix_group", "perm_table",
-                 "ord_crit")
+                 "ord_crit", "ord_queue")
     LIBRARY_KNOBS = ("force_generic", "ww_wave", "rnn_wave", "rnn_spec", "rnn_soup", "big_wave", "fix_group",
-                     "soup_lanes", "ord_crit")
+                     "soup_lanes", "ord_crit", "ord_queue")
 
     def validate(self):
         if self.finish_mode not in ("batch", "serial"):

@@ -112,3 +112,16 @@ def test_plan_returns_the_engine_arguments_it_assumed():
     assert q["n_total"] < s["n_total"] and q["n_total"] <= 2 ** 30 - 1
     assert q["limited_by"] in ("hbm", "ordered version codes (int32)")
 
+
+
+def test_every_library_knob_is_an_exec_config_field(monkeypatch):
+    """each libsrnn knob (ops/_lib.py KNOBS) can be set from ExecConfig, ord_queue included"""
+    assert set(ExecConfig.LIBRARY_KNOBS) == set(_lib.KNOBS)
+    monkeypatch.setenv("SRNN_ORD_QUEUE", "0")
+    assert ExecConfig().resolved().ord_queue is False
+    monkeypatch.delenv("SRNN_ORD_QUEUE")
+    try:
+        ExecConfig(ord_queue=False).apply_library()
+        assert _lib.get_knob("ord_queue") == 0
+    finally:
+        _lib.set_knob("ord_queue", -1)
