@@ -5,21 +5,27 @@ Metric (BASELINE.json): "self-application steps/sec (whole node) for 100k-partic
 One step = one soup generation (reference ``Soup.evolve``, code/soup.py:51-87) for every
 particle: attacks (rate 0.1), learn_from (rate 0.1, severity 1), 20 self-train epochs,
 divergent/zero respawn, plus the per-generation fixpoint census (``Soup.count``,
-code/soup.py:89-103) all-reduced over ranks.  The soup configuration is the reference's
-active soup demo (code/soup.py:127-138: WeightwiseNeuralNetwork(2, 2), train=20,
-remove_divergent, remove_zero, epsilon=1e-4).  Random-init weights, fp32 (the reference's
-dtype; bf16 would make the 1e-4 fixpoint test meaningless).
+code/soup.py:89-103).  The soup configuration is the reference's active soup demo
+(code/soup.py:127-138: WeightwiseNeuralNetwork(2, 2), train=20, remove_divergent, remove_zero,
+epsilon=1e-4).  Random-init weights, fp32 (the reference's dtype; bf16 would make the 1e-4
+fixpoint test meaningless).
+
+Semantics (``--order``): ``sequential`` (default) is the reference's own generation -- in
+place, in index order: particle k sees every change made by particles < k in the same
+generation -- computed on the device by its dependency DAG, bitwise the serial loop
+(csrc/srnn_ordered.h).  ``synchronous`` is the Jacobi variant (every read from the
+generation-start table): different dynamics, reported only as a side number
+(``config.jacobi``) next to the reference-order headline on one GPU.
 
 Scaling (``--scaling``): ``strong`` (default) is the metric as BASELINE.json writes it -- ONE
 100k-particle soup at any GPU count (100k / N particles per rank); ``weak`` keeps
 ``--particles-per-gpu`` per rank (an N x 100k soup).
 
 Multi-GPU (N>1): one process per GPU, each rank owns a contiguous shard of ONE global soup
-(partners uniform over all slots).  Per generation (soup_engine.py, serial schedule) each
-rank packs the rows other ranks need (attackers of their victims, teachers their learners
-requested one generation ahead), ONE all-to-all on the soup's own RCCL communicator over
-xGMI moves them, and ONE launch runs the exchange's post and the evolve of every local slot.
-Single GPU: the fused generation kernel, 20/16/8/4/2 generations per hipGraph.
+(partners uniform over all slots).  The reference order shards by a replicated plan and one
+all-gather of each dependency level's outputs (csrc/srnn_ordered_sh.h); the Jacobi variant by
+ONE all-to-all per generation on the soup's own RCCL communicator over xGMI
+(csrc/srnn_shard.hip).
 
 value = particles x generations / second over the whole job (max time over ranks).
 
@@ -48,15 +54,14 @@ def parse_args(argv=None):
                          "weak: --particles-per-gpu on every rank")
     ap.add_argument("--particles", type=int, default=100_000, help="soup size (strong scaling)")
     ap.add_argument("--particles-per-gpu", type=int, default=100_000, help="per-rank soup size (weak scaling)")
-    ap.add_argument("--order", choices=["sequential", "synchronous"], default="synchronous",
-                    help="sequential: the reference's in-place, index-ordered generation (DAG-scheduled; sharded by "
-                         "replicated plan + per-level all-gathers); synchronous: every read from the generation-start "
-                         "table (Jacobi)")
-    ap.add_argument("--reference-order-steps", type=int, default=None,
-                    help="synchronous headline: ALSO time this many generations of the same soup in the reference's "
-                         "sequential order on the same ranks (reported under config.reference_order); -1: --steps; "
-                         "default: --steps on one GPU, off on several (the sharded reference order all-gathers per "
-                         "dependency level: it is measured on request, never at the cost of the headline run); 0: off")
+    ap.add_argument("--order", choices=["sequential", "synchronous"], default="sequential",
+                    help="sequential (default): the reference's in-place, index-ordered generation (DAG-scheduled, "
+                         "bitwise the serial loop; sharded by replicated plan + per-level all-gathers); synchronous: "
+                         "the Jacobi variant, every read from the generation-start table")
+    ap.add_argument("--side-steps", "--reference-order-steps", dest="side_steps", type=int, default=None,
+                    help="ALSO time this many generations of the same soup in the OTHER order on the same ranks "
+                         "(config.jacobi beside a reference-order headline, config.reference_order beside a Jacobi "
+                         "one); -1: --steps; default: --steps on one GPU, off on several; 0: off")
     ap.add_argument("--train", type=int, default=20)
     ap.add_argument("--attacking-rate", type=float, default=0.1)
     ap.add_argument("--learn-from-rate", type=float, default=0.1)
@@ -103,40 +108,60 @@ def model_string(args) -> str:
     return "Soup of WeightwiseNeuralNetwork(width=2, depth=2), " + ", ".join(parts)
 
 
-def _reference_order_side(args, spec, n_total, params, dev, d, execution, k_ref, sync, backend):
-    """The same soup in the reference's sequential order on the same ranks, timed after the
-    headline's region (a second number, never part of the headline value).  A failure is
-    reported in the line instead of costing the headline."""
+def _agree(d, ok: bool, dev, backend) -> bool:
+    """Every rank's verdict (MIN) before anything collective depends on a local outcome."""
+    if not d.enabled:
+        return ok
+    import torch
+    import torch.distributed as dist
+    t = torch.tensor([1 if ok else 0], dtype=torch.int32, device=dev if backend == "nccl" else "cpu")
+    dist.all_reduce(t, op=dist.ReduceOp.MIN)
+    return bool(t.item())
+
+
+def _side(args, order, spec, n_total, params, dev, d, execution, k_side, sync, backend):
+    """The same soup in the other order on the same ranks, timed after the headline's region (a
+    second number, never part of the headline value).  A failure is reported in the line instead
+    of costing the headline: the ranks agree after every step that can fail locally (the engine's
+    allocations, the graph capture) before any of them enters a collective of the measurement."""
     import torch
     import torch.distributed as dist
     from self_replicating_neural_networks_amd.soup_engine import SoupEngine
 
+    label = "reference-order" if order == "sequential" else "jacobi"
+    eng, err = None, None
     try:
-        ro = SoupEngine(spec, n_total, params, device=dev, seed=args.seed, dist=d, execution=execution,
-                        order="sequential")
-        ro.stats = not args.no_stats
+        eng = SoupEngine(spec, n_total, params, device=dev, seed=args.seed, dist=d, execution=execution,
+                         order=order)
+        eng.stats = not args.no_stats
+    except Exception as e:  # noqa: BLE001
+        err = e
+    if not _agree(d, err is None, dev, backend):
+        return {"semantics": label, "error": f"{type(err).__name__}: {err}"[:500] if err else "failed on another rank"}
+    try:
         if dev.type == "cuda" and not args.no_graph:
-            ro.capture(warmup=1)  # (single rank: hipGraphs; sharded: eager, its level count is read back)
-        ro.evolve(args.warmup)
+            eng.capture(warmup=1)  # (collective and agreed inside; sharded reference order: eager)
+        eng.evolve(args.warmup)
         sync()
         d.barrier()
         sync()
         t1 = time.perf_counter()
-        ro.evolve(k_ref)
+        eng.evolve(k_side)
         sync()
         d.barrier()
         sync()
         tr = torch.tensor([time.perf_counter() - t1], dtype=torch.float64, device=dev if backend == "nccl" else "cpu")
         if d.enabled:
             dist.all_reduce(tr, op=dist.ReduceOp.MAX)
-        dt_ref = float(tr.item())
-        out = {"semantics": "reference-order", "steps": k_ref, "warmup": args.warmup,
-               "ms_per_step": dt_ref / k_ref * 1e3, "value": n_total * k_ref / dt_ref,
-               "unit": "particle-generations/s", "final_census": ro.count(), "levels": ro.ordered_levels()}
-        ro.release_graphs()
+        dt = float(tr.item())
+        out = {"semantics": label, "steps": k_side, "warmup": args.warmup, "ms_per_step": dt / k_side * 1e3,
+               "value": n_total * k_side / dt, "unit": "particle-generations/s", "final_census": eng.count()}
+        if order == "sequential":
+            out["levels"] = eng.ordered_levels()
+        eng.release_graphs()
         return out
     except Exception as e:  # noqa: BLE001 -- the headline line must still be printed
-        return {"semantics": "reference-order", "error": f"{type(e).__name__}: {e}"[:500]}
+        return {"semantics": label, "error": f"{type(e).__name__}: {e}"[:500]}
 
 
 def main(argv=None):
@@ -155,7 +180,7 @@ def main(argv=None):
     from self_replicating_neural_networks_amd.arch import ArchSpec
     from self_replicating_neural_networks_amd.config import ExecConfig
     from self_replicating_neural_networks_amd.parallel.dist import from_env
-    from self_replicating_neural_networks_amd.soup_engine import SoupEngine
+    from self_replicating_neural_networks_amd.soup_engine import ORD_ERR_EMULATED, SoupEngine
 
     if args.force_sharded:
         os.environ["SRNN_FORCE_SHARDED"] = "1"
@@ -205,7 +230,12 @@ def main(argv=None):
     if err:
         # rows that did not fit the exchange capacity were dropped: the generations are invalid
         raise SystemExit(f"soup row exchange failed ({err}): the measured generations are invalid")
-    census = eng.count()
+    oerr = eng.ordered_error_all()
+    if oerr & ~ORD_ERR_EMULATED:
+        raise SystemExit(f"reference-order generation failed (error bits {oerr}): the measured generations are invalid")
+    # (a one-rank timing model of a sharded reference order -- SRNN_ORDSH_EMULATE -- runs 1/R of the
+    # turns: a timing, not a soup; its census is not taken)
+    census = eng.count() if not oerr else "invalid: one-rank timing model (SRNN_ORDSH_EMULATE)"
     value = n_total * args.steps / dt
     # what RCCL itself reports about the soup's communicator on every rank (ncclCommCount /
     # ncclCommUserRank): the line shows that the collective really spanned N ranks
@@ -217,24 +247,26 @@ def main(argv=None):
         allr = allr.view(d.world, 2).cpu().tolist()
         comm = {"library": d.native.library, "rccl_nranks": [r[0] for r in allr],
                 "rccl_user_ranks": [r[1] for r in allr]}
-    # the same soup in the reference's order (DAG-scheduled; sharded over the same ranks), timed
-    # after the headline's region: a second number, never part of the headline value
-    ref_order = None
-    k_ref = args.reference_order_steps
-    if k_ref is None:
-        k_ref = -1 if d.world == 1 else 0
-    k_ref = args.steps if k_ref < 0 else k_ref
-    if k_ref > 0 and args.order == "synchronous":
+    # the same soup in the other order, timed after the headline's region: a second number, never
+    # part of the headline value
+    side = None
+    k_side = args.side_steps
+    if k_side is None:
+        k_side = -1 if d.world == 1 else 0
+    k_side = args.steps if k_side < 0 else k_side
+    other = "synchronous" if args.order == "sequential" else "sequential"
+    if k_side > 0:
         eng.release_graphs()
-        ref_order = _reference_order_side(args, spec, n_total, params, dev, d, execution, k_ref, sync, backend)
+        side = _side(args, other, spec, n_total, params, dev, d, execution, k_side, sync, backend)
     if d.rank == 0:
         print(json.dumps({
             "metric": "self-application steps/sec (whole node) for 100k-particle soup",
             "value": value,
             "unit": "particle-generations/s",
-            # which soup semantics `value` measures: "jacobi" (synchronous: every read from the
-            # generation-start table) or "reference-order" (code/soup.py:51-87, in place, index order);
-            # a jacobi headline carries the reference-order number under config.reference_order
+            # which soup semantics `value` measures: "reference-order" (code/soup.py:51-87, in place,
+            # index order: the reference's own) or "jacobi" (the synchronous variant: every read from
+            # the generation-start table); the other order's number rides along as config.jacobi /
+            # config.reference_order
             "semantics": "reference-order" if args.order == "sequential" else "jacobi",
             "n_gpus": d.world,
             "steps": args.steps,
@@ -257,7 +289,9 @@ def main(argv=None):
                        "sharded_schedule": getattr(eng, "schedule", None) if getattr(eng, "x2", False) else None,
                        "census_every_step": eng.stats, "final_census": census, "order": args.order,
                        "ordered_levels": eng.ordered_levels() if args.order == "sequential" else None,
-                       "reference_order": ref_order},
+                       "ord_pipeline": eng._ord_pipe,
+                       "jacobi": side if other == "synchronous" else None,
+                       "reference_order": side if other == "sequential" else None},
         }), flush=True)
     eng.release_graphs()  # graph executables reference the RCCL communicator
     d.close()

@@ -53,6 +53,12 @@ enum SrnnFlag : uint32_t {
                                      // (internal: set by the library from SRNN_KNOB_ORD_QUEUE)
   SRNN_F_PTAB_READY = 1u << 23,      // ptab already holds this generation's permutations (built by the
                                      // sharded pack): the generation launch does not rebuild them
+  SRNN_F_ORD_PLANNED = 1u << 25,     // OP_SOUP_ORDERED: o_src / o_list / o_ctl / ptab already hold this
+                                     // generation's plan (OP_ORD_PLAN, issued one generation ahead): no
+                                     // planning launches, and the close consumes this generation's lists
+                                     // without linking the next one's (the next OP_ORD_PLAN links them)
+  SRNN_F_ORD_NEXT = 1u << 26,        // OP_ORD_PLAN: plan generation gen + 1 (the one after the generation
+                                     // in flight) instead of gen
 };
 
 // Attack-list entries (uint32, SRNN_NIL ends a list).  Single rank: the attacker's row
@@ -211,9 +217,14 @@ enum SrnnOp {
                            // o_levels, 2 pack their outputs, 3 unpack the gathered outputs, 4 close
                            // this rank's rows, 5 link the next generation's attacks
                            // (srnn_ordered_sh.h)
+  OP_ORD_PLAN = 24,     // the plan of a single-rank reference-order generation into o_src / o_list /
+                        // o_ctl / ptab: its attack lists linked into heads / nexts (NIL on entry),
+                        // source versions, stored-output marks, pending records + consumer lists
+                        // (device) or levels (host), the critical turns' permutations.  Weight
+                        // independent: issued on a side stream while the previous generation runs
 };
 
-int srnn_abi_version();  // 26
+int srnn_abi_version();  // 27
 int64_t srnn_args_size();  // sizeof(SrnnArgs): the ctypes mirror checks its layout against it
 int64_t srnn_cfg_size();
 int srnn_has_config(const SrnnCfg* cfg);

@@ -1996,7 +1996,7 @@ __global__ __launch_bounds__(TB) void k_ordbig_close(SrnnCfg c, SrnnArgs a) {
   float w[T::P];
   R::load_staged(a.W, r < a.n ? (int32_t)r : -1, w, s_stg);
   if (r < a.n) {
-    if (a.o_src[4 * r + 3] < 0) atomicOr(a.o_ctl + ord::ERRW, 4);  // never ran: a scheduling bug
+    if (a.o_src[4 * r + 3] < 0) atomicOr(a.o_ctl + ord::ERRW, ord::ERR_NOT_RUN);  // never ran: a scheduling bug
     const int64_t ja = ord::last_attacker_before(a, r, a.n);
     a.heads[r] = SRNN_NIL;  // consumed: NIL for the generation after next
     if (ja > r) {  // attacked after its own turn: the last attack's output
@@ -2004,9 +2004,11 @@ __global__ __launch_bounds__(TB) void k_ordbig_close(SrnnCfg c, SrnnArgs a) {
       R::store(R::at(a.W, r), w);
     }
     rs = a.respawn[r] != 0;
-    int64_t at, te;
-    Dec::decision(a, r, gen + 1, at, te);
-    if (at >= 0) Dec::link(a.heads_next, a.nexts_next, at, (uint32_t)r);
+    if (!(a.flags & SRNN_F_ORD_PLANNED)) {  // (planned ahead: the next OP_ORD_PLAN links them)
+      int64_t at, te;
+      Dec::decision(a, r, gen + 1, at, te);
+      if (at >= 0) Dec::link(a.heads_next, a.nexts_next, at, (uint32_t)r);
+    }
     if (census) k = sclassify<T, S>(w, RowSummary<T>(w), a.eps, (a.flags & SRNN_F_FIX_SEC) != 0, c.aggregator);
   }
   if ((a.flags & SRNN_F_GEN_COUNTS) && gb == 0 && lane == 0) Dec::set_gen(a, gen + 1);
@@ -2029,29 +2031,20 @@ __global__ __launch_bounds__(TB) void k_ordbig_close(SrnnCfg c, SrnnArgs a) {
 // sample); the finish (uids, census, counter) follows unless the caller batches it
 template <class T, class S, bool SHUF>
 int big_soup_ordered(const SrnnCfg& c, const SrnnArgs& a) {
-  if (a.world > 1 || a.lo != 0 || a.n_total != a.n || a.n >= (int64_t)(1 << 30)) {
-    set_error("ordered soup generation: one unsharded table of < 2^30 rows");
-    return -5;
-  }
-  if (!a.W || !a.W2 || !a.W3 || !a.o_src || !a.o_list || !a.o_ctl || !a.heads || !a.nexts || !a.heads_next ||
-      !a.nexts_next || !a.respawn || !(a.flags & SRNN_F_TWO_PHASE) || !a.temp) {
-    set_error("ordered soup generation needs W, W2, W3, o_src, o_list, o_ctl, both attack lists, respawn and "
-              "two-phase block stats (temp)");
+  const bool planned = (a.flags & SRNN_F_ORD_PLANNED) != 0;
+  if (!ord_single_table(a)) return -5;
+  if (!a.W || !a.W2 || !a.W3 || !a.o_src || !a.o_list || !a.o_ctl || !a.heads || !a.nexts ||
+      (!planned && (!a.heads_next || !a.nexts_next)) || !a.respawn || !(a.flags & SRNN_F_TWO_PHASE) || !a.temp) {
+    set_error("ordered soup generation needs W, W2, W3, o_src, o_list, o_ctl, the attack lists (both unless "
+              "planned ahead), respawn and two-phase block stats (temp)");
     return -5;
   }
   const int64_t nb = (a.n + TB - 1) / TB;
   if (nb <= 0) return 0;
   hipStream_t st = (hipStream_t)a.stream;
-  hipLaunchKernelGGL((k_ord_plan<1>), dim3((unsigned)nb), dim3(TB), 0, st, c, a);
-  hipLaunchKernelGGL((k_ord_mark<1>), dim3((unsigned)nb), dim3(TB), 0, st, c, a);
-  SrnnArgs ra = a;
-  const bool crit = knob(SRNN_KNOB_ORD_CRIT, 1) != 0;
-  if (knob(SRNN_KNOB_ORD_QUEUE, 1) != 0) ra.flags |= SRNN_F_ORD_QUEUE;
-  if (crit) {
-    ra.flags |= SRNN_F_ORD_CRIT;
-    ra.x_groups = (int32_t)std::min<int64_t>(nb, (ord::rec_total(a.n) + TB - 1) / TB);
-  }
-  hipLaunchKernelGGL((k_ord_count<1>), dim3((unsigned)nb), dim3(TB), 0, st, c, ra);
+  if (!planned) ord_plan_dev<1, void>(c, a, false);
+  const SrnnArgs ra = ord_run_args(a, nb);
+  const bool crit = (ra.flags & SRNN_F_ORD_CRIT) != 0;
   hipLaunchKernelGGL((k_ord_run<BigOrdPol<T, S, SHUF>>), dim3((unsigned)(nb + (crit ? ra.x_groups : 0))), dim3(TB), 0,
                      st, c, ra);
   hipLaunchKernelGGL((k_ordbig_close<T, S, SHUF>), dim3((unsigned)nb), dim3(TB), 0, st, c, a);
@@ -2092,6 +2085,14 @@ int big_run_s(int op, const SrnnCfg& c, const SrnnArgs& a) {
       if (r) return r;
       break;
     }
+    case OP_ORD_PLAN:  // (shape independent, recompute depth 1: soup_ord_plan's device path)
+      if (!ord_single_table(a)) return -5;
+      if (!a.o_src || !a.o_list || !a.o_ctl || !a.heads || !a.nexts) {
+        set_error("ordered generation plan needs o_src, o_list, o_ctl and the planned generation's attack lists");
+        return -5;
+      }
+      ord_plan_dev<1, void>(c, a, true);
+      break;
     case OP_SOUP_DECIDE: {
       // decisions are shape independent: every global slot
       if (a.n_total <= 0) return 0;
@@ -2113,7 +2114,7 @@ int big_run_s(int op, const SrnnCfg& c, const SrnnArgs& a) {
 constexpr bool big_serves(int op, int dtype, int shuffler) {
   if (op == OP_INIT || op == OP_PERTURB || op == OP_RESPAWN || op == OP_APPLY || op == OP_CLASSIFY ||
       op == OP_TRAIN || op == OP_LEARN || op == OP_SOUP_EVOLVE || op == OP_RESPAWN_SEQ || op == OP_SOUP_DECIDE ||
-      op == OP_SOUP_ORDERED)
+      op == OP_SOUP_ORDERED || op == OP_ORD_PLAN)
     return true;
   return op == OP_RUN_FIXPOINT && dtype == 0 && shuffler == 0;
 }

@@ -78,6 +78,7 @@ const char* op_name(int op) {
     case OP_X2_POST: return "srnn:x2_post";
     case OP_SOUP_ORDERED: return "srnn:soup_ordered";
     case OP_SOUP_ORDERED_SH: return "srnn:soup_ordered_sh";
+    case OP_ORD_PLAN: return "srnn:ord_plan";
     default: return "srnn:op";
   }
 }
@@ -202,7 +203,7 @@ static int with_scratch(int op, const SrnnCfg* c, const SrnnArgs* a) {
 
 extern "C" {
 
-int srnn_abi_version() { return 26; }
+int srnn_abi_version() { return 27; }
 
 
 // layout check of the ctypes mirror (ops/_lib.py): sizeof(SrnnArgs) / sizeof(SrnnCfg)

@@ -11,6 +11,7 @@
 #include "srnn_core.h"
 #include "srnn_abi.h"
 #include <thread>
+#include <type_traits>
 #include <vector>
 #include <algorithm>
 #include <climits>
@@ -1968,6 +1969,7 @@ int run_net_op(int op, const SrnnCfg& c, const SrnnArgs& a) {
     case OP_SOUP_SEQ: return soup_seq<Net, S>(c, a);
     case OP_SOUP_ORDERED: return soup_ordered<Net, S>(c, a);
     case OP_SOUP_ORDERED_SH: return soup_ordered_sh<Net, S>(c, a);
+    case OP_ORD_PLAN: return soup_ord_plan<Net, S>(c, a);
     default: set_error("unknown op"); return -1;
   }
 }

@@ -60,11 +60,16 @@ constexpr int32_t SRC_ATK = INT32_MIN + 1;
 constexpr int32_t SRC_NONE = INT32_MIN + 2;
 constexpr int MAX_LEVELS = 16;  // dependency levels reported one by one (deeper: one bin)
 // o_ctl words: [MAXLW] deepest level (host path), [ERRW] error bits -- STICKY: set by any
-// generation, never cleared by the next one (2: an unstored attack output past the recompute
-// depth, a marking bug; 4: a turn that never ran; 8: a ready-queue entry never written), [PART0 + p] records (pending turns) of
+// generation, never cleared by the next one (ERR_* below; SoupEngine.ORD_ERRORS lists them),
+// [PART0 + p] records (pending turns) of
 // partition p, [CRIT0 + p] producers of later turns in partition p (the producer's block mod
 // NPART; k_ord_count appends a producer when its first consumer registers)
 constexpr int MAXLW = 17, ERRW = 18;
+constexpr int32_t ERR_UNSTORED = 2;  // an attack output past the recompute depth left unstored (marking bug)
+constexpr int32_t ERR_NOT_RUN = 4;   // a turn that never ran (scheduling bug)
+constexpr int32_t ERR_QUEUE = 8;     // a ready-queue entry never written (scheduling bug)
+constexpr int32_t ERR_PACK = 16;     // sharded: a level's records overflowed the send buffer (sizing bug)
+// (32: set by the engine -- a one-rank timing model of a sharded generation ran 1/R of the turns)
 // pending records (and the run order) live in NPART partitions (partition p: the workgroups
 // b = p mod NPART, appended by one counter each: no chip-wide contended counter)
 constexpr int NPART = 64, PART0 = 2 * MAX_LEVELS + 3;
@@ -83,6 +88,12 @@ constexpr int REC = 32;    // record words: {turn, np, producers[NPROD], count, 
 constexpr int R_PROD = 2, R_CNT = R_PROD + NPROD, R_RDY = R_CNT + 1, R_NEXT = R_RDY + 1;
 constexpr int32_t EMPTY = -1;
 static_assert(R_NEXT + NPROD <= REC, "record layout");
+
+// the generation a plan is for: the one in flight, or -- SRNN_F_ORD_NEXT, OP_ORD_PLAN issued one
+// generation ahead on a side stream -- the one after it
+SRNN_HD int32_t plan_gen(const SrnnArgs& a) {
+  return (a.gen_ptr ? a.gen_ptr[0] : a.gen) + ((a.flags & SRNN_F_ORD_NEXT) ? 1 : 0);
+}
 
 SRNN_HD int32_t code_A(int64_t j) { return (int32_t)(2 * j); }
 SRNN_HD int32_t code_E(int64_t j) { return (int32_t)(2 * j + 1); }
@@ -411,7 +422,19 @@ __device__ __forceinline__ void publish(const SrnnArgs& a, int64_t k, int32_t& r
 
 }  // namespace ord
 
-// (plan / mark / count: shape independent, one instantiation per recompute depth)
+// (link / plan / mark / count: shape independent, one instantiation per recompute depth)
+// OP_ORD_PLAN: the planned generation's attack lists -- every row joins its victim's list (the
+// lists are NIL on entry: the close two generations before consumed them)
+template <int RB>
+__global__ __launch_bounds__(TB) void k_ord_link(SrnnArgs a) {
+  using Dec = typename ord::OrdSched<RB>::Dec;
+  const int64_t r = (int64_t)blockIdx.x * TB + threadIdx.x;
+  if (r >= a.n) return;
+  int64_t at, te;
+  Dec::decision(a, r, ord::plan_gen(a), at, te);
+  if (at >= 0) Dec::link(a.heads, a.nexts, at, (uint32_t)r);
+}
+
 template <int RB>
 __global__ __launch_bounds__(TB) void k_ord_plan(SrnnCfg, SrnnArgs a) {
   const int64_t k = (int64_t)blockIdx.x * TB + threadIdx.x;
@@ -420,7 +443,7 @@ __global__ __launch_bounds__(TB) void k_ord_plan(SrnnCfg, SrnnArgs a) {
     for (int w = threadIdx.x; w < ord::CTL_WORDS; w += TB)
       if (w != ord::ERRW) a.o_ctl[w] = 0;
   if (k < a.n) {
-    ord::OrdSched<RB>::plan(a, k, a.gen_ptr ? a.gen_ptr[0] : a.gen);
+    ord::OrdSched<RB>::plan(a, k, ord::plan_gen(a));
     ord::ready_queue(a)[k] = ord::EMPTY;  // (at most one queue entry per pending turn: < n)
   }
 }
@@ -444,7 +467,7 @@ __global__ __launch_bounds__(TB) void k_ord_count(SrnnCfg, SrnnArgs a) {
   int np = 0;
   bool bad = false;
   if (valid) np = O::producers(a, k, nullptr, bad);
-  if (bad) atomicOr(a.o_ctl + ord::ERRW, 2);
+  if (bad) atomicOr(a.o_ctl + ord::ERRW, ord::ERR_UNSTORED);
   const bool pend = valid && np > 0;
   const int part = (int)(blockIdx.x % ord::NPART);
   const int32_t i = ord::wave_append(a.o_ctl + ord::PART0 + part, pend);
@@ -483,7 +506,7 @@ __global__ __launch_bounds__(TB) void k_ord_ptab(SrnnArgs a, int32_t E) {
   const int part = ((int)blockIdx.y / npair) % ord::NPART, p = (int)blockIdx.y % npair;
   const int64_t cap = ord::rec_cap(a.n), stride = 2 * ord::rec_total(a.n);
   const int64_t cnt = ord::ld_level(a.o_ctl + (grp ? ord::CRIT0 : ord::PART0) + part), q0 = part * cap;
-  const int32_t gen = a.gen_ptr ? a.gen_ptr[0] : a.gen;
+  const int32_t gen = ord::plan_gen(a);
   const Rng rng{(uint32_t)a.seed, (uint32_t)(a.seed >> 32)};
   const uint32_t c0 = (uint32_t)gen * 1024u + 512u + 2u * (uint32_t)p;  // even: one draw, two epochs
   for (int64_t i = (int64_t)blockIdx.x * TB + threadIdx.x; i < cnt; i += (int64_t)gridDim.x * TB) {
@@ -629,7 +652,7 @@ __global__ __launch_bounds__(TB) void k_ord_run(SrnnCfg c, SrnnArgs a) {
         // and the entry skipped, rather than a wave that never ends)
         int32_t q, polls = 0;
         while ((q = ord::ld_level(qa + qb + lane)) == ord::EMPTY && ++polls < (1 << 24)) __builtin_amdgcn_s_sleep(1);
-        if (q == ord::EMPTY) atomicOr(a.o_ctl + ord::ERRW, 8);
+        if (q == ord::EMPTY) atomicOr(a.o_ctl + ord::ERRW, ord::ERR_QUEUE);
         else prow = q;
       }
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
@@ -697,13 +720,15 @@ __global__ __launch_bounds__(TB) void k_ord_close(SrnnCfg c, SrnnArgs a) {
   bool rs = false;
   int8_t k = -1;
   if (r < a.n) {
-    if (a.o_src[4 * r + 3] < 0) atomicOr(a.o_ctl + ord::ERRW, 4);  // never ran: a scheduling bug
+    if (a.o_src[4 * r + 3] < 0) atomicOr(a.o_ctl + ord::ERRW, ord::ERR_NOT_RUN);  // never ran: a scheduling bug
     float w[Net::P];
     ord::Ord<Net, S>::close_row(c, a, r, gen, perm, w);
     rs = a.respawn[r] != 0;
-    int64_t at, te;
-    I::decision(a, r, gen + 1, at, te);
-    if (at >= 0) I::link(a.heads_next, a.nexts_next, at, (uint32_t)r);
+    if (!(a.flags & SRNN_F_ORD_PLANNED)) {  // (planned ahead: the next OP_ORD_PLAN links them)
+      int64_t at, te;
+      I::decision(a, r, gen + 1, at, te);
+      if (at >= 0) I::link(a.heads_next, a.nexts_next, at, (uint32_t)r);
+    }
     if (census)
       k = I::classify_w(w, a.eps, (a.flags & SRNN_F_FIX_SEC) != 0, I::actx(a, c, (uint64_t)r, 0x7FFFFFF0u, perm));
   }
@@ -724,7 +749,115 @@ __global__ __launch_bounds__(TB) void k_ord_close(SrnnCfg c, SrnnArgs a) {
 }
 
 #include "srnn_pair.h"
-#include "srnn_ordered_sh.h"
+
+// The plan of a reference-order generation (o_src / o_list / o_ctl / ptab): weight independent --
+// decisions are a pure function of (seed, slot, generation) -- so the engine issues it one
+// generation ahead (OP_ORD_PLAN with SRNN_F_ORD_NEXT) on a side stream, beside the generation in
+// flight, whose run launch leaves most of the chip idle behind its few dependent chains; the
+// generation itself (SRNN_F_ORD_PLANNED) is then run + close.  `link`: the planned generation's
+// attack lists are linked into heads / nexts first (else they are this generation's, linked by
+// the previous close).
+
+// the run (and count) launch's scheduling flags from the knobs, and the critical-list waves: the
+// list holds at most one entry per pending record's producer slot; waves past its end return
+inline SrnnArgs ord_run_args(const SrnnArgs& a, int64_t nb) {
+  SrnnArgs ra = a;
+  if (knob(SRNN_KNOB_ORD_QUEUE, 1) != 0) ra.flags |= SRNN_F_ORD_QUEUE;
+  if (knob(SRNN_KNOB_ORD_CRIT, 1) != 0) {
+    ra.flags |= SRNN_F_ORD_CRIT;
+    ra.x_groups = (int32_t)std::min<int64_t>(nb, (ord::rec_total(a.n) + TB - 1) / TB);
+  }
+  return ra;
+}
+
+// device: [link ->] plan -> mark -> count (records, consumer lists, critical list) -> the
+// critical turns' epoch permutations (PT: the nibble Weightwise net of the table, void: none)
+template <int RB, class PT>
+void ord_plan_dev(const SrnnCfg& c, const SrnnArgs& a, bool link) {
+  const int64_t nb = (a.n + TB - 1) / TB;
+  if (nb <= 0) return;
+  hipStream_t st = (hipStream_t)a.stream;
+  if (link) hipLaunchKernelGGL((k_ord_link<RB>), dim3((unsigned)nb), dim3(TB), 0, st, a);
+  hipLaunchKernelGGL((k_ord_plan<RB>), dim3((unsigned)nb), dim3(TB), 0, st, c, a);
+  hipLaunchKernelGGL((k_ord_mark<RB>), dim3((unsigned)nb), dim3(TB), 0, st, c, a);
+  const SrnnArgs ra = ord_run_args(a, nb);
+  hipLaunchKernelGGL((k_ord_count<RB>), dim3((unsigned)nb), dim3(TB), 0, st, c, ra);
+  if constexpr (!std::is_void_v<PT>) {
+    const int32_t E = (a.severity > 0 ? a.severity : 0) + (a.epochs > 0 ? a.epochs : 0);
+    if (a.ptab && (a.flags & SRNN_F_SHUFFLE) && E > 0) {
+      const bool crit = (ra.flags & SRNN_F_ORD_CRIT) != 0;
+      const int64_t est = std::max<int64_t>(a.n / 12 / ord::NPART, 1);
+      hipLaunchKernelGGL((k_ord_ptab<PT>),
+                         dim3((unsigned)((est + TB - 1) / TB), (unsigned)((crit ? 2 : 1) * ord::NPART * ((E + 1) / 2))),
+                         dim3(TB), 0, st, a, E);
+    }
+  }
+}
+
+// host: [link ->] plan -> mark -> every turn's level (producers precede their consumers in index
+// order); o_ctl[MAXLW] the deepest level
+template <int RB>
+void ord_plan_host(const SrnnArgs& a, bool link) {
+  using O = ord::OrdSched<RB>;
+  const int32_t gen = ord::plan_gen(a);
+  for (int w = 0; w < ord::CTL_WORDS; ++w)
+    if (w != ord::ERRW) a.o_ctl[w] = 0;
+  if (link)
+    for (int64_t r = 0; r < a.n; ++r) {
+      int64_t at, te;
+      O::Dec::decision(a, r, gen, at, te);
+      if (at >= 0) {
+        a.nexts[r] = a.heads[at];
+        a.heads[at] = (uint32_t)r;
+      }
+    }
+  host_parallel(a.n, [&](int64_t k) { O::plan(a, k, gen); });
+  for (int64_t k = 0; k < a.n; ++k) O::mark(a, k);
+  int32_t maxl = 0;
+  for (int64_t k = 0; k < a.n; ++k) {
+    int32_t pr[ord::NPROD];
+    bool bad = false;
+    const int np = O::producers(a, k, pr, bad);
+    if (bad) a.o_ctl[ord::ERRW] |= ord::ERR_UNSTORED;
+    int32_t lv = 0;
+    for (int q = 0; q < np; ++q) lv = std::max(lv, a.o_src[4 * (int64_t)pr[q] + 3] + 1);
+    a.o_src[4 * k + 3] = lv;
+    maxl = std::max(maxl, lv);
+  }
+  a.o_ctl[ord::MAXLW] = maxl;
+}
+
+// a single unsharded table of < 2^30 rows (int32 version codes)
+inline bool ord_single_table(const SrnnArgs& a) {
+  if (a.world > 1 || a.lo != 0 || a.n_total != a.n || a.n >= (int64_t)(1 << 30)) {
+    set_error("ordered soup generation: one unsharded table of < 2^30 rows");
+    return false;
+  }
+  return true;
+}
+
+// OP_ORD_PLAN of a lane-template net (the big aggregating nets: srnn_bignet.h)
+template <class Net, class S>
+int soup_ord_plan(const SrnnCfg& c, const SrnnArgs& a) {
+  constexpr int RB = ord::Ord<Net, S>::RB;
+  if (!ord_single_table(a)) return -5;
+  if (!a.o_src || !a.o_list || !a.o_ctl || !a.heads || !a.nexts) {
+    set_error("ordered generation plan needs o_src, o_list, o_ctl and the planned generation's (NIL) attack lists");
+    return -5;
+  }
+  if (!a.dev) {
+    ord_plan_host<RB>(a, true);
+    return 0;
+  }
+  using PT = std::conditional_t<(Net::KIND == 0 && Net::P <= 16), Net, void>;
+  ord_plan_dev<RB, PT>(c, a, true);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) {
+    set_error(hipGetErrorString(e));
+    return -3;
+  }
+  return 0;
+}
 
 // OP_SOUP_ORDERED: one sequential (reference-order) generation of a single-rank table.
 // W2: generation-start rows, W: the generation's rows (E versions, then the final table),
@@ -732,45 +865,32 @@ __global__ __launch_bounds__(TB) void k_ord_close(SrnnCfg c, SrnnArgs a) {
 // o_levels: dependency levels the host path runs as separate passes (the rest: one pass per
 // level as well; the device schedules by continuation and ignores it);
 // heads / nexts: this generation's attack lists (consumed), heads_next / nexts_next: the
-// next generation's (linked here).  Device: the block stats of the two-phase fused
+// next generation's (linked here, unless SRNN_F_ORD_PLANNED: the plan was built ahead by
+// OP_ORD_PLAN, which links its own lists).  Device: the block stats of the two-phase fused
 // generation in temp (SRNN_F_TWO_PHASE); host: the finish inline (uids, census, counter).
 template <class Net, class S>
 int soup_ordered(const SrnnCfg& c, const SrnnArgs& a) {
   using I = Item<Net, S>;
   using O = ord::Ord<Net, S>;
-  if (a.world > 1 || a.lo != 0 || a.n_total != a.n || a.n >= (int64_t)(1 << 30)) {
-    set_error("ordered soup generation: one unsharded table of < 2^30 rows");
-    return -5;
-  }
-  if (!a.W || !a.W2 || !a.W3 || !a.o_src || !a.o_list || !a.o_ctl || !a.heads || !a.nexts || !a.heads_next ||
-      !a.nexts_next || !a.respawn || a.o_levels < 1 || a.o_levels > ord::MAX_LEVELS) {
-    set_error("ordered soup generation needs W, W2, W3, o_src, o_list, o_ctl, both attack lists, respawn and "
-              "1 <= o_levels <= 16");
+  const bool planned = (a.flags & SRNN_F_ORD_PLANNED) != 0;
+  if (!ord_single_table(a)) return -5;
+  if (!a.W || !a.W2 || !a.W3 || !a.o_src || !a.o_list || !a.o_ctl || !a.heads || !a.nexts ||
+      (!planned && (!a.heads_next || !a.nexts_next)) || !a.respawn || a.o_levels < 1 ||
+      a.o_levels > ord::MAX_LEVELS) {
+    set_error("ordered soup generation needs W, W2, W3, o_src, o_list, o_ctl, the attack lists (both unless "
+              "planned ahead), respawn and 1 <= o_levels <= 16");
     return -5;
   }
   if (!a.dev) {
     const int32_t gen = I::gen_of(a);
-    for (int w = 0; w < ord::CTL_WORDS; ++w)
-      if (w != ord::ERRW) a.o_ctl[w] = 0;
-    host_parallel(a.n, [&](int64_t k) { O::plan(a, k, gen); });
-    for (int64_t k = 0; k < a.n; ++k) O::mark(a, k);
+    if (!planned) ord_plan_host<O::RB>(a, false);
     // levels in index order (every producer precedes its consumer)
     std::vector<std::vector<int64_t>> lists;
-    int32_t maxl = 0;
     for (int64_t k = 0; k < a.n; ++k) {
-      int32_t* s = a.o_src + 4 * k;
-      int32_t pr[ord::NPROD];
-      bool bad = false;
-      const int np = O::producers(a, k, pr, bad);
-      if (bad) a.o_ctl[ord::ERRW] |= 2;
-      int32_t lv = 0;
-      for (int q = 0; q < np; ++q) lv = std::max(lv, a.o_src[4 * (int64_t)pr[q] + 3] + 1);
-      s[3] = lv;
-      maxl = std::max(maxl, lv);
+      const int32_t lv = a.o_src[4 * k + 3];
       if ((size_t)lv >= lists.size()) lists.resize((size_t)lv + 1);
       lists[(size_t)lv].push_back(k);
     }
-    a.o_ctl[ord::MAXLW] = maxl;
     for (const auto& li : lists)
       host_parallel((int64_t)li.size(), [&](int64_t q) {
         float4 samp[Net::P + 1];
@@ -787,14 +907,15 @@ int soup_ordered(const SrnnCfg& c, const SrnnArgs& a) {
         ks[(size_t)r] = I::classify_w(w, a.eps, (a.flags & SRNN_F_FIX_SEC) != 0,
                                       I::actx(a, c, (uint64_t)r, 0x7FFFFFF0u, perm));
     });
-    for (int64_t r = 0; r < a.n; ++r) {
-      int64_t at, te;
-      I::decision(a, r, gen + 1, at, te);
-      if (at >= 0) {
-        a.nexts_next[r] = a.heads_next[at];
-        a.heads_next[at] = (uint32_t)r;
+    if (!planned)
+      for (int64_t r = 0; r < a.n; ++r) {
+        int64_t at, te;
+        I::decision(a, r, gen + 1, at, te);
+        if (at >= 0) {
+          a.nexts_next[r] = a.heads_next[at];
+          a.heads_next[at] = (uint32_t)r;
+        }
       }
-    }
     uint64_t cs[5] = {0, 0, 0, 0, 0};
     for (int64_t r = 0; r < a.n; ++r)
       if (ks[(size_t)r] >= 0) cs[ks[(size_t)r]]++;
@@ -820,26 +941,10 @@ int soup_ordered(const SrnnCfg& c, const SrnnArgs& a) {
   const int64_t nb = (a.n + TB - 1) / TB;
   if (nb <= 0) return 0;
   hipStream_t st = (hipStream_t)a.stream;
-  hipLaunchKernelGGL((k_ord_plan<O::RB>), dim3((unsigned)nb), dim3(TB), 0, st, c, a);
-  hipLaunchKernelGGL((k_ord_mark<O::RB>), dim3((unsigned)nb), dim3(TB), 0, st, c, a);
-  SrnnArgs ra = a;
-  const bool crit = knob(SRNN_KNOB_ORD_CRIT, 1) != 0;
-  if (knob(SRNN_KNOB_ORD_QUEUE, 1) != 0) ra.flags |= SRNN_F_ORD_QUEUE;
-  if (crit) {
-    ra.flags |= SRNN_F_ORD_CRIT;
-    // critical-list waves of the run launch: the list holds at most one entry per pending
-    // record's producer slot; the launch's waves past its end return at once
-    ra.x_groups = (int32_t)std::min<int64_t>(nb, (ord::rec_total(a.n) + TB - 1) / TB);
-  }
-  hipLaunchKernelGGL((k_ord_count<O::RB>), dim3((unsigned)nb), dim3(TB), 0, st, c, ra);
-  if constexpr (Net::KIND == 0 && Net::P <= 16) {
-    const int32_t E = (a.severity > 0 ? a.severity : 0) + (a.epochs > 0 ? a.epochs : 0);
-    if (a.ptab && (a.flags & SRNN_F_SHUFFLE) && E > 0) {
-      const int64_t est = std::max<int64_t>(a.n / 12 / ord::NPART, 1);
-      hipLaunchKernelGGL((k_ord_ptab<Net>), dim3((unsigned)((est + TB - 1) / TB), (unsigned)((crit ? 2 : 1) * ord::NPART * ((E + 1) / 2))),
-                         dim3(TB), 0, st, a, E);
-    }
-  }
+  using PT = std::conditional_t<(Net::KIND == 0 && Net::P <= 16), Net, void>;
+  if (!planned) ord_plan_dev<O::RB, PT>(c, a, false);
+  const SrnnArgs ra = ord_run_args(a, nb);
+  const bool crit = (ra.flags & SRNN_F_ORD_CRIT) != 0;
   hipLaunchKernelGGL((k_ord_run<OrdLanePol<Net, S>>), dim3((unsigned)(nb + (crit ? ra.x_groups : 0))), dim3(TB), 0, st, c, ra);
   hipLaunchKernelGGL((k_ord_close<Net, S>), dim3((unsigned)nb), dim3(TB), 0, st, c, a);
   if (!(a.flags & SRNN_F_GEN_COUNTS)) {
@@ -853,3 +958,5 @@ int soup_ordered(const SrnnCfg& c, const SrnnArgs& a) {
   }
   return 0;
 }
+
+#include "srnn_ordered_sh.h"

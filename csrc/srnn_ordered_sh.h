@@ -91,7 +91,7 @@ __global__ __launch_bounds__(TB) void k_ordsh_pack(SrnnArgs a, int32_t L) {
   const int32_t pos = ord::wave_append(a.x_ctl, mine);
   if (!mine) return;
   if ((int64_t)pos >= a.x_blk) {  // the caller sized the buffer for this level: a bug
-    atomicOr(a.o_ctl + ord::ERRW, 8);
+    atomicOr(a.o_ctl + ord::ERRW, ord::ERR_PACK);
     return;
   }
   char* r = reinterpret_cast<char*>(a.sendbuf) + (int64_t)pos * RECB;
@@ -133,7 +133,7 @@ __global__ __launch_bounds__(TB) void k_ordsh_close(SrnnCfg c, SrnnArgs a) {
   __shared__ uint8_t s_perm[TB * PERM];
   const int64_t r = a.o_lo + (int64_t)blockIdx.x * TB + threadIdx.x;
   if (r >= a.o_hi) return;
-  if (a.o_src[4 * r + 3] < 0) atomicOr(a.o_ctl + ord::ERRW, 4);
+  if (a.o_src[4 * r + 3] < 0) atomicOr(a.o_ctl + ord::ERRW, ord::ERR_NOT_RUN);
   float w[Net::P];
   ord::Ord<Net, S>::close_row(c, a, r, I::gen_of(a), s_perm + threadIdx.x * PERM, w);
   if (a.rowflags) a.rowflags[r] = a.respawn[r] != 0;
@@ -178,25 +178,9 @@ int soup_ordered_sh(const SrnnCfg& c, const SrnnArgs& a) {
   const int64_t nrec = phase == ordsh::UNPACK ? (int64_t)a.world * a.x_blk : 0;
   if (!a.dev) {
     switch (phase) {
-      case ordsh::PLAN: {
-        for (int w = 0; w < ord::CTL_WORDS; ++w)
-          if (w != ord::ERRW) a.o_ctl[w] = 0;
-        host_parallel(a.n, [&](int64_t k) { O::plan(a, k, gen); });
-        for (int64_t k = 0; k < a.n; ++k) O::mark(a, k);
-        int32_t maxl = 0;
-        for (int64_t k = 0; k < a.n; ++k) {  // producers precede their consumers
-          int32_t pr[ord::NPROD];
-          bool bad = false;
-          const int np = O::producers(a, k, pr, bad);
-          if (bad) a.o_ctl[ord::ERRW] |= 2;
-          int32_t lv = 0;
-          for (int q = 0; q < np; ++q) lv = std::max(lv, a.o_src[4 * (int64_t)pr[q] + 3] + 1);
-          a.o_src[4 * k + 3] = lv;
-          maxl = std::max(maxl, lv);
-        }
-        a.o_ctl[ord::MAXLW] = maxl;
+      case ordsh::PLAN:
+        ord_plan_host<O::RB>(a, false);
         return 0;
-      }
       case ordsh::LEVEL: {
         std::vector<int64_t> li;
         for (int64_t k = a.o_lo; k < a.o_hi; ++k)
@@ -213,7 +197,7 @@ int soup_ordered_sh(const SrnnCfg& c, const SrnnArgs& a) {
         for (int64_t k = a.o_lo; k < a.o_hi; ++k) {
           if (a.o_src[4 * k + 3] != L) continue;
           if (pos >= a.x_blk) {
-            a.o_ctl[ord::ERRW] |= 8;
+            a.o_ctl[ord::ERRW] |= ord::ERR_PACK;
             break;
           }
           char* r = reinterpret_cast<char*>(a.sendbuf) + pos * RECB;

@@ -306,8 +306,86 @@ static void seq_soup(const SrnnCfg& c, int64_t n, int steps) {
   CHECK(W[0] == W[1] && uid[0] == uid[1] && next[0] == next[1] && gen[0][0] == 1 + steps && gen[1][0] == 1 + steps);
 }
 
+// ---- reference-order generation (OP_SOUP_ORDERED): the plan inline, or built one generation
+// ahead by OP_ORD_PLAN into the other of two plan sets (SRNN_F_ORD_PLANNED / _NEXT), both
+// bitwise the serial loop (OP_SOUP_SEQ) ---------------------------------------------------------
+static int64_t ord_words(int64_t n) {  // ops/_lib.py ord_src_words
+  const int64_t rec = 64 * ((((n + 63) / 64) + 63) / 64) * 64;
+  return 6 * n + 34 * rec;
+}
+static void ordered_soup(const SrnnCfg& c, int64_t n, int gens, bool pipe) {
+  const size_t R = (size_t)(n * c.pp);
+  std::vector<float> seqW(R), buf[2] = {std::vector<float>(R), std::vector<float>(R)}, W3(R);
+  std::vector<int64_t> suid((size_t)n), uid((size_t)n), snext(1, n), next(1, n), scp((size_t)n), cp((size_t)n);
+  std::vector<int32_t> sgen(1, 1), ring = {1, 1}, osrc[2], olist[2], octl[2];
+  std::vector<uint32_t> heads[2], nexts[2];
+  std::vector<int8_t> sact((size_t)n), act((size_t)n), srs((size_t)n), rs((size_t)n);
+  std::vector<float> sloss((size_t)n), loss((size_t)n);
+  std::vector<uint64_t> counts(6, 0);
+  for (int q = 0; q < 2; ++q) {
+    osrc[q].assign((size_t)ord_words(n), 0), olist[q].assign((size_t)n, 0), octl[q].assign(165, 0);
+    heads[q].assign((size_t)n, 0xFFFFFFFFu), nexts[q].assign((size_t)n, 0xFFFFFFFFu);
+  }
+  for (int64_t j = 0; j < n; ++j) suid[(size_t)j] = uid[(size_t)j] = j;
+  SrnnArgs ia{};
+  ia.n = n, ia.seed = 19, ia.W = seqW.data(), ia.uid = suid.data();
+  run(OP_INIT, c, ia);
+  buf[0] = seqW;
+  auto base = [&]() {
+    SrnnArgs a{};
+    a.n = a.n_total = n, a.seed = 19, a.lr = 0.01f, a.eps = 1e-4f;
+    a.attacking_rate = 0.3f, a.learn_from_rate = 0.3f, a.epochs = 2, a.severity = 2;
+    a.flags = SRNN_F_SHUFFLE | SRNN_F_REMOVE_DIVERGENT | SRNN_F_REMOVE_ZERO | SRNN_F_FUSED_CENSUS;
+    return a;
+  };
+  SrnnArgs sa = base();
+  sa.W = seqW.data(), sa.gen_ptr = sgen.data(), sa.uid_base = snext.data(), sa.uid_out = suid.data();
+  sa.action = sact.data(), sa.counterpart = scp.data(), sa.loss = sloss.data(), sa.respawn = srs.data();
+  sa.steps = gens;
+  run(OP_SOUP_SEQ, c, sa);
+  auto plan_args = [&](int q, bool nxt, int p) {
+    SrnnArgs a = base();
+    a.gen_ptr = ring.data() + p;
+    a.o_src = osrc[q].data(), a.o_list = olist[q].data(), a.o_ctl = octl[q].data();
+    a.heads = heads[q].data(), a.nexts = nexts[q].data();
+    if (nxt) a.flags |= SRNN_F_ORD_NEXT;
+    return a;
+  };
+  int p = 0;
+  if (pipe) {
+    run(OP_ORD_PLAN, c, plan_args(0, false, 0));
+  } else {
+    SrnnArgs d = base();
+    d.gen_ptr = ring.data(), d.heads = heads[0].data(), d.nexts = nexts[0].data();
+    run(OP_SOUP_DECIDE, c, d);
+  }
+  for (int g = 0; g < gens; ++g) {
+    const int q = pipe ? p : 0;
+    if (pipe) run(OP_ORD_PLAN, c, plan_args(1 - p, true, p));
+    SrnnArgs a = base();
+    a.W2 = buf[p].data(), a.W = buf[1 - p].data(), a.W3 = W3.data();
+    a.gen_ptr = ring.data() + p, a.gen_out = ring.data() + (1 - p);
+    a.o_src = osrc[q].data(), a.o_list = olist[q].data(), a.o_ctl = octl[q].data(), a.o_levels = 4;
+    a.heads = heads[p].data(), a.nexts = nexts[p].data();
+    a.heads_next = heads[1 - p].data(), a.nexts_next = nexts[1 - p].data();
+    a.uid_base = next.data(), a.uid_out = uid.data(), a.counts = counts.data();
+    a.action = act.data(), a.counterpart = cp.data(), a.loss = loss.data(), a.respawn = rs.data();
+    if (pipe) a.flags |= SRNN_F_ORD_PLANNED;
+    run(OP_SOUP_ORDERED, c, a);
+    CHECK(octl[q][18] == 0);  // error bits
+    p = 1 - p;
+  }
+  CHECK(std::memcmp(buf[p].data(), seqW.data(), R * 4) == 0);
+  CHECK(uid == suid && next == snext && act == sact && rs == srs && cp == scp);
+  CHECK(std::memcmp(loss.data(), sloss.data(), (size_t)n * 4) == 0);
+  CHECK(ring[(size_t)p] == sgen[0]);
+}
+
 int main() {
-  CHECK(srnn_abi_version() == 26);
+  CHECK(srnn_abi_version() == 27);
+  ordered_soup(ww22(), 257, 4, true);
+  ordered_soup(ww22(), 257, 4, false);
+  ordered_soup(agg422(), 129, 3, true);
   seq_soup(ww22(), 257, 4);
   seq_soup(agg422(), 129, 3);
   ops_smoke(ww22(), 1000);

@@ -117,6 +117,9 @@ class ExecConfig:
     perm_table: Optional[bool] = None       # SRNN_PERM_TABLE: a generation's SGD permutations precomputed by
                                             # one launch ahead of it (nibble Weightwise nets on the device;
                                             # None: the reference order's pending turns only)
+    ord_pipeline: bool = True               # SRNN_ORD_PIPELINE: a single-rank reference-order generation's plan
+                                            # (lists, versions, records, permutations) is built one generation
+                                            # ahead on a side stream, beside the generation in flight
 
     _ENV = dict(finish_mode="SRNN_FINISH_MODE", finish_par="SRNN_FINISH_PAR", graph_chunks="SRNN_GRAPH_CHUNKS",
                 x2_schedule="SRNN_X2_SCHEDULE", x2_prio="SRNN_X2_PRIO", x2_emulate_remote="SRNN_X2_EMULATE_REMOTE",
@@ -126,7 +129,7 @@ class ExecConfig:
                 fix_group="SRNN_FIX_GROUP", soup_lanes="SRNN_SOUP_LANES", ord_crit="SRNN_ORD_CRIT", ord_queue="SRNN_ORD_QUEUE",
                 ordsh_emulate="SRNN_ORDSH_EMULATE",
                 order_levels="SRNN_ORDER_LEVELS",
-                perm_table="SRNN_PERM_TABLE")
+                perm_table="SRNN_PERM_TABLE", ord_pipeline="SRNN_ORD_PIPELINE")
     # Optional[bool] knobs whose None means "the built-in choice" (by population size, ...)
     TRI_STATE = ("force_generic", "rnn_wave", "rnn_spec", "rnn_soup", "big_wave", "fix_group", "perm_table",
                  "ord_crit", "ord_queue")

@@ -158,7 +158,15 @@ def _fill_rows(path: str, lo: int, hi: int, P: int, rows: torch.Tensor, uid: tor
 
 
 def save_engine(eng, path: str, chunk_bytes: int = CHUNK_BYTES) -> str:
-    """Write this rank's shard (+ the manifest on rank 0). Collective when sharded."""
+    """Write this rank's shard (+ the manifest on rank 0). Collective when sharded.  An engine
+    whose rows are invalid (exchange or reference-order error bits on any rank) is refused on
+    every rank before anything is written."""
+    err = eng.exchange_error()
+    oerr = eng.ordered_error_all()
+    if err or oerr:
+        from ..soup_engine import describe_ordered_error
+        why = err or f"reference-order error bits {oerr} ({describe_ordered_error(oerr)})"
+        raise RuntimeError(f"refusing to checkpoint a soup with invalid rows: {why}")
     os.makedirs(path, exist_ok=True)
     _write_shard(path, eng.lo, eng.hi, eng.local_rows(), eng.uid, eng.spec.P, chunk_bytes)
     if eng.dist.rank == 0:

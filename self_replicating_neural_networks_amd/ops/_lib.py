@@ -20,7 +20,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 # SRNN_LIB: load another build of the library (A/B of compiler flags on the GPU box)
 LIB_PATH = os.environ.get("SRNN_LIB") or os.path.join(_HERE, "libsrnn.so")
 CSRC = os.path.normpath(os.path.join(_HERE, "..", "..", "csrc"))
-ABI_VERSION = 26
+ABI_VERSION = 27
 
 # SrnnOp (csrc/srnn_abi.h)
 OP_INIT = 0
@@ -43,6 +43,7 @@ OP_X2_PACK = 20   # sharded soup, all-to-all exchange: finish + next decisions +
 OP_X2_POST = 21   # sharded soup: uids, census, received notices / requests
 OP_SOUP_ORDERED = 22  # reference-order (sequential) generation, DAG-scheduled (csrc/srnn_ordered.h)
 OP_SOUP_ORDERED_SH = 23  # one phase of a sharded reference-order generation (csrc/srnn_ordered_sh.h)
+OP_ORD_PLAN = 24  # the plan of a reference-order generation (lists, versions, records, permutations)
 ORDSH_PLAN, ORDSH_LEVEL, ORDSH_PACK, ORDSH_UNPACK, ORDSH_CLOSE, ORDSH_LINK = range(6)
 ORD_CTL_WORDS = 165   # o_ctl words of an ordered generation (csrc/srnn_ordered.h)
 ORD_MAXLW, ORD_ERRW = 17, 18
@@ -87,6 +88,8 @@ FLAG_X2_PRIO = 1 << 19
 FLAG_X2_BOTH = 1 << 20
 FLAG_X2_POST_FUSED = 1 << 21
 FLAG_PTAB_READY = 1 << 23  # ptab already holds the generation's permutations (the sharded pack built them)
+FLAG_ORD_PLANNED = 1 << 25  # OP_SOUP_ORDERED: the plan is already built (OP_ORD_PLAN one generation ahead)
+FLAG_ORD_NEXT = 1 << 26  # OP_ORD_PLAN: plan generation gen + 1 (the one after the generation in flight)
 
 X2_HDR = 12           # int64 header words of an exchange block
 X2_REMOTE_WAVES = 4096

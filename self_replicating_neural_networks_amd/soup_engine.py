@@ -67,6 +67,17 @@ MAX_SLOTS_DIRECT = 2 ** 32 - 2
 ORDERED_MAX_ROWS = 2 ** 30 - 1
 X2_ERRORS = {1: "exchange capacity overflow (rows, notices or requests dropped)",
              4: "exchange protocol mismatch (row tag / slot range)"}
+# reference-order error bits (csrc/srnn_ordered.h ord::ERR_*), sticky over an engine's life
+ORD_ERRORS = {2: "an attack output past the recompute depth left unstored (marking bug)",
+              4: "a turn that never ran (scheduling bug)",
+              8: "a ready-queue entry never written (scheduling bug)",
+              16: "a level's exchange records overflowed the send buffer (sharded; sizing bug)",
+              32: "a one-rank timing model of a sharded generation (SRNN_ORDSH_EMULATE) ran only 1/R of the turns"}
+ORD_ERR_EMULATED = 32
+
+
+def describe_ordered_error(bits: int) -> str:
+    return "; ".join(f"{b}: {msg}" for b, msg in ORD_ERRORS.items() if bits & b) or f"error bits {bits}"
 
 
 def _p(t):
@@ -116,28 +127,49 @@ def _finish_batch(nb: int, chunks) -> int:
     return max(1, min(max(list(chunks) or [1]), (512 << 20) // (nb * 32)))
 
 
-def ordered_bytes(spec: ArchSpec, n: int, dtype=torch.float32, epochs: int = 0) -> int:
-    """Device bytes of the reference-order generation's buffers for ``n`` rows
-    (SoupEngine._init_ordered): the stored attack outputs W3 (n rows of the table), the turns'
-    source codes + levels, the stored flags and the pending records (csrc/srnn_ordered.h
-    o_src), the tail's list, the control words, and -- nibble Weightwise nets with shuffled
+def ordered_bytes(spec: ArchSpec, n: int, dtype=torch.float32, epochs: int = 0, plan_sets: int = 1) -> int:
+    """Device bytes of the reference-order generation's buffers for ``n`` planned turns
+    (SoupEngine._init_ordered): the stored attack outputs W3 (n rows of the table), and per plan
+    set the turns' source codes + levels, the stored flags and the pending records (csrc/srnn_ordered.h
+    o_src), the turns' record list, the control words, and -- nibble Weightwise nets with shuffled
     SGD on the device -- the pending records' epoch permutations (``epochs`` = train +
-    learn_from_severity)."""
+    learn_from_severity; 0: no table).  ``plan_sets``: 2 for a pipelined single-rank engine (the
+    next generation's plan is built while this one runs)."""
     n1 = max(int(n), 1)
     rb = spec.PP * torch.empty((), dtype=dtype).element_size()
     rec = _lib.ord_rec_total(n1)
-    b = n * rb + 4 * _lib.ord_src_words(n1) + 4 * n1 + 4 * _lib.ORD_CTL_WORDS
+    per_set = 4 * _lib.ord_src_words(n1) + 4 * n1 + 4 * _lib.ORD_CTL_WORDS
     if spec.kind == "weightwise" and spec.P <= 16 and epochs > 0 and (n + 4096) * epochs * 8 <= (2 << 30):
-        b += 2 * rec * epochs * 8  # permutation table: pending records + critical roots
+        per_set += 2 * rec * epochs * 8  # permutation table: pending records + critical roots
+    return int(n * rb + plan_sets * per_set)
+
+
+def sharded_ordered_bytes(spec: ArchSpec, n_total: int, world: int, dtype=torch.float32) -> int:
+    """Device bytes one rank adds for a reference-order soup sharded over ``world`` ranks
+    (csrc/srnn_ordered_sh.h, SoupEngine._init_ordered): every rank plans ALL n_total turns and holds
+    the version tables of all rows -- W3 and the E versions (_fw) -- plus the replicated attack lists
+    of both parities and one level's exchange records (send: its own turns, receive: every rank's).
+    No permutation table (the level launches draw inline)."""
+    rb = spec.PP * torch.empty((), dtype=dtype).element_size()
+    N = max(int(n_total), 1)
+    cap = max(-(-N // world), 1)
+    recb = 16 + 2 * rb  # csrc ordsh::rec_bytes
+    b = ordered_bytes(spec, N, dtype, epochs=0, plan_sets=1)
+    b += N * rb                      # _fw: the E version of every row
+    b += 2 * 2 * N * 4 + 16          # replicated heads + nexts of both parities, level-pack counters
+    b += (1 + world) * cap * recb    # send + receive records of one level
     return int(b)
 
 
 def engine_bytes(spec: ArchSpec, n_total: int, world: int = 1, dtype=torch.float32, exchange: str = "alltoall",
                  attacking_rate: float = 0.1, learn_from_rate: float = 0.1, segment: int = 0,
-                 diagnostics: bool = True, order: str = "synchronous", epochs: int = 0) -> int:
+                 diagnostics: bool = True, order: str = "synchronous", epochs: int = 0,
+                 ord_pipeline: bool = True) -> int:
     """Device bytes one rank of a SoupEngine allocates (the tensors of ``__init__``);
     ``order="sequential"`` adds the reference-order generation's buffers (``ordered_bytes``,
-    ``epochs`` = train + learn_from_severity for its permutation table)."""
+    ``epochs`` = train + learn_from_severity for its permutation table; two plan sets with
+    ``ord_pipeline``).  A sharded reference-order soup runs on the all-gather layout whatever
+    ``exchange`` says, with the replicated plan of ``sharded_ordered_bytes``."""
     R = world
     n = -(-n_total // R)
     rb = spec.PP * torch.empty((), dtype=dtype).element_size()
@@ -145,7 +177,7 @@ def engine_bytes(spec: ArchSpec, n_total: int, world: int = 1, dtype=torch.float
     b = 2 * n * rb + n * 8 + n * 1 + 2 * n * 4 + nb * 8 + 8 * 4  # tables, uid, respawn, heads, ballots
     if diagnostics:
         b += n * (1 + 8 + 4)  # action, counterpart, loss
-    if R > 1 and exchange == "alltoall":
+    if R > 1 and exchange == "alltoall" and order != "sequential":
         cr, cn, cq = x2_capacities(n_total, R, attacking_rate, learn_from_rate, segment)
         xb = rb + 16
         blk = -(-(_lib.X2_HDR * 8 + cr * xb + cn * 16 + cq * 8) // 16) * 16
@@ -157,13 +189,16 @@ def engine_bytes(spec: ArchSpec, n_total: int, world: int = 1, dtype=torch.float
         b += 2 * nb * 32                     # block stats of two generations
         b += 2 * R * blk                     # send + receive buffers
     elif R > 1:
-        b += 2 * n_total * 4 + n_total * rb + n * 4  # links per global slot, gathered table, row flags
+        b += 2 * n_total * 4 + n_total * rb + n * 4 + nb * 32  # links per global slot, gathered table, row flags
     else:
         b += 2 * n * 4 + nb * 32  # links, block stats
         # the batched-finish ring, sized as SoupEngine._init_single_or_allgather sizes it
         b += _finish_batch(nb, ExecConfig().resolved().graph_chunks) * (nb * 8 + 2) * 4
     if order == "sequential":
-        b += ordered_bytes(spec, n, dtype, epochs)
+        if R > 1:
+            b += sharded_ordered_bytes(spec, n_total, R, dtype)
+        else:
+            b += ordered_bytes(spec, n, dtype, epochs, plan_sets=2 if ord_pipeline else 1)
     return int(b)
 
 
@@ -188,7 +223,7 @@ def plan_population(spec: ArchSpec, dtype=torch.float32, exchange: str = "alltoa
         else:
             hi = mid - 1
     n_fit = lo
-    if world > 1 and exchange == "alltoall":
+    if world > 1 and exchange == "alltoall" and order != "sequential":
         # local rows + received rows of a rank stay below 2^32 - 1 (capacities as _init_x2
         # computes them, segment included)
         lo2, hi2 = 1, 1 << 50
@@ -203,8 +238,10 @@ def plan_population(spec: ArchSpec, dtype=torch.float32, exchange: str = "alltoa
     else:
         limit = MAX_SLOTS_DIRECT
     why = "uint32 list entries"
-    if order == "sequential" and ORDERED_MAX_ROWS * world < limit:
-        limit, why = ORDERED_MAX_ROWS * world, "ordered version codes (int32)"
+    # (every rank of a sharded reference-order soup plans all n_total turns: the int32 version
+    # codes bound the whole soup, not a shard)
+    if order == "sequential" and ORDERED_MAX_ROWS < limit:
+        limit, why = ORDERED_MAX_ROWS, "ordered version codes (int32)"
     n_total = min(n_fit, limit)
     return dict(n_total=n_total, n_total_fit=n_fit, limited_by="hbm" if n_fit <= limit else why,
                 bytes_per_gpu=engine_bytes(spec, n_total, **kw),
@@ -318,6 +355,7 @@ class SoupEngine:
             self.nexts = [torch.full((n_links,), -1, **i32) for _ in range(2)]
             self._init_single_or_allgather(nb)
         self.cfg = _lib.make_cfg(spec, self.dtype_code)
+        self._ord_pipe = False      # reference order: plan built one generation ahead (_init_ordered)
         if order == "sequential":
             self._init_ordered()
         # initial particles: uids 0..n_total-1, keyed init (identical for any rank count)
@@ -334,6 +372,8 @@ class SoupEngine:
         elif init:
             K.init_rows(spec, local, self.uid, self.seed)
         self._perm_table()  # allocated here, never inside a graph capture
+        if self._ord_pipe:
+            self._perm_table(1)
 
     # ------------------------------------------------------------------ state
     def _init_single_or_allgather(self, nb):
@@ -378,22 +418,28 @@ class SoupEngine:
             return bool(pt)
         return self.order == "sequential" or self.n <= self.PERM_TABLE_MAX_N
 
-    def _perm_table(self):
+    def _perm_table(self, q: int = 0):
         """The generation's SGD epoch permutations, precomputed by one launch before the
         generation kernel (k_perm_table; nibble Weightwise nets with shuffle, on the device):
         [severity + train][n] uint64, reallocated when the epoch count grows.  None where the
-        kernels draw them inline (host, other shapes, > 2 GB of table)."""
+        kernels draw them inline (host, other shapes, > 2 GB of table).  ``q``: the plan set of a
+        pipelined reference-order engine (the next generation's table is drawn while this one
+        runs)."""
         if (self.device.type != "cuda" or self.spec.kind != "weightwise" or self.spec.P > 16 or not self.shuffle
                 or self.generic or not self._use_perm_table()):
             return None
+        if self.order == "sequential" and self.dist.enabled:
+            return None  # (the sharded reference order's level launches draw their permutations inline)
         E = max(int(self.params.get("train", 0)), 0) + max(int(self.params.get("learn_from_severity", 1)), 0)
         if E <= 0 or (self.n + 4096) * E * 8 > (2 << 30):
             return None
         # (reference order: the pending records' rows and the critical roots' rows, csrc k_ord_ptab)
         rows = 2 * _lib.ord_rec_total(self.n) if self.order == "sequential" else self.n
-        t = getattr(self, "_ptab", None)
+        name = "_ptab1" if q else "_ptab"
+        t = getattr(self, name, None)
         if t is None or t.numel() < rows * E:
-            self._ptab = t = torch.zeros(rows * E, dtype=torch.int64, device=self.device)
+            t = torch.zeros(rows * E, dtype=torch.int64, device=self.device)
+            setattr(self, name, t)
         return t
 
     def _init_ordered(self):
@@ -435,7 +481,27 @@ class SoupEngine:
             self._sh_recv = torch.zeros(self.dist.world * max(cap, 1) * self._sh_recb // 8, dtype=torch.int64,
                                         device=dev)
         self._octl = torch.zeros(_lib.ORD_CTL_WORDS, dtype=torch.int32, device=dev)
+        # single rank: the plan of generation t+1 is built (OP_ORD_PLAN) while generation t runs --
+        # on a side stream on the device -- into the other of two plan sets, indexed like the attack
+        # lists by the ping-pong parity (ExecConfig.ord_pipeline)
+        self._ord_pipe = not sharded and bool(self.execution.ord_pipeline)
+        self._osrc1 = self._olist1 = self._octl1 = None
+        self._ord_side = None
+        if self._ord_pipe:
+            self._osrc1 = torch.zeros_like(self._osrc)
+            self._olist1 = torch.zeros_like(self._olist)
+            self._octl1 = torch.zeros_like(self._octl)
+            self._ord_side = torch.cuda.Stream(dev) if dev.type == "cuda" else None
         self._rec_rows = None  # recording: every particle's state before any respawn
+
+    def _ord_set(self, q: int):
+        """Plan set q of the reference-order generation: (o_src, o_list, o_ctl)."""
+        return (self._osrc, self._olist, self._octl) if q == 0 else (self._osrc1, self._olist1, self._octl1)
+
+    def _ord_last(self) -> int:
+        """The plan set of the last generation that ran (pipelined: the other parity's -- this
+        parity's holds the next generation's plan, not run yet)."""
+        return 1 - self._p if self._ord_pipe else 0
 
     def ordered_levels(self) -> Dict[str, int]:
         """Dependency levels of the last reference-order generation (a turn's level: 1 + its
@@ -447,12 +513,12 @@ class SoupEngine:
         are recomputed by the turns that read them)."""
         C = self.order_levels
         n = self._ord_n
-        lv = self._osrc[:4 * n].view(n, 4)[:, 3] if n else self._osrc[:0]
+        osrc, _, octl = self._ord_set(self._ord_last())
+        lv = osrc[:4 * n].view(n, 4)[:, 3] if n else osrc[:0]
         hist = torch.bincount(lv.clamp(0, _lib.ORD_MAX_LEVELS).long(), minlength=_lib.ORD_MAX_LEVELS + 1)
         hist = hist.cpu().tolist()
-        c = self._octl.cpu().tolist()
-        err = c[_lib.ORD_ERRW] | (4 if n and int((lv < 0).sum().item()) else 0)
-        stored = int(self._osrc[4 * n:5 * n].sum().item()) if n else 0
+        err = self.ordered_error() | (4 if n and int((lv < 0).sum().item()) else 0)
+        stored = int(osrc[4 * n:5 * n].sum().item()) if n else 0
         return dict(levels=hist[:C], tail=sum(hist[C:]), max_level=int(lv.max().item()) if n else 0,
                     pending=n - hist[0], error=err, stored_attacks=stored)
 
@@ -469,7 +535,7 @@ class SoupEngine:
         """The last traced generation per dependency level: turns, first start and last end (us
         after the generation's first turn started), mean / max turn duration (us)."""
         t = self._otrace.view(-1, 2).cpu().double()[:self.n]
-        lv = self._osrc[:4 * self.n].view(self.n, 4)[:, 3].cpu()
+        lv = self._ord_set(self._ord_last())[0][:4 * self.n].view(self.n, 4)[:, 3].cpu()
         ok = t[:, 0] > 0
         t0 = t[ok, 0].min()
         out = {}
@@ -483,8 +549,28 @@ class SoupEngine:
         return out
 
     def ordered_error(self) -> int:
-        """The reference-order generations' error bits, sticky over the engine's life (0: none)."""
-        return int(self._octl[_lib.ORD_ERRW].item()) if self.order == "sequential" else 0
+        """This rank's reference-order error bits (ORD_ERRORS), sticky over the engine's life (0:
+        none); read without communicating (``ordered_error_all``: every rank's)."""
+        if self.order != "sequential":
+            return 0
+        e = int(self._octl[_lib.ORD_ERRW].item())
+        if self._octl1 is not None:
+            e |= int(self._octl1[_lib.ORD_ERRW].item())
+        return e
+
+    def ordered_error_all(self) -> int:
+        """The reference-order error bits of ANY rank, OR-ed (a sharded generation sets some bits
+        on one rank only: its own rows' close, its own level's pack).  COLLECTIVE: every rank must
+        call it, so every rank raises together instead of one leaving the others in a collective."""
+        e = self.ordered_error()
+        if not self.dist.enabled or self.order != "sequential":
+            return e
+        out = torch.zeros(self.dist.world, dtype=torch.int64, device=self.device)
+        self.dist.all_gather_into(out, torch.tensor([e], dtype=torch.int64, device=self.device))
+        v = 0
+        for x in out.cpu().tolist():
+            v |= int(x)
+        return v
 
     def _init_x2(self, n_links):
         dev, R = self.device, self.dist.world
@@ -666,7 +752,12 @@ class SoupEngine:
             if self._census_fused():
                 fa.flags |= _lib.FLAG_FUSED_CENSUS | (_lib.FLAG_FIX_SEC if self.stats_with_sec else 0)
             if self.order == "sequential":
-                fa.W3, fa.o_src, fa.o_list, fa.o_ctl = _p(self._abuf), _p(self._osrc), _p(self._olist), _p(self._octl)
+                q = self._p if self._ord_pipe else 0
+                osrc, olist, octl = self._ord_set(q)
+                fa.W3, fa.o_src, fa.o_list, fa.o_ctl = _p(self._abuf), _p(osrc), _p(olist), _p(octl)
+                fa.ptab = _p(self._perm_table(q))
+                if self._ord_pipe:
+                    fa.flags |= _lib.FLAG_ORD_PLANNED
                 fa.o_levels = self.order_levels
                 fa.o_trace = _p(getattr(self, "_otrace", None))
             ca = fa
@@ -745,7 +836,17 @@ class SoupEngine:
         recorder maps them to uids as of each turn (a counterpart slot < k that respawned at
         its own turn is already the newborn)."""
         spec, cfg = self.spec, self.cfg
-        if not self._lists_ready:
+        side = main = None
+        if self._ord_pipe:
+            if not self._lists_ready:  # the first generation's plan (later ones: planned ahead)
+                _lib.run(_lib.OP_ORD_PLAN, spec, self._plan_args(False), cfg)
+            # the next generation's plan beside this one (weight independent); it overwrites the
+            # plan set and attack lists the previous generation's close finished with
+            if self._ord_side is not None:
+                side, main = self._ord_side, torch.cuda.current_stream(self.device)
+                side.wait_stream(main)
+            _lib.run(_lib.OP_ORD_PLAN, spec, self._plan_args(True), cfg)
+        elif not self._lists_ready:
             _lib.run(_lib.OP_SOUP_DECIDE, spec, a, cfg)
         rec = record and self.recorder is not None
         if rec:
@@ -757,6 +858,8 @@ class SoupEngine:
             _lib.run(_lib.OP_SOUP_ORDERED, spec, ca, cfg)
         finally:
             ca.traj = None
+            if side is not None:
+                main.wait_stream(side)  # the next generation starts on a complete plan
         self._lists_ready = True
         self._p = 1 - self._p
         if self.finish_mode == "batch":
@@ -768,6 +871,25 @@ class SoupEngine:
             self.classify_local(self.stats_with_sec, zero=False)
         if rec:
             self.recorder.on_evolved(self, rows=self._rec_rows, old_uid=uid0, ordered=True)
+
+    def _plan_args(self, nxt: bool) -> _lib.SrnnArgs:
+        """OP_ORD_PLAN arguments: the plan of the generation about to run (``nxt`` False: the
+        first one, on the current stream, into this parity's plan set and lists) or of the one
+        after it (into the other parity's, on the side stream)."""
+        key = self._cache_key("plan", nxt)
+        a = self._arg_cache.get(key)
+        if a is None:
+            q = 1 - self._p if nxt else self._p
+            a = self._args(self._ord_side if nxt else None)
+            osrc, olist, octl = self._ord_set(q)
+            a.o_src, a.o_list, a.o_ctl = _p(osrc), _p(olist), _p(octl)
+            a.heads, a.nexts = _p(self.heads[q]), _p(self.nexts[q])
+            a.ptab = _p(self._perm_table(q))
+            a.o_levels = self.order_levels
+            if nxt:
+                a.flags |= _lib.FLAG_ORD_NEXT
+            self._arg_cache[key] = a
+        return a
 
     def _sh_args(self, phase: int, level: int = 0) -> _lib.SrnnArgs:
         """Argument block of a sharded reference-order phase, in the global view (csrc
@@ -787,6 +909,10 @@ class SoupEngine:
             em = int(self.execution.ordsh_emulate)
             if self.dist.world == 1 and em > 1:  # timing model of `em` ranks: this one runs 1/em of the turns
                 a.o_hi = a.o_lo + -(-N // em)
+                # the other turns never run: the rows are invalid -- a sticky error bit, so count()
+                # and checkpoints refuse them (an environment variable left over from profiling
+                # must not pass for a soup)
+                self._octl[_lib.ORD_ERRW] |= ORD_ERR_EMULATED
             a.W2, a.W, a.W3 = _p(self.full), _p(self._fw), _p(self._abuf)
             a.o_src, a.o_list, a.o_ctl = _p(self._osrc), _p(self._olist), _p(self._octl)
             a.heads, a.nexts = _p(self._sh_heads[self._p]), _p(self._sh_nexts[self._p])
@@ -1115,10 +1241,10 @@ class SoupEngine:
         err = self.exchange_error()
         if err:
             raise RuntimeError(f"soup row exchange failed ({err}): results are invalid")
-        e = self.ordered_error()
+        e = self.ordered_error_all()
         if e:
-            raise RuntimeError(f"reference-order generation: error bits {e} (2: an unstored attack output past "
-                               "the recompute depth, 4: a turn that never ran); results are invalid")
+            raise RuntimeError(f"reference-order generation: error bits {e} ({describe_ordered_error(e)}); results are "
+                               "invalid")
         c = torch.zeros(6, dtype=torch.int64, device=self.device)
         cls, _ = K.classify(self.spec, self.local_rows(), self.eps, with_sec, uid=None, seed=self.seed,
                             scratch=self._scratch, ctr=0x7FFFFFF0, counts=c, key_offset=self.lo)
@@ -1212,7 +1338,8 @@ class SoupEngine:
                  "counterpart", "loss", "respawn", "counts", "census", "err", "full", "stats_all", "_blockstat",
                  "_done", "_bs_ring", "x_dep", "x_rlist", "x_rcount", "x_rslot", "x_satt", "x_cno", "x_crq",
                  "x_srep", "x_nsrep", "x_part", "x_ctl", "x_bstat", "x_hpre", "x_hgrp", "sendbuf", "recvbuf",
-                 "_abuf", "_osrc", "_olist", "_octl", "_ptab"]
+                 "_abuf", "_osrc", "_olist", "_octl", "_ptab", "_osrc1", "_olist1", "_octl1", "_ptab1",
+                 "_fw", "_sh_heads", "_sh_nexts", "_sh_cnt", "_sh_send", "_sh_recv"]
         out = []
         for k in names:
             v = getattr(self, k, None)
@@ -1315,8 +1442,11 @@ class SoupEngine:
             if not self._primed:
                 self._x2_prime()
         elif self.fused and not self._lists_ready and not self.dist.enabled:
-            a, _, _ = self._gen_args()
-            _lib.run(_lib.OP_SOUP_DECIDE, self.spec, a, self.cfg)
+            if self._ord_pipe:
+                _lib.run(_lib.OP_ORD_PLAN, self.spec, self._plan_args(False), self.cfg)
+            else:
+                a, _, _ = self._gen_args()
+                _lib.run(_lib.OP_SOUP_DECIDE, self.spec, a, self.cfg)
             self._lists_ready = True
 
     def _chunk_sizes(self):

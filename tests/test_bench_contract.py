@@ -63,29 +63,41 @@ def test_bench_world_size_mismatch_exits_nonzero():
     assert "WORLD_SIZE=2" in p.stderr
 
 
-def test_bench_reports_the_reference_order_by_default():
-    """a 1-rank run (the driver's BENCH form) always carries the same soup timed in the
-    reference's in-place order next to the headline, and says which semantics `value` is"""
+def test_bench_headline_is_the_reference_order():
+    """the headline `value` is the reference's own soup semantics (in place, index order); a 1-rank
+    run (the driver's BENCH form) carries the Jacobi variant of the same soup beside it
+    (config.jacobi), and --order synchronous swaps the two"""
     d = _bench("--particles", "1500")
-    assert d["semantics"] == "jacobi"
-    ro = d["config"]["reference_order"]
-    assert ro is not None and ro["semantics"] == "reference-order" and ro["steps"] == d["steps"]
-    assert ro["ms_per_step"] > 0 and ro["value"] > 0 and sum(ro["final_census"].values()) == 1500
-    assert ro["levels"]["error"] == 0 and sum(ro["levels"]["levels"]) + ro["levels"]["tail"] == 1500
-    off = _bench("--particles", "1500", "--reference-order-steps", "0")
-    assert off["config"]["reference_order"] is None
-    seq = _bench("--particles", "1500", "--order", "sequential")
-    assert seq["semantics"] == "reference-order" and seq["config"]["reference_order"] is None
+    assert d["semantics"] == "reference-order" and d["config"]["order"] == "sequential"
+    assert "reference (sequential) order" in d["config"]["model"]
+    lv = d["config"]["ordered_levels"]
+    assert lv["error"] == 0 and sum(lv["levels"]) + lv["tail"] == 1500
+    assert d["config"]["ord_pipeline"] is True and d["config"]["reference_order"] is None
+    j = d["config"]["jacobi"]
+    assert j is not None and j["semantics"] == "jacobi" and j["steps"] == d["steps"]
+    assert j["ms_per_step"] > 0 and j["value"] > 0 and sum(j["final_census"].values()) == 1500
+    off = _bench("--particles", "1500", "--side-steps", "0")
+    assert off["config"]["jacobi"] is None and off["config"]["reference_order"] is None
+    # the same reference-order soup whatever else runs in the process
+    assert off["config"]["final_census"] == d["config"]["final_census"]
+    sync = _bench("--particles", "1500", "--order", "synchronous")
+    assert sync["semantics"] == "jacobi" and sync["config"]["jacobi"] is None
+    ro = sync["config"]["reference_order"]
+    assert ro["semantics"] == "reference-order" and ro["final_census"] == d["config"]["final_census"]
+    assert ro["levels"]["error"] == 0
+    # the old spelling of the side-measurement flag still works
+    assert _bench("--particles", "1500", "--reference-order-steps", "0")["config"]["jacobi"] is None
 
 
 def test_bench_reference_order_on_two_ranks():
-    """the reference order shards: --gpus 2 --order sequential runs, and a 2-rank Jacobi headline
-    carries the same soup in the reference order on request, with the census of the 1-rank run
-    (bitwise the same soup on any rank count)"""
-    two = _bench("--gpus", "2", "--particles", "1200", "--order", "sequential")
+    """the reference order shards: --gpus 2 is the sharded reference order by default, with the
+    census of the 1-rank run (bitwise the same soup on any rank count); the Jacobi side number on
+    several ranks is on request only"""
+    two = _bench("--gpus", "2", "--particles", "1200")
     assert two["n_gpus"] == 2 and two["semantics"] == "reference-order"
-    one = _bench("--particles", "1200", "--order", "sequential")
+    assert two["config"]["jacobi"] is None  # on request only
+    one = _bench("--particles", "1200", "--side-steps", "0")
     assert two["config"]["final_census"] == one["config"]["final_census"]
-    side = _bench("--gpus", "2", "--particles", "1200", "--reference-order-steps", "-1")
+    side = _bench("--gpus", "2", "--particles", "1200", "--order", "synchronous", "--side-steps", "-1")
+    assert side["semantics"] == "jacobi"
     assert side["config"]["reference_order"]["final_census"] == one["config"]["final_census"]
-    assert _bench("--gpus", "2", "--particles", "1200")["config"]["reference_order"] is None  # on request only

@@ -94,12 +94,43 @@ def test_engine_bytes_matches_a_constructed_single_rank_engine(n, diag, order):
         nb = max(-(-n // 64), 1)
         held += _finish_batch(nb, e._chunk_sizes()) * (nb * 8 + 2) * 4
     if order == "sequential":
-        # the pending records' permutation table is a GPU-only buffer too (train 1 + severity 1)
-        assert getattr(e, "_ptab", None) is None
-        held += 2 * _lib.ord_rec_total(n) * 2 * 8
+        # the pending records' permutation tables (one per plan set: the next generation's plan is
+        # built while this one runs) are GPU-only buffers too (train 1 + severity 1)
+        assert getattr(e, "_ptab", None) is None and e._ord_pipe and e._osrc1 is not None
+        held += 2 * (2 * _lib.ord_rec_total(n) * 2 * 8)
         assert est > engine_bytes(spec, n, diagnostics=diag) + n * spec.PP * 4  # W3 alone is a table
     # the model may round a few small control tensors up; never low by more than 1 %
     assert est >= held * 0.99 and est <= held * 1.05 + 512, (est, held)
+
+
+@pytest.mark.parametrize("world,rank", [(8, 0), (8, 7), (3, 1)])
+@pytest.mark.parametrize("exchange", ["alltoall", "allgather"])
+def test_engine_bytes_of_a_sharded_reference_order_rank(world, rank, exchange):
+    """order='sequential' over several ranks: the estimate covers what one rank of the sharded
+    reference order really allocates -- the replicated plan and version tables of ALL turns on the
+    all-gather layout (whatever `exchange` says), no permutation table"""
+    from self_replicating_neural_networks_amd.parallel.dist import Dist
+    spec = ArchSpec.weightwise(2, 2)
+    n = 5003
+    e = SoupEngine(spec, n, dict(train=1), device="cpu", dist=Dist(world=world, rank=rank), exchange=exchange,
+                   order="sequential")
+    assert not e.x2 and not e._ord_pipe and e._perm_table() is None
+    est = engine_bytes(spec, n, world=world, exchange=exchange, order="sequential", epochs=2)
+    held = _held_bytes(e)
+    assert est >= held * 0.99 and est <= held * 1.05 + 512, (est, held)
+    # the replicated O(n_total) buffers dominate: far more than n_total / world rows' worth
+    assert est > engine_bytes(spec, n, world=world, exchange="allgather") + n * spec.PP * 4 * 2
+
+
+def test_sharded_reference_order_plan_is_capped_by_the_whole_soup():
+    """every rank plans all n_total turns (int32 version codes): the soup, not a shard, stays
+    below 2^30, and the plan fits the replicated buffers"""
+    spec = ArchSpec.weightwise(2, 2)
+    p = plan_population(spec, torch.float16, world=8, order="sequential", epochs=21)
+    assert p["n_total"] <= 2 ** 30 - 1
+    assert p["bytes_per_gpu"] <= 0.9 * 288e9
+    assert p["bytes_per_gpu"] == engine_bytes(spec, p["n_total"], world=8, dtype=torch.float16, order="sequential",
+                                              epochs=21, diagnostics=False)
 
 
 def test_plan_returns_the_engine_arguments_it_assumed():

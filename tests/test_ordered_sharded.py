@@ -84,3 +84,71 @@ def test_sharded_reference_order_other_nets(tmp_path, spec, world):
 
 def test_sharded_reference_order_bench_params_bf16(tmp_path):
     _run(tmp_path, ArchSpec.weightwise(2, 2), 2, params=BENCH, dtype="bfloat16")
+
+
+def _error_worker(rank, world, port, out_dir):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from self_replicating_neural_networks_amd.io.checkpoint import save_engine
+        from self_replicating_neural_networks_amd.ops import _lib
+        d = Dist(rank, world, 0, None)
+        e = SoupEngine(ArchSpec.weightwise(2, 2), 101, HOT, device="cpu", seed=3, dist=d, order="sequential")
+        e.evolve(1)
+        if rank == world - 1:  # a bit only this rank's kernels could have set (its own rows' close)
+            e._octl[_lib.ORD_ERRW] |= 4
+        msgs = []
+        for call in (e.count, lambda: save_engine(e, os.path.join(out_dir, "ckpt"))):
+            try:
+                call()
+                msgs.append("ok")
+            except RuntimeError as err:
+                msgs.append(str(err))
+        dist.barrier()  # every rank got here: none of them was left inside a collective
+        with open(os.path.join(out_dir, f"err{rank}.txt"), "w") as f:
+            f.write("\n".join(msgs))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_an_error_bit_on_one_rank_raises_on_every_rank(tmp_path):
+    """count() and save_engine() OR the reference-order error word over the ranks before raising:
+    an error set on one rank alone makes every rank raise together (no rank waits in a collective
+    the raising rank never enters), and the message names the bit"""
+    world = 3
+    mp.start_processes(_error_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, start_method="spawn",
+                       join=True)
+    for r in range(world):
+        msgs = open(os.path.join(tmp_path, f"err{r}.txt")).read().split("\n")
+        assert len(msgs) == 2 and all("error bits 4" in m and "never ran" in m for m in msgs), msgs
+    assert not os.path.exists(os.path.join(tmp_path, "ckpt"))
+
+
+def _emulate_worker(rank, world, port, out_dir):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from self_replicating_neural_networks_amd.config import ExecConfig
+        d = Dist(0, 1, 0, None, force=True)
+        e = SoupEngine(ArchSpec.weightwise(2, 2), 200, HOT, device="cpu", seed=3, dist=d, order="sequential",
+                       execution=ExecConfig(ordsh_emulate=4))
+        e.evolve(2)
+        bits = e.ordered_error()
+        try:
+            e.count()
+            msg = "ok"
+        except RuntimeError as err:
+            msg = str(err)
+        with open(os.path.join(out_dir, "emu.txt"), "w") as f:
+            f.write(f"{bits}\n{msg}")
+    finally:
+        dist.destroy_process_group()
+
+
+def test_one_rank_timing_model_marks_its_rows_invalid(tmp_path):
+    """SRNN_ORDSH_EMULATE > 1 (a one-rank timing model of R ranks) runs 1/R of the turns: a sticky
+    error bit makes count() (and checkpoints) refuse the rows instead of passing them for a soup"""
+    mp.start_processes(_emulate_worker, args=(1, _free_port(), str(tmp_path)), nprocs=1, start_method="spawn",
+                       join=True)
+    bits, msg = open(os.path.join(tmp_path, "emu.txt")).read().split("\n", 1)
+    assert int(bits) & 32 and "SRNN_ORDSH_EMULATE" in msg
