@@ -43,3 +43,23 @@ for n in (64, 1024, 65536):
         print(json.dumps(dict(n=n, shuffle=shuffle, ms={k: round(v, 4) for k, v in res.items()},
                               us_per_epoch=round(slope * 1e3, 4), cycles_per_step_at_2_4GHz=round(slope * 1e-3 * 2.4e9 / spec.P, 1))),
               flush=True)
+
+# the same chain inside a synchronous soup generation (k_soup_gen, lane per particle) and on a
+# lane pair per particle (k_soup_gen2, SRNN_SOUP_LANES=2): 64 particles, train 20 vs 220
+from self_replicating_neural_networks_amd.ops import _lib  # noqa: E402
+from self_replicating_neural_networks_amd.soup_engine import SoupEngine  # noqa: E402
+
+for lanes in (1, 2):
+    _lib.set_knob("soup_lanes", lanes)
+    res = {}
+    for tr in (20, 220):
+        p = dict(attacking_rate=0.0, learn_from_rate=0.0, train=tr, remove_divergent=True, remove_zero=True,
+                 epsilon=1e-4)
+        eng = SoupEngine(spec, 64, p, device=dev, seed=0)
+        eng.evolve(2)
+        res[tr] = t_ms(lambda: eng.evolve(1))
+    slope = (res[220] - res[20]) / 200
+    print(json.dumps(dict(soup_lanes=lanes, n=64, ms={k: round(v, 4) for k, v in res.items()},
+                          us_per_epoch=round(slope * 1e3, 4), cycles_per_step_at_2_4GHz=round(slope * 1e-3 * 2.4e9 / 14, 1))),
+          flush=True)
+_lib.set_knob("soup_lanes", -1)

@@ -18,6 +18,7 @@ def main():
     ap.add_argument("--particles", type=int, default=100_000)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--gens", type=int, default=2)
+    ap.add_argument("--slots", type=int, default=2, help="8: per-phase stamps (library built with -DSRNN_ORD_TRACE_FINE)")
     args = ap.parse_args()
     import torch
     from self_replicating_neural_networks_amd.arch import ArchSpec
@@ -27,7 +28,7 @@ def main():
                   remove_divergent=True, remove_zero=True, epsilon=1e-4)
     eng = SoupEngine(ArchSpec.weightwise(2, 2), args.particles, params, device="cuda", order="sequential")
     eng.evolve(args.warmup)
-    eng.ordered_trace(True)
+    eng.ordered_trace(True, slots=args.slots)
     for g in range(args.gens):
         eng.evolve(1)
         torch.cuda.synchronize()

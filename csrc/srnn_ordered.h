@@ -221,6 +221,18 @@ constexpr int ord_rb() {
   return Net::P <= 20 ? 2 : 1;
 }
 
+// fine turn trace (diagnostic build, -DSRNN_ORD_TRACE_FINE): s_memrealtime at the phases of a
+// turn into o_trace[8k + i] (0 start, 1 own row, 2 attack, 3 teacher row, 4 learn_from epochs,
+// 5 self-train, 6 stores, 7 published); the shipped build records 0 and 7 only ([2k], [2k + 1])
+#if defined(__HIP_DEVICE_COMPILE__) && defined(SRNN_ORD_TRACE_FINE)
+#define SRNN_ORD_STAMP(a, k, i) \
+  if ((a).o_trace) (a).o_trace[8 * (k) + (i)] = __builtin_amdgcn_s_memrealtime()
+constexpr int TRACE_SLOTS = 8;
+#else
+#define SRNN_ORD_STAMP(a, k, i)
+constexpr int TRACE_SLOTS = 2;
+#endif
+
 template <class Net, class S>
 struct Ord : OrdSched<ord_rb<Net>()> {
   using I = Item<Net, S>;
@@ -270,6 +282,7 @@ struct Ord : OrdSched<ord_rb<Net>()> {
     };
     float w[P], f[P], o[P];
     mat<RB>(a, s[0], w, ap);
+    SRNN_ORD_STAMP(a, k, 1);
     int8_t act = A_NONE;
     int64_t cp = -1;
     if (at >= 0) {  // 1. attack: the victim's row becomes f_k(victim) (A(k))
@@ -284,6 +297,7 @@ struct Ord : OrdSched<ord_rb<Net>()> {
       act = A_ATTACKING;
       cp = at;
     }
+    SRNN_ORD_STAMP(a, k, 2);
     TrainCtx tc;
     tc.lr = a.lr;
     tc.rng = I::rng(a);
@@ -294,9 +308,9 @@ struct Ord : OrdSched<ord_rb<Net>()> {
     tc.shuffle = (a.flags & SRNN_F_SHUFFLE) != 0;
     tc.stride = SAMP_STRIDE;
     tc.aggregator = c.aggregator;
-    if (a.ptab && a.dev && prow >= 0) {  // precomputed by k_ord_ptab
-      tc.ptab = a.ptab + prow;
-      tc.pstride = 2 * rec_total(a.n);
+    if (a.ptab && a.dev && prow >= 0) {  // precomputed by k_ord_ptab: the turn's epochs side by side
+      tc.ptab = a.ptab + prow * (int64_t)((a.severity > 0 ? a.severity : 0) + (a.epochs > 0 ? a.epochs : 0));
+      tc.pstride = 1;
       tc.pbase = tc.ctr;
     }
     float loss = 0.f;
@@ -304,6 +318,7 @@ struct Ord : OrdSched<ord_rb<Net>()> {
       if (s[2] == SRC_SELF) I::copy(f, w);
       else if (s[2] == SRC_ATK) I::copy(f, o);
       else mat<RB>(a, s[2], f, ap);
+      SRNN_ORD_STAMP(a, k, 3);
       if constexpr (Net::KIND == 0) {
         if (a.severity > 0) loss = Net::template train_epochs<false>(w, f, a.severity, tc);
       } else {
@@ -312,6 +327,7 @@ struct Ord : OrdSched<ord_rb<Net>()> {
       act = A_LEARN_FROM;
       cp = te;
     }
+    SRNN_ORD_STAMP(a, k, 4);
     if (a.epochs > 0) {  // 3. self-train
       if constexpr (Net::KIND == 0) {
         loss = Net::template train_epochs<true>(w, f, a.epochs, tc);
@@ -324,6 +340,7 @@ struct Ord : OrdSched<ord_rb<Net>()> {
       act = A_TRAIN_SELF;
       cp = -1;
     }
+    SRNN_ORD_STAMP(a, k, 5);
     I::q(w);  // 4. respawn (the stored state decides; the zero test on the old particle)
     int8_t rs = 0;
     if ((a.flags & SRNN_F_REMOVE_DIVERGENT) && is_diverged<P>(w)) rs = 1;
@@ -335,6 +352,7 @@ struct Ord : OrdSched<ord_rb<Net>()> {
     if (a.counterpart) a.counterpart[k] = cp;
     if (a.loss) a.loss[k] = loss;
     if (a.respawn) a.respawn[k] = rs;
+    SRNN_ORD_STAMP(a, k, 6);
   }
 
   // row r after the generation: the last attack after its own turn, else E(r) (in W);
@@ -394,15 +412,27 @@ __device__ __forceinline__ int32_t wave_sum(int32_t v) {
 // record whose count this lane takes to zero joins the lane's ready list (linked through the
 // records' R_RDY words, `nready` long); k_ord_run shares the lists out over its wave.
 // ROWS = false (level propagation only): nothing but the producer's level -- an agent-scope atomic
-// store -- is handed over, so its completion (vmcnt) before the decrements replaces the release
-template <bool ROWS = true>
-__device__ __forceinline__ void publish(const SrnnArgs& a, int64_t k, int32_t& ready, int32_t& nready) {
+// store -- is handed over, so its completion (vmcnt) before the decrements replaces the release.
+// PRIVATE (the ready-queue run, where a lane keeps the first record it made ready): a turn with ONE
+// consumer whose only producer it is hands that consumer to itself -- nothing the turn wrote is
+// read by another lane of this launch -- so the drain and the release are skipped and `priv` tells
+// the caller that the continuation needs no acquire either (the chains of a generation's deep
+// tail are such links: a release + an acquire is ~3 us of a ~33 us link, profiles/r6*).
+template <bool ROWS = true, bool PRIVATE = false>
+__device__ __forceinline__ void publish(const SrnnArgs& a, int64_t k, int32_t& ready, int32_t& nready, bool& priv) {
+  priv = false;
   const int32_t h = cons_head(a)[k];
   if (h == EMPTY) return;
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  if constexpr (ROWS) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (kept: ROCm 7.2 may drop the fence's own wait)
+  if constexpr (PRIVATE) {
+    const int32_t* r0 = pend(a, h);
+    priv = r0[1] == 1 && r0[R_NEXT] == EMPTY;
+  }
+  if (!priv) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if constexpr (ROWS) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (kept: ROCm 7.2 may drop the fence's own wait)
+    }
   }
   for (int32_t q = h; q != EMPTY;) {
     int32_t* rec = pend(a, q);
@@ -418,6 +448,11 @@ __device__ __forceinline__ void publish(const SrnnArgs& a, int64_t k, int32_t& r
     }
     q = nxt;
   }
+}
+template <bool ROWS = true>
+__device__ __forceinline__ void publish(const SrnnArgs& a, int64_t k, int32_t& ready, int32_t& nready) {
+  bool priv;
+  publish<ROWS, false>(a, k, ready, nready, priv);
 }
 
 }  // namespace ord
@@ -498,13 +533,16 @@ __global__ __launch_bounds__(TB) void k_ord_count(SrnnCfg, SrnnArgs a) {
 // launch instead of on their latency-bound chains: the pending records (rows q < rec_total) and
 // the roots that have consumers (row rec_total + their run-order slot).  Thread (turn, epoch
 // pair), workgroup row y = (group, partition, pair), grid-stride over the partition's entries.
+// A row's E words are side by side (ptab[row * E + e]): the chain that reads them one epoch
+// ahead touches one cache line / page per turn -- with the epochs 2 rec_total words apart (~1.6 MB
+// at 100k) every epoch's word was its own page walk, ~0.5 us of stall per epoch (profiles/r6*).
 template <class Net>
 __global__ __launch_bounds__(TB) void k_ord_ptab(SrnnArgs a, int32_t E) {
   constexpr int P = Net::P;
   const int npair = (E + 1) / 2;
   const int grp = (int)blockIdx.y / (ord::NPART * npair);  // 0: records, 1: critical roots
   const int part = ((int)blockIdx.y / npair) % ord::NPART, p = (int)blockIdx.y % npair;
-  const int64_t cap = ord::rec_cap(a.n), stride = 2 * ord::rec_total(a.n);
+  const int64_t cap = ord::rec_cap(a.n);
   const int64_t cnt = ord::ld_level(a.o_ctl + (grp ? ord::CRIT0 : ord::PART0) + part), q0 = part * cap;
   const int32_t gen = ord::plan_gen(a);
   const Rng rng{(uint32_t)a.seed, (uint32_t)(a.seed >> 32)};
@@ -514,8 +552,8 @@ __global__ __launch_bounds__(TB) void k_ord_ptab(SrnnArgs a, int32_t E) {
     const int64_t k = grp ? ord::run_order(a)[q] : ord::pend(a, q)[0];
     const int64_t row = grp ? ord::rec_total(a.n) + q : q;
     const U4 r = perm_draw(rng, (uint64_t)(a.lo + k), c0, P_SHUFFLE);
-    a.ptab[2 * p * stride + row] = perm_from_bits<P>(perm_bits(r, c0));
-    if (2 * p + 1 < E) a.ptab[(2 * p + 1) * stride + row] = perm_from_bits<P>(perm_bits(r, c0 + 1u));
+    a.ptab[row * E + 2 * p] = perm_from_bits<P>(perm_bits(r, c0));
+    if (2 * p + 1 < E) a.ptab[row * E + 2 * p + 1] = perm_from_bits<P>(perm_bits(r, c0 + 1u));
   }
 }
 
@@ -591,24 +629,37 @@ __global__ __launch_bounds__(TB) void k_ord_run(SrnnCfg c, SrnnArgs a) {
     if (k < a.n && a.o_list[k] < 0 && !(ncw && ord::cons_head(a)[k] != ord::EMPTY)) cur = k;
   }
   if (cur >= 0) ord::st_level(a.o_src + 4 * cur + 3, 0);
-  int32_t ready = ord::EMPTY, nready = 0;
+  int32_t ready = ord::EMPTY, nready = 0, curlvl = 0;  // (curlvl: the level of this lane's turn)
+  const bool queue = (a.flags & SRNN_F_ORD_QUEUE) != 0;
   for (;;) {
+    bool priv = false;  // this lane's next turn is its private continuation (no acquire needed)
+    int32_t lvl = 0;    // this lane's turn's level
+    int32_t keep = ord::EMPTY;  // (ready-queue run) the first record this lane made ready
     if (cur >= 0) {
       const uint64_t t0 = a.o_trace ? __builtin_amdgcn_s_memrealtime() : 0;
       Pol::turn(c, a, cur, gen, s_sh, prow);
-      ord::publish(a, cur, ready, nready);
+      if (queue) ord::publish<true, true>(a, cur, ready, nready, priv);
+      else ord::publish(a, cur, ready, nready);
+      lvl = curlvl;
       if (a.o_trace) {
-        a.o_trace[2 * cur] = t0;
-        a.o_trace[2 * cur + 1] = __builtin_amdgcn_s_memrealtime();
+        a.o_trace[ord::TRACE_SLOTS * cur] = t0;
+        a.o_trace[ord::TRACE_SLOTS * cur + ord::TRACE_SLOTS - 1] = __builtin_amdgcn_s_memrealtime();
       }
     }
     if (a.flags & SRNN_F_ORD_QUEUE) {
-      // the generation's ready queue: this wave's ready records are appended (one counter add per
-      // wave), then the wave claims up to TB entries, whoever made them ready -- every
+      // the generation's ready queue.  The first record a lane made ready is that lane's own next
+      // turn (the continuation stays on the producer's lane: a chain of dependent turns pays no
+      // queue round trips); the lane's other ready records are appended (one counter add per
+      // wave), then the wave claims entries for its free lanes, whoever made them ready -- every
       // continuation round runs a full wave of turns instead of the few its own producers freed.
-      // A record is appended by a wave that claims afterwards, so none is left behind when the
-      // others have left; a claimed slot is written right after its tail add (the spin is short).
+      // A record is appended by a wave that claims afterwards (a wave never leaves while a lane
+      // still has a kept turn), so none is left behind when the others have left; a claimed slot
+      // is written right after its tail add (the spin is short).
       int32_t* qa = ord::ready_queue(a);
+      if (nready > 0) {
+        keep = ready;
+        if (--nready > 0) ready = ord::pend(a, keep)[ord::R_RDY];
+      }
       const int32_t total = ord::wave_sum(nready);
       if (total) {
         int32_t pre = nready;
@@ -627,13 +678,15 @@ __global__ __launch_bounds__(TB) void k_ord_run(SrnnCfg c, SrnnArgs a) {
           --nready;
         }
       }
+      const unsigned long long kept = __ballot(keep != ord::EMPTY);
+      const int32_t room = TB - (int32_t)__popcll(kept);
       int32_t qb = 0, m = 0;
-      if (lane == 0) {
+      if (lane == 0 && room > 0) {
         for (;;) {
           int32_t h = ord::ld_level(a.o_ctl + ord::QH);
           const int32_t avail = ord::ld_level(a.o_ctl + ord::QT) - h;
           if (avail <= 0) break;
-          const int32_t want = avail < TB ? avail : TB;
+          const int32_t want = avail < room ? avail : room;
           if (__hip_atomic_compare_exchange_strong(a.o_ctl + ord::QH, &h, h + want, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
                                                    __HIP_MEMORY_SCOPE_AGENT)) {
             qb = h;
@@ -644,20 +697,26 @@ __global__ __launch_bounds__(TB) void k_ord_run(SrnnCfg c, SrnnArgs a) {
       }
       qb = __shfl(qb, 0);
       m = __shfl(m, 0);
-      if (m == 0) break;
+      if (m == 0 && !kept) break;
       cur = -1;
-      prow = -1;
-      if (lane < m) {
+      prow = keep;
+      // the claimed entries go to the lanes without a kept turn, in lane order
+      const int32_t slot = (int32_t)__popcll(~kept & ((1ull << lane) - 1ull));
+      if (keep == ord::EMPTY && slot < m) {
         // (bounded: a slot still unwritten after ~2^24 polls is a scheduling bug -- error bit 8
         // and the entry skipped, rather than a wave that never ends)
         int32_t q, polls = 0;
-        while ((q = ord::ld_level(qa + qb + lane)) == ord::EMPTY && ++polls < (1 << 24)) __builtin_amdgcn_s_sleep(1);
+        while ((q = ord::ld_level(qa + qb + slot)) == ord::EMPTY && ++polls < (1 << 24)) __builtin_amdgcn_s_sleep(1);
         if (q == ord::EMPTY) atomicOr(a.o_ctl + ord::ERRW, ord::ERR_QUEUE);
         else prow = q;
       }
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      if (lane < m && prow >= 0) cur = ord::pend(a, prow)[0];
+      // the producers' rows (released before their decrements) are visible after an acquire; a
+      // wave whose every continuation is private skips it (its lanes read only what they wrote)
+      if (__ballot(prow >= 0 && !(priv && keep == prow))) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      if (prow >= 0) cur = ord::pend(a, prow)[0];
     } else {
     // the wave's ready records, one per lane (the rest stay in their lists for the next round)
     const int32_t total = ord::wave_sum(nready);
@@ -693,13 +752,17 @@ __global__ __launch_bounds__(TB) void k_ord_run(SrnnCfg c, SrnnArgs a) {
       raised = true;
     }
     if (cur >= 0) {
-      const int32_t* rec = ord::pend(a, prow);
-      int32_t lv = 0;
-      for (int t = 0; t < rec[1]; ++t) {
-        const int32_t lp = ord::ld_level(a.o_src + 4 * (int64_t)rec[ord::R_PROD + t] + 3);
-        lv = lv > lp ? lv : lp;
+      int32_t lv = lvl;  // (a private continuation's one producer is this lane's last turn)
+      if (!(priv && keep == prow)) {
+        const int32_t* rec = ord::pend(a, prow);
+        lv = 0;
+        for (int t = 0; t < rec[1]; ++t) {
+          const int32_t lp = ord::ld_level(a.o_src + 4 * (int64_t)rec[ord::R_PROD + t] + 3);
+          lv = lv > lp ? lv : lp;
+        }
       }
       ord::st_level(a.o_src + 4 * cur + 3, lv + 1);
+      curlvl = lv + 1;
     }
   }
 }

@@ -522,30 +522,70 @@ class SoupEngine:
         return dict(levels=hist[:C], tail=sum(hist[C:]), max_level=int(lv.max().item()) if n else 0,
                     pending=n - hist[0], error=err, stored_attacks=stored)
 
-    def ordered_trace(self, on: bool = True) -> None:
+    # phases of a turn in a library built with -DSRNN_ORD_TRACE_FINE (csrc/srnn_ordered.h)
+    TRACE_PHASES = ("own row", "attack", "teacher row", "learn_from", "self-train", "stores", "publish")
+
+    def ordered_trace(self, on: bool = True, slots: int = 2) -> None:
         """Record, on the device, when each turn of the next reference-order generations starts
         and ends (s_memrealtime, 100 MHz; debug: a few stores per turn).  Read it with
-        ``ordered_timeline()``."""
+        ``ordered_timeline()``.  ``slots=8``: a library built with -DSRNN_ORD_TRACE_FINE also stamps
+        the phases of every turn (TRACE_PHASES)."""
         if self.order != "sequential" or self.device.type != "cuda":
             raise ValueError("the turn trace is a device reference-order generation's")
-        self._otrace = torch.zeros(2 * max(self.n, 1), dtype=torch.int64, device=self.device) if on else None
+        self._otrace_slots = int(slots)
+        self._otrace = (torch.zeros(self._otrace_slots * max(self.n, 1), dtype=torch.int64, device=self.device)
+                        if on else None)
         self._arg_cache.clear()
 
     def ordered_timeline(self) -> Dict[str, list]:
         """The last traced generation per dependency level: turns, first start and last end (us
-        after the generation's first turn started), mean / max turn duration (us)."""
-        t = self._otrace.view(-1, 2).cpu().double()[:self.n]
-        lv = self._ord_set(self._ord_last())[0][:4 * self.n].view(self.n, 4)[:, 3].cpu()
+        after the generation's first turn started), mean / max turn duration (us), and the hand-off
+        of each dependent turn -- its start minus its last producer's end (publish, ready queue,
+        claim, acquire, record and level reads) -- mean / max per level.  ``critical``: the chain
+        that ends last, turn by turn (start, end, hand-off before it)."""
+        n = self.n
+        S = getattr(self, "_otrace_slots", 2)
+        raw = self._otrace.view(-1, S).cpu().double()[:n]
+        t = raw[:, [0, S - 1]]
+        osrc, _, octl = self._ord_set(self._ord_last())
+        src = osrc.cpu()
+        lv = src[:4 * n].view(n, 4)[:, 3]
         ok = t[:, 0] > 0
         t0 = t[ok, 0].min()
+        us = (t - t0) / 100.0
+        # the pending records: turn, producers (csrc/srnn_ordered.h pend / rec_cap)
+        rec_total = _lib.ord_rec_total(n)
+        cap = rec_total // _lib.ORD_NPART
+        base = 6 * n
+        ctl = octl.cpu().tolist()
+        prods = {}
+        for part in range(_lib.ORD_NPART):
+            for q in range(part * cap, part * cap + int(ctl[2 * _lib.ORD_MAX_LEVELS + 3 + part])):
+                r = src[base + _lib.ORD_REC * q: base + _lib.ORD_REC * (q + 1)].tolist()
+                prods[int(r[0])] = [int(x) for x in r[2:2 + int(r[1])]]
+        hand = {k: float(us[k, 0] - max(us[p, 1] for p in ps)) for k, ps in prods.items() if ok[k]}
         out = {}
         for L in range(int(lv.max()) + 1):
             m = ok & (lv == L)
             if int(m.sum()) == 0:
                 continue
-            s, e = (t[m, 0] - t0) / 100.0, (t[m, 1] - t0) / 100.0
+            s, e = us[m, 0], us[m, 1]
+            h = [hand[k] for k in torch.nonzero(m).flatten().tolist() if k in hand]
             out[L] = dict(turns=int(m.sum()), first_start=float(s.min()), last_start=float(s.max()),
-                          last_end=float(e.max()), mean_us=float((e - s).mean()), max_us=float((e - s).max()))
+                          last_end=float(e.max()), mean_us=float((e - s).mean()), max_us=float((e - s).max()),
+                          handoff_mean_us=sum(h) / len(h) if h else None, handoff_max_us=max(h) if h else None)
+        k = int(torch.argmax(torch.where(ok, us[:, 1], torch.full_like(us[:, 1], -1e30))))
+        chain = []
+        while True:
+            step = dict(turn=k, level=int(lv[k]), start=float(us[k, 0]), end=float(us[k, 1]), handoff=hand.get(k))
+            if S == 8:  # phase durations (us) of the fine trace
+                ph = raw[k].tolist()
+                step["phases"] = {name: (ph[i + 1] - ph[i]) / 100.0 for i, name in enumerate(self.TRACE_PHASES)}
+            chain.append(step)
+            if k not in prods:
+                break
+            k = max(prods[k], key=lambda p: float(us[p, 1]))
+        out["critical"] = chain[::-1]
         return out
 
     def ordered_error(self) -> int:
