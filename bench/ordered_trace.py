@@ -18,7 +18,7 @@ def main():
     ap.add_argument("--particles", type=int, default=100_000)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--gens", type=int, default=2)
-    ap.add_argument("--slots", type=int, default=2, help="8: per-phase stamps (library built with -DSRNN_ORD_TRACE_FINE)")
+    ap.add_argument("--slots", type=int, default=2, help="10: per-phase stamps + the self-train clock (library built with -DSRNN_ORD_TRACE_FINE)")
     args = ap.parse_args()
     import torch
     from self_replicating_neural_networks_amd.arch import ArchSpec

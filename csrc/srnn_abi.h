@@ -59,6 +59,10 @@ enum SrnnFlag : uint32_t {
                                      // without linking the next one's (the next OP_ORD_PLAN links them)
   SRNN_F_ORD_NEXT = 1u << 26,        // OP_ORD_PLAN: plan generation gen + 1 (the one after the generation
                                      // in flight) instead of gen
+  SRNN_F_ORD_INPLAN = 1u << 28,      // OP_SOUP_ORDERED (planned): the run launch's last workgroups build
+                                     // the NEXT generation's plan into o_src_next / o_list_next /
+                                     // o_ctl_next / ptab_next and the lists heads_next / nexts_next while
+                                     // this generation's turns run (one launch, no second stream)
 };
 
 // Attack-list entries (uint32, SRNN_NIL ends a list).  Single rank: the attacker's row
@@ -168,7 +172,7 @@ struct SrnnArgs {
                         // [ord::rec_total(n)] critical list (producers of later turns) |
                         // [ord::rec_total(n)] ready queue (records in the order they became ready)
   int32_t* o_list;      // [n] the pending record of each turn (-1: no producer)
-  int32_t* o_ctl;       // [ord::CTL_WORDS = 165] record / critical-list counts per partition, ready-queue
+  int32_t* o_ctl;       // [ord::CTL_WORDS = 166] record / critical-list counts per partition, ready-queue
                         // head and tail, max level
                         // (host), error bits (sticky: the plan kernel clears every word but that one)
   int32_t o_levels;     // dependency levels the host path reports one by one (1..16; the device
@@ -184,6 +188,14 @@ struct SrnnArgs {
   // ---- the reference-order generation sharded over ranks (OP_SOUP_ORDERED_SH): this rank's turns
   // [o_lo, o_hi) of the n global ones (every other field in the global view: n = n_total, lo = 0)
   int64_t o_lo, o_hi;
+  // ---- SRNN_F_ORD_INPLAN: the plan set of the next generation (see o_src / o_list / o_ctl / ptab) and
+  // the number of workgroups of the run launch that build it
+  int32_t* o_src_next;
+  int32_t* o_list_next;
+  int32_t* o_ctl_next;
+  uint64_t* ptab_next;
+  int32_t o_plan_groups;
+  int32_t pad4;
 };
 
 #define SRNN_X2_HDR 12  // int64 header words of an X2 exchange block (see srnn_shard.hip)
@@ -224,7 +236,7 @@ enum SrnnOp {
                         // independent: issued on a side stream while the previous generation runs
 };
 
-int srnn_abi_version();  // 27
+int srnn_abi_version();  // 28
 int64_t srnn_args_size();  // sizeof(SrnnArgs): the ctypes mirror checks its layout against it
 int64_t srnn_cfg_size();
 int srnn_has_config(const SrnnCfg* cfg);

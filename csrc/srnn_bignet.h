@@ -1968,6 +1968,8 @@ struct BigOrd : ord::OrdSched<1> {
 // the run policy of k_ord_run: the chunk ids of the shuffled outputs in LDS (stride TBROW)
 template <class T, class S, bool SHUF>
 struct BigOrdPol {
+  static constexpr int RB = 1;  // the plan's recompute depth (big nets)
+  using PT = void;              // no permutation table (an aggregating net's SGD step has one sample)
   struct Shared {
     uint32_t cw[SHUF ? ChunkPerm<T>::NW * TB : 1];
   };
@@ -1988,6 +1990,7 @@ __global__ __launch_bounds__(TB) void k_ordbig_close(SrnnCfg c, SrnnArgs a) {
   const int lane = threadIdx.x;
   const int32_t gen = a.gen_ptr ? a.gen_ptr[0] : a.gen;
   const bool census = !SHUF && (a.flags & SRNN_F_FUSED_CENSUS) != 0;
+  if ((a.flags & SRNN_F_ORD_INPLAN) && gb == 0 && threadIdx.x == 0) a.o_ctl[ord::BARW] = 0;
   bool rs = false;
   int8_t k = -1;
   // the E rows through the wave's staging area (coalesced passes, as the synchronous soup's
@@ -2039,14 +2042,13 @@ int big_soup_ordered(const SrnnCfg& c, const SrnnArgs& a) {
               "planned ahead), respawn and two-phase block stats (temp)");
     return -5;
   }
+  if (!ord_inplan_ok(a)) return -5;
   const int64_t nb = (a.n + TB - 1) / TB;
   if (nb <= 0) return 0;
   hipStream_t st = (hipStream_t)a.stream;
   if (!planned) ord_plan_dev<1, void>(c, a, false);
   const SrnnArgs ra = ord_run_args(a, nb);
-  const bool crit = (ra.flags & SRNN_F_ORD_CRIT) != 0;
-  hipLaunchKernelGGL((k_ord_run<BigOrdPol<T, S, SHUF>>), dim3((unsigned)(nb + (crit ? ra.x_groups : 0))), dim3(TB), 0,
-                     st, c, ra);
+  hipLaunchKernelGGL((k_ord_run<BigOrdPol<T, S, SHUF>>), dim3((unsigned)ord_run_grid(ra, nb)), dim3(TB), 0, st, c, ra);
   hipLaunchKernelGGL((k_ordbig_close<T, S, SHUF>), dim3((unsigned)nb), dim3(TB), 0, st, c, a);
   if (!(a.flags & SRNN_F_GEN_COUNTS)) {
     constexpr int FNT = SRNN_FINISH_NT;

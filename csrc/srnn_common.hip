@@ -203,7 +203,7 @@ static int with_scratch(int op, const SrnnCfg* c, const SrnnArgs* a) {
 
 extern "C" {
 
-int srnn_abi_version() { return 27; }
+int srnn_abi_version() { return 28; }
 
 
 // layout check of the ctypes mirror (ops/_lib.py): sizeof(SrnnArgs) / sizeof(SrnnCfg)

@@ -69,14 +69,17 @@ constexpr int32_t ERR_UNSTORED = 2;  // an attack output past the recompute dept
 constexpr int32_t ERR_NOT_RUN = 4;   // a turn that never ran (scheduling bug)
 constexpr int32_t ERR_QUEUE = 8;     // a ready-queue entry never written (scheduling bug)
 constexpr int32_t ERR_PACK = 16;     // sharded: a level's records overflowed the send buffer (sizing bug)
+constexpr int32_t ERR_PLAN_BARRIER = 64;  // a plan workgroup gave up at a phase barrier (scheduling bug)
 // (32: set by the engine -- a one-rank timing model of a sharded generation ran 1/R of the turns)
 // pending records (and the run order) live in NPART partitions (partition p: the workgroups
 // b = p mod NPART, appended by one counter each: no chip-wide contended counter)
 constexpr int NPART = 64, PART0 = 2 * MAX_LEVELS + 3;
 constexpr int CRIT0 = PART0 + NPART;
-// [QH], [QT]: head / tail of the generation's ready queue (SRNN_F_ORD_QUEUE)
-constexpr int QH = CRIT0 + NPART, QT = QH + 1;
-constexpr int CTL_WORDS = QT + 1;
+// [QH], [QT]: head / tail of the generation's ready queue (SRNN_F_ORD_QUEUE); [BARW]: the arrivals
+// at the phase barriers of the workgroups that build this set's plan inside the previous
+// generation's run launch (SRNN_F_ORD_INPLAN; zeroed by the close of the generation that used it)
+constexpr int QH = CRIT0 + NPART, QT = QH + 1, BARW = QT + 1;
+constexpr int CTL_WORDS = BARW + 1;
 // o_src layout: [n][4] {own, victim, teacher, level} | [n] stored flags of A(j) | [n] consumer-list
 // heads (pending records reading E(j) / A(j), EMPTY-terminated) | [rec_total(n)][REC] pending
 // records | [rec_total(n)] the critical list (producers of later turns; partition p: the producers
@@ -93,6 +96,11 @@ static_assert(R_NEXT + NPROD <= REC, "record layout");
 // generation ahead on a side stream -- the one after it
 SRNN_HD int32_t plan_gen(const SrnnArgs& a) {
   return (a.gen_ptr ? a.gen_ptr[0] : a.gen) + ((a.flags & SRNN_F_ORD_NEXT) ? 1 : 0);
+}
+
+// epochs a turn trains (learn_from severity + self-train): the permutation-table row length
+SRNN_HD int32_t table_epochs(const SrnnArgs& a) {
+  return (a.severity > 0 ? a.severity : 0) + (a.epochs > 0 ? a.epochs : 0);
 }
 
 SRNN_HD int32_t code_A(int64_t j) { return (int32_t)(2 * j); }
@@ -222,15 +230,24 @@ constexpr int ord_rb() {
 }
 
 // fine turn trace (diagnostic build, -DSRNN_ORD_TRACE_FINE): s_memrealtime at the phases of a
-// turn into o_trace[8k + i] (0 start, 1 own row, 2 attack, 3 teacher row, 4 learn_from epochs,
+// turn into o_trace[10k + i] (0 start, 1 own row, 2 attack, 3 teacher row, 4 learn_from epochs,
 // 5 self-train, 6 stores, 7 published); the shipped build records 0 and 7 only ([2k], [2k + 1])
+// (8, 9: the shader-clock counter s_memtime at the self-train's start and end: the clock the chain
+// ran at is their difference over the real-time one)
+// (10: the permutation-table row the turn trained with, -1: drawn inline; 11: spare)
 #if defined(__HIP_DEVICE_COMPILE__) && defined(SRNN_ORD_TRACE_FINE)
-#define SRNN_ORD_STAMP(a, k, i) \
-  if ((a).o_trace) (a).o_trace[8 * (k) + (i)] = __builtin_amdgcn_s_memrealtime()
-constexpr int TRACE_SLOTS = 8;
+#define SRNN_ORD_STAMP(a, k, i)                                                        \
+  if ((a).o_trace) {                                                                   \
+    (a).o_trace[12 * (k) + (i)] = __builtin_amdgcn_s_memrealtime();                   \
+    if ((i) == 4 || (i) == 5) (a).o_trace[12 * (k) + 4 + (i)] = __builtin_amdgcn_s_memtime(); \
+  }
+#define SRNN_ORD_NOTE(a, k, i, v) \
+  if ((a).o_trace) (a).o_trace[12 * (k) + (i)] = (uint64_t)(v)
+constexpr int TRACE_SLOTS = 12, TRACE_END = 7;
 #else
 #define SRNN_ORD_STAMP(a, k, i)
-constexpr int TRACE_SLOTS = 2;
+#define SRNN_ORD_NOTE(a, k, i, v)
+constexpr int TRACE_SLOTS = 2, TRACE_END = 1;
 #endif
 
 template <class Net, class S>
@@ -309,10 +326,11 @@ struct Ord : OrdSched<ord_rb<Net>()> {
     tc.stride = SAMP_STRIDE;
     tc.aggregator = c.aggregator;
     if (a.ptab && a.dev && prow >= 0) {  // precomputed by k_ord_ptab: the turn's epochs side by side
-      tc.ptab = a.ptab + prow * (int64_t)((a.severity > 0 ? a.severity : 0) + (a.epochs > 0 ? a.epochs : 0));
+      tc.ptab = a.ptab + prow * (int64_t)table_epochs(a);
       tc.pstride = 1;
       tc.pbase = tc.ctr;
     }
+    SRNN_ORD_NOTE(a, k, 10, tc.ptab ? prow : -1);
     float loss = 0.f;
     if (te >= 0) {  // 2. learn_from the teacher's current row
       if (s[2] == SRC_SELF) I::copy(f, w);
@@ -389,7 +407,6 @@ __device__ __forceinline__ int32_t ld_level(const int32_t* p) {
 __device__ __forceinline__ void st_level(int32_t* p, int32_t v) {
   __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
-
 // wave-aggregated append: this lane's position among the wave's `want` lanes after one
 // atomicAdd on ctr (every lane of the wave calls it)
 __device__ __forceinline__ int32_t wave_append(int32_t* ctr, bool want) {
@@ -457,17 +474,95 @@ __device__ __forceinline__ void publish(const SrnnArgs& a, int64_t k, int32_t& r
 
 }  // namespace ord
 
-// (link / plan / mark / count: shape independent, one instantiation per recompute depth)
-// OP_ORD_PLAN: the planned generation's attack lists -- every row joins its victim's list (the
-// lists are NIL on entry: the close two generations before consumed them)
+// (link / plan / mark / count: shape independent, one instantiation per recompute depth).  Each
+// phase is a per-item (or per-64-item chunk) body, run by its own launch (OP_ORD_PLAN) or by the
+// plan workgroups of a run launch (SRNN_F_ORD_INPLAN, ord_plan_group below).
+namespace ord {
+// the planned generation's attack lists: row r joins its victim's list (the lists are NIL on entry:
+// the close two generations before consumed them)
+template <int RB>
+__device__ __forceinline__ void link_item(const SrnnArgs& a, int64_t r) {
+  using Dec = typename OrdSched<RB>::Dec;
+  int64_t at, te;
+  Dec::decision(a, r, plan_gen(a), at, te);
+  if (at >= 0) Dec::link(a.heads, a.nexts, at, (uint32_t)r);
+}
+template <int RB>
+__device__ __forceinline__ void plan_item(const SrnnArgs& a, int64_t k) {
+  OrdSched<RB>::plan(a, k, plan_gen(a));
+  ready_queue(a)[k] = EMPTY;  // (at most one queue entry per pending turn: < n)
+}
+// every turn of 64-turn chunk `ci` counts its producers; a turn with producers becomes a pending
+// record of the chunk's partition (producers written straight into the record, deduplicated) and
+// is pushed onto each producer's consumer list.  No turn runs before the lists are complete.
+// (One wave per chunk: the record slots are appended wave-wide.)
+template <int RB>
+__device__ __forceinline__ void count_chunk(const SrnnArgs& a, int64_t ci) {
+  using O = OrdSched<RB>;
+  const int lane = threadIdx.x & 63;
+  const int64_t k = ci * TB + lane;
+  const bool valid = k < a.n;
+  int np = 0;
+  bool bad = false;
+  if (valid) np = O::producers(a, k, nullptr, bad);
+  if (bad) atomicOr(a.o_ctl + ERRW, ERR_UNSTORED);
+  const bool pd = valid && np > 0;
+  const int part = (int)(ci % NPART);
+  const int32_t i = wave_append(a.o_ctl + PART0 + part, pd);
+  if (pd) {
+    const int64_t q = part * rec_cap(a.n) + i;
+    int32_t* rec = pend(a, q);
+    bool bad2 = false;
+    int32_t* pr = rec + R_PROD;
+    const int m = dedupe(pr, O::producers(a, k, pr, bad2));
+    rec[0] = (int32_t)k;
+    rec[1] = m;
+    rec[R_CNT] = m;
+    a.o_list[k] = (int32_t)q;
+    int32_t* heads = cons_head(a);
+    for (int s = 0; s < m; ++s) {
+      const int32_t old = atomicExch(heads + pr[s], (int32_t)q);
+      rec[R_NEXT + s] = old;
+      if (old == EMPTY && (a.flags & SRNN_F_ORD_CRIT)) {  // pr[s]'s first consumer: a critical turn
+        const int pp = (int)((pr[s] / TB) % NPART);
+        const int32_t pos = atomicAdd(a.o_ctl + CRIT0 + pp, 1);
+        run_order(a)[pp * rec_cap(a.n) + pos] = pr[s];
+      }
+    }
+  }
+}
+// the epoch permutations of the turns on the generation's critical paths, drawn in parallel instead
+// of on their latency-bound chains: the pending records (rows q < rec_total) and the roots that have
+// consumers (row rec_total + their run-order slot).  Task y = (group, partition, epoch pair); items
+// i0, i0 + step, ... of the partition's entries.  A row's E words are side by side
+// (ptab[row * E + e]): the chain that reads them one epoch ahead touches one cache line / page per
+// turn -- with the epochs 2 rec_total words apart (~1.6 MB at 100k) every epoch's word was its own
+// page walk, ~0.5 us of stall per epoch (profiles/r6*).
+template <class Net>
+__device__ __forceinline__ void ptab_task(const SrnnArgs& a, int32_t E, int y, int64_t i0, int64_t step) {
+  constexpr int P = Net::P;
+  const int npair = (E + 1) / 2;
+  const int grp = y / (NPART * npair);  // 0: records, 1: critical roots
+  const int part = (y / npair) % NPART, p = y % npair;
+  const int64_t cnt = ld_level(a.o_ctl + (grp ? CRIT0 : PART0) + part), q0 = part * rec_cap(a.n);
+  const int32_t gen = plan_gen(a);
+  const Rng rng{(uint32_t)a.seed, (uint32_t)(a.seed >> 32)};
+  const uint32_t c0 = (uint32_t)gen * 1024u + 512u + 2u * (uint32_t)p;  // even: one draw, two epochs
+  for (int64_t i = i0; i < cnt; i += step) {
+    const int64_t q = q0 + i;
+    const int64_t k = grp ? run_order(a)[q] : pend(a, q)[0];
+    const int64_t row = grp ? rec_total(a.n) + q : q;
+    const U4 r = perm_draw(rng, (uint64_t)(a.lo + k), c0, P_SHUFFLE);
+    a.ptab[row * E + 2 * p] = perm_from_bits<P>(perm_bits(r, c0));
+    if (2 * p + 1 < E) a.ptab[row * E + 2 * p + 1] = perm_from_bits<P>(perm_bits(r, c0 + 1u));
+  }
+}
+}  // namespace ord
+
 template <int RB>
 __global__ __launch_bounds__(TB) void k_ord_link(SrnnArgs a) {
-  using Dec = typename ord::OrdSched<RB>::Dec;
   const int64_t r = (int64_t)blockIdx.x * TB + threadIdx.x;
-  if (r >= a.n) return;
-  int64_t at, te;
-  Dec::decision(a, r, ord::plan_gen(a), at, te);
-  if (at >= 0) Dec::link(a.heads, a.nexts, at, (uint32_t)r);
+  if (r < a.n) ord::link_item<RB>(a, r);
 }
 
 template <int RB>
@@ -477,10 +572,7 @@ __global__ __launch_bounds__(TB) void k_ord_plan(SrnnCfg, SrnnArgs a) {
   if (blockIdx.x == 0)
     for (int w = threadIdx.x; w < ord::CTL_WORDS; w += TB)
       if (w != ord::ERRW) a.o_ctl[w] = 0;
-  if (k < a.n) {
-    ord::OrdSched<RB>::plan(a, k, ord::plan_gen(a));
-    ord::ready_queue(a)[k] = ord::EMPTY;  // (at most one queue entry per pending turn: < n)
-  }
+  if (k < a.n) ord::plan_item<RB>(a, k);
 }
 
 template <int RB>
@@ -489,73 +581,84 @@ __global__ __launch_bounds__(TB) void k_ord_mark(SrnnCfg, SrnnArgs a) {
   if (k < a.n) ord::OrdSched<RB>::mark(a, k);
 }
 
-// every turn counts its producers; a turn with producers becomes a pending record of this
-// workgroup's partition (producers written straight into the record, deduplicated) and is
-// pushed onto each producer's consumer list.  No turn runs here, so every list is complete
-// before k_ord_run walks any of them.
 template <int RB>
 __global__ __launch_bounds__(TB) void k_ord_count(SrnnCfg, SrnnArgs a) {
-  using O = ord::OrdSched<RB>;
-  const int lane = threadIdx.x;
-  const int64_t k = (int64_t)blockIdx.x * TB + lane;
-  const bool valid = k < a.n;
-  int np = 0;
-  bool bad = false;
-  if (valid) np = O::producers(a, k, nullptr, bad);
-  if (bad) atomicOr(a.o_ctl + ord::ERRW, ord::ERR_UNSTORED);
-  const bool pend = valid && np > 0;
-  const int part = (int)(blockIdx.x % ord::NPART);
-  const int32_t i = ord::wave_append(a.o_ctl + ord::PART0 + part, pend);
-  if (pend) {
-    const int64_t q = part * ord::rec_cap(a.n) + i;
-    int32_t* rec = ord::pend(a, q);
-    bool bad2 = false;
-    int32_t* pr = rec + ord::R_PROD;
-    const int m = ord::dedupe(pr, O::producers(a, k, pr, bad2));
-    rec[0] = (int32_t)k;
-    rec[1] = m;
-    rec[ord::R_CNT] = m;
-    a.o_list[k] = (int32_t)q;
-    int32_t* heads = ord::cons_head(a);
-    for (int s = 0; s < m; ++s) {
-      const int32_t old = atomicExch(heads + pr[s], (int32_t)q);
-      rec[ord::R_NEXT + s] = old;
-      if (old == ord::EMPTY && (a.flags & SRNN_F_ORD_CRIT)) {  // pr[s]'s first consumer: a critical turn
-        const int pp = (int)((pr[s] / TB) % ord::NPART);
-        const int32_t pos = atomicAdd(a.o_ctl + ord::CRIT0 + pp, 1);
-        ord::run_order(a)[pp * ord::rec_cap(a.n) + pos] = pr[s];
-      }
+  ord::count_chunk<RB>(a, blockIdx.x);
+}
+
+// workgroup row y = (group, partition, pair), grid-stride over the partition's entries
+template <class Net>
+__global__ __launch_bounds__(TB) void k_ord_ptab(SrnnArgs a, int32_t E) {
+  ord::ptab_task<Net>(a, E, (int)blockIdx.y, (int64_t)blockIdx.x * TB + threadIdx.x, (int64_t)gridDim.x * TB);
+}
+
+// ptab tasks of a plan: (records + critical roots) x partitions x epoch pairs
+SRNN_HD int ord_ptab_rows(const SrnnArgs& a, int32_t E) {
+  return ((a.flags & SRNN_F_ORD_CRIT) ? 2 : 1) * ord::NPART * ((E + 1) / 2);
+}
+
+namespace ord {
+// all plan workgroups of a run launch have finished the phase: arrivals counted on the plan set's
+// BARW word.  The phase's stores are released before the arrival and the other workgroups' are
+// acquired after the wait.  Bounded: a barrier still short after ~2^24 polls (~1 s) sets
+// ERR_PLAN_BARRIER and lets the workgroup go on -- a wrong plan instead of a launch that never ends.
+// (Only plan workgroups wait here, only on each other, and they are the launch's last workgroups:
+// every turn workgroup is dispatched before them and never waits on them.)
+__device__ __forceinline__ void plan_barrier(int32_t* bar, int32_t target, int32_t* errw) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+  if ((threadIdx.x & 63) == 0) {
+    __hip_atomic_fetch_add(bar, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    int32_t polls = 0;
+    while (__hip_atomic_load(bar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target && ++polls < (1 << 24))
+      __builtin_amdgcn_s_sleep(4);
+    if (polls >= (1 << 24)) atomicOr(errw, ERR_PLAN_BARRIER);
+  }
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+// SRNN_F_ORD_INPLAN: plan workgroup w of G builds the NEXT generation's plan (the *_next buffers and
+// lists) while this generation's turns run -- link, plan, mark, count, permutations, the phases
+// separated by plan_barrier -- instead of launches on a second stream, whose cross-queue
+// dependencies cost ~10 us of idle queue per generation inside a hipGraph (profiles/r6a).
+template <int RB, class PT>
+__device__ void plan_group(const SrnnArgs& a, int64_t w, int64_t G) {
+  SrnnArgs pa = a;
+  pa.o_src = a.o_src_next;
+  pa.o_list = a.o_list_next;
+  pa.o_ctl = a.o_ctl_next;
+  pa.ptab = a.ptab_next;
+  pa.heads = a.heads_next;
+  pa.nexts = a.nexts_next;
+  pa.flags |= SRNN_F_ORD_NEXT;
+  const int lane = threadIdx.x & 63;
+  const int64_t nb = (a.n + TB - 1) / TB;
+  int32_t* bar = pa.o_ctl + BARW;
+  int32_t* errw = pa.o_ctl + ERRW;
+  if (w == 0)  // the plan's control words (the sticky error word and the barrier counter excepted)
+    for (int i = lane; i < CTL_WORDS; i += 64)
+      if (i != ERRW && i != BARW) pa.o_ctl[i] = 0;
+  for (int64_t ci = w; ci < nb; ci += G)
+    if (ci * TB + lane < a.n) link_item<RB>(pa, ci * TB + lane);
+  plan_barrier(bar, (int32_t)G, errw);
+  for (int64_t ci = w; ci < nb; ci += G)
+    if (ci * TB + lane < a.n) plan_item<RB>(pa, ci * TB + lane);
+  plan_barrier(bar, (int32_t)(2 * G), errw);
+  for (int64_t ci = w; ci < nb; ci += G)
+    if (ci * TB + lane < a.n) OrdSched<RB>::mark(pa, ci * TB + lane);
+  plan_barrier(bar, (int32_t)(3 * G), errw);
+  for (int64_t ci = w; ci < nb; ci += G) count_chunk<RB>(pa, ci);
+  if constexpr (!std::is_void_v<PT>) {
+    const int32_t E = table_epochs(pa);
+    if (pa.ptab && (pa.flags & SRNN_F_SHUFFLE) && E > 0) {
+      plan_barrier(bar, (int32_t)(4 * G), errw);
+      const int Y = ord_ptab_rows(pa, E);
+      for (int64_t y = w; y < Y; y += G) ptab_task<PT>(pa, E, (int)y, lane, 64);
     }
   }
 }
-
-// the epoch permutations of the turns on the generation's critical paths, drawn in one parallel
-// launch instead of on their latency-bound chains: the pending records (rows q < rec_total) and
-// the roots that have consumers (row rec_total + their run-order slot).  Thread (turn, epoch
-// pair), workgroup row y = (group, partition, pair), grid-stride over the partition's entries.
-// A row's E words are side by side (ptab[row * E + e]): the chain that reads them one epoch
-// ahead touches one cache line / page per turn -- with the epochs 2 rec_total words apart (~1.6 MB
-// at 100k) every epoch's word was its own page walk, ~0.5 us of stall per epoch (profiles/r6*).
-template <class Net>
-__global__ __launch_bounds__(TB) void k_ord_ptab(SrnnArgs a, int32_t E) {
-  constexpr int P = Net::P;
-  const int npair = (E + 1) / 2;
-  const int grp = (int)blockIdx.y / (ord::NPART * npair);  // 0: records, 1: critical roots
-  const int part = ((int)blockIdx.y / npair) % ord::NPART, p = (int)blockIdx.y % npair;
-  const int64_t cap = ord::rec_cap(a.n);
-  const int64_t cnt = ord::ld_level(a.o_ctl + (grp ? ord::CRIT0 : ord::PART0) + part), q0 = part * cap;
-  const int32_t gen = ord::plan_gen(a);
-  const Rng rng{(uint32_t)a.seed, (uint32_t)(a.seed >> 32)};
-  const uint32_t c0 = (uint32_t)gen * 1024u + 512u + 2u * (uint32_t)p;  // even: one draw, two epochs
-  for (int64_t i = (int64_t)blockIdx.x * TB + threadIdx.x; i < cnt; i += (int64_t)gridDim.x * TB) {
-    const int64_t q = q0 + i;
-    const int64_t k = grp ? ord::run_order(a)[q] : ord::pend(a, q)[0];
-    const int64_t row = grp ? ord::rec_total(a.n) + q : q;
-    const U4 r = perm_draw(rng, (uint64_t)(a.lo + k), c0, P_SHUFFLE);
-    a.ptab[row * E + 2 * p] = perm_from_bits<P>(perm_bits(r, c0));
-    if (2 * p + 1 < E) a.ptab[row * E + 2 * p + 1] = perm_from_bits<P>(perm_bits(r, c0 + 1u));
-  }
-}
+}  // namespace ord
 
 // the g-th entry of the critical list (-1: past its end) and its slot; the wave's exclusive prefix
 // of the partitions' counts in s_c (64 partitions = one per lane)
@@ -594,6 +697,8 @@ template <class Net, class S>
 struct OrdLanePol {
   static constexpr int SAMP = samp_slots<Net>();
   static constexpr int PERM = (Net::P + 4) & ~3;
+  static constexpr int RB = ord::Ord<Net, S>::RB;  // the plan's recompute depth
+  using PT = std::conditional_t<(Net::KIND == 0 && Net::P <= 16), Net, void>;  // the permutation-table net
   struct Shared {
     float4 samp[TB * SAMP];
     uint8_t perm[TB * PERM];
@@ -612,8 +717,14 @@ __global__ __launch_bounds__(TB) void k_ord_run(SrnnCfg c, SrnnArgs a) {
   int64_t cur = -1, prow = -1;
   bool raised = false;
   // with the critical list: its waves first (the grid's first a.x_groups workgroups), at raised
-  // priority, permutations from the table; then every other turn without producers in index order
+  // priority, permutations from the table; then every other turn without producers in index order;
+  // with SRNN_F_ORD_INPLAN the last a.o_plan_groups workgroups build the next generation's plan
   const int64_t ncw = (a.flags & SRNN_F_ORD_CRIT) ? a.x_groups : 0;
+  const int64_t nturn = ncw + (a.n + TB - 1) / TB;
+  if ((a.flags & SRNN_F_ORD_INPLAN) && (int64_t)blockIdx.x >= nturn) {
+    ord::plan_group<Pol::RB, typename Pol::PT>(a, (int64_t)blockIdx.x - nturn, a.o_plan_groups);
+    return;
+  }
   if ((int64_t)blockIdx.x < ncw) {
     __shared__ int32_t s_c[64];
     int64_t slot = -1;
@@ -643,7 +754,7 @@ __global__ __launch_bounds__(TB) void k_ord_run(SrnnCfg c, SrnnArgs a) {
       lvl = curlvl;
       if (a.o_trace) {
         a.o_trace[ord::TRACE_SLOTS * cur] = t0;
-        a.o_trace[ord::TRACE_SLOTS * cur + ord::TRACE_SLOTS - 1] = __builtin_amdgcn_s_memrealtime();
+        a.o_trace[ord::TRACE_SLOTS * cur + ord::TRACE_END] = __builtin_amdgcn_s_memrealtime();
       }
     }
     if (a.flags & SRNN_F_ORD_QUEUE) {
@@ -780,6 +891,8 @@ __global__ __launch_bounds__(TB) void k_ord_close(SrnnCfg c, SrnnArgs a) {
   uint8_t* perm = s_perm + lane * PERM;
   const int32_t gen = I::gen_of(a);
   const bool census = (a.flags & SRNN_F_FUSED_CENSUS) != 0;
+  // (in-run planning: this set's barrier counter is free for the plan two generations on)
+  if ((a.flags & SRNN_F_ORD_INPLAN) && gb == 0 && lane == 0) a.o_ctl[ord::BARW] = 0;
   bool rs = false;
   int8_t k = -1;
   if (r < a.n) {
@@ -823,6 +936,34 @@ __global__ __launch_bounds__(TB) void k_ord_close(SrnnCfg c, SrnnArgs a) {
 
 // the run (and count) launch's scheduling flags from the knobs, and the critical-list waves: the
 // list holds at most one entry per pending record's producer slot; waves past its end return
+// the run launch's workgroups: critical-list waves, turn waves, plan workgroups (SRNN_F_ORD_INPLAN)
+inline int64_t ord_run_grid(const SrnnArgs& ra, int64_t nb) {
+  return nb + ((ra.flags & SRNN_F_ORD_CRIT) ? ra.x_groups : 0) + ((ra.flags & SRNN_F_ORD_INPLAN) ? ra.o_plan_groups : 0);
+}
+// SRNN_F_ORD_INPLAN needs the next plan set, its lists and 1..4096 plan workgroups
+inline bool ord_inplan_ok(const SrnnArgs& a) {
+  if (!(a.flags & SRNN_F_ORD_INPLAN)) return true;
+  if (!(a.flags & SRNN_F_ORD_PLANNED) || !a.o_src_next || !a.o_list_next || !a.o_ctl_next || !a.heads_next ||
+      !a.nexts_next || a.o_plan_groups < 1 || a.o_plan_groups > 4096) {
+    set_error("in-run planning (SRNN_F_ORD_INPLAN) needs a planned generation, the next plan set (o_src_next, "
+              "o_list_next, o_ctl_next), the next attack lists and 1..4096 plan workgroups");
+    return false;
+  }
+  return true;
+}
+// the next generation's plan arguments of an in-run planning generation (host path)
+inline SrnnArgs ord_next_plan_args(const SrnnArgs& a) {
+  SrnnArgs pa = a;
+  pa.o_src = a.o_src_next;
+  pa.o_list = a.o_list_next;
+  pa.o_ctl = a.o_ctl_next;
+  pa.ptab = a.ptab_next;
+  pa.heads = a.heads_next;
+  pa.nexts = a.nexts_next;
+  pa.flags |= SRNN_F_ORD_NEXT;
+  return pa;
+}
+
 inline SrnnArgs ord_run_args(const SrnnArgs& a, int64_t nb) {
   SrnnArgs ra = a;
   if (knob(SRNN_KNOB_ORD_QUEUE, 1) != 0) ra.flags |= SRNN_F_ORD_QUEUE;
@@ -846,13 +987,11 @@ void ord_plan_dev(const SrnnCfg& c, const SrnnArgs& a, bool link) {
   const SrnnArgs ra = ord_run_args(a, nb);
   hipLaunchKernelGGL((k_ord_count<RB>), dim3((unsigned)nb), dim3(TB), 0, st, c, ra);
   if constexpr (!std::is_void_v<PT>) {
-    const int32_t E = (a.severity > 0 ? a.severity : 0) + (a.epochs > 0 ? a.epochs : 0);
+    const int32_t E = ord::table_epochs(a);
     if (a.ptab && (a.flags & SRNN_F_SHUFFLE) && E > 0) {
-      const bool crit = (ra.flags & SRNN_F_ORD_CRIT) != 0;
       const int64_t est = std::max<int64_t>(a.n / 12 / ord::NPART, 1);
-      hipLaunchKernelGGL((k_ord_ptab<PT>),
-                         dim3((unsigned)((est + TB - 1) / TB), (unsigned)((crit ? 2 : 1) * ord::NPART * ((E + 1) / 2))),
-                         dim3(TB), 0, st, a, E);
+      hipLaunchKernelGGL((k_ord_ptab<PT>), dim3((unsigned)((est + TB - 1) / TB), (unsigned)ord_ptab_rows(ra, E)), dim3(TB),
+                         0, st, ra, E);
     }
   }
 }
@@ -944,6 +1083,7 @@ int soup_ordered(const SrnnCfg& c, const SrnnArgs& a) {
               "planned ahead), respawn and 1 <= o_levels <= 16");
     return -5;
   }
+  if (!ord_inplan_ok(a)) return -5;
   if (!a.dev) {
     const int32_t gen = I::gen_of(a);
     if (!planned) ord_plan_host<O::RB>(a, false);
@@ -995,6 +1135,7 @@ int soup_ordered(const SrnnCfg& c, const SrnnArgs& a) {
       for (int q = 0; q < 5; ++q) a.counts[q] = census ? cs[q] : 0;
       a.counts[5] = (uint64_t)total;
     }
+    if (a.flags & SRNN_F_ORD_INPLAN) ord_plan_host<O::RB>(ord_next_plan_args(a), true);  // the next plan
     return 0;
   }
   if (!(a.flags & SRNN_F_TWO_PHASE) || !a.temp) {
@@ -1007,8 +1148,7 @@ int soup_ordered(const SrnnCfg& c, const SrnnArgs& a) {
   using PT = std::conditional_t<(Net::KIND == 0 && Net::P <= 16), Net, void>;
   if (!planned) ord_plan_dev<O::RB, PT>(c, a, false);
   const SrnnArgs ra = ord_run_args(a, nb);
-  const bool crit = (ra.flags & SRNN_F_ORD_CRIT) != 0;
-  hipLaunchKernelGGL((k_ord_run<OrdLanePol<Net, S>>), dim3((unsigned)(nb + (crit ? ra.x_groups : 0))), dim3(TB), 0, st, c, ra);
+  hipLaunchKernelGGL((k_ord_run<OrdLanePol<Net, S>>), dim3((unsigned)ord_run_grid(ra, nb)), dim3(TB), 0, st, c, ra);
   hipLaunchKernelGGL((k_ord_close<Net, S>), dim3((unsigned)nb), dim3(TB), 0, st, c, a);
   if (!(a.flags & SRNN_F_GEN_COUNTS)) {
     constexpr int FNT = SRNN_FINISH_NT;

@@ -313,7 +313,8 @@ static int64_t ord_words(int64_t n) {  // ops/_lib.py ord_src_words
   const int64_t rec = 64 * ((((n + 63) / 64) + 63) / 64) * 64;
   return 6 * n + 34 * rec;
 }
-static void ordered_soup(const SrnnCfg& c, int64_t n, int gens, bool pipe) {
+// pipe 0: inline plan, 1: OP_ORD_PLAN one generation ahead, 2: the generation call plans the next one
+static void ordered_soup(const SrnnCfg& c, int64_t n, int gens, int pipe) {
   const size_t R = (size_t)(n * c.pp);
   std::vector<float> seqW(R), buf[2] = {std::vector<float>(R), std::vector<float>(R)}, W3(R);
   std::vector<int64_t> suid((size_t)n), uid((size_t)n), snext(1, n), next(1, n), scp((size_t)n), cp((size_t)n);
@@ -323,7 +324,7 @@ static void ordered_soup(const SrnnCfg& c, int64_t n, int gens, bool pipe) {
   std::vector<float> sloss((size_t)n), loss((size_t)n);
   std::vector<uint64_t> counts(6, 0);
   for (int q = 0; q < 2; ++q) {
-    osrc[q].assign((size_t)ord_words(n), 0), olist[q].assign((size_t)n, 0), octl[q].assign(165, 0);
+    osrc[q].assign((size_t)ord_words(n), 0), olist[q].assign((size_t)n, 0), octl[q].assign(166, 0);
     heads[q].assign((size_t)n, 0xFFFFFFFFu), nexts[q].assign((size_t)n, 0xFFFFFFFFu);
   }
   for (int64_t j = 0; j < n; ++j) suid[(size_t)j] = uid[(size_t)j] = j;
@@ -361,7 +362,7 @@ static void ordered_soup(const SrnnCfg& c, int64_t n, int gens, bool pipe) {
   }
   for (int g = 0; g < gens; ++g) {
     const int q = pipe ? p : 0;
-    if (pipe) run(OP_ORD_PLAN, c, plan_args(1 - p, true, p));
+    if (pipe == 1) run(OP_ORD_PLAN, c, plan_args(1 - p, true, p));
     SrnnArgs a = base();
     a.W2 = buf[p].data(), a.W = buf[1 - p].data(), a.W3 = W3.data();
     a.gen_ptr = ring.data() + p, a.gen_out = ring.data() + (1 - p);
@@ -371,6 +372,11 @@ static void ordered_soup(const SrnnCfg& c, int64_t n, int gens, bool pipe) {
     a.uid_base = next.data(), a.uid_out = uid.data(), a.counts = counts.data();
     a.action = act.data(), a.counterpart = cp.data(), a.loss = loss.data(), a.respawn = rs.data();
     if (pipe) a.flags |= SRNN_F_ORD_PLANNED;
+    if (pipe == 2) {
+      a.flags |= SRNN_F_ORD_INPLAN;
+      a.o_src_next = osrc[1 - p].data(), a.o_list_next = olist[1 - p].data(), a.o_ctl_next = octl[1 - p].data();
+      a.o_plan_groups = 1;
+    }
     run(OP_SOUP_ORDERED, c, a);
     CHECK(octl[q][18] == 0);  // error bits
     p = 1 - p;
@@ -382,10 +388,11 @@ static void ordered_soup(const SrnnCfg& c, int64_t n, int gens, bool pipe) {
 }
 
 int main() {
-  CHECK(srnn_abi_version() == 27);
-  ordered_soup(ww22(), 257, 4, true);
-  ordered_soup(ww22(), 257, 4, false);
-  ordered_soup(agg422(), 129, 3, true);
+  CHECK(srnn_abi_version() == 28);
+  ordered_soup(ww22(), 257, 4, 0);
+  ordered_soup(ww22(), 257, 4, 1);
+  ordered_soup(ww22(), 257, 4, 2);
+  ordered_soup(agg422(), 129, 3, 2);
   seq_soup(ww22(), 257, 4);
   seq_soup(agg422(), 129, 3);
   ops_smoke(ww22(), 1000);

@@ -117,9 +117,12 @@ class ExecConfig:
     perm_table: Optional[bool] = None       # SRNN_PERM_TABLE: a generation's SGD permutations precomputed by
                                             # one launch ahead of it (nibble Weightwise nets on the device;
                                             # None: the reference order's pending turns only)
-    ord_pipeline: bool = True               # SRNN_ORD_PIPELINE: a single-rank reference-order generation's plan
+    ord_pipeline: str = "stream"            # SRNN_ORD_PIPELINE: a single-rank reference-order generation's plan
                                             # (lists, versions, records, permutations) is built one generation
-                                            # ahead on a side stream, beside the generation in flight
+                                            # ahead -- "stream": by launches on a side stream (a hipGraph join per
+                                            # generation); "kernel": by the last workgroups of the run launch in
+                                            # flight (measured slower: 0.288 vs 0.176 ms, profiles/r6a); "off":
+                                            # inline, before each run (True / False: stream / off)
 
     _ENV = dict(finish_mode="SRNN_FINISH_MODE", finish_par="SRNN_FINISH_PAR", graph_chunks="SRNN_GRAPH_CHUNKS",
                 x2_schedule="SRNN_X2_SCHEDULE", x2_prio="SRNN_X2_PRIO", x2_emulate_remote="SRNN_X2_EMULATE_REMOTE",
@@ -147,7 +150,14 @@ class ExecConfig:
             raise ValueError("x2_emulate_remote is a fraction in [0, 1]")
         if not 1 <= int(self.order_levels) <= 16:
             raise ValueError("order_levels must be in 1..16")
+        if self.ord_pipeline not in ("kernel", "stream", "off"):
+            raise ValueError("ord_pipeline must be kernel, stream or off")
         return self
+
+    def __post_init__(self):
+        # (booleans of the earlier on/off knob: on = the side-stream form)
+        if isinstance(self.ord_pipeline, bool):
+            object.__setattr__(self, "ord_pipeline", "stream" if self.ord_pipeline else "off")
 
     def resolved(self) -> "ExecConfig":
         """This config with every knob whose environment variable is set overridden by it."""
@@ -163,6 +173,8 @@ class ExecConfig:
                                           reverse=True))
             elif f.name in ("finish_mode", "x2_schedule"):
                 kw[f.name] = v
+            elif f.name == "ord_pipeline":
+                kw[f.name] = {"1": "stream", "true": "stream", "on": "stream", "0": "off", "false": "off"}.get(v.lower(), v)
             elif f.name == "x2_emulate_remote":
                 kw[f.name] = float(v)
             elif f.name in ("soup_lanes", "order_levels", "ww_wave", "ordsh_emulate"):

@@ -20,7 +20,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 # SRNN_LIB: load another build of the library (A/B of compiler flags on the GPU box)
 LIB_PATH = os.environ.get("SRNN_LIB") or os.path.join(_HERE, "libsrnn.so")
 CSRC = os.path.normpath(os.path.join(_HERE, "..", "..", "csrc"))
-ABI_VERSION = 27
+ABI_VERSION = 28
 
 # SrnnOp (csrc/srnn_abi.h)
 OP_INIT = 0
@@ -45,8 +45,9 @@ OP_SOUP_ORDERED = 22  # reference-order (sequential) generation, DAG-scheduled (
 OP_SOUP_ORDERED_SH = 23  # one phase of a sharded reference-order generation (csrc/srnn_ordered_sh.h)
 OP_ORD_PLAN = 24  # the plan of a reference-order generation (lists, versions, records, permutations)
 ORDSH_PLAN, ORDSH_LEVEL, ORDSH_PACK, ORDSH_UNPACK, ORDSH_CLOSE, ORDSH_LINK = range(6)
-ORD_CTL_WORDS = 165   # o_ctl words of an ordered generation (csrc/srnn_ordered.h)
+ORD_CTL_WORDS = 166   # o_ctl words of an ordered generation (csrc/srnn_ordered.h)
 ORD_MAXLW, ORD_ERRW = 17, 18
+ORD_BARW = 165        # phase-barrier arrivals of the in-run planning workgroups
 ORD_NPART = 64        # partitions of the pending records
 ORD_REC = 32          # int32 words per pending record
 ORD_MAX_LEVELS = 16   # dependency levels reported one by one (deeper: one bin)
@@ -90,6 +91,7 @@ FLAG_X2_POST_FUSED = 1 << 21
 FLAG_PTAB_READY = 1 << 23  # ptab already holds the generation's permutations (the sharded pack built them)
 FLAG_ORD_PLANNED = 1 << 25  # OP_SOUP_ORDERED: the plan is already built (OP_ORD_PLAN one generation ahead)
 FLAG_ORD_NEXT = 1 << 26  # OP_ORD_PLAN: plan generation gen + 1 (the one after the generation in flight)
+FLAG_ORD_INPLAN = 1 << 28  # OP_SOUP_ORDERED: the run launch builds the next generation's plan (*_next buffers)
 
 X2_HDR = 12           # int64 header words of an exchange block
 X2_REMOTE_WAVES = 4096
@@ -141,6 +143,9 @@ class SrnnArgs(ctypes.Structure):
         ("o_trace", _P),
         # the sharded reference-order generation: this rank's turns [o_lo, o_hi)
         ("o_lo", _I64), ("o_hi", _I64),
+        # SRNN_F_ORD_INPLAN: the next generation's plan set, built by the run launch's last workgroups
+        ("o_src_next", _P), ("o_list_next", _P), ("o_ctl_next", _P), ("ptab_next", _P),
+        ("o_plan_groups", _I32), ("pad4", _I32),
     ]
 
 

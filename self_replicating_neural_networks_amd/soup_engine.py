@@ -356,6 +356,8 @@ class SoupEngine:
             self._init_single_or_allgather(nb)
         self.cfg = _lib.make_cfg(spec, self.dtype_code)
         self._ord_pipe = False      # reference order: plan built one generation ahead (_init_ordered)
+        self._ord_side = None       # ... on this side stream (device, mode "stream")
+        self._ord_mode = "off"      # ... by the run launch ("kernel") or the side stream ("stream")
         if order == "sequential":
             self._init_ordered()
         # initial particles: uids 0..n_total-1, keyed init (identical for any rank count)
@@ -481,17 +483,24 @@ class SoupEngine:
             self._sh_recv = torch.zeros(self.dist.world * max(cap, 1) * self._sh_recb // 8, dtype=torch.int64,
                                         device=dev)
         self._octl = torch.zeros(_lib.ORD_CTL_WORDS, dtype=torch.int32, device=dev)
-        # single rank: the plan of generation t+1 is built (OP_ORD_PLAN) while generation t runs --
-        # on a side stream on the device -- into the other of two plan sets, indexed like the attack
-        # lists by the ping-pong parity (ExecConfig.ord_pipeline)
-        self._ord_pipe = not sharded and bool(self.execution.ord_pipeline)
+        # single rank: the plan of generation t+1 is built while generation t runs, into the other of
+        # two plan sets, indexed like the attack lists by the ping-pong parity (ExecConfig.ord_pipeline):
+        # "stream" -- by OP_ORD_PLAN on a side stream, joined before the next run (the join costs ~10 us
+        # of idle queue inside a hipGraph, the plan ~40 us of launches: profiles/r6a); "kernel" -- by
+        # the last workgroups of generation t's run launch (SRNN_F_ORD_INPLAN; measured slower: grid
+        # barriers between the plan phases cost more than the join; the host path plans after the
+        # generation)
+        mode = self.execution.ord_pipeline
+        self._ord_pipe = not sharded and mode != "off"
+        self._ord_mode = mode if self._ord_pipe else "off"
         self._osrc1 = self._olist1 = self._octl1 = None
         self._ord_side = None
         if self._ord_pipe:
             self._osrc1 = torch.zeros_like(self._osrc)
             self._olist1 = torch.zeros_like(self._olist)
             self._octl1 = torch.zeros_like(self._octl)
-            self._ord_side = torch.cuda.Stream(dev) if dev.type == "cuda" else None
+            if mode == "stream" and dev.type == "cuda":
+                self._ord_side = torch.cuda.Stream(dev)
         self._rec_rows = None  # recording: every particle's state before any respawn
 
     def _ord_set(self, q: int):
@@ -528,8 +537,8 @@ class SoupEngine:
     def ordered_trace(self, on: bool = True, slots: int = 2) -> None:
         """Record, on the device, when each turn of the next reference-order generations starts
         and ends (s_memrealtime, 100 MHz; debug: a few stores per turn).  Read it with
-        ``ordered_timeline()``.  ``slots=8``: a library built with -DSRNN_ORD_TRACE_FINE also stamps
-        the phases of every turn (TRACE_PHASES)."""
+        ``ordered_timeline()``.  ``slots=10``: a library built with -DSRNN_ORD_TRACE_FINE also stamps
+        the phases of every turn (TRACE_PHASES) and the shader clock over its self-train."""
         if self.order != "sequential" or self.device.type != "cuda":
             raise ValueError("the turn trace is a device reference-order generation's")
         self._otrace_slots = int(slots)
@@ -546,7 +555,7 @@ class SoupEngine:
         n = self.n
         S = getattr(self, "_otrace_slots", 2)
         raw = self._otrace.view(-1, S).cpu().double()[:n]
-        t = raw[:, [0, S - 1]]
+        t = raw[:, [0, 7 if S >= 8 else S - 1]]
         osrc, _, octl = self._ord_set(self._ord_last())
         src = osrc.cpu()
         lv = src[:4 * n].view(n, 4)[:, 3]
@@ -578,9 +587,14 @@ class SoupEngine:
         chain = []
         while True:
             step = dict(turn=k, level=int(lv[k]), start=float(us[k, 0]), end=float(us[k, 1]), handoff=hand.get(k))
-            if S == 8:  # phase durations (us) of the fine trace
+            if S >= 8:  # phase durations (us) of the fine trace; the self-train's shader clock (GHz)
                 ph = raw[k].tolist()
                 step["phases"] = {name: (ph[i + 1] - ph[i]) / 100.0 for i, name in enumerate(self.TRACE_PHASES)}
+                if S >= 10 and ph[5] > ph[4]:
+                    step["train_clock_ghz"] = (ph[9] - ph[8]) / ((ph[5] - ph[4]) * 10.0)
+                if S >= 12:
+                    r = int(raw[k, 10].item()) if raw[k, 10] < 2 ** 62 else -1
+                    step["ptab_row"] = r
             chain.append(step)
             if k not in prods:
                 break
@@ -798,6 +812,12 @@ class SoupEngine:
                 fa.ptab = _p(self._perm_table(q))
                 if self._ord_pipe:
                     fa.flags |= _lib.FLAG_ORD_PLANNED
+                if self._ord_mode == "kernel":  # the run launch also builds the next generation's plan
+                    nsrc, nlist, nctl = self._ord_set(1 - q)
+                    fa.flags |= _lib.FLAG_ORD_INPLAN
+                    fa.o_src_next, fa.o_list_next, fa.o_ctl_next = _p(nsrc), _p(nlist), _p(nctl)
+                    fa.ptab_next = _p(self._perm_table(1 - q))
+                    fa.o_plan_groups = self.plan_groups(self.n)
                 fa.o_levels = self.order_levels
                 fa.o_trace = _p(getattr(self, "_otrace", None))
             ca = fa
@@ -880,12 +900,13 @@ class SoupEngine:
         if self._ord_pipe:
             if not self._lists_ready:  # the first generation's plan (later ones: planned ahead)
                 _lib.run(_lib.OP_ORD_PLAN, spec, self._plan_args(False), cfg)
-            # the next generation's plan beside this one (weight independent); it overwrites the
-            # plan set and attack lists the previous generation's close finished with
-            if self._ord_side is not None:
-                side, main = self._ord_side, torch.cuda.current_stream(self.device)
-                side.wait_stream(main)
-            _lib.run(_lib.OP_ORD_PLAN, spec, self._plan_args(True), cfg)
+            if self._ord_mode == "stream":
+                # the next generation's plan beside this one (weight independent); it overwrites the
+                # plan set and attack lists the previous generation's close finished with
+                if self._ord_side is not None:
+                    side, main = self._ord_side, torch.cuda.current_stream(self.device)
+                    side.wait_stream(main)
+                _lib.run(_lib.OP_ORD_PLAN, spec, self._plan_args(True), cfg)
         elif not self._lists_ready:
             _lib.run(_lib.OP_SOUP_DECIDE, spec, a, cfg)
         rec = record and self.recorder is not None
@@ -911,6 +932,13 @@ class SoupEngine:
             self.classify_local(self.stats_with_sec, zero=False)
         if rec:
             self.recorder.on_evolved(self, rows=self._rec_rows, old_uid=uid0, ordered=True)
+
+    @staticmethod
+    def plan_groups(n: int) -> int:
+        """Workgroups of a run launch that build the next generation's plan (ord_pipeline "kernel"):
+        one per 64-turn chunk up to 512 -- each plan phase then takes a few chunks per workgroup, well
+        inside the run's dependent tail (csrc/srnn_ordered.h ord::plan_group)."""
+        return max(1, min(512, -(-int(n) // 64)))
 
     def _plan_args(self, nxt: bool) -> _lib.SrnnArgs:
         """OP_ORD_PLAN arguments: the plan of the generation about to run (``nxt`` False: the

@@ -72,7 +72,7 @@ def test_bench_headline_is_the_reference_order():
     assert "reference (sequential) order" in d["config"]["model"]
     lv = d["config"]["ordered_levels"]
     assert lv["error"] == 0 and sum(lv["levels"]) + lv["tail"] == 1500
-    assert d["config"]["ord_pipeline"] is True and d["config"]["reference_order"] is None
+    assert d["config"]["ord_pipeline"] == "stream" and d["config"]["reference_order"] is None
     j = d["config"]["jacobi"]
     assert j is not None and j["semantics"] == "jacobi" and j["steps"] == d["steps"]
     assert j["ms_per_step"] > 0 and j["value"] > 0 and sum(j["final_census"].values()) == 1500

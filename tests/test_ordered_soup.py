@@ -37,15 +37,16 @@ def _same(ordered: SoupEngine, seq: SequentialSoupEngine, P: int):
 
 
 @pytest.mark.parametrize("spec", SPECS, ids=IDS)
-@pytest.mark.parametrize("levels,pipe", [(4, True), (1, True), (4, False)])
+@pytest.mark.parametrize("levels,pipe", [(4, "kernel"), (1, "kernel"), (4, "stream"), (4, "off")])
 def test_host_ordered_generation_is_the_serial_loop(spec, levels, pipe):
     """host path of OP_SOUP_ORDERED == OP_SOUP_SEQ bitwise, generation by generation (levels=1
-    sends every turn past level 0 through the tail; pipe: each generation's plan built by
-    OP_ORD_PLAN while the previous one runs, into the other plan set)"""
+    sends every turn past level 0 through the tail; pipe: each generation's plan built one
+    generation ahead into the other plan set -- by the generation call itself ("kernel") or by
+    OP_ORD_PLAN ("stream") -- or inline ("off"))"""
     n, seed = 300, 5
     o = SoupEngine(spec, n, HOT, device="cpu", seed=seed, order="sequential",
                    execution=ExecConfig(order_levels=levels, ord_pipeline=pipe))
-    assert o._ord_pipe == pipe
+    assert o._ord_mode == pipe
     s = SequentialSoupEngine(spec, n, HOT, seed=seed)
     _same(o, s, spec.P)
     deep = 0
@@ -126,16 +127,17 @@ def test_ordered_soup_records_reference_states():
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("spec", SPECS, ids=IDS)
-@pytest.mark.parametrize("pipe", [True, False], ids=["pipelined", "inline-plan"])
+@pytest.mark.parametrize("pipe", ["kernel", "stream", "off"])
 def test_device_ordered_generation_is_the_serial_loop(spec, pipe):
-    """device OP_SOUP_ORDERED (plan -> run by continuation -> close; pipelined: the plan of the
-    next generation built on a side stream while this one runs) == the serial loop on the same
-    device (k_soup_seq, one lane) bitwise, eager and captured in hipGraphs"""
+    """device OP_SOUP_ORDERED (plan -> run by continuation -> close; the plan of the next
+    generation built while this one runs -- by the run launch's last workgroups ("kernel") or on a
+    side stream ("stream") -- or inline ("off")) == the serial loop on the same device (k_soup_seq,
+    one lane) bitwise, eager and captured in hipGraphs"""
     n, seed = 3000, 7
     for graphs in (False, True):
         o = SoupEngine(spec, n, HOT, device="cuda", seed=seed, order="sequential",
                        execution=ExecConfig(ord_pipeline=pipe))
-        assert o._ord_pipe == pipe
+        assert o._ord_mode == pipe
         # the same starting rows (the device init contracts a*b+c, the host's does not)
         s = SequentialSoupEngine(spec, n, HOT, seed=seed, device="cuda", weights=o.local_rows()[:, :spec.P].cpu())
         if graphs:
