@@ -289,7 +289,7 @@ def main(argv=None):
                        "sharded_schedule": getattr(eng, "schedule", None) if getattr(eng, "x2", False) else None,
                        "census_every_step": eng.stats, "final_census": census, "order": args.order,
                        "ordered_levels": eng.ordered_levels() if args.order == "sequential" else None,
-                       "ord_pipeline": eng._ord_mode,
+                       "ord_pipeline": eng._ord_mode, "ord_census_side": eng._ord_census_side,
                        "jacobi": side if other == "synchronous" else None,
                        "reference_order": side if other == "sequential" else None},
         }), flush=True)

@@ -63,6 +63,10 @@ enum SrnnFlag : uint32_t {
                                      // the NEXT generation's plan into o_src_next / o_list_next /
                                      // o_ctl_next / ptab_next and the lists heads_next / nexts_next while
                                      // this generation's turns run (one launch, no second stream)
+  SRNN_F_ORD_CENSUS_LATER = 1u << 29, // OP_SOUP_ORDERED: the close writes the final rows, respawn ballots and
+                                     // the counter only; the census of the final rows (block-stat class
+                                     // counts) is OP_ORD_CENSUS's, issued on the side stream beside the
+                                     // next generation
 };
 
 // Attack-list entries (uint32, SRNN_NIL ends a list).  Single rank: the attacker's row
@@ -229,6 +233,8 @@ enum SrnnOp {
                            // o_levels, 2 pack their outputs, 3 unpack the gathered outputs, 4 close
                            // this rank's rows, 5 link the next generation's attacks
                            // (srnn_ordered_sh.h)
+  OP_ORD_CENSUS = 25,   // the census of a reference-order generation's final rows (W) into the class counts
+                        // of its two-phase block stats (temp), after a close with SRNN_F_ORD_CENSUS_LATER
   OP_ORD_PLAN = 24,     // the plan of a single-rank reference-order generation into o_src / o_list /
                         // o_ctl / ptab: its attack lists linked into heads / nexts (NIL on entry),
                         // source versions, stored-output marks, pending records + consumer lists

@@ -79,6 +79,7 @@ const char* op_name(int op) {
     case OP_SOUP_ORDERED: return "srnn:soup_ordered";
     case OP_SOUP_ORDERED_SH: return "srnn:soup_ordered_sh";
     case OP_ORD_PLAN: return "srnn:ord_plan";
+    case OP_ORD_CENSUS: return "srnn:ord_census";
     default: return "srnn:op";
   }
 }

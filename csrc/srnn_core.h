@@ -508,6 +508,9 @@ struct TrainCtx {
   const uint64_t* ptab = nullptr;
   int64_t pstride = 0;
   uint32_t pbase = 0;
+#if defined(SRNN_ORD_TRACE_FINE)
+  uint64_t* etrace = nullptr;  // diagnostic build: s_memrealtime at each table epoch's start
+#endif
 };
 
 struct ApplyCtx {
@@ -627,6 +630,9 @@ struct Weightwise {
     const float lr2 = 2.0f * c.lr;  // folded step -(2 lr) * err (train_epoch)
     float loss = 0.f;
     for (int e = 0; e < E; ++e) {
+#if defined(SRNN_ORD_TRACE_FINE) && defined(__HIP_DEVICE_COMPILE__)
+      if (SELF && c.etrace && e < 24) c.etrace[e] = __builtin_amdgcn_s_memrealtime();
+#endif
       if (SELF && e > 0)
 #pragma unroll
         for (int k = 0; k < P; ++k) reinterpret_cast<float*>(&c.samp[k * c.stride])[0] = w[k];

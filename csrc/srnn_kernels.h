@@ -1970,6 +1970,7 @@ int run_net_op(int op, const SrnnCfg& c, const SrnnArgs& a) {
     case OP_SOUP_ORDERED: return soup_ordered<Net, S>(c, a);
     case OP_SOUP_ORDERED_SH: return soup_ordered_sh<Net, S>(c, a);
     case OP_ORD_PLAN: return soup_ord_plan<Net, S>(c, a);
+    case OP_ORD_CENSUS: return soup_ord_census<Net, S>(c, a);
     default: set_error("unknown op"); return -1;
   }
 }

@@ -234,16 +234,17 @@ constexpr int ord_rb() {
 // 5 self-train, 6 stores, 7 published); the shipped build records 0 and 7 only ([2k], [2k + 1])
 // (8, 9: the shader-clock counter s_memtime at the self-train's start and end: the clock the chain
 // ran at is their difference over the real-time one)
-// (10: the permutation-table row the turn trained with, -1: drawn inline; 11: spare)
+// (10: the permutation-table row the turn trained with, -1: drawn inline; 11: spare; 12..35: the
+// start of each self-train epoch)
 #if defined(__HIP_DEVICE_COMPILE__) && defined(SRNN_ORD_TRACE_FINE)
 #define SRNN_ORD_STAMP(a, k, i)                                                        \
   if ((a).o_trace) {                                                                   \
-    (a).o_trace[12 * (k) + (i)] = __builtin_amdgcn_s_memrealtime();                   \
-    if ((i) == 4 || (i) == 5) (a).o_trace[12 * (k) + 4 + (i)] = __builtin_amdgcn_s_memtime(); \
+    (a).o_trace[36 * (k) + (i)] = __builtin_amdgcn_s_memrealtime();                   \
+    if ((i) == 4 || (i) == 5) (a).o_trace[36 * (k) + 4 + (i)] = __builtin_amdgcn_s_memtime(); \
   }
 #define SRNN_ORD_NOTE(a, k, i, v) \
-  if ((a).o_trace) (a).o_trace[12 * (k) + (i)] = (uint64_t)(v)
-constexpr int TRACE_SLOTS = 12, TRACE_END = 7;
+  if ((a).o_trace) (a).o_trace[36 * (k) + (i)] = (uint64_t)(v)
+constexpr int TRACE_SLOTS = 36, TRACE_END = 7;
 #else
 #define SRNN_ORD_STAMP(a, k, i)
 #define SRNN_ORD_NOTE(a, k, i, v)
@@ -331,6 +332,14 @@ struct Ord : OrdSched<ord_rb<Net>()> {
       tc.pbase = tc.ctr;
     }
     SRNN_ORD_NOTE(a, k, 10, tc.ptab ? prow : -1);
+#if defined(SRNN_ORD_TRACE_FINE) && defined(__HIP_DEVICE_COMPILE__)
+    // where the turn runs: HW_ID (wave slot, SIMD, CU, SH, SE) | XCC_ID << 32
+    SRNN_ORD_NOTE(a, k, 11, ((uint64_t)__builtin_amdgcn_s_getreg(20 | (31 << 11)) << 32) |
+                                (uint64_t)(uint32_t)__builtin_amdgcn_s_getreg(4 | (31 << 11)));
+#endif
+#if defined(SRNN_ORD_TRACE_FINE)
+    tc.etrace = a.o_trace ? a.o_trace + 36 * k + 12 : nullptr;
+#endif
     float loss = 0.f;
     if (te >= 0) {  // 2. learn_from the teacher's current row
       if (s[2] == SRC_SELF) I::copy(f, w);
@@ -374,7 +383,9 @@ struct Ord : OrdSched<ord_rb<Net>()> {
   }
 
   // row r after the generation: the last attack after its own turn, else E(r) (in W);
-  // consumes r's attack list.  w receives the final row as a reload would see it.
+  // consumes r's attack list.  w receives the final row as a reload would see it (ROW = false:
+  // only a recomputed final row is written, nothing is loaded -- the census comes later).
+  template <bool ROW = true>
   SRNN_HD static void close_row(const SrnnCfg& c, const SrnnArgs& a, int64_t r, int32_t gen, uint8_t* perm, float* w) {
     const int64_t ja = last_attacker_before(a, r, a.n);
     a.heads[r] = SRNN_NIL;  // consumed: NIL for the generation after next
@@ -384,7 +395,7 @@ struct Ord : OrdSched<ord_rb<Net>()> {
       };
       mat<RB>(a, code_A(ja), w, ap);
       I::store(I::rowp(a.W, r), w);
-    } else {
+    } else if constexpr (ROW) {
       I::load(I::rowp(a.W, r), w);
     }
   }
@@ -895,17 +906,19 @@ __global__ __launch_bounds__(TB) void k_ord_close(SrnnCfg c, SrnnArgs a) {
   if ((a.flags & SRNN_F_ORD_INPLAN) && gb == 0 && lane == 0) a.o_ctl[ord::BARW] = 0;
   bool rs = false;
   int8_t k = -1;
+  const bool later = (a.flags & SRNN_F_ORD_CENSUS_LATER) != 0;  // the census: k_ord_census, beside the next run
   if (r < a.n) {
     if (a.o_src[4 * r + 3] < 0) atomicOr(a.o_ctl + ord::ERRW, ord::ERR_NOT_RUN);  // never ran: a scheduling bug
     float w[Net::P];
-    ord::Ord<Net, S>::close_row(c, a, r, gen, perm, w);
+    if (later) ord::Ord<Net, S>::template close_row<false>(c, a, r, gen, perm, w);
+    else ord::Ord<Net, S>::close_row(c, a, r, gen, perm, w);
     rs = a.respawn[r] != 0;
     if (!(a.flags & SRNN_F_ORD_PLANNED)) {  // (planned ahead: the next OP_ORD_PLAN links them)
       int64_t at, te;
       I::decision(a, r, gen + 1, at, te);
       if (at >= 0) I::link(a.heads_next, a.nexts_next, at, (uint32_t)r);
     }
-    if (census)
+    if (census && !later)
       k = I::classify_w(w, a.eps, (a.flags & SRNN_F_FIX_SEC) != 0, I::actx(a, c, (uint64_t)r, 0x7FFFFFF0u, perm));
   }
   if ((a.flags & SRNN_F_GEN_COUNTS) && gb == 0 && lane == 0) I::set_gen(a, gen + 1);
@@ -922,6 +935,51 @@ __global__ __launch_bounds__(TB) void k_ord_close(SrnnCfg c, SrnnArgs a) {
     mine[3] = (unsigned long long)cnt[4];
     if ((a.flags & SRNN_F_BORN_TOTAL) && m) atomicAdd(bs + ((a.n + TB - 1) / TB) * 4, (unsigned long long)__popcll(m));
   }
+}
+
+// the census of the final rows after a close with SRNN_F_ORD_CENSUS_LATER: the class counts of each
+// 64-row block into its block stats (words 1..3; the close wrote the respawn ballot, word 0)
+template <class Net, class S>
+__global__ __launch_bounds__(TB) void k_ord_census(SrnnCfg c, SrnnArgs a) {
+  using I = Item<Net, S>;
+  constexpr int PERM = (Net::P + 4) & ~3;
+  __shared__ uint8_t s_perm[TB * PERM];
+  const int64_t gb = blockIdx.x;
+  const int64_t r = gb * TB + threadIdx.x;
+  const int lane = threadIdx.x;
+  int8_t k = -1;
+  if (r < a.n) {
+    float w[Net::P];
+    I::load(I::rowp(a.W, r), w);
+    k = I::classify_w(w, a.eps, (a.flags & SRNN_F_FIX_SEC) != 0,
+                      I::actx(a, c, (uint64_t)r, 0x7FFFFFF0u, s_perm + lane * PERM));
+  }
+  uint32_t cnt[5];
+#pragma unroll
+  for (int q = 0; q < 5; ++q) cnt[q] = (uint32_t)__popcll(__ballot(k == q));
+  if (lane == 0) {
+    unsigned long long* mine = reinterpret_cast<unsigned long long*>(a.temp) + gb * 4;
+    mine[1] = (unsigned long long)cnt[0] | ((unsigned long long)cnt[1] << 32);
+    mine[2] = (unsigned long long)cnt[2] | ((unsigned long long)cnt[3] << 32);
+    mine[3] = (unsigned long long)cnt[4];
+  }
+}
+
+template <class Net, class S>
+int soup_ord_census(const SrnnCfg& c, const SrnnArgs& a) {
+  if (!a.dev || !a.W || !a.temp || a.n < 0) {
+    set_error("ordered census: device, final rows W and the generation's block stats (temp)");
+    return -5;
+  }
+  const int64_t nb = (a.n + TB - 1) / TB;
+  if (nb <= 0) return 0;
+  hipLaunchKernelGGL((k_ord_census<Net, S>), dim3((unsigned)nb), dim3(TB), 0, (hipStream_t)a.stream, c, a);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) {
+    set_error(hipGetErrorString(e));
+    return -3;
+  }
+  return 0;
 }
 
 #include "srnn_pair.h"

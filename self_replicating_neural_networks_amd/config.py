@@ -123,6 +123,9 @@ class ExecConfig:
                                             # generation); "kernel": by the last workgroups of the run launch in
                                             # flight (measured slower: 0.288 vs 0.176 ms, profiles/r6a); "off":
                                             # inline, before each run (True / False: stream / off)
+    ord_census_side: bool = True            # SRNN_ORD_CENSUS_SIDE: with the side-stream plan, each generation's
+                                            # census runs on the side stream beside the next run, the close keeps
+                                            # only the final rows, ballots and counter
 
     _ENV = dict(finish_mode="SRNN_FINISH_MODE", finish_par="SRNN_FINISH_PAR", graph_chunks="SRNN_GRAPH_CHUNKS",
                 x2_schedule="SRNN_X2_SCHEDULE", x2_prio="SRNN_X2_PRIO", x2_emulate_remote="SRNN_X2_EMULATE_REMOTE",
@@ -132,7 +135,8 @@ class ExecConfig:
                 fix_group="SRNN_FIX_GROUP", soup_lanes="SRNN_SOUP_LANES", ord_crit="SRNN_ORD_CRIT", ord_queue="SRNN_ORD_QUEUE",
                 ordsh_emulate="SRNN_ORDSH_EMULATE",
                 order_levels="SRNN_ORDER_LEVELS",
-                perm_table="SRNN_PERM_TABLE", ord_pipeline="SRNN_ORD_PIPELINE")
+                perm_table="SRNN_PERM_TABLE", ord_pipeline="SRNN_ORD_PIPELINE",
+                ord_census_side="SRNN_ORD_CENSUS_SIDE")
     # Optional[bool] knobs whose None means "the built-in choice" (by population size, ...)
     TRI_STATE = ("force_generic", "rnn_wave", "rnn_spec", "rnn_soup", "big_wave", "fix_group", "perm_table",
                  "ord_crit", "ord_queue")

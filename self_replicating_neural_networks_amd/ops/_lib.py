@@ -44,6 +44,7 @@ OP_X2_POST = 21   # sharded soup: uids, census, received notices / requests
 OP_SOUP_ORDERED = 22  # reference-order (sequential) generation, DAG-scheduled (csrc/srnn_ordered.h)
 OP_SOUP_ORDERED_SH = 23  # one phase of a sharded reference-order generation (csrc/srnn_ordered_sh.h)
 OP_ORD_PLAN = 24  # the plan of a reference-order generation (lists, versions, records, permutations)
+OP_ORD_CENSUS = 25  # the census of a reference-order generation's final rows into its block stats
 ORDSH_PLAN, ORDSH_LEVEL, ORDSH_PACK, ORDSH_UNPACK, ORDSH_CLOSE, ORDSH_LINK = range(6)
 ORD_CTL_WORDS = 166   # o_ctl words of an ordered generation (csrc/srnn_ordered.h)
 ORD_MAXLW, ORD_ERRW = 17, 18
@@ -92,6 +93,7 @@ FLAG_PTAB_READY = 1 << 23  # ptab already holds the generation's permutations (t
 FLAG_ORD_PLANNED = 1 << 25  # OP_SOUP_ORDERED: the plan is already built (OP_ORD_PLAN one generation ahead)
 FLAG_ORD_NEXT = 1 << 26  # OP_ORD_PLAN: plan generation gen + 1 (the one after the generation in flight)
 FLAG_ORD_INPLAN = 1 << 28  # OP_SOUP_ORDERED: the run launch builds the next generation's plan (*_next buffers)
+FLAG_ORD_CENSUS_LATER = 1 << 29  # OP_SOUP_ORDERED: the census is OP_ORD_CENSUS's, beside the next generation
 
 X2_HDR = 12           # int64 header words of an exchange block
 X2_REMOTE_WAVES = 4096

@@ -80,6 +80,14 @@ def describe_ordered_error(bits: int) -> str:
     return "; ".join(f"{b}: {msg}" for b, msg in ORD_ERRORS.items() if bits & b) or f"error bits {bits}"
 
 
+class _nullcontext:
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        return False
+
+
 def _p(t):
     return ctypes.c_void_p(t.data_ptr()) if t is not None else None
 
@@ -358,6 +366,8 @@ class SoupEngine:
         self._ord_pipe = False      # reference order: plan built one generation ahead (_init_ordered)
         self._ord_side = None       # ... on this side stream (device, mode "stream")
         self._ord_mode = "off"      # ... by the run launch ("kernel") or the side stream ("stream")
+        self._ord_census_side = False  # ... with the census of each generation beside the next one
+        self._census_due = None
         if order == "sequential":
             self._init_ordered()
         # initial particles: uids 0..n_total-1, keyed init (identical for any rank count)
@@ -501,6 +511,12 @@ class SoupEngine:
             self._octl1 = torch.zeros_like(self._octl)
             if mode == "stream" and dev.type == "cuda":
                 self._ord_side = torch.cuda.Stream(dev)
+        # (stream mode) the census of a generation's final rows runs on the side stream beside the
+        # next generation's run (OP_ORD_CENSUS), leaving the close on the critical path only the
+        # final rows, ballots and counter
+        self._ord_census_side = (self._ord_side is not None and bool(self.execution.ord_census_side) and
+                                 _lib.supports(self.spec, _lib.OP_ORD_CENSUS, True, self.dtype_code))
+        self._census_due = None  # the block stats of a generation whose census is still to run
         self._rec_rows = None  # recording: every particle's state before any respawn
 
     def _ord_set(self, q: int):
@@ -595,6 +611,17 @@ class SoupEngine:
                 if S >= 12:
                     r = int(raw[k, 10].item()) if raw[k, 10] < 2 ** 62 else -1
                     step["ptab_row"] = r
+                if S >= 36:  # each self-train epoch's duration (us)
+                    ep = [x for x in ph[12:36] if x > 0] + [ph[5]]
+                    step["epochs_us"] = [round((b - a) / 100.0, 2) for a, b in zip(ep, ep[1:])]
+                    # the other turns that ran on the same SIMD (HW_ID + XCC_ID) during its self-train
+                    hw = self._otrace.view(-1, S)[:n, 11].cpu()
+                    simd = ((hw >> 32) << 16) | (hw & 0xFF30)  # xcc, se, sh, cu, simd (no wave slot / pipe)
+                    mine = int(simd[k])
+                    lo_t, hi_t = float(ph[4]), float(ph[5])
+                    other = (simd == mine) & ok & (raw[:, 0] < hi_t) & (raw[:, 7] > lo_t)
+                    other[k] = False
+                    step["simd_neighbours"] = int(other.sum())
             chain.append(step)
             if k not in prods:
                 break
@@ -812,6 +839,8 @@ class SoupEngine:
                 fa.ptab = _p(self._perm_table(q))
                 if self._ord_pipe:
                     fa.flags |= _lib.FLAG_ORD_PLANNED
+                if self._ord_census_side and (fa.flags & _lib.FLAG_FUSED_CENSUS):
+                    fa.flags |= _lib.FLAG_ORD_CENSUS_LATER
                 if self._ord_mode == "kernel":  # the run launch also builds the next generation's plan
                     nsrc, nlist, nctl = self._ord_set(1 - q)
                     fa.flags |= _lib.FLAG_ORD_INPLAN
@@ -902,10 +931,13 @@ class SoupEngine:
                 _lib.run(_lib.OP_ORD_PLAN, spec, self._plan_args(False), cfg)
             if self._ord_mode == "stream":
                 # the next generation's plan beside this one (weight independent); it overwrites the
-                # plan set and attack lists the previous generation's close finished with
+                # plan set and attack lists the previous generation's close finished with; first the
+                # previous generation's census, if its close left it
                 if self._ord_side is not None:
                     side, main = self._ord_side, torch.cuda.current_stream(self.device)
                     side.wait_stream(main)
+                with torch.cuda.stream(side) if side is not None else _nullcontext():
+                    self._run_census_due()
                 _lib.run(_lib.OP_ORD_PLAN, spec, self._plan_args(True), cfg)
         elif not self._lists_ready:
             _lib.run(_lib.OP_SOUP_DECIDE, spec, a, cfg)
@@ -921,6 +953,8 @@ class SoupEngine:
             ca.traj = None
             if side is not None:
                 main.wait_stream(side)  # the next generation starts on a complete plan
+        if ca.flags & _lib.FLAG_ORD_CENSUS_LATER:
+            self._census_due = (ca.W, ca.temp, ca.temp_bytes, ca.flags)
         self._lists_ready = True
         self._p = 1 - self._p
         if self.finish_mode == "batch":
@@ -1047,6 +1081,7 @@ class SoupEngine:
         m = self._pending_fin
         if m == 0:
             return
+        self._run_census_due()  # (the last generation's class counts complete its block stats)
         a = self._args()
         a.n = self.n
         a.steps = m
@@ -1058,8 +1093,28 @@ class SoupEngine:
         _lib.run(_lib.OP_GEN_FINISH, self.spec, a, self.cfg)
         self._pending_fin = 0
 
+    def _run_census_due(self):
+        """The census a reference-order close left (FLAG_ORD_CENSUS_LATER), on the current stream."""
+        if self._census_due is None:
+            return
+        W, temp, temp_bytes, flags = self._census_due
+        key = ("census", W, temp, self._stream_key())
+        a = self._arg_cache.get(key)
+        if a is None:
+            a = self._args()
+            a.W, a.temp, a.temp_bytes = W, temp, temp_bytes
+            a.flags = flags & (_lib.FLAG_FIX_SEC | _lib.FLAG_FUSED_CENSUS)
+            self._arg_cache[key] = a
+        _lib.run(_lib.OP_ORD_CENSUS, self.spec, a, self.cfg)
+        self._census_due = None
+
+    def _stream_key(self):
+        return torch.cuda.current_stream(self.device).cuda_stream if self.device.type == "cuda" else 0
+
     def _join_side(self):
-        """Run any batched finish still due (uids, census, next_uid are final after this)."""
+        """Run any census and batched finish still due (uids, census, next_uid are final after this)."""
+        if self._census_due is not None:
+            self._run_census_due()  # (on the main stream: it reads the rows the close just wrote)
         if not self.x2 and self._pending_fin:
             self._finish_pending()
 
@@ -1536,12 +1591,13 @@ class SoupEngine:
         self._chunk = self._chunks[0] if self._chunks else None
 
     def _flags_state(self):
-        return (self._lists_ready, self._pending_fin if not self.x2 else 0)
+        return (self._lists_ready, self._pending_fin if not self.x2 else 0, self._census_due)
 
     def _set_flags_state(self, st):
         self._lists_ready = st[0]
         if not self.x2:
             self._pending_fin = st[1]
+        self._census_due = st[2]
 
     def _capture_chunk_g(self, s, p0, pend0, G):
         """A graph of G consecutive generations (G even: it starts and ends at parity
