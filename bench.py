@@ -281,6 +281,7 @@ def main(argv=None):
                        "global_batch": n_total, "particles_per_gpu": n_total / d.world, "seq_len": None,
                        "parallelism": f"population-dp{d.world}", "device": args.device, "hip_graph": graphed,
                        "multi_generation_graph": eng._chunk is not None,
+                       "two_graph_chunks": any(c[3] is not None for c in eng._chunks),
                        "collectives": comm if comm is not None
                        else (f"torch.distributed ({backend})" if d.enabled else None),
                        "world_size": d.world, "execution": execution.in_force(),

@@ -59,7 +59,13 @@ enum SrnnFlag : uint32_t {
                                      // without linking the next one's (the next OP_ORD_PLAN links them)
   SRNN_F_ORD_NEXT = 1u << 26,        // OP_ORD_PLAN: plan generation gen + 1 (the one after the generation
                                      // in flight) instead of gen
-  SRNN_F_ORD_INPLAN = 1u << 28,      // OP_SOUP_ORDERED (planned): the run launch's last workgroups build
+  SRNN_F_ORD_SYNC = 1u << 27,        // OP_ORD_PLAN (next) / OP_SOUP_ORDERED (planned): the plan and the
+                                     // generation are ordered by the o_sync counters instead of stream
+                                     // events (two hipGraphs on two streams, no cross-queue edge): the
+                                     // plan waits until the run of the generation before it has started
+                                     // (its close is done) and counts itself done; the close waits for
+                                     // the next generation's plan (bounded: ~2 s, then an error bit)
+  SRNN_F_ORD_INPLAN = 1u << 28,      // OP_SOUP_ORDERED (planned): the run launch's last o_plan_groups workgroups build
                                      // the NEXT generation's plan into o_src_next / o_list_next /
                                      // o_ctl_next / ptab_next and the lists heads_next / nexts_next while
                                      // this generation's turns run (one launch, no second stream)
@@ -200,6 +206,12 @@ struct SrnnArgs {
   uint64_t* ptab_next;
   int32_t o_plan_groups;
   int32_t pad4;
+  // ---- SRNN_F_ORD_SYNC: 4 monotonic int32 counters shared by the main and the side stream:
+  // runs started, plans gated, plans done, closes waited (srnn_ordered.h ord::SYNC_*)
+  int32_t* o_sync;
+  // ---- (internal, set by the library from SRNN_KNOB_ORD_SHADOW) shadow lanes of a reference-order run
+  int32_t o_shadow;
+  int32_t pad5;
 };
 
 #define SRNN_X2_HDR 12  // int64 header words of an X2 exchange block (see srnn_shard.hip)
@@ -242,7 +254,7 @@ enum SrnnOp {
                         // independent: issued on a side stream while the previous generation runs
 };
 
-int srnn_abi_version();  // 28
+int srnn_abi_version();  // 29
 int64_t srnn_args_size();  // sizeof(SrnnArgs): the ctypes mirror checks its layout against it
 int64_t srnn_cfg_size();
 int srnn_has_config(const SrnnCfg* cfg);
@@ -267,8 +279,11 @@ enum SrnnKnob {
   SRNN_KNOB_ORD_CRIT = 8,       // SRNN_ORD_CRIT: reference-order generations run the producers of later turns
                                 // first, at raised wave priority (default 1)
   SRNN_KNOB_ORD_QUEUE = 9,      // SRNN_ORD_QUEUE: reference-order continuations through one ready queue
-                                //   (1, default) or run by the producers' waves (0)
-  SRNN_KNOB_COUNT = 10
+                                //   (1) or run by the producers' waves (0, default: measured faster)
+  SRNN_KNOB_ORD_SHADOW = 10,    // SRNN_ORD_SHADOW: a reference-order round with at most this many turns in a
+                                //   wave runs each on several lanes (the idle lanes repeat a busy lane's
+                                //   turn; 0: off; default 63: every round below a full wave)
+  SRNN_KNOB_COUNT = 11
 };
 void srnn_set_knob(int knob, int value);
 int srnn_get_knob(int knob);

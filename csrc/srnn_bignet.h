@@ -1968,6 +1968,7 @@ struct BigOrd : ord::OrdSched<1> {
 // the run policy of k_ord_run: the chunk ids of the shuffled outputs in LDS (stride TBROW)
 template <class T, class S, bool SHUF>
 struct BigOrdPol {
+  static constexpr bool SHADOW = false;  // (the turn's staged reads are wave-cooperative)
   static constexpr int RB = 1;  // the plan's recompute depth (big nets)
   using PT = void;              // no permutation table (an aggregating net's SGD step has one sample)
   struct Shared {
@@ -2028,6 +2029,9 @@ __global__ __launch_bounds__(TB) void k_ordbig_close(SrnnCfg c, SrnnArgs a) {
     mine[3] = (unsigned long long)cnt[4];
     if ((a.flags & SRNN_F_BORN_TOTAL) && m) atomicAdd(bs + ((a.n + TB - 1) / TB) * 4, (unsigned long long)__popcll(m));
   }
+  // SRNN_F_ORD_SYNC: the launch ends (and the next run starts) once the next generation's plan is done
+  if ((a.flags & SRNN_F_ORD_SYNC) && gb == 0 && lane == 0)
+    ord::sync_wait(a.o_sync, ord::SYNC_CLOSE, ord::SYNC_PLAN, a.o_ctl + ord::ERRW);
 }
 // OP_SOUP_ORDERED of a big aggregating net (device): soup_ordered's launch sequence with this
 // family's run policy and close (no permutation table: an aggregating net's SGD step has one
@@ -2042,7 +2046,7 @@ int big_soup_ordered(const SrnnCfg& c, const SrnnArgs& a) {
               "planned ahead), respawn and two-phase block stats (temp)");
     return -5;
   }
-  if (!ord_inplan_ok(a)) return -5;
+  if (!ord_inplan_ok(a) || !ord_sync_ok(a)) return -5;
   const int64_t nb = (a.n + TB - 1) / TB;
   if (nb <= 0) return 0;
   hipStream_t st = (hipStream_t)a.stream;
@@ -2091,6 +2095,10 @@ int big_run_s(int op, const SrnnCfg& c, const SrnnArgs& a) {
       if (!ord_single_table(a)) return -5;
       if (!a.o_src || !a.o_list || !a.o_ctl || !a.heads || !a.nexts) {
         set_error("ordered generation plan needs o_src, o_list, o_ctl and the planned generation's attack lists");
+        return -5;
+      }
+      if ((a.flags & SRNN_F_ORD_SYNC) && (!a.o_sync || !(a.flags & SRNN_F_ORD_NEXT))) {
+        set_error("SRNN_F_ORD_SYNC: a device plan of the next generation with the o_sync counters");
         return -5;
       }
       ord_plan_dev<1, void>(c, a, true);

@@ -116,8 +116,10 @@ namespace {
 const char* const g_knob_env[SRNN_KNOB_COUNT] = {"SRNN_FORCE_GENERIC", "SRNN_RNN_WAVE", "SRNN_RNN_SPEC",
                                                  "SRNN_RNN_SOUP",      "SRNN_WW_WAVE",  "SRNN_BIG_WAVE",
                                                  "SRNN_FIX_GROUP",     "SRNN_SOUP_LANES", "SRNN_ORD_CRIT",
-                                                 "SRNN_ORD_QUEUE"};
-int g_knob[SRNN_KNOB_COUNT] = {-1, -1, -1, -1, -1, -1, -1, -1, -1};
+                                                 "SRNN_ORD_QUEUE",     "SRNN_ORD_SHADOW"};
+// (every knob starts at -1 = its built-in default)
+int g_knob[SRNN_KNOB_COUNT] = {-1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1};
+static_assert(sizeof(g_knob) / sizeof(g_knob[0]) == SRNN_KNOB_COUNT && SRNN_KNOB_COUNT == 11, "one -1 per knob");
 }  // namespace
 namespace srnn {
 int knob(int id, int dflt) {
@@ -204,7 +206,7 @@ static int with_scratch(int op, const SrnnCfg* c, const SrnnArgs* a) {
 
 extern "C" {
 
-int srnn_abi_version() { return 28; }
+int srnn_abi_version() { return 29; }
 
 
 // layout check of the ctypes mirror (ops/_lib.py): sizeof(SrnnArgs) / sizeof(SrnnCfg)

@@ -70,7 +70,10 @@ constexpr int32_t ERR_NOT_RUN = 4;   // a turn that never ran (scheduling bug)
 constexpr int32_t ERR_QUEUE = 8;     // a ready-queue entry never written (scheduling bug)
 constexpr int32_t ERR_PACK = 16;     // sharded: a level's records overflowed the send buffer (sizing bug)
 constexpr int32_t ERR_PLAN_BARRIER = 64;  // a plan workgroup gave up at a phase barrier (scheduling bug)
+constexpr int32_t ERR_SYNC = 128;    // SRNN_F_ORD_SYNC: a wait on the other stream gave up after ~2 s
 // (32: set by the engine -- a one-rank timing model of a sharded generation ran 1/R of the turns)
+// o_sync counters (SRNN_F_ORD_SYNC): runs started, plans gated, plans done, closes that waited
+constexpr int SYNC_RUN = 0, SYNC_GATE = 1, SYNC_PLAN = 2, SYNC_CLOSE = 3, SYNC_WORDS = 4;
 // pending records (and the run order) live in NPART partitions (partition p: the workgroups
 // b = p mod NPART, appended by one counter each: no chip-wide contended counter)
 constexpr int NPART = 64, PART0 = 2 * MAX_LEVELS + 3;
@@ -629,6 +632,41 @@ __device__ __forceinline__ void plan_barrier(int32_t* bar, int32_t target, int32
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
+// SRNN_F_ORD_SYNC (one thread): count `mine` up by one (its own counter, touched by this stream only)
+// and wait until the other stream's counter `other` has reached it.  Bounded by the shader's real-time
+// clock (100 MHz): after ~2 s the wait sets ERR_SYNC and gives up -- a wrong generation, reported,
+// instead of a launch that never ends (e.g. two streams that landed on one hardware queue).
+__device__ __forceinline__ void sync_wait(int32_t* sync, int mine, int other, int32_t* errw) {
+  const int32_t t = __hip_atomic_load(sync + mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1;
+  __hip_atomic_store(sync + mine, t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+  while ((int32_t)(__hip_atomic_load(sync + other, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - t) < 0) {
+    if (__builtin_amdgcn_s_memrealtime() - t0 > 200000000ull) {
+      atomicOr(errw, ERR_SYNC);
+      break;
+    }
+    __builtin_amdgcn_s_sleep(2);
+  }
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+}
+}  // namespace ord
+
+// SRNN_F_ORD_SYNC, side stream: before a plan overwrites its set, the run of the generation before it
+// has started -- so that generation's predecessor, the last user of the set, has closed
+template <int D = 0>  // (a template: one weak definition across the translation units)
+__global__ void k_ord_gate(SrnnArgs a) {
+  if (threadIdx.x == 0) ord::sync_wait(a.o_sync, ord::SYNC_GATE, ord::SYNC_RUN, a.o_ctl + ord::ERRW);
+}
+// ... and after its last phase, the plan counts itself done (its launches' stores released first)
+template <int D = 0>
+__global__ void k_ord_signal(SrnnArgs a) {
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    __hip_atomic_fetch_add(a.o_sync + ord::SYNC_PLAN, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
+namespace ord {
 // SRNN_F_ORD_INPLAN: plan workgroup w of G builds the NEXT generation's plan (the *_next buffers and
 // lists) while this generation's turns run -- link, plan, mark, count, permutations, the phases
 // separated by plan_barrier -- instead of launches on a second stream, whose cross-queue
@@ -706,6 +744,7 @@ __device__ __forceinline__ int64_t ord_crit_at(const SrnnArgs& a, int64_t g, int
 // in srnn_bignet.h; the schedule itself is shape independent)
 template <class Net, class S>
 struct OrdLanePol {
+  static constexpr bool SHADOW = true;  // a turn is one lane's: idle lanes may repeat it (k_ord_run)
   static constexpr int SAMP = samp_slots<Net>();
   static constexpr int PERM = (Net::P + 4) & ~3;
   static constexpr int RB = ord::Ord<Net, S>::RB;  // the plan's recompute depth
@@ -724,19 +763,25 @@ __global__ __launch_bounds__(TB) void k_ord_run(SrnnCfg c, SrnnArgs a) {
   __shared__ typename Pol::Shared s_sh;
   __shared__ int32_t s_q[TB];
   const int lane = threadIdx.x;
+  // (SRNN_F_ORD_SYNC: this run has started, so the close before it is done -- the side stream's plan
+  // of the next generation may overwrite that close's plan set)
+  if ((a.flags & SRNN_F_ORD_SYNC) && blockIdx.x == 0 && lane == 0)
+    __hip_atomic_fetch_add(a.o_sync + ord::SYNC_RUN, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   const int32_t gen = a.gen_ptr ? a.gen_ptr[0] : a.gen;
   int64_t cur = -1, prow = -1;
   bool raised = false;
   // with the critical list: its waves first (the grid's first a.x_groups workgroups), at raised
   // priority, permutations from the table; then every other turn without producers in index order;
   // with SRNN_F_ORD_INPLAN the last a.o_plan_groups workgroups build the next generation's plan
+  // (dispatched after the turn workgroups: measured faster than before them, profiles/r6a r6o)
   const int64_t ncw = (a.flags & SRNN_F_ORD_CRIT) ? a.x_groups : 0;
   const int64_t nturn = ncw + (a.n + TB - 1) / TB;
-  if ((a.flags & SRNN_F_ORD_INPLAN) && (int64_t)blockIdx.x >= nturn) {
-    ord::plan_group<Pol::RB, typename Pol::PT>(a, (int64_t)blockIdx.x - nturn, a.o_plan_groups);
+  const int64_t bid = blockIdx.x;
+  if ((a.flags & SRNN_F_ORD_INPLAN) && bid >= nturn) {
+    ord::plan_group<Pol::RB, typename Pol::PT>(a, bid - nturn, a.o_plan_groups);
     return;
   }
-  if ((int64_t)blockIdx.x < ncw) {
+  if (bid < ncw) {
     __shared__ int32_t s_c[64];
     int64_t slot = -1;
     cur = ord_crit_at(a, (int64_t)blockIdx.x * TB + lane, s_c, slot);
@@ -747,7 +792,7 @@ __global__ __launch_bounds__(TB) void k_ord_run(SrnnCfg c, SrnnArgs a) {
       raised = true;
     }
   } else {
-    const int64_t k = ((int64_t)blockIdx.x - ncw) * TB + lane;
+    const int64_t k = (bid - ncw) * TB + lane;
     if (k < a.n && a.o_list[k] < 0 && !(ncw && ord::cons_head(a)[k] != ord::EMPTY)) cur = k;
   }
   if (cur >= 0) ord::st_level(a.o_src + 4 * cur + 3, 0);
@@ -757,15 +802,40 @@ __global__ __launch_bounds__(TB) void k_ord_run(SrnnCfg c, SrnnArgs a) {
     bool priv = false;  // this lane's next turn is its private continuation (no acquire needed)
     int32_t lvl = 0;    // this lane's turn's level
     int32_t keep = ord::EMPTY;  // (ready-queue run) the first record this lane made ready
+    // shadow lanes (a.o_shadow, SRNN_KNOB_ORD_SHADOW): in a round of at most o_shadow turns, every
+    // idle lane repeats a busy lane's turn -- the same reads, the same arithmetic, the same values
+    // stored to the same addresses -- and publishes nothing.  A lone lane's SGD chain runs ~15-35 %
+    // slower per epoch than a full wave's (profiles/r6a r6o-r6p); the chain links of a generation
+    // are mostly lone kept continuations.
+    bool shadow = false;
+    if constexpr (Pol::SHADOW) {
+      const unsigned long long busy = __ballot(cur >= 0);
+      const int nbusy = (int)__popcll(busy);
+      if (nbusy > 0 && nbusy < TB && nbusy <= a.o_shadow) {  // (wave uniform)
+        unsigned long long m = busy;
+        for (int i = lane % nbusy; i > 0; --i) m &= m - 1;
+        const int src = cur >= 0 ? lane : (int)__ffsll((long long)m) - 1;
+        const int64_t c2 = __shfl(cur, src), p2 = __shfl(prow, src);
+        if (cur < 0) {
+          cur = c2;
+          prow = p2;
+          shadow = true;
+        }
+        // (a shadow reads rows its owner lane may have written in an earlier round of this wave)
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+      }
+    }
     if (cur >= 0) {
       const uint64_t t0 = a.o_trace ? __builtin_amdgcn_s_memrealtime() : 0;
       Pol::turn(c, a, cur, gen, s_sh, prow);
-      if (queue) ord::publish<true, true>(a, cur, ready, nready, priv);
-      else ord::publish(a, cur, ready, nready);
-      lvl = curlvl;
-      if (a.o_trace) {
-        a.o_trace[ord::TRACE_SLOTS * cur] = t0;
-        a.o_trace[ord::TRACE_SLOTS * cur + ord::TRACE_END] = __builtin_amdgcn_s_memrealtime();
+      if (!shadow) {
+        if (queue) ord::publish<true, true>(a, cur, ready, nready, priv);
+        else ord::publish(a, cur, ready, nready);
+        lvl = curlvl;
+        if (a.o_trace) {
+          a.o_trace[ord::TRACE_SLOTS * cur] = t0;
+          a.o_trace[ord::TRACE_SLOTS * cur + ord::TRACE_END] = __builtin_amdgcn_s_memrealtime();
+        }
       }
     }
     if (a.flags & SRNN_F_ORD_QUEUE) {
@@ -935,6 +1005,9 @@ __global__ __launch_bounds__(TB) void k_ord_close(SrnnCfg c, SrnnArgs a) {
     mine[3] = (unsigned long long)cnt[4];
     if ((a.flags & SRNN_F_BORN_TOTAL) && m) atomicAdd(bs + ((a.n + TB - 1) / TB) * 4, (unsigned long long)__popcll(m));
   }
+  // SRNN_F_ORD_SYNC: the launch ends (and the next run starts) once the next generation's plan is done
+  if ((a.flags & SRNN_F_ORD_SYNC) && gb == 0 && lane == 0)
+    ord::sync_wait(a.o_sync, ord::SYNC_CLOSE, ord::SYNC_PLAN, a.o_ctl + ord::ERRW);
 }
 
 // the census of the final rows after a close with SRNN_F_ORD_CENSUS_LATER: the class counts of each
@@ -1009,6 +1082,15 @@ inline bool ord_inplan_ok(const SrnnArgs& a) {
   }
   return true;
 }
+// SRNN_F_ORD_SYNC on a generation: device, planned ahead (by a synchronised plan), the counters
+inline bool ord_sync_ok(const SrnnArgs& a) {
+  if (!(a.flags & SRNN_F_ORD_SYNC)) return true;
+  if (!a.dev || !a.o_sync || !(a.flags & SRNN_F_ORD_PLANNED) || (a.flags & SRNN_F_ORD_INPLAN)) {
+    set_error("SRNN_F_ORD_SYNC: a device generation planned ahead on the side stream, with the o_sync counters");
+    return false;
+  }
+  return true;
+}
 // the next generation's plan arguments of an in-run planning generation (host path)
 inline SrnnArgs ord_next_plan_args(const SrnnArgs& a) {
   SrnnArgs pa = a;
@@ -1024,7 +1106,10 @@ inline SrnnArgs ord_next_plan_args(const SrnnArgs& a) {
 
 inline SrnnArgs ord_run_args(const SrnnArgs& a, int64_t nb) {
   SrnnArgs ra = a;
-  if (knob(SRNN_KNOB_ORD_QUEUE, 1) != 0) ra.flags |= SRNN_F_ORD_QUEUE;
+  // (defaults measured, profiles/r6a r6q: per-wave lists 0.173 ms vs the ready queue 0.296; shadow
+  // lanes in every round below a full wave 0.165)
+  if (knob(SRNN_KNOB_ORD_QUEUE, 0) != 0) ra.flags |= SRNN_F_ORD_QUEUE;
+  ra.o_shadow = std::max(0, knob(SRNN_KNOB_ORD_SHADOW, 63));
   if (knob(SRNN_KNOB_ORD_CRIT, 1) != 0) {
     ra.flags |= SRNN_F_ORD_CRIT;
     ra.x_groups = (int32_t)std::min<int64_t>(nb, (ord::rec_total(a.n) + TB - 1) / TB);
@@ -1039,6 +1124,8 @@ void ord_plan_dev(const SrnnCfg& c, const SrnnArgs& a, bool link) {
   const int64_t nb = (a.n + TB - 1) / TB;
   if (nb <= 0) return;
   hipStream_t st = (hipStream_t)a.stream;
+  const bool sync = link && (a.flags & SRNN_F_ORD_SYNC);
+  if (sync) hipLaunchKernelGGL(k_ord_gate<0>, dim3(1), dim3(64), 0, st, a);
   if (link) hipLaunchKernelGGL((k_ord_link<RB>), dim3((unsigned)nb), dim3(TB), 0, st, a);
   hipLaunchKernelGGL((k_ord_plan<RB>), dim3((unsigned)nb), dim3(TB), 0, st, c, a);
   hipLaunchKernelGGL((k_ord_mark<RB>), dim3((unsigned)nb), dim3(TB), 0, st, c, a);
@@ -1052,6 +1139,7 @@ void ord_plan_dev(const SrnnCfg& c, const SrnnArgs& a, bool link) {
                          0, st, ra, E);
     }
   }
+  if (sync) hipLaunchKernelGGL(k_ord_signal<0>, dim3(1), dim3(64), 0, st, a);
 }
 
 // host: [link ->] plan -> mark -> every turn's level (producers precede their consumers in index
@@ -1105,6 +1193,10 @@ int soup_ord_plan(const SrnnCfg& c, const SrnnArgs& a) {
     set_error("ordered generation plan needs o_src, o_list, o_ctl and the planned generation's (NIL) attack lists");
     return -5;
   }
+  if ((a.flags & SRNN_F_ORD_SYNC) && (!a.dev || !a.o_sync || !(a.flags & SRNN_F_ORD_NEXT))) {
+    set_error("SRNN_F_ORD_SYNC: a device plan of the next generation with the o_sync counters");
+    return -5;
+  }
   if (!a.dev) {
     ord_plan_host<RB>(a, true);
     return 0;
@@ -1141,7 +1233,7 @@ int soup_ordered(const SrnnCfg& c, const SrnnArgs& a) {
               "planned ahead), respawn and 1 <= o_levels <= 16");
     return -5;
   }
-  if (!ord_inplan_ok(a)) return -5;
+  if (!ord_inplan_ok(a) || !ord_sync_ok(a)) return -5;
   if (!a.dev) {
     const int32_t gen = I::gen_of(a);
     if (!planned) ord_plan_host<O::RB>(a, false);

@@ -10,14 +10,17 @@ export TMPDIR=/tmp
 TAG=${1:-round}
 step() { local name=$1 lim=$2; shift 2; timeout -k 10 $lim "$@" > gpurun_out/${name}_$TAG.log 2>&1; local rc=$?;
          echo "[$name rc=$rc] $(tail -1 gpurun_out/${name}_$TAG.log | cut -c1-200)"; return $rc; }
-SRNN_LIB=$PWD/ab/libsrnn_fine.so step hw 200 python bench/ordered_trace.py --slots 36 --gens 3 || exit 1
-SRNN_LIB=$PWD/ab/libsrnn_fine.so step hw3k 200 python bench/ordered_trace.py --slots 36 --particles 3000 --gens 4 || exit 1
-# same-box A/B of the census on the side stream (1, default) against the census in the close (0)
+timeout -k 10 600 python -u -m pytest tests/test_ordered_soup.py tests/test_ordered_bignet_gpu.py -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/pytest_$TAG.log 2>&1
+rc=$?; tail -1 gpurun_out/pytest_$TAG.log; [ $rc -eq 0 ] || exit $rc
+# same-box A/B: ready queue (now really the default) / per-wave lists; shadow lanes off / 8 / 63
 for i in 1 2; do
-  for cs in 1 0; do
-    SRNN_ORD_CENSUS_SIDE=$cs step cs${cs}_$i 300 python bench.py --steps 50 --warmup 5 --side-steps 0 || exit 1
-  done
+  step q1_$i 300 python bench.py --steps 50 --warmup 5 --side-steps 0 || exit 1
+  SRNN_ORD_QUEUE=0 step q0_$i 300 python bench.py --steps 50 --warmup 5 --side-steps 0 || exit 1
+  SRNN_ORD_SHADOW=8 step s8_$i 300 python bench.py --steps 50 --warmup 5 --side-steps 0 || exit 1
+  SRNN_ORD_SHADOW=63 step s63_$i 300 python bench.py --steps 50 --warmup 5 --side-steps 0 || exit 1
+  SRNN_ORD_QUEUE=0 SRNN_ORD_SHADOW=63 step q0s63_$i 300 python bench.py --steps 50 --warmup 5 --side-steps 0 || exit 1
 done
-SRNN_ORD_CENSUS_SIDE=0 step prof0 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof0_$TAG -o t --output-format csv -- python3 bench.py --steps 20 --warmup 5 --side-steps 0 || exit 1
-for f in cs1_1 cs0_1 cs1_2 cs0_2; do python3 -c "import json,sys; d=json.loads(open(sys.argv[1]).read().splitlines()[-1]); print(sys.argv[2], '%.4f' % d['ms_per_step'], d['config']['ord_pipeline'])" gpurun_out/${f}_$TAG.log $f; done
+step tr 200 python bench/ordered_trace.py --gens 2 || exit 1
+SRNN_ORD_SHADOW=63 step trs 200 python bench/ordered_trace.py --gens 2 || exit 1
+for f in q1_1 q0_1 s8_1 s63_1 q0s63_1 q1_2 q0_2 s8_2 s63_2 q0s63_2; do python3 -c "import json,sys; d=json.loads(open(sys.argv[1]).read().splitlines()[-1]); print(sys.argv[2], '%.4f' % d['ms_per_step'], d['config']['execution']['library']['ord_queue'], d['config']['execution']['library']['ord_shadow'], d['config']['final_census'])" gpurun_out/${f}_$TAG.log $f; done
 echo done

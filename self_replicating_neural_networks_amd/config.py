@@ -108,7 +108,11 @@ class ExecConfig:
     ord_crit: Optional[bool] = None         # SRNN_ORD_CRIT: reference-order generations run the producers of
                                             # later turns first, at raised wave priority (None: on)
     ord_queue: Optional[bool] = None        # SRNN_ORD_QUEUE: reference-order continuations through one ready
-                                            # queue per generation (None: on; off: per-wave lists)
+                                            # queue per generation, or per-wave lists (None: lists, measured
+                                            # faster -- 0.173 vs 0.296 ms, profiles/r6a r6q)
+    ord_shadow: Optional[int] = None        # SRNN_ORD_SHADOW: a reference-order round of at most this many
+                                            # turns in a wave runs each on several lanes (None: 63, every round
+                                            # below a full wave; 0: off)
     ordsh_emulate: int = 0                  # SRNN_ORDSH_EMULATE: one-rank timing model of R ranks of a sharded
                                             # reference-order generation (the rank runs 1/R of the turns;
                                             # the other turns never run: timing only, results invalid)
@@ -126,6 +130,11 @@ class ExecConfig:
     ord_census_side: bool = True            # SRNN_ORD_CENSUS_SIDE: with the side-stream plan, each generation's
                                             # census runs on the side stream beside the next run, the close keeps
                                             # only the final rows, ballots and counter
+    ord_graph_sync: bool = True             # SRNN_ORD_GRAPH_SYNC: with the side-stream plan, a multi-generation
+                                            # hipGraph is TWO graphs replayed on two streams (the generations on
+                                            # the current one, their plans on a high-priority side stream),
+                                            # ordered by device counters instead of a cross-queue join per
+                                            # generation (SRNN_F_ORD_SYNC; validated bitwise, else not used)
 
     _ENV = dict(finish_mode="SRNN_FINISH_MODE", finish_par="SRNN_FINISH_PAR", graph_chunks="SRNN_GRAPH_CHUNKS",
                 x2_schedule="SRNN_X2_SCHEDULE", x2_prio="SRNN_X2_PRIO", x2_emulate_remote="SRNN_X2_EMULATE_REMOTE",
@@ -133,15 +142,16 @@ class ExecConfig:
                 force_generic="SRNN_FORCE_GENERIC", ww_wave="SRNN_WW_WAVE", rnn_wave="SRNN_RNN_WAVE",
                 rnn_spec="SRNN_RNN_SPEC", rnn_soup="SRNN_RNN_SOUP", big_wave="SRNN_BIG_WAVE",
                 fix_group="SRNN_FIX_GROUP", soup_lanes="SRNN_SOUP_LANES", ord_crit="SRNN_ORD_CRIT", ord_queue="SRNN_ORD_QUEUE",
+                ord_shadow="SRNN_ORD_SHADOW",
                 ordsh_emulate="SRNN_ORDSH_EMULATE",
                 order_levels="SRNN_ORDER_LEVELS",
                 perm_table="SRNN_PERM_TABLE", ord_pipeline="SRNN_ORD_PIPELINE",
-                ord_census_side="SRNN_ORD_CENSUS_SIDE")
+                ord_census_side="SRNN_ORD_CENSUS_SIDE", ord_graph_sync="SRNN_ORD_GRAPH_SYNC")
     # Optional[bool] knobs whose None means "the built-in choice" (by population size, ...)
     TRI_STATE = ("force_generic", "rnn_wave", "rnn_spec", "rnn_soup", "big_wave", "fix_group", "perm_table",
                  "ord_crit", "ord_queue")
     LIBRARY_KNOBS = ("force_generic", "ww_wave", "rnn_wave", "rnn_spec", "rnn_soup", "big_wave", "fix_group",
-                     "soup_lanes", "ord_crit", "ord_queue")
+                     "soup_lanes", "ord_crit", "ord_queue", "ord_shadow")
 
     def validate(self):
         if self.finish_mode not in ("batch", "serial"):
@@ -181,7 +191,7 @@ class ExecConfig:
                 kw[f.name] = {"1": "stream", "true": "stream", "on": "stream", "0": "off", "false": "off"}.get(v.lower(), v)
             elif f.name == "x2_emulate_remote":
                 kw[f.name] = float(v)
-            elif f.name in ("soup_lanes", "order_levels", "ww_wave", "ordsh_emulate"):
+            elif f.name in ("soup_lanes", "order_levels", "ww_wave", "ordsh_emulate", "ord_shadow"):
                 kw[f.name] = int(v)
             elif f.name in self.TRI_STATE:
                 kw[f.name] = _tri_state(v)

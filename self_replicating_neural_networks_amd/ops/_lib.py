@@ -20,7 +20,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 # SRNN_LIB: load another build of the library (A/B of compiler flags on the GPU box)
 LIB_PATH = os.environ.get("SRNN_LIB") or os.path.join(_HERE, "libsrnn.so")
 CSRC = os.path.normpath(os.path.join(_HERE, "..", "..", "csrc"))
-ABI_VERSION = 28
+ABI_VERSION = 29
 
 # SrnnOp (csrc/srnn_abi.h)
 OP_INIT = 0
@@ -92,6 +92,7 @@ FLAG_X2_POST_FUSED = 1 << 21
 FLAG_PTAB_READY = 1 << 23  # ptab already holds the generation's permutations (the sharded pack built them)
 FLAG_ORD_PLANNED = 1 << 25  # OP_SOUP_ORDERED: the plan is already built (OP_ORD_PLAN one generation ahead)
 FLAG_ORD_NEXT = 1 << 26  # OP_ORD_PLAN: plan generation gen + 1 (the one after the generation in flight)
+FLAG_ORD_SYNC = 1 << 27  # OP_ORD_PLAN / OP_SOUP_ORDERED: ordered by the o_sync counters (two graphs, two streams)
 FLAG_ORD_INPLAN = 1 << 28  # OP_SOUP_ORDERED: the run launch builds the next generation's plan (*_next buffers)
 FLAG_ORD_CENSUS_LATER = 1 << 29  # OP_SOUP_ORDERED: the census is OP_ORD_CENSUS's, beside the next generation
 
@@ -147,7 +148,7 @@ class SrnnArgs(ctypes.Structure):
         ("o_lo", _I64), ("o_hi", _I64),
         # SRNN_F_ORD_INPLAN: the next generation's plan set, built by the run launch's last workgroups
         ("o_src_next", _P), ("o_list_next", _P), ("o_ctl_next", _P), ("ptab_next", _P),
-        ("o_plan_groups", _I32), ("pad4", _I32),
+        ("o_plan_groups", _I32), ("pad4", _I32), ("o_sync", _P), ("o_shadow", _I32), ("pad5", _I32),
     ]
 
 
@@ -260,11 +261,11 @@ def supports(spec, op: int, device: bool, dtype: int = DTYPE_FP32) -> bool:
 # execution knobs (csrc/srnn_abi.h SrnnKnob; config.py ExecConfig): the environment variable
 # of a knob, when set, overrides what is set here
 KNOBS = {"force_generic": 0, "rnn_wave": 1, "rnn_spec": 2, "rnn_soup": 3, "ww_wave": 4, "big_wave": 5,
-         "fix_group": 6, "soup_lanes": 7, "ord_crit": 8, "ord_queue": 9}
+         "fix_group": 6, "soup_lanes": 7, "ord_crit": 8, "ord_queue": 9, "ord_shadow": 10}
 KNOB_ENV = {"force_generic": "SRNN_FORCE_GENERIC", "rnn_wave": "SRNN_RNN_WAVE", "rnn_spec": "SRNN_RNN_SPEC",
             "rnn_soup": "SRNN_RNN_SOUP", "ww_wave": "SRNN_WW_WAVE", "big_wave": "SRNN_BIG_WAVE",
             "fix_group": "SRNN_FIX_GROUP", "soup_lanes": "SRNN_SOUP_LANES", "ord_crit": "SRNN_ORD_CRIT",
-            "ord_queue": "SRNN_ORD_QUEUE"}
+            "ord_queue": "SRNN_ORD_QUEUE", "ord_shadow": "SRNN_ORD_SHADOW"}
 
 
 def set_knob(name: str, value: int) -> None:

@@ -72,7 +72,9 @@ ORD_ERRORS = {2: "an attack output past the recompute depth left unstored (marki
               4: "a turn that never ran (scheduling bug)",
               8: "a ready-queue entry never written (scheduling bug)",
               16: "a level's exchange records overflowed the send buffer (sharded; sizing bug)",
-              32: "a one-rank timing model of a sharded generation (SRNN_ORDSH_EMULATE) ran only 1/R of the turns"}
+              32: "a one-rank timing model of a sharded generation (SRNN_ORDSH_EMULATE) ran only 1/R of the turns",
+              64: "an in-run plan workgroup gave up at a phase barrier (scheduling bug)",
+              128: "a counter-ordered graph waited > 2 s for the other stream (SRNN_F_ORD_SYNC)"}
 ORD_ERR_EMULATED = 32
 
 
@@ -368,6 +370,9 @@ class SoupEngine:
         self._ord_mode = "off"      # ... by the run launch ("kernel") or the side stream ("stream")
         self._ord_census_side = False  # ... with the census of each generation beside the next one
         self._census_due = None
+        self._ord_decouple = False  # ... multi-generation graphs as two counter-ordered graphs (SRNN_F_ORD_SYNC)
+        self._osync = None
+        self._sync = False
         if order == "sequential":
             self._init_ordered()
         # initial particles: uids 0..n_total-1, keyed init (identical for any rank count)
@@ -510,7 +515,12 @@ class SoupEngine:
             self._olist1 = torch.zeros_like(self._olist)
             self._octl1 = torch.zeros_like(self._octl)
             if mode == "stream" and dev.type == "cuda":
-                self._ord_side = torch.cuda.Stream(dev)
+                # (ord_graph_sync: the side stream's multi-generation graphs wait on the main stream's
+                # counters and the other way round -- the two streams must not share a hardware queue;
+                # the high-priority one is drawn from a queue pool of its own)
+                self._ord_decouple = bool(self.execution.ord_graph_sync)
+                self._ord_side = torch.cuda.Stream(dev, priority=-1 if self._ord_decouple else 0)
+                self._osync = torch.zeros(4, dtype=torch.int32, device=dev)  # csrc ord::SYNC_*
         # (stream mode) the census of a generation's final rows runs on the side stream beside the
         # next generation's run (OP_ORD_CENSUS), leaving the close on the critical path only the
         # final rows, ballots and counter
@@ -785,7 +795,8 @@ class SoupEngine:
     def _cache_key(self, *extra):
         stream = torch.cuda.current_stream(self.device).cuda_stream if self.device.type == "cuda" else 0
         return (self._p, stream, tuple(sorted((k, str(v)) for k, v in self.params.items())), self.stats,
-                self.stats_with_sec, self.lr, self.shuffle, self._pending_fin if not self.x2 else 0) + extra
+                self.stats_with_sec, self.lr, self.shuffle, self._pending_fin if not self.x2 else 0,
+                self._sync) + extra
 
     # ------------------------------------------------------------------ single rank / all-gather
     def _gen_args(self):
@@ -839,7 +850,10 @@ class SoupEngine:
                 fa.ptab = _p(self._perm_table(q))
                 if self._ord_pipe:
                     fa.flags |= _lib.FLAG_ORD_PLANNED
-                if self._ord_census_side and (fa.flags & _lib.FLAG_FUSED_CENSUS):
+                if self._sync:  # (two counter-ordered graphs: the census stays in the close)
+                    fa.flags |= _lib.FLAG_ORD_SYNC
+                    fa.o_sync = _p(self._osync)
+                elif self._ord_census_side and (fa.flags & _lib.FLAG_FUSED_CENSUS):
                     fa.flags |= _lib.FLAG_ORD_CENSUS_LATER
                 if self._ord_mode == "kernel":  # the run launch also builds the next generation's plan
                     nsrc, nlist, nctl = self._ord_set(1 - q)
@@ -926,7 +940,9 @@ class SoupEngine:
         its own turn is already the newborn)."""
         spec, cfg = self.spec, self.cfg
         side = main = None
-        if self._ord_pipe:
+        if self._sync:  # (a two-graph chunk: the plans are the side graph's, _capture_side)
+            assert self._lists_ready and record is False
+        elif self._ord_pipe:
             if not self._lists_ready:  # the first generation's plan (later ones: planned ahead)
                 _lib.run(_lib.OP_ORD_PLAN, spec, self._plan_args(False), cfg)
             if self._ord_mode == "stream":
@@ -990,6 +1006,9 @@ class SoupEngine:
             a.o_levels = self.order_levels
             if nxt:
                 a.flags |= _lib.FLAG_ORD_NEXT
+                if self._sync:
+                    a.flags |= _lib.FLAG_ORD_SYNC
+                    a.o_sync = _p(self._osync)
             self._arg_cache[key] = a
         return a
 
@@ -1389,7 +1408,7 @@ class SoupEngine:
                     and self.trajectory is None and self.metrics is None):
                 # G generations in one graph launch (no inter-graph gaps)
                 self._join_side()
-                ch[0].replay()
+                self._replay_chunk(ch)
                 self.time += ch[2]
                 left -= ch[2]
                 self._pending = self.dist.enabled
@@ -1461,7 +1480,7 @@ class SoupEngine:
                  "counterpart", "loss", "respawn", "counts", "census", "err", "full", "stats_all", "_blockstat",
                  "_done", "_bs_ring", "x_dep", "x_rlist", "x_rcount", "x_rslot", "x_satt", "x_cno", "x_crq",
                  "x_srep", "x_nsrep", "x_part", "x_ctl", "x_bstat", "x_hpre", "x_hgrp", "sendbuf", "recvbuf",
-                 "_abuf", "_osrc", "_olist", "_octl", "_ptab", "_osrc1", "_olist1", "_octl1", "_ptab1",
+                 "_abuf", "_osrc", "_olist", "_octl", "_ptab", "_osrc1", "_olist1", "_octl1", "_ptab1", "_osync",
                  "_fw", "_sh_heads", "_sh_nexts", "_sh_cnt", "_sh_send", "_sh_recv"]
         out = []
         for k in names:
@@ -1602,7 +1621,16 @@ class SoupEngine:
     def _capture_chunk_g(self, s, p0, pend0, G):
         """A graph of G consecutive generations (G even: it starts and ends at parity
         p0) replayed as one launch, removing the per-generation graph-launch gap;
-        validated bitwise against G eager generations (all ranks agree or none use it)."""
+        validated bitwise against G eager generations (all ranks agree or none use it).
+        Reference order with the side-stream plan (ExecConfig.ord_graph_sync): first as TWO
+        graphs -- the G runs + closes, and on the side stream the G plans of the generations
+        after them -- ordered by device counters (SRNN_F_ORD_SYNC) instead of a cross-queue join
+        per generation (~10 us of idle queue each, profiles/r6a); the one-graph form if that
+        capture or its validation fails."""
+        if self._ord_decouple and self._lists_ready:
+            ch = self._capture_chunk_sync(s, p0, pend0, G)
+            if ch is not None:
+                return ch
         ok = True
         gc = torch.cuda.CUDAGraph()
         flags0 = self._flags_state()
@@ -1620,14 +1648,57 @@ class SoupEngine:
         ok = self._agree(ok)
         if ok:
             ok = self._agree(self._validate_replay(lambda: gc.replay(), G, parity_after=p0))
-        return (gc, p0, G) if ok else None
+        return (gc, p0, G, None) if ok else None
+
+    def _capture_chunk_sync(self, s, p0, pend0, G):
+        """The two-graph form of a G-generation chunk (see _capture_chunk_g): main graph = G x
+        (run + close, the close waiting for the next plan) + the batched finish; side graph = G x
+        (gate on the run counter, plan of the next generation, done count)."""
+        gc, gs = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
+        flags0 = self._flags_state()
+        ok = True
+        self._sync = True
+        try:
+            with torch.cuda.graph(gc, stream=s, capture_error_mode="thread_local"):
+                for _ in range(G):
+                    self._generation()
+                self._join_side()
+            self._p = p0
+            with torch.cuda.graph(gs, stream=self._ord_side, capture_error_mode="thread_local"):
+                for g in range(G):
+                    self._p = p0 ^ (g & 1)
+                    _lib.run(_lib.OP_ORD_PLAN, self.spec, self._plan_args(True), self.cfg)
+        except Exception as e:  # noqa: BLE001
+            import sys
+            print(f"two-graph capture failed ({type(e).__name__}: {e}); one graph", file=sys.stderr)
+            ok = False
+        finally:
+            self._sync = False
+        self._p, self._pending = p0, pend0
+        self._set_flags_state(flags0)
+        ch = (gc, p0, G, gs)
+        ok = self._agree(ok)
+        if ok:
+            ok = self._agree(self._validate_replay(lambda: self._replay_chunk(ch), G, parity_after=p0))
+        return ch if ok else None
+
+    def _replay_chunk(self, ch):
+        """Replay a multi-generation chunk; a two-graph chunk's side graph first, on the side stream
+        (after the work already queued on this one: its first plan overwrites the set of the
+        generation before the chunk), the two then run on their own, ordered by the counters."""
+        if ch[3] is not None:
+            main = torch.cuda.current_stream(self.device)
+            self._ord_side.wait_stream(main)
+            with torch.cuda.stream(self._ord_side):
+                ch[3].replay()
+        ch[0].replay()
 
     def release_graphs(self):
         """Drop the captured graphs (before tearing down the process group: an RCCL
         communicator must not be destroyed while graph executables still reference it)."""
         if self._graphs is not None or self._chunks:
             torch.cuda.synchronize(self.device)
-            for g in (self._graphs or []) + [c[0] for c in self._chunks]:
+            for g in (self._graphs or []) + [c[0] for c in self._chunks] + [c[3] for c in self._chunks if c[3]]:
                 g.reset()
             self._graphs = None
             self._chunk = None
@@ -1669,6 +1740,11 @@ class SoupEngine:
             if isinstance(getattr(self, k, None), torch.Tensor)}
         same = all(torch.equal(x.view(torch.uint8), y.view(torch.uint8))
                    for x, y in zip(state, eager) if id(x) in keep)
+        # (reference order: and no error bit the eager generations did not raise either)
+        for ctl in (self._octl, self._octl1) if self.order == "sequential" else ():
+            if ctl is not None:
+                i = next(k for k, x in enumerate(state) if x is ctl)
+                same = same and int(ctl[_lib.ORD_ERRW]) == int(eager[i][_lib.ORD_ERRW])
         for t, v in zip(state, saved):
             t.copy_(v)
         self._p, self._pending, self.time = p0, pend0, t0

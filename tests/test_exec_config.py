@@ -2,6 +2,7 @@
 variables as overrides, the library knobs in force, and the engines reading the config
 instead of the environment.  Plus the planner's byte model against a constructed engine
 (engine_bytes vs the tensors a SoupEngine really holds)."""
+import os
 import json
 
 import pytest
@@ -156,3 +157,17 @@ def test_every_library_knob_is_an_exec_config_field(monkeypatch):
         assert _lib.get_knob("ord_queue") == 0
     finally:
         _lib.set_knob("ord_queue", -1)
+
+
+def test_every_library_knob_starts_at_its_default():
+    """a fresh library reports -1 (the built-in default) for every knob without its environment
+    variable (a short initialiser once left the last knob at 0: the ready queue silently off)"""
+    import subprocess
+    import sys
+    env = {k: v for k, v in os.environ.items() if k not in _lib.KNOB_ENV.values()}
+    code = ("from self_replicating_neural_networks_amd.ops import _lib; "
+            "print(sorted(set(_lib.get_knob(k) for k in _lib.KNOBS)))")
+    out = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=120,
+                         cwd=os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    assert out.returncode == 0, out.stderr[-2000:]
+    assert out.stdout.strip().splitlines()[-1] == "[-1]"

@@ -127,29 +127,63 @@ def test_ordered_soup_records_reference_states():
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("spec", SPECS, ids=IDS)
-@pytest.mark.parametrize("pipe", ["kernel", "stream", "off"])
+@pytest.mark.parametrize("pipe", ["kernel", "stream", "stream-1g", "off"])
 def test_device_ordered_generation_is_the_serial_loop(spec, pipe):
     """device OP_SOUP_ORDERED (plan -> run by continuation -> close; the plan of the next
-    generation built while this one runs -- by the run launch's last workgroups ("kernel") or on a
-    side stream ("stream") -- or inline ("off")) == the serial loop on the same device (k_soup_seq,
-    one lane) bitwise, eager and captured in hipGraphs"""
+    generation built while this one runs -- by the last workgroups of the run launch ("kernel") or on a
+    side stream ("stream": multi-generation graphs as two graphs on two streams ordered by device
+    counters; "stream-1g": one graph, a fork / join per generation) -- or inline ("off")) == the
+    serial loop on the same device (k_soup_seq, one lane) bitwise, eager and captured in hipGraphs"""
     n, seed = 3000, 7
+    mode = pipe.split("-")[0]
     for graphs in (False, True):
         o = SoupEngine(spec, n, HOT, device="cuda", seed=seed, order="sequential",
-                       execution=ExecConfig(ord_pipeline=pipe))
-        assert o._ord_mode == pipe
+                       execution=ExecConfig(ord_pipeline=mode, ord_graph_sync=pipe == "stream"))
+        assert o._ord_mode == mode
         # the same starting rows (the device init contracts a*b+c, the host's does not)
         s = SequentialSoupEngine(spec, n, HOT, seed=seed, device="cuda", weights=o.local_rows()[:, :spec.P].cpu())
         if graphs:
             assert o.capture(warmup=1)
             s.evolve(1)  # capture runs one warmup generation eagerly
+            # (every chunk validated bitwise against eager generations; the two-graph form kept)
+            assert any(c[3] is not None for c in o._chunks) == (pipe == "stream")
         _same(o, s, spec.P)
-        for _ in range(3):
-            o.evolve(2)
-            s.evolve(2)
+        for k in (2, 4, 1, 2):  # chunks of 2 and 4, a single-generation graph between them
+            o.evolve(k)
+            s.evolve(k)
+            _same(o, s, spec.P)
+        assert o.ordered_levels()["error"] == 0
+        if o._osync is not None and graphs and pipe == "stream":
+            c = o._osync.cpu().tolist()  # runs / gates and plans / closes in step
+            assert c[0] == c[1] and c[2] == c[3] and c[0] > 0
+        o.release_graphs()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("spec", SPECS, ids=IDS)
+@pytest.mark.parametrize("queue,shadow", [(True, 0), (False, 0), (True, 8), (True, 63), (False, 63)])
+def test_device_ordered_queue_and_shadow_lanes(spec, queue, shadow):
+    """the continuation schedules -- one ready queue per generation or per-wave lists, with or
+    without shadow lanes (idle lanes of a small round repeating a busy lane's turn, publishing
+    nothing) -- are all the serial loop bitwise, in two-graph chunks"""
+    n, seed = 3000, 5
+    ex = ExecConfig(ord_queue=queue, ord_shadow=shadow)
+    try:
+        ex.apply_library()
+        o = SoupEngine(spec, n, HOT, device="cuda", seed=seed, order="sequential", execution=ex)
+        s = SequentialSoupEngine(spec, n, HOT, seed=seed, device="cuda", weights=o.local_rows()[:, :spec.P].cpu())
+        assert _lib.get_knob("ord_queue") == int(queue) and _lib.get_knob("ord_shadow") == shadow
+        assert o.capture(warmup=1)
+        s.evolve(1)
+        for k in (2, 4, 1):
+            o.evolve(k)
+            s.evolve(k)
             _same(o, s, spec.P)
         assert o.ordered_levels()["error"] == 0
         o.release_graphs()
+    finally:
+        _lib.set_knob("ord_queue", -1)
+        _lib.set_knob("ord_shadow", -1)
 
 
 @pytest.mark.gpu
