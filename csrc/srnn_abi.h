@@ -212,6 +212,10 @@ struct SrnnArgs {
   // ---- (internal, set by the library from SRNN_KNOB_ORD_SHADOW) shadow lanes of a reference-order run
   int32_t o_shadow;
   int32_t pad5;
+  // ---- OP_SOUP_ORDERED (device, lane nets): the block stats of the PREVIOUS generation, whose close
+  // ran with SRNN_F_ORD_CENSUS_LATER: extra workgroups of this generation's run launch classify its
+  // final rows (this generation's W2) into them.  null: none
+  uint64_t* o_census_temp;
 };
 
 #define SRNN_X2_HDR 12  // int64 header words of an X2 exchange block (see srnn_shard.hip)
@@ -254,7 +258,7 @@ enum SrnnOp {
                         // independent: issued on a side stream while the previous generation runs
 };
 
-int srnn_abi_version();  // 29
+int srnn_abi_version();  // 30
 int64_t srnn_args_size();  // sizeof(SrnnArgs): the ctypes mirror checks its layout against it
 int64_t srnn_cfg_size();
 int srnn_has_config(const SrnnCfg* cfg);
@@ -282,7 +286,7 @@ enum SrnnKnob {
                                 //   (1) or run by the producers' waves (0, default: measured faster)
   SRNN_KNOB_ORD_SHADOW = 10,    // SRNN_ORD_SHADOW: a reference-order round with at most this many turns in a
                                 //   wave runs each on several lanes (the idle lanes repeat a busy lane's
-                                //   turn; 0: off; default 63: every round below a full wave)
+                                //   turn; 0: off; default 32)
   SRNN_KNOB_COUNT = 11
 };
 void srnn_set_knob(int knob, int value);

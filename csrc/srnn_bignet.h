@@ -1969,6 +1969,7 @@ struct BigOrd : ord::OrdSched<1> {
 template <class T, class S, bool SHUF>
 struct BigOrdPol {
   static constexpr bool SHADOW = false;  // (the turn's staged reads are wave-cooperative)
+  static constexpr bool CENSUS = false;  // (its census stays in the close)
   static constexpr int RB = 1;  // the plan's recompute depth (big nets)
   using PT = void;              // no permutation table (an aggregating net's SGD step has one sample)
   struct Shared {
@@ -2047,6 +2048,10 @@ int big_soup_ordered(const SrnnCfg& c, const SrnnArgs& a) {
     return -5;
   }
   if (!ord_inplan_ok(a) || !ord_sync_ok(a)) return -5;
+  if (a.o_census_temp) {
+    set_error("big ordered generation: no census in the run launch (o_census_temp)");
+    return -5;
+  }
   const int64_t nb = (a.n + TB - 1) / TB;
   if (nb <= 0) return 0;
   hipStream_t st = (hipStream_t)a.stream;

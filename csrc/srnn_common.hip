@@ -206,7 +206,7 @@ static int with_scratch(int op, const SrnnCfg* c, const SrnnArgs* a) {
 
 extern "C" {
 
-int srnn_abi_version() { return 29; }
+int srnn_abi_version() { return 30; }
 
 
 // layout check of the ctypes mirror (ops/_lib.py): sizeof(SrnnArgs) / sizeof(SrnnCfg)

@@ -742,9 +742,36 @@ __device__ __forceinline__ int64_t ord_crit_at(const SrnnArgs& a, int64_t g, int
 // producer's.  The wave ends when no lane has a ready record left.
 // (Pol: the turn of a net family and its LDS -- OrdLanePol below, the big aggregating nets'
 // in srnn_bignet.h; the schedule itself is shape independent)
+// the class counts of the 64-row block gb of final rows W into its block stats (words 1..3; the
+// close wrote the respawn ballot, word 0): the census of a close with SRNN_F_ORD_CENSUS_LATER, by
+// k_ord_census or by extra workgroups of the next generation's run launch (o_census_temp)
+template <class Net, class S>
+__device__ void ord_census_block(const SrnnCfg& c, const SrnnArgs& a, const float* W, uint64_t* temp, int64_t gb,
+                                 uint8_t* perm) {
+  using I = Item<Net, S>;
+  const int lane = threadIdx.x & 63;
+  const int64_t r = gb * TB + lane;
+  int8_t k = -1;
+  if (r < a.n) {
+    float w[Net::P];
+    I::load(I::rowp(W, r), w);
+    k = I::classify_w(w, a.eps, (a.flags & SRNN_F_FIX_SEC) != 0, I::actx(a, c, (uint64_t)r, 0x7FFFFFF0u, perm));
+  }
+  uint32_t cnt[5];
+#pragma unroll
+  for (int q = 0; q < 5; ++q) cnt[q] = (uint32_t)__popcll(__ballot(k == q));
+  if (lane == 0) {
+    uint64_t* mine = temp + gb * 4;
+    mine[1] = (uint64_t)cnt[0] | ((uint64_t)cnt[1] << 32);
+    mine[2] = (uint64_t)cnt[2] | ((uint64_t)cnt[3] << 32);
+    mine[3] = (uint64_t)cnt[4];
+  }
+}
+
 template <class Net, class S>
 struct OrdLanePol {
-  static constexpr bool SHADOW = true;  // a turn is one lane's: idle lanes may repeat it (k_ord_run)
+  static constexpr bool SHADOW = true;
+  static constexpr bool CENSUS = true;  // extra run workgroups may take the previous close's census  // a turn is one lane's: idle lanes may repeat it (k_ord_run)
   static constexpr int SAMP = samp_slots<Net>();
   static constexpr int PERM = (Net::P + 4) & ~3;
   static constexpr int RB = ord::Ord<Net, S>::RB;  // the plan's recompute depth
@@ -756,6 +783,10 @@ struct OrdLanePol {
   __device__ static void turn(const SrnnCfg& c, const SrnnArgs& a, int64_t k, int32_t gen, Shared& sh, int64_t prow) {
     const int lane = threadIdx.x;
     ord::Ord<Net, S>::turn(c, a, k, gen, samp_lane<Net>(sh.samp, lane), sh.perm + lane * PERM, prow);
+  }
+  // the previous generation's census: its final rows are this generation's start rows W2
+  __device__ static void census(const SrnnCfg& c, const SrnnArgs& a, int64_t gb, Shared& sh) {
+    ord_census_block<Net, S>(c, a, a.W2, a.o_census_temp, gb, sh.perm + threadIdx.x * PERM);
   }
 };
 template <class Pol>
@@ -774,12 +805,20 @@ __global__ __launch_bounds__(TB) void k_ord_run(SrnnCfg c, SrnnArgs a) {
   // priority, permutations from the table; then every other turn without producers in index order;
   // with SRNN_F_ORD_INPLAN the last a.o_plan_groups workgroups build the next generation's plan
   // (dispatched after the turn workgroups: measured faster than before them, profiles/r6a r6o)
+  // (with o_census_temp, the ncen workgroups after the turn workgroups take the previous close's census)
   const int64_t ncw = (a.flags & SRNN_F_ORD_CRIT) ? a.x_groups : 0;
   const int64_t nturn = ncw + (a.n + TB - 1) / TB;
+  const int64_t ncen = a.o_census_temp ? (a.n + TB - 1) / TB : 0;
   const int64_t bid = blockIdx.x;
-  if ((a.flags & SRNN_F_ORD_INPLAN) && bid >= nturn) {
-    ord::plan_group<Pol::RB, typename Pol::PT>(a, bid - nturn, a.o_plan_groups);
+  if ((a.flags & SRNN_F_ORD_INPLAN) && bid >= nturn + ncen) {
+    ord::plan_group<Pol::RB, typename Pol::PT>(a, bid - nturn - ncen, a.o_plan_groups);
     return;
+  }
+  if constexpr (Pol::CENSUS) {
+    if (bid >= nturn && bid < nturn + ncen) {
+      Pol::census(c, a, bid - nturn, s_sh);
+      return;
+    }
   }
   if (bid < ncw) {
     __shared__ int32_t s_c[64];
@@ -1014,28 +1053,9 @@ __global__ __launch_bounds__(TB) void k_ord_close(SrnnCfg c, SrnnArgs a) {
 // 64-row block into its block stats (words 1..3; the close wrote the respawn ballot, word 0)
 template <class Net, class S>
 __global__ __launch_bounds__(TB) void k_ord_census(SrnnCfg c, SrnnArgs a) {
-  using I = Item<Net, S>;
   constexpr int PERM = (Net::P + 4) & ~3;
   __shared__ uint8_t s_perm[TB * PERM];
-  const int64_t gb = blockIdx.x;
-  const int64_t r = gb * TB + threadIdx.x;
-  const int lane = threadIdx.x;
-  int8_t k = -1;
-  if (r < a.n) {
-    float w[Net::P];
-    I::load(I::rowp(a.W, r), w);
-    k = I::classify_w(w, a.eps, (a.flags & SRNN_F_FIX_SEC) != 0,
-                      I::actx(a, c, (uint64_t)r, 0x7FFFFFF0u, s_perm + lane * PERM));
-  }
-  uint32_t cnt[5];
-#pragma unroll
-  for (int q = 0; q < 5; ++q) cnt[q] = (uint32_t)__popcll(__ballot(k == q));
-  if (lane == 0) {
-    unsigned long long* mine = reinterpret_cast<unsigned long long*>(a.temp) + gb * 4;
-    mine[1] = (unsigned long long)cnt[0] | ((unsigned long long)cnt[1] << 32);
-    mine[2] = (unsigned long long)cnt[2] | ((unsigned long long)cnt[3] << 32);
-    mine[3] = (unsigned long long)cnt[4];
-  }
+  ord_census_block<Net, S>(c, a, a.W, reinterpret_cast<uint64_t*>(a.temp), blockIdx.x, s_perm + threadIdx.x * PERM);
 }
 
 template <class Net, class S>
@@ -1069,7 +1089,8 @@ int soup_ord_census(const SrnnCfg& c, const SrnnArgs& a) {
 // list holds at most one entry per pending record's producer slot; waves past its end return
 // the run launch's workgroups: critical-list waves, turn waves, plan workgroups (SRNN_F_ORD_INPLAN)
 inline int64_t ord_run_grid(const SrnnArgs& ra, int64_t nb) {
-  return nb + ((ra.flags & SRNN_F_ORD_CRIT) ? ra.x_groups : 0) + ((ra.flags & SRNN_F_ORD_INPLAN) ? ra.o_plan_groups : 0);
+  return nb + ((ra.flags & SRNN_F_ORD_CRIT) ? ra.x_groups : 0) + ((ra.flags & SRNN_F_ORD_INPLAN) ? ra.o_plan_groups : 0) +
+         (ra.o_census_temp ? nb : 0);
 }
 // SRNN_F_ORD_INPLAN needs the next plan set, its lists and 1..4096 plan workgroups
 inline bool ord_inplan_ok(const SrnnArgs& a) {
@@ -1106,10 +1127,10 @@ inline SrnnArgs ord_next_plan_args(const SrnnArgs& a) {
 
 inline SrnnArgs ord_run_args(const SrnnArgs& a, int64_t nb) {
   SrnnArgs ra = a;
-  // (defaults measured, profiles/r6a r6q: per-wave lists 0.173 ms vs the ready queue 0.296; shadow
-  // lanes in every round below a full wave 0.165)
+  // (defaults measured, profiles/r6a r6q-r6r: per-wave lists 0.173 ms vs the ready queue 0.296; shadow
+  // lanes in rounds of <= 32 turns 0.160-0.162, <= 16 0.161-0.162, <= 63 0.163-0.165, off 0.172-0.173)
   if (knob(SRNN_KNOB_ORD_QUEUE, 0) != 0) ra.flags |= SRNN_F_ORD_QUEUE;
-  ra.o_shadow = std::max(0, knob(SRNN_KNOB_ORD_SHADOW, 63));
+  ra.o_shadow = std::max(0, knob(SRNN_KNOB_ORD_SHADOW, 32));
   if (knob(SRNN_KNOB_ORD_CRIT, 1) != 0) {
     ra.flags |= SRNN_F_ORD_CRIT;
     ra.x_groups = (int32_t)std::min<int64_t>(nb, (ord::rec_total(a.n) + TB - 1) / TB);

@@ -12,15 +12,17 @@ step() { local name=$1 lim=$2; shift 2; timeout -k 10 $lim "$@" > gpurun_out/${n
          echo "[$name rc=$rc] $(tail -1 gpurun_out/${name}_$TAG.log | cut -c1-200)"; return $rc; }
 timeout -k 10 600 python -u -m pytest tests/test_ordered_soup.py tests/test_ordered_bignet_gpu.py -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/pytest_$TAG.log 2>&1
 rc=$?; tail -1 gpurun_out/pytest_$TAG.log; [ $rc -eq 0 ] || exit $rc
-# same-box A/B: ready queue (now really the default) / per-wave lists; shadow lanes off / 8 / 63
+# same-box A/B: shadow threshold (per-wave lists, the default) and the census in the next run (default)
+# against the census in the close
 for i in 1 2; do
-  step q1_$i 300 python bench.py --steps 50 --warmup 5 --side-steps 0 || exit 1
-  SRNN_ORD_QUEUE=0 step q0_$i 300 python bench.py --steps 50 --warmup 5 --side-steps 0 || exit 1
-  SRNN_ORD_SHADOW=8 step s8_$i 300 python bench.py --steps 50 --warmup 5 --side-steps 0 || exit 1
-  SRNN_ORD_SHADOW=63 step s63_$i 300 python bench.py --steps 50 --warmup 5 --side-steps 0 || exit 1
-  SRNN_ORD_QUEUE=0 SRNN_ORD_SHADOW=63 step q0s63_$i 300 python bench.py --steps 50 --warmup 5 --side-steps 0 || exit 1
+  step sh63_$i 300 python bench.py --steps 50 --warmup 5 --side-steps 0 || exit 1
+  SRNN_ORD_CENSUS_SIDE=0 step cen0_$i 300 python bench.py --steps 50 --warmup 5 --side-steps 0 || exit 1
+  for sh in 0 16 32; do
+    SRNN_ORD_SHADOW=$sh step sh${sh}_$i 300 python bench.py --steps 50 --warmup 5 --side-steps 0 || exit 1
+  done
 done
+step prof 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_$TAG -o t --output-format csv -- python3 bench.py --steps 20 --warmup 5 --side-steps 0 || exit 1
 step tr 200 python bench/ordered_trace.py --gens 2 || exit 1
-SRNN_ORD_SHADOW=63 step trs 200 python bench/ordered_trace.py --gens 2 || exit 1
-for f in q1_1 q0_1 s8_1 s63_1 q0s63_1 q1_2 q0_2 s8_2 s63_2 q0s63_2; do python3 -c "import json,sys; d=json.loads(open(sys.argv[1]).read().splitlines()[-1]); print(sys.argv[2], '%.4f' % d['ms_per_step'], d['config']['execution']['library']['ord_queue'], d['config']['execution']['library']['ord_shadow'], d['config']['final_census'])" gpurun_out/${f}_$TAG.log $f; done
+step b1 300 python bench.py --steps 20 --warmup 5 || exit 1
+for f in sh63_1 cen0_1 sh0_1 sh16_1 sh32_1 sh63_2 cen0_2 sh0_2 sh16_2 sh32_2 b1; do python3 -c "import json,sys; d=json.loads(open(sys.argv[1]).read().splitlines()[-1]); print(sys.argv[2], '%.4f' % d['ms_per_step'], d['config']['execution']['library']['ord_queue'], d['config']['execution']['library']['ord_shadow'], d['config']['final_census'])" gpurun_out/${f}_$TAG.log $f; done
 echo done

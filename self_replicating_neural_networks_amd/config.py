@@ -111,8 +111,8 @@ class ExecConfig:
                                             # queue per generation, or per-wave lists (None: lists, measured
                                             # faster -- 0.173 vs 0.296 ms, profiles/r6a r6q)
     ord_shadow: Optional[int] = None        # SRNN_ORD_SHADOW: a reference-order round of at most this many
-                                            # turns in a wave runs each on several lanes (None: 63, every round
-                                            # below a full wave; 0: off)
+                                            # turns in a wave runs each on several lanes (None: 32, measured best
+                                            # of 16 / 32 / 63; 0: off)
     ordsh_emulate: int = 0                  # SRNN_ORDSH_EMULATE: one-rank timing model of R ranks of a sharded
                                             # reference-order generation (the rank runs 1/R of the turns;
                                             # the other turns never run: timing only, results invalid)

@@ -20,7 +20,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 # SRNN_LIB: load another build of the library (A/B of compiler flags on the GPU box)
 LIB_PATH = os.environ.get("SRNN_LIB") or os.path.join(_HERE, "libsrnn.so")
 CSRC = os.path.normpath(os.path.join(_HERE, "..", "..", "csrc"))
-ABI_VERSION = 29
+ABI_VERSION = 30
 
 # SrnnOp (csrc/srnn_abi.h)
 OP_INIT = 0
@@ -148,7 +148,7 @@ class SrnnArgs(ctypes.Structure):
         ("o_lo", _I64), ("o_hi", _I64),
         # SRNN_F_ORD_INPLAN: the next generation's plan set, built by the run launch's last workgroups
         ("o_src_next", _P), ("o_list_next", _P), ("o_ctl_next", _P), ("ptab_next", _P),
-        ("o_plan_groups", _I32), ("pad4", _I32), ("o_sync", _P), ("o_shadow", _I32), ("pad5", _I32),
+        ("o_plan_groups", _I32), ("pad4", _I32), ("o_sync", _P), ("o_shadow", _I32), ("pad5", _I32), ("o_census_temp", _P),
     ]
 
 

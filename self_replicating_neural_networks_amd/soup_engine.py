@@ -850,10 +850,12 @@ class SoupEngine:
                 fa.ptab = _p(self._perm_table(q))
                 if self._ord_pipe:
                     fa.flags |= _lib.FLAG_ORD_PLANNED
-                if self._sync:  # (two counter-ordered graphs: the census stays in the close)
+                if self._sync:  # (two counter-ordered graphs)
                     fa.flags |= _lib.FLAG_ORD_SYNC
                     fa.o_sync = _p(self._osync)
-                elif self._ord_census_side and (fa.flags & _lib.FLAG_FUSED_CENSUS):
+                if self._ord_census_side and (fa.flags & _lib.FLAG_FUSED_CENSUS):
+                    # the census of the final rows after the close: on the side stream beside the
+                    # next run, or (two-graph chunks) by extra workgroups of the next run launch
                     fa.flags |= _lib.FLAG_ORD_CENSUS_LATER
                 if self._ord_mode == "kernel":  # the run launch also builds the next generation's plan
                     nsrc, nlist, nctl = self._ord_set(1 - q)
@@ -963,10 +965,17 @@ class SoupEngine:
                 self._rec_rows = torch.zeros_like(self._abuf)
             ca.traj = _p(self._rec_rows)
             uid0 = self.uid.clone()
+        if self._sync and self._census_due is not None:
+            # the previous close's census by this run launch (its final rows are this generation's W2)
+            W, temp, _, _ = self._census_due
+            assert W == ca.W2, "census rows are the next generation's start rows"
+            ca.o_census_temp = temp
+            self._census_due = None
         try:
             _lib.run(_lib.OP_SOUP_ORDERED, spec, ca, cfg)
         finally:
             ca.traj = None
+            ca.o_census_temp = None
             if side is not None:
                 main.wait_stream(side)  # the next generation starts on a complete plan
         if ca.flags & _lib.FLAG_ORD_CENSUS_LATER:
@@ -1679,7 +1688,8 @@ class SoupEngine:
         ch = (gc, p0, G, gs)
         ok = self._agree(ok)
         if ok:
-            ok = self._agree(self._validate_replay(lambda: self._replay_chunk(ch), G, parity_after=p0))
+            ok = self._agree(self._validate_replay(lambda: self._replay_chunk(ch), G, parity_after=p0,
+                                                   ring=self.finish_mode == "batch"))
         return ch if ok else None
 
     def _replay_chunk(self, ch):
@@ -1711,7 +1721,7 @@ class SoupEngine:
                 self._p = 1 - self._p
         return self._validate_replay(replay, 2)
 
-    def _validate_replay(self, replay, gens: int, parity_after=None) -> bool:
+    def _validate_replay(self, replay, gens: int, parity_after=None, ring: bool = False) -> bool:
         """Run ``gens`` eager generations from the current state, restore it, run
         ``replay`` (the captured equivalent), compare bitwise, restore again."""
         state = self._state()
@@ -1738,6 +1748,10 @@ class SoupEngine:
         keep = {id(t) for t in self._bufs} | {id(getattr(self, k)) for k in (
             "uid", "next_uid", "_gen_ring", "counts", "census", "loss", "respawn", "action", "counterpart", "err")
             if isinstance(getattr(self, k, None), torch.Tensor)}
+        if ring and isinstance(getattr(self, "_bs_ring", None), torch.Tensor):
+            # (a chunk batches its finishes like the eager generations: every generation's census and
+            # ballots, wherever they ran, compared too)
+            keep.add(id(self._bs_ring))
         same = all(torch.equal(x.view(torch.uint8), y.view(torch.uint8))
                    for x, y in zip(state, eager) if id(x) in keep)
         # (reference order: and no error bit the eager generations did not raise either)
