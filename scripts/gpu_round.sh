@@ -10,17 +10,10 @@ export TMPDIR=/tmp
 TAG=${1:-round}
 step() { local name=$1 lim=$2; shift 2; timeout -k 10 $lim "$@" > gpurun_out/${name}_$TAG.log 2>&1; local rc=$?;
          echo "[$name rc=$rc] $(tail -1 gpurun_out/${name}_$TAG.log | cut -c1-200)"; return $rc; }
-timeout -k 10 600 python -u -m pytest tests/test_ordered_soup.py tests/test_ordered_bignet_gpu.py tests/test_exact_oracle_gpu.py tests/test_ordered_sharded_gpu.py -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/pytest_$TAG.log 2>&1
-rc=$?; tail -1 gpurun_out/pytest_$TAG.log; [ $rc -eq 0 ] || exit $rc
-# same-box A/B: version rows stored write-through, publish without a release (this build) against
-# the previous build (ab/libsrnn_base.so)
-B=$PWD/ab/libsrnn_base.so
-for i in 1 2 3; do
-  step new_$i 300 python bench.py --steps 50 --warmup 5 --side-steps 0 || exit 1
-  SRNN_LIB=$B step base_$i 300 python bench.py --steps 50 --warmup 5 --side-steps 0 || exit 1
-done
-step tr 200 python bench/ordered_trace.py --gens 2 || exit 1
-SRNN_LIB=$B step trb 200 python bench/ordered_trace.py --gens 2 || exit 1
-step prof 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_$TAG -o t --output-format csv -- python3 bench.py --steps 20 --warmup 5 --side-steps 0 || exit 1
-for f in new_1 base_1 new_2 base_2 new_3 base_3; do python3 -c "import json,sys; d=json.loads(open(sys.argv[1]).read().splitlines()[-1]); print(sys.argv[2], '%.4f' % d['ms_per_step'], d['config']['final_census'])" gpurun_out/${f}_$TAG.log $f; done
+# one SQ counter pass of the reference-order bench, shadow lanes on (default) and off
+C1="SQ_INSTS_VALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_WAIT_INST_ANY"
+timeout -s KILL 200 rocprofv3 --pmc $C1 -d gpurun_out/pmc_sh32_$TAG -o p --output-format csv -- python3 bench.py --steps 5 --warmup 2 --side-steps 0 > gpurun_out/pmc_sh32_$TAG.log 2>&1 || exit 1
+echo "pmc shadow 32 ok"
+SRNN_ORD_SHADOW=0 timeout -s KILL 200 rocprofv3 --pmc $C1 -d gpurun_out/pmc_sh0_$TAG -o p --output-format csv -- python3 bench.py --steps 5 --warmup 2 --side-steps 0 > gpurun_out/pmc_sh0_$TAG.log 2>&1 || exit 1
+echo "pmc shadow 0 ok"
 echo done

@@ -171,3 +171,24 @@ def test_every_library_knob_starts_at_its_default():
                          cwd=os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
     assert out.returncode == 0, out.stderr[-2000:]
     assert out.stdout.strip().splitlines()[-1] == "[-1]"
+
+
+def test_reference_order_stream_knobs_from_the_environment(monkeypatch):
+    """the round-6 reference-order knobs: two counter-ordered graphs per chunk (bool), shadow lanes
+    (int threshold, a library knob), the census beside the next generation (bool)"""
+    monkeypatch.setenv("SRNN_ORD_GRAPH_SYNC", "0")
+    monkeypatch.setenv("SRNN_ORD_SHADOW", "16")
+    monkeypatch.setenv("SRNN_ORD_CENSUS_SIDE", "0")
+    ex = ExecConfig().resolved()
+    assert ex.ord_graph_sync is False and ex.ord_shadow == 16 and ex.ord_census_side is False
+    assert _lib.get_knob("ord_shadow") == 16  # (the library reads the variable itself)
+    monkeypatch.delenv("SRNN_ORD_SHADOW")
+    assert ExecConfig().ord_graph_sync is True and _lib.get_knob("ord_shadow") == -1
+    try:
+        ExecConfig(ord_shadow=0).apply_library()
+        assert _lib.get_knob("ord_shadow") == 0
+    finally:
+        _lib.set_knob("ord_shadow", -1)
+    # host engines: no side stream, no counters, never a two-graph chunk
+    eng = SoupEngine(ArchSpec.weightwise(2, 2), 64, dict(train=1), order="sequential")
+    assert eng._osync is None and eng._ord_decouple is False and eng._chunks == []
