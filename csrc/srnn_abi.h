@@ -258,7 +258,7 @@ enum SrnnOp {
                         // independent: issued on a side stream while the previous generation runs
 };
 
-int srnn_abi_version();  // 30
+int srnn_abi_version();  // 31
 int64_t srnn_args_size();  // sizeof(SrnnArgs): the ctypes mirror checks its layout against it
 int64_t srnn_cfg_size();
 int srnn_has_config(const SrnnCfg* cfg);
@@ -291,5 +291,8 @@ enum SrnnKnob {
 };
 void srnn_set_knob(int knob, int value);
 int srnn_get_knob(int knob);
+// launches a waiter on stream `side` (bounded: timeout_us) and a setter on `main_stream`; after both
+// finished flag[1] is 1 when the two streams ran concurrently, 2 when the waiter timed out
+int srnn_stream_probe(int32_t* flag, void* side, void* main_stream, int64_t timeout_us);
 int64_t srnn_generic_scratch_bytes(const SrnnCfg* cfg, int64_t n, int64_t max_lanes);
 }

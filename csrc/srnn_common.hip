@@ -204,9 +204,41 @@ static int with_scratch(int op, const SrnnCfg* c, const SrnnArgs* a) {
   return dispatch(op, c, &b);
 }
 
+// ---- do two streams run concurrently?  (SRNN_F_ORD_SYNC graphs order their two streams by device
+// counters: a profiler that serialises kernels -- rocprofv3 --pmc -- or two streams that share a
+// hardware queue would turn every wait into a timeout.)  The waiter on `side` spins (bounded by
+// `timeout_us` of the 100 MHz real-time clock) for the flag the setter on `main` raises; f[1]:
+// 1 seen, 2 timed out.
+__global__ void k_stream_probe_wait(int32_t* f, int64_t ticks) {
+  if (threadIdx.x != 0) return;
+  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+  while (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 1) {
+    if ((int64_t)(__builtin_amdgcn_s_memrealtime() - t0) > ticks) {
+      __hip_atomic_store(f + 1, 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      return;
+    }
+    __builtin_amdgcn_s_sleep(2);
+  }
+  __hip_atomic_store(f + 1, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__global__ void k_stream_probe_set(int32_t* f) {
+  if (threadIdx.x == 0) __hip_atomic_store(f, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 extern "C" {
 
-int srnn_abi_version() { return 30; }
+int srnn_abi_version() { return 31; }
+
+int srnn_stream_probe(int32_t* flag, void* side, void* main_stream, int64_t timeout_us) {
+  hipLaunchKernelGGL(k_stream_probe_wait, dim3(1), dim3(64), 0, (hipStream_t)side, flag, timeout_us * 100);
+  hipLaunchKernelGGL(k_stream_probe_set, dim3(1), dim3(64), 0, (hipStream_t)main_stream, flag);
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) {
+    srnn::set_error(hipGetErrorString(e));
+    return -3;
+  }
+  return 0;
+}
 
 
 // layout check of the ctypes mirror (ops/_lib.py): sizeof(SrnnArgs) / sizeof(SrnnCfg)

@@ -388,7 +388,7 @@ static void ordered_soup(const SrnnCfg& c, int64_t n, int gens, int pipe) {
 }
 
 int main() {
-  CHECK(srnn_abi_version() == 30);
+  CHECK(srnn_abi_version() == 31);
   ordered_soup(ww22(), 257, 4, 0);
   ordered_soup(ww22(), 257, 4, 1);
   ordered_soup(ww22(), 257, 4, 2);

@@ -10,10 +10,8 @@ export TMPDIR=/tmp
 TAG=${1:-round}
 step() { local name=$1 lim=$2; shift 2; timeout -k 10 $lim "$@" > gpurun_out/${name}_$TAG.log 2>&1; local rc=$?;
          echo "[$name rc=$rc] $(tail -1 gpurun_out/${name}_$TAG.log | cut -c1-200)"; return $rc; }
-# one SQ counter pass of the reference-order bench, shadow lanes on (default) and off
-C1="SQ_INSTS_VALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_WAIT_INST_ANY"
-timeout -s KILL 200 rocprofv3 --pmc $C1 -d gpurun_out/pmc_sh32_$TAG -o p --output-format csv -- python3 bench.py --steps 5 --warmup 2 --side-steps 0 > gpurun_out/pmc_sh32_$TAG.log 2>&1 || exit 1
-echo "pmc shadow 32 ok"
-SRNN_ORD_SHADOW=0 timeout -s KILL 200 rocprofv3 --pmc $C1 -d gpurun_out/pmc_sh0_$TAG -o p --output-format csv -- python3 bench.py --steps 5 --warmup 2 --side-steps 0 > gpurun_out/pmc_sh0_$TAG.log 2>&1 || exit 1
-echo "pmc shadow 0 ok"
+timeout -k 10 600 python -u -m pytest tests/test_ordered_soup.py tests/test_ordered_bignet_gpu.py tests/test_exact_oracle_gpu.py -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/pytest_$TAG.log 2>&1
+rc=$?; tail -1 gpurun_out/pytest_$TAG.log; [ $rc -eq 0 ] || exit $rc
+step b1 300 python bench.py --steps 20 --warmup 5 || exit 1
+step b2 300 python bench.py --steps 50 --warmup 5 --side-steps 0 || exit 1
 echo done

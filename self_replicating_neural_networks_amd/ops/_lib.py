@@ -20,7 +20,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 # SRNN_LIB: load another build of the library (A/B of compiler flags on the GPU box)
 LIB_PATH = os.environ.get("SRNN_LIB") or os.path.join(_HERE, "libsrnn.so")
 CSRC = os.path.normpath(os.path.join(_HERE, "..", "..", "csrc"))
-ABI_VERSION = 30
+ABI_VERSION = 31
 
 # SrnnOp (csrc/srnn_abi.h)
 OP_INIT = 0
@@ -214,7 +214,8 @@ def lib():
                            ("srnn_comm_all_gather", [vp, vp, vp, i64, vp]),
                            ("srnn_comm_all_reduce_i64", [vp, vp, vp, i64, vp]),
                            ("srnn_comm_count", [vp]), ("srnn_comm_user_rank", [vp]),
-                           ("srnn_set_knob", [ctypes.c_int, ctypes.c_int]), ("srnn_get_knob", [ctypes.c_int])):
+                           ("srnn_set_knob", [ctypes.c_int, ctypes.c_int]), ("srnn_get_knob", [ctypes.c_int]),
+                           ("srnn_stream_probe", [vp, vp, vp, i64])):
             f = getattr(L, name)
             f.argtypes = args
             f.restype = ctypes.c_int
@@ -266,6 +267,20 @@ KNOB_ENV = {"force_generic": "SRNN_FORCE_GENERIC", "rnn_wave": "SRNN_RNN_WAVE", 
             "rnn_soup": "SRNN_RNN_SOUP", "ww_wave": "SRNN_WW_WAVE", "big_wave": "SRNN_BIG_WAVE",
             "fix_group": "SRNN_FIX_GROUP", "soup_lanes": "SRNN_SOUP_LANES", "ord_crit": "SRNN_ORD_CRIT",
             "ord_queue": "SRNN_ORD_QUEUE", "ord_shadow": "SRNN_ORD_SHADOW"}
+
+
+def streams_concurrent(side, main, device, timeout_us: int = 20000) -> bool:
+    """True when kernels on the two torch streams run at the same time (a waiter on ``side`` sees
+    the flag a setter on ``main`` raises within ``timeout_us``): False under a profiler that
+    serialises kernels or when the two streams share one hardware queue."""
+    import torch
+    flag = torch.zeros(2, dtype=torch.int32, device=device)
+    torch.cuda.synchronize(device)
+    if lib().srnn_stream_probe(ctypes.c_void_p(flag.data_ptr()), ctypes.c_void_p(side.cuda_stream),
+                               ctypes.c_void_p(main.cuda_stream), int(timeout_us)) != 0:
+        return False
+    torch.cuda.synchronize(device)
+    return int(flag[1].item()) == 1
 
 
 def set_knob(name: str, value: int) -> None:

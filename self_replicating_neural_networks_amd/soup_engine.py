@@ -1636,7 +1636,7 @@ class SoupEngine:
         after them -- ordered by device counters (SRNN_F_ORD_SYNC) instead of a cross-queue join
         per generation (~10 us of idle queue each, profiles/r6a); the one-graph form if that
         capture or its validation fails."""
-        if self._ord_decouple and self._lists_ready:
+        if self._ord_decouple and self._lists_ready and self._streams_concurrent():
             ch = self._capture_chunk_sync(s, p0, pend0, G)
             if ch is not None:
                 return ch
@@ -1658,6 +1658,20 @@ class SoupEngine:
         if ok:
             ok = self._agree(self._validate_replay(lambda: gc.replay(), G, parity_after=p0))
         return (gc, p0, G, None) if ok else None
+
+    def _streams_concurrent(self) -> bool:
+        """(once per engine) whether kernels on the side stream and the current one run at the same
+        time -- a two-graph chunk's counters need it: under a profiler that serialises kernels
+        (rocprofv3 --pmc) or on a shared hardware queue every wait would run into its timeout.
+        Agreed over the ranks."""
+        if getattr(self, "_conc", None) is None:
+            ok = _lib.streams_concurrent(self._ord_side, torch.cuda.current_stream(self.device), self.device)
+            if not ok:
+                import sys
+                print("side stream does not run beside the current one (serialising profiler?): "
+                      "one-graph chunks", file=sys.stderr)
+            self._conc = self._agree(ok)
+        return self._conc
 
     def _capture_chunk_sync(self, s, p0, pend0, G):
         """The two-graph form of a G-generation chunk (see _capture_chunk_g): main graph = G x

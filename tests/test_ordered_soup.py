@@ -254,3 +254,41 @@ def test_ordered_error_bits_are_sticky():
     assert o.ordered_error() == 2 and o.ordered_levels()["error"] == 2
     with pytest.raises(RuntimeError, match="error bits 2"):
         o.count()
+
+
+@pytest.mark.gpu
+def test_stream_probe_and_serialised_kernels_fall_back_to_one_graph():
+    """the two-graph chunks need the side stream to run beside the current one: the probe says so on
+    a normal process; with kernels serialised (AMD_SERIALIZE_KERNEL=3, like a counter-collecting
+    profiler) it says no and the engine keeps one-graph chunks -- the soup bitwise the same"""
+    import os
+    import subprocess
+    import sys
+    side = torch.cuda.Stream(priority=-1)
+    assert _lib.streams_concurrent(side, torch.cuda.current_stream(), torch.device("cuda", 0))
+    code = """
+import torch, json
+from self_replicating_neural_networks_amd.arch import ArchSpec
+from self_replicating_neural_networks_amd.soup_engine import SoupEngine
+hot = dict(attacking_rate=0.3, learn_from_rate=0.3, train=2, learn_from_severity=2, remove_divergent=True,
+           remove_zero=True, epsilon=1e-4)
+o = SoupEngine(ArchSpec.weightwise(2, 2), 2000, hot, device="cuda", seed=3, order="sequential")
+assert o.capture(warmup=1)
+o.evolve(4)
+print(json.dumps(dict(two=any(c[3] is not None for c in o._chunks), conc=o._conc,
+                      rows=o.local_rows()[:, :14].contiguous().view(torch.int32).long().sum().item(),
+                      uids=o.uid.sum().item(), err=o.ordered_levels()["error"])))
+"""
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    out = {}
+    for ser in ("0", "3"):
+        env = dict(os.environ, AMD_SERIALIZE_KERNEL=ser)
+        p = subprocess.run([sys.executable, "-c", code], env=env, cwd=root, capture_output=True, text=True,
+                           timeout=240)
+        assert p.returncode == 0, p.stderr[-2000:]
+        out[ser] = __import__("json").loads(p.stdout.strip().splitlines()[-1])
+    assert out["0"]["conc"] and out["0"]["two"]
+    assert not out["3"]["conc"] and not out["3"]["two"]
+    # (the rows' bit patterns summed: the same soup, NaN rows of divergent particles included)
+    assert out["0"]["rows"] == out["3"]["rows"] and out["0"]["uids"] == out["3"]["uids"]
+    assert out["0"]["err"] == out["3"]["err"] == 0
