@@ -67,7 +67,10 @@ __global__ __launch_bounds__(TB) void k_ordsh_levels(SrnnArgs a) {
   if (maxl) atomicMax(a.o_ctl + ord::MAXLW, maxl);
 }
 
-// this rank's turns of level L (lane per own turn; the others return at once)
+// this rank's turns of level L (lane per own turn; a wave without one returns at once).  A wave
+// with at most a.o_shadow of them (the deep levels are sparse) runs each on several lanes: the idle
+// lanes repeat a busy lane's turn -- identical values to identical addresses -- as k_ord_run's
+// shadow lanes (a lone lane's SGD chain is ~16 % slower than a full wave's, profiles/r6a)
 template <class Net, class S>
 __global__ __launch_bounds__(TB) void k_ordsh_level(SrnnCfg c, SrnnArgs a, int32_t L) {
   using I = Item<Net, S>;
@@ -76,9 +79,19 @@ __global__ __launch_bounds__(TB) void k_ordsh_level(SrnnCfg c, SrnnArgs a, int32
   __shared__ float4 s_samp[TB * SAMP];
   __shared__ uint8_t s_perm[TB * PERM];
   const int lane = threadIdx.x;
-  const int64_t k = a.o_lo + (int64_t)blockIdx.x * TB + lane;
-  if (k < a.o_hi && a.o_src[4 * k + 3] == L)
-    ord::Ord<Net, S>::turn(c, a, k, I::gen_of(a), samp_lane<Net>(s_samp, lane), s_perm + lane * PERM);
+  int64_t k = a.o_lo + (int64_t)blockIdx.x * TB + lane;
+  bool mine = k < a.o_hi && a.o_src[4 * k + 3] == L;
+  const unsigned long long busy = __ballot(mine);
+  if (!busy) return;
+  const int nbusy = (int)__popcll(busy);
+  if (nbusy < TB && nbusy <= a.o_shadow) {  // (wave uniform)
+    unsigned long long m = busy;
+    for (int i = lane % nbusy; i > 0; --i) m &= m - 1;
+    const int src = mine ? lane : (int)__ffsll((long long)m) - 1;
+    k = __shfl(k, src);
+    mine = true;
+  }
+  if (mine) ord::Ord<Net, S>::turn(c, a, k, I::gen_of(a), samp_lane<Net>(s_samp, lane), s_perm + lane * PERM);
 }
 
 // records of this rank's level-L outputs (append order is irrelevant: records carry their slot)
@@ -264,7 +277,11 @@ int soup_ordered_sh(const SrnnCfg& c, const SrnnArgs& a) {
       hipLaunchKernelGGL((k_ordsh_levels<Net, S>), dim3(nb), dim3(TB), 0, st, a);
       break;
     case ordsh::LEVEL:
-      hipLaunchKernelGGL((k_ordsh_level<Net, S>), dim3(nbo), dim3(TB), 0, st, c, a, L);
+      {
+        SrnnArgs la = a;
+        la.o_shadow = std::max(0, knob(SRNN_KNOB_ORD_SHADOW, 32));
+        hipLaunchKernelGGL((k_ordsh_level<Net, S>), dim3(nbo), dim3(TB), 0, st, c, la, L);
+      }
       break;
     case ordsh::PACK:
       hipLaunchKernelGGL((k_ordsh_pack<Net, S>), dim3(nbo), dim3(TB), 0, st, a, L);

@@ -1078,11 +1078,7 @@ class SoupEngine:
             _lib.run(_lib.OP_SOUP_DECIDE, spec, self._sh_args(_lib.ORDSH_PLAN), cfg)
         d.all_gather_rows(self.full.view(torch.int32), self.table_in.view(torch.int32), N)
         run(_lib.ORDSH_PLAN)
-        lv = self._osrc[:4 * N].view(N, 4)[:, 3]
-        maxl = int(self._octl[_lib.ORD_MAXLW].item())
-        counts = torch.stack([torch.bincount(lv[lo:hi].clamp(min=0).long(), minlength=maxl + 1)[:maxl + 1]
-                              for lo, hi in (d.shard_of_rank(r, N) for r in range(R))])
-        caps = counts.max(dim=0).values.cpu().tolist()  # records per rank and level: the same on every rank
+        caps, maxl = self._sh_level_caps(N, R)  # records per rank and level: the same on every rank
         recw = self._sh_recb // 8
         for L in range(maxl + 1):
             run(_lib.ORDSH_LEVEL, L)
@@ -1102,6 +1098,33 @@ class SoupEngine:
         self._p = 1 - self._p
         self._pending = True
         self._flush()
+
+    _SH_LEVEL_BINS = 64
+
+    def _sh_level_caps(self, N: int, R: int):
+        """The largest count of one rank's turns at each dependency level (every rank plans the
+        whole generation, so every rank computes the same numbers) and the deepest level, read back
+        in ONE device-to-host copy: turns binned by (rank of the slot, level) with a scatter-add --
+        the rank of slot k is ((k + 1) R - 1) // N for the shards [r N / R, (r + 1) N / R) -- instead
+        of a bincount per rank (each one a host synchronisation)."""
+        B = self._SH_LEVEL_BINS
+        lv = self._osrc[:4 * N].view(N, 4)[:, 3]
+        if N <= (1 << 24):
+            if getattr(self, "_sh_key", None) is None or self._sh_key.numel() != N:
+                k = torch.arange(N, dtype=torch.int64, device=self.device)
+                self._sh_key = ((k + 1) * R - 1) // N * B
+                self._sh_one = torch.ones(N, dtype=torch.int64, device=self.device)
+            key = self._sh_key + lv.clamp(0, B - 1).long()
+            cnt = torch.zeros(R * B, dtype=torch.int64, device=self.device).scatter_add_(0, key, self._sh_one)
+            info = torch.cat([cnt.view(R, B).max(dim=0).values,
+                              self._octl[_lib.ORD_MAXLW:_lib.ORD_MAXLW + 1].long()]).cpu().tolist()
+            maxl = int(info[-1])
+            if maxl < B:
+                return info[:maxl + 1], maxl
+        maxl = int(self._octl[_lib.ORD_MAXLW].item())
+        counts = torch.stack([torch.bincount(lv[lo:hi].clamp(min=0).long(), minlength=maxl + 1)[:maxl + 1]
+                              for lo, hi in (self.dist.shard_of_rank(r, N) for r in range(R))])
+        return counts.max(dim=0).values.cpu().tolist(), maxl
 
     def _finish_pending(self):
         """Batch mode: ONE finish launch for the generations whose block stats wait in the
