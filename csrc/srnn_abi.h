@@ -205,7 +205,7 @@ struct SrnnArgs {
   int32_t* o_ctl_next;
   uint64_t* ptab_next;
   int32_t o_plan_groups;
-  int32_t pad4;
+  int32_t o_bulk_delay;  // (internal, SRNN_KNOB_ORD_BULK_DELAY) us the run's turn waves wait before their first turn
   // ---- SRNN_F_ORD_SYNC: 4 monotonic int32 counters shared by the main and the side stream:
   // runs started, plans gated, plans done, closes waited (srnn_ordered.h ord::SYNC_*)
   int32_t* o_sync;
@@ -287,7 +287,9 @@ enum SrnnKnob {
   SRNN_KNOB_ORD_SHADOW = 10,    // SRNN_ORD_SHADOW: a reference-order round with at most this many turns in a
                                 //   wave runs each on several lanes (the idle lanes repeat a busy lane's
                                 //   turn; 0: off; default 32)
-  SRNN_KNOB_COUNT = 11
+  SRNN_KNOB_ORD_BULK_DELAY = 11, // SRNN_ORD_BULK_DELAY: microseconds a reference-order run's turn waves (not the
+                                 //   critical-list waves) wait before their first turn (default 12)
+  SRNN_KNOB_COUNT = 12
 };
 void srnn_set_knob(int knob, int value);
 int srnn_get_knob(int knob);

@@ -116,10 +116,10 @@ namespace {
 const char* const g_knob_env[SRNN_KNOB_COUNT] = {"SRNN_FORCE_GENERIC", "SRNN_RNN_WAVE", "SRNN_RNN_SPEC",
                                                  "SRNN_RNN_SOUP",      "SRNN_WW_WAVE",  "SRNN_BIG_WAVE",
                                                  "SRNN_FIX_GROUP",     "SRNN_SOUP_LANES", "SRNN_ORD_CRIT",
-                                                 "SRNN_ORD_QUEUE",     "SRNN_ORD_SHADOW"};
+                                                 "SRNN_ORD_QUEUE",     "SRNN_ORD_SHADOW", "SRNN_ORD_BULK_DELAY"};
 // (every knob starts at -1 = its built-in default)
-int g_knob[SRNN_KNOB_COUNT] = {-1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1};
-static_assert(sizeof(g_knob) / sizeof(g_knob[0]) == SRNN_KNOB_COUNT && SRNN_KNOB_COUNT == 11, "one -1 per knob");
+int g_knob[SRNN_KNOB_COUNT] = {-1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1};
+static_assert(sizeof(g_knob) / sizeof(g_knob[0]) == SRNN_KNOB_COUNT && SRNN_KNOB_COUNT == 12, "one -1 per knob");
 }  // namespace
 namespace srnn {
 int knob(int id, int dflt) {

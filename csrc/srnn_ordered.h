@@ -833,6 +833,10 @@ __global__ __launch_bounds__(TB) void k_ord_run(SrnnCfg c, SrnnArgs a) {
   } else {
     const int64_t k = (bid - ncw) * TB + lane;
     if (k < a.n && a.o_list[k] < 0 && !(ncw && ord::cons_head(a)[k] != ord::EMPTY)) cur = k;
+    if (a.o_bulk_delay > 0) {  // (SRNN_KNOB_ORD_BULK_DELAY: the critical roots first, at full clock)
+      const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+      while (__builtin_amdgcn_s_memrealtime() - t0 < (uint64_t)a.o_bulk_delay * 100u) __builtin_amdgcn_s_sleep(16);
+    }
   }
   if (cur >= 0) ord::st_level(a.o_src + 4 * cur + 3, 0);
   int32_t ready = ord::EMPTY, nready = 0, curlvl = 0;  // (curlvl: the level of this lane's turn)
@@ -1131,6 +1135,10 @@ inline SrnnArgs ord_run_args(const SrnnArgs& a, int64_t nb) {
   // lanes in rounds of <= 32 turns 0.160-0.162, <= 16 0.161-0.162, <= 63 0.163-0.165, off 0.172-0.173)
   if (knob(SRNN_KNOB_ORD_QUEUE, 0) != 0) ra.flags |= SRNN_F_ORD_QUEUE;
   ra.o_shadow = std::max(0, knob(SRNN_KNOB_ORD_SHADOW, 32));
+  // (the turn waves start 12 us after the critical-list waves: the roots' SGD chains run their first
+  // epochs before the bulk pulls the clock down; measured 0: 0.163-0.164 ms, 6: 0.160-0.162, 10:
+  // 0.158-0.161, 14: 0.159-0.160, 20: 0.159-0.160, 35: 0.164, profiles/r6a r6i-r6j)
+  ra.o_bulk_delay = std::min(1000, std::max(0, knob(SRNN_KNOB_ORD_BULK_DELAY, 12)));
   if (knob(SRNN_KNOB_ORD_CRIT, 1) != 0) {
     ra.flags |= SRNN_F_ORD_CRIT;
     ra.x_groups = (int32_t)std::min<int64_t>(nb, (ord::rec_total(a.n) + TB - 1) / TB);

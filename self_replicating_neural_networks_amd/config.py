@@ -113,6 +113,9 @@ class ExecConfig:
     ord_shadow: Optional[int] = None        # SRNN_ORD_SHADOW: a reference-order round of at most this many
                                             # turns in a wave runs each on several lanes (None: 32, measured best
                                             # of 16 / 32 / 63; 0: off)
+    ord_bulk_delay: Optional[int] = None    # SRNN_ORD_BULK_DELAY: microseconds a reference-order run's turn
+                                            # waves wait before their first turn, the critical chain's root
+                                            # ahead of the bulk (None: 12, measured best of 0-35)
     ordsh_emulate: int = 0                  # SRNN_ORDSH_EMULATE: one-rank timing model of R ranks of a sharded
                                             # reference-order generation (the rank runs 1/R of the turns;
                                             # the other turns never run: timing only, results invalid)
@@ -142,7 +145,7 @@ class ExecConfig:
                 force_generic="SRNN_FORCE_GENERIC", ww_wave="SRNN_WW_WAVE", rnn_wave="SRNN_RNN_WAVE",
                 rnn_spec="SRNN_RNN_SPEC", rnn_soup="SRNN_RNN_SOUP", big_wave="SRNN_BIG_WAVE",
                 fix_group="SRNN_FIX_GROUP", soup_lanes="SRNN_SOUP_LANES", ord_crit="SRNN_ORD_CRIT", ord_queue="SRNN_ORD_QUEUE",
-                ord_shadow="SRNN_ORD_SHADOW",
+                ord_shadow="SRNN_ORD_SHADOW", ord_bulk_delay="SRNN_ORD_BULK_DELAY",
                 ordsh_emulate="SRNN_ORDSH_EMULATE",
                 order_levels="SRNN_ORDER_LEVELS",
                 perm_table="SRNN_PERM_TABLE", ord_pipeline="SRNN_ORD_PIPELINE",
@@ -151,7 +154,7 @@ class ExecConfig:
     TRI_STATE = ("force_generic", "rnn_wave", "rnn_spec", "rnn_soup", "big_wave", "fix_group", "perm_table",
                  "ord_crit", "ord_queue")
     LIBRARY_KNOBS = ("force_generic", "ww_wave", "rnn_wave", "rnn_spec", "rnn_soup", "big_wave", "fix_group",
-                     "soup_lanes", "ord_crit", "ord_queue", "ord_shadow")
+                     "soup_lanes", "ord_crit", "ord_queue", "ord_shadow", "ord_bulk_delay")
 
     def validate(self):
         if self.finish_mode not in ("batch", "serial"):
@@ -191,7 +194,7 @@ class ExecConfig:
                 kw[f.name] = {"1": "stream", "true": "stream", "on": "stream", "0": "off", "false": "off"}.get(v.lower(), v)
             elif f.name == "x2_emulate_remote":
                 kw[f.name] = float(v)
-            elif f.name in ("soup_lanes", "order_levels", "ww_wave", "ordsh_emulate", "ord_shadow"):
+            elif f.name in ("soup_lanes", "order_levels", "ww_wave", "ordsh_emulate", "ord_shadow", "ord_bulk_delay"):
                 kw[f.name] = int(v)
             elif f.name in self.TRI_STATE:
                 kw[f.name] = _tri_state(v)

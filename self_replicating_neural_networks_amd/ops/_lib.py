@@ -148,7 +148,7 @@ class SrnnArgs(ctypes.Structure):
         ("o_lo", _I64), ("o_hi", _I64),
         # SRNN_F_ORD_INPLAN: the next generation's plan set, built by the run launch's last workgroups
         ("o_src_next", _P), ("o_list_next", _P), ("o_ctl_next", _P), ("ptab_next", _P),
-        ("o_plan_groups", _I32), ("pad4", _I32), ("o_sync", _P), ("o_shadow", _I32), ("pad5", _I32), ("o_census_temp", _P),
+        ("o_plan_groups", _I32), ("o_bulk_delay", _I32), ("o_sync", _P), ("o_shadow", _I32), ("pad5", _I32), ("o_census_temp", _P),
     ]
 
 
@@ -262,11 +262,11 @@ def supports(spec, op: int, device: bool, dtype: int = DTYPE_FP32) -> bool:
 # execution knobs (csrc/srnn_abi.h SrnnKnob; config.py ExecConfig): the environment variable
 # of a knob, when set, overrides what is set here
 KNOBS = {"force_generic": 0, "rnn_wave": 1, "rnn_spec": 2, "rnn_soup": 3, "ww_wave": 4, "big_wave": 5,
-         "fix_group": 6, "soup_lanes": 7, "ord_crit": 8, "ord_queue": 9, "ord_shadow": 10}
+         "fix_group": 6, "soup_lanes": 7, "ord_crit": 8, "ord_queue": 9, "ord_shadow": 10, "ord_bulk_delay": 11}
 KNOB_ENV = {"force_generic": "SRNN_FORCE_GENERIC", "rnn_wave": "SRNN_RNN_WAVE", "rnn_spec": "SRNN_RNN_SPEC",
             "rnn_soup": "SRNN_RNN_SOUP", "ww_wave": "SRNN_WW_WAVE", "big_wave": "SRNN_BIG_WAVE",
             "fix_group": "SRNN_FIX_GROUP", "soup_lanes": "SRNN_SOUP_LANES", "ord_crit": "SRNN_ORD_CRIT",
-            "ord_queue": "SRNN_ORD_QUEUE", "ord_shadow": "SRNN_ORD_SHADOW"}
+            "ord_queue": "SRNN_ORD_QUEUE", "ord_shadow": "SRNN_ORD_SHADOW", "ord_bulk_delay": "SRNN_ORD_BULK_DELAY"}
 
 
 def streams_concurrent(side, main, device, timeout_us: int = 20000) -> bool:
