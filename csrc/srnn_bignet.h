@@ -2056,7 +2056,10 @@ int big_soup_ordered(const SrnnCfg& c, const SrnnArgs& a) {
   if (nb <= 0) return 0;
   hipStream_t st = (hipStream_t)a.stream;
   if (!planned) ord_plan_dev<1, void>(c, a, false);
-  const SrnnArgs ra = ord_run_args(a, nb);
+  SrnnArgs ra = ord_run_args(a, nb);
+  // (no head start for the critical roots by default: a 1M soup's bulk is the generation's work, and
+  // delaying its first round cost 0.5-1.5 %, profiles/r6a r6n)
+  ra.o_bulk_delay = std::min(1000, std::max(0, knob(SRNN_KNOB_ORD_BULK_DELAY, 0)));
   hipLaunchKernelGGL((k_ord_run<BigOrdPol<T, S, SHUF>>), dim3((unsigned)ord_run_grid(ra, nb)), dim3(TB), 0, st, c, ra);
   hipLaunchKernelGGL((k_ordbig_close<T, S, SHUF>), dim3((unsigned)nb), dim3(TB), 0, st, c, a);
   if (!(a.flags & SRNN_F_GEN_COUNTS)) {

@@ -833,7 +833,9 @@ __global__ __launch_bounds__(TB) void k_ord_run(SrnnCfg c, SrnnArgs a) {
   } else {
     const int64_t k = (bid - ncw) * TB + lane;
     if (k < a.n && a.o_list[k] < 0 && !(ncw && ord::cons_head(a)[k] != ord::EMPTY)) cur = k;
-    if (a.o_bulk_delay > 0) {  // (SRNN_KNOB_ORD_BULK_DELAY: the critical roots first, at full clock)
+    // (SRNN_KNOB_ORD_BULK_DELAY: the critical roots first, at full clock -- only the first residency
+    // round of turn waves waits: a soup of many rounds (1M big-net turns) would pay it per round)
+    if (a.o_bulk_delay > 0 && bid - ncw < 2048) {
       const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
       while (__builtin_amdgcn_s_memrealtime() - t0 < (uint64_t)a.o_bulk_delay * 100u) __builtin_amdgcn_s_sleep(16);
     }

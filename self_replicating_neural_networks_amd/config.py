@@ -115,7 +115,8 @@ class ExecConfig:
                                             # of 16 / 32 / 63; 0: off)
     ord_bulk_delay: Optional[int] = None    # SRNN_ORD_BULK_DELAY: microseconds a reference-order run's turn
                                             # waves wait before their first turn, the critical chain's root
-                                            # ahead of the bulk (None: 12, measured best of 0-35)
+                                            # ahead of the bulk (None: 12 for the lane nets, first residency
+                                            # round only, measured best of 0-35; 0 for the big nets)
     ordsh_emulate: int = 0                  # SRNN_ORDSH_EMULATE: one-rank timing model of R ranks of a sharded
                                             # reference-order generation (the rank runs 1/R of the turns;
                                             # the other turns never run: timing only, results invalid)
